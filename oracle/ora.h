@@ -1,0 +1,108 @@
+// ============================================================================
+// ORACLE — TEST INFRASTRUCTURE ONLY.
+// A plain single-threaded CPU restatement of the reference (kennychenfs/KataCoffee)
+// self-play hot path: Coffee rules, V1 encoder, residual-net forward, MCTS
+// (KataGo search semantics restated for Coffee), move choice and training rows.
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+// it; the product (katacoffee_amd/) never links or calls it.
+//
+// Parity pinning (see DESIGN.md "Oracle"):
+//   rules / zobrist / state hash : bit-exact vs tests/golden/rules_*.npz, produced
+//                                  by the reference's own cpp/game (oracle/_ref)
+//   Rand / t-dist CDF table      : tests/golden/rand_kat.npz, tdist3.npz (reference)
+//   NN layers                    : tests/golden/nnlayers_*.npz (reference testnn.cpp KATs)
+//   encoder / search / rows      : "parity unpinned" by any reference test — the
+//                                  reference does not compile for these (SURVEY §0,
+//                                  §8c); pinned by SPEC decisions in DESIGN.md.
+// ============================================================================
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace ora {
+
+constexpr int MAX_LEN = 10;
+constexpr int MAX_AREA = MAX_LEN * MAX_LEN;
+constexpr int MAX_P = 4 * MAX_AREA;
+constexpr int ARR = (MAX_LEN + 1) * (MAX_LEN + 2) + 1;
+constexpr int NUM_SPATIAL = 15;  // README "V1" table (SPEC a6)
+constexpr int NUM_GLOBAL = 1;
+constexpr int HIST = 5;
+
+struct H128 {
+  uint64_t h0 = 0, h1 = 0;
+  H128 operator^(const H128& o) const { return H128{h0 ^ o.h0, h1 ^ o.h1}; }
+  bool operator==(const H128& o) const { return h0 == o.h0 && h1 == o.h1; }
+};
+
+struct Tables {
+  H128 board[ARR][4];
+  H128 board2[ARR][4];
+  H128 player[4];
+  H128 sizeX[MAX_LEN + 1];
+  H128 sizeY[MAX_LEN + 1];
+  H128 gameOver;
+  float cdf[2000];  // t-dist(3) CDF on [-50,50] (search.cpp:111-116)
+  bool loaded = false;
+};
+extern Tables T;
+
+struct Geom {
+  int X, Y, W, A, P;
+  Geom(int x = 5, int y = 5, int w = 4) : X(x), Y(y), W(w), A(x * y), P(4 * x * y) {}
+};
+
+// Board state (board.h:112-228 + the parts of BoardHistory the hot path reads).
+struct Board {
+  uint8_t c[MAX_AREA];   // 0 empty, 1 black, 2 white; cell = y*X + x
+  int8_t lastCell;       // -1 = none
+  int8_t lastDir;        // 0 N, 1 W, 2 NW, 3 NE, 4 NONE (board.h:41-47)
+  uint8_t pla;           // player to move
+  uint8_t finished;      // BoardHistory::isGameFinished
+  uint8_t winner;        // 0 = draw / none
+  int16_t turn;          // moves played from the start
+  int8_t histCell[HIST]; // [0] = last move ... [4] = 5 moves ago, -1 absent
+  int8_t histDir[HIST];
+  H128 posHash;          // Board::pos_hash
+};
+
+void boardInit(const Geom& g, Board& b);
+bool isLegal(const Geom& g, const Board& b, int cell, int dir);
+bool hasAnyLegal(const Geom& g, const Board& b);
+int maxRun(const Geom& g, const Board& b, int cell);
+void playMove(const Geom& g, Board& b, int cell, int dir);  // updates finished/winner (SPEC B16)
+H128 stateHash(const Geom& g, const Board& b);               // graph-search key (SPEC a20)
+int spotOf(const Geom& g, int cell);
+void encodeV1(const Geom& g, const Board& b, int sym, float* bin /*15*A*/, float* glob /*1*/);
+int symCell(const Geom& g, int cell, int sym);
+int symDir(int dir, int sym);
+
+// --------------------------------------------------------------------------
+// Neural net (Coffee b-blocks x c-channels; eigenbackend.cpp:888-1377 semantics)
+struct ModelCfg {
+  int cin = NUM_SPATIAL, gin = NUM_GLOBAL;
+  int C = 96, Cg = 32, p1 = 32, g1 = 32, v1 = 32, v2 = 64;
+  int nblocks = 6;
+  int kinds[32] = {0, 0, 1, 0, 1, 0};  // 0 regular, 1 gpool
+};
+struct Model {
+  ModelCfg cfg;
+  // All tensors f32, layout documented in katacoffee_amd/csrc/model_format.h
+  std::vector<float> convInit, globInit;
+  struct Block {
+    int kind;
+    std::vector<float> bn1s, bn1b, conv1, conv1g, bngs, bngb, linG, bn2s, bn2b, conv2;
+  };
+  std::vector<Block> blocks;
+  std::vector<float> tips, tipb;
+  std::vector<float> pConv1, pConvG, pBiasG, pLinG, pBias2, pConv2;
+  std::vector<float> vConv1, vBias1, vLin2, vB2, vLin3, vB3, vLinM, vBM;
+};
+bool modelLoad(const char* path, Model& m);
+// n boards of size X*Y; bin NCHW [n][cin][A], glob [n][gin];
+// outputs: policy logits [n][4][A], value logits [n][2], misc [n][2].
+// mode 0: fp32; mode 1: emulate the GPU kernel's bf16 rounding points.
+void nnForward(const Model& m, int X, int Y, int n, const float* bin, const float* glob,
+               float* policy, float* value, float* misc, int mode, int threads);
+
+}  // namespace ora

@@ -1,0 +1,196 @@
+// ORACLE (test infrastructure only) — extern "C" surface for the Python test
+// harness (ctypes) and bench.py's cpu_baseline leg.  Never linked by the product.
+#include <cstdio>
+#include <cstring>
+
+#include "ora.h"
+#include "ora_search.h"
+
+using namespace ora;
+
+extern "C" {
+
+int ora_load_tables(const uint64_t* board, const uint64_t* board2, const uint64_t* player, const uint64_t* sizeX,
+                    const uint64_t* sizeY, const uint64_t* gameOver, const float* cdf) {
+  memcpy(T.board, board, sizeof(T.board));
+  memcpy(T.board2, board2, sizeof(T.board2));
+  memcpy(T.player, player, sizeof(T.player));
+  memcpy(T.sizeX, sizeX, sizeof(T.sizeX));
+  memcpy(T.sizeY, sizeY, sizeof(T.sizeY));
+  memcpy(&T.gameOver, gameOver, sizeof(T.gameOver));
+  memcpy(T.cdf, cdf, sizeof(T.cdf));
+  T.loaded = true;
+  return 0;
+}
+
+static void toBoard(const Geom& g, Board& b, const uint8_t* colors, int lastCell, int lastDir, int pla,
+                    const int8_t* histCell, const int8_t* histDir) {
+  boardInit(g, b);
+  H128 h = b.posHash;
+  for(int c = 0; c < g.A; c++) {
+    b.c[c] = colors[c];
+    if(colors[c] == 1 || colors[c] == 2)
+      h = h ^ T.board[spotOf(g, c)][colors[c]];
+  }
+  b.posHash = h;
+  b.lastCell = (int8_t)lastCell;
+  b.lastDir = (int8_t)lastDir;
+  b.pla = (uint8_t)pla;
+  for(int i = 0; i < HIST; i++) {
+    b.histCell[i] = histCell ? histCell[i] : (i == 0 ? (int8_t)lastCell : (int8_t)-1);
+    b.histDir[i] = histDir ? histDir[i] : (i == 0 ? (int8_t)lastDir : (int8_t)4);
+  }
+}
+
+// Legal mask for n positions: legal[i][dir*A + cell] (NNPos::xydToPos order).
+int ora_rules_batch(int X, int Y, int W, int n, const uint8_t* colors, const int8_t* lastCell, const int8_t* lastDir,
+                    const uint8_t* pla, uint8_t* legal, uint8_t* hasLegal) {
+  Geom g(X, Y, W);
+  for(int i = 0; i < n; i++) {
+    Board b;
+    toBoard(g, b, colors + (size_t)i * g.A, lastCell[i], lastDir[i], pla[i], nullptr, nullptr);
+    bool any = false;
+    for(int p = 0; p < g.P; p++) {
+      bool ok = isLegal(g, b, p % g.A, p / g.A);
+      legal[(size_t)i * g.P + p] = ok ? 1 : 0;
+      any = any || ok;
+    }
+    hasLegal[i] = any ? 1 : 0;
+  }
+  return 0;
+}
+
+// Plays move[i] (pos = dir*A + cell) on each position; reports the post-move state.
+int ora_play_batch(int X, int Y, int W, int n, const uint8_t* colors, const int8_t* lastCell, const int8_t* lastDir,
+                   const uint8_t* pla, const int32_t* move, uint8_t* outColors, uint8_t* finished, uint8_t* winner,
+                   int32_t* maxRunOut, uint64_t* posHash, uint64_t* stHash) {
+  Geom g(X, Y, W);
+  for(int i = 0; i < n; i++) {
+    Board b;
+    toBoard(g, b, colors + (size_t)i * g.A, lastCell[i], lastDir[i], pla[i], nullptr, nullptr);
+    int cell = move[i] % g.A, dir = move[i] / g.A;
+    playMove(g, b, cell, dir);
+    memcpy(outColors + (size_t)i * g.A, b.c, g.A);
+    finished[i] = b.finished;
+    winner[i] = b.winner;
+    maxRunOut[i] = maxRun(g, b, cell);
+    posHash[2 * i] = b.posHash.h0;
+    posHash[2 * i + 1] = b.posHash.h1;
+    H128 s = stateHash(g, b);
+    stHash[2 * i] = s.h0;
+    stHash[2 * i + 1] = s.h1;
+  }
+  return 0;
+}
+
+int ora_encode_batch(int X, int Y, int W, int n, const uint8_t* colors, const int8_t* histCell, const int8_t* histDir,
+                     const uint8_t* pla, const int32_t* sym, float* bin, float* glob) {
+  Geom g(X, Y, W);
+  for(int i = 0; i < n; i++) {
+    Board b;
+    const int8_t* hc = histCell + (size_t)i * HIST;
+    const int8_t* hd = histDir + (size_t)i * HIST;
+    toBoard(g, b, colors + (size_t)i * g.A, hc[0], hd[0], pla[i], hc, hd);
+    encodeV1(g, b, sym[i], bin + (size_t)i * NUM_SPATIAL * g.A, glob + i);
+  }
+  return 0;
+}
+
+int ora_fake_net(int X, int Y, int W, int n, const float* bin, float* out /*[n][P+4]*/) {
+  Geom g(X, Y, W);
+  for(int i = 0; i < n; i++) {
+    float* o = out + (size_t)i * (g.P + 4);
+    fakeNet(g, bin + (size_t)i * NUM_SPATIAL * g.A, o, o + g.P, o + g.P + 2);
+  }
+  return 0;
+}
+
+void* ora_model_load(const char* path) {
+  Model* m = new Model();
+  if(!modelLoad(path, *m)) {
+    delete m;
+    return nullptr;
+  }
+  return m;
+}
+void ora_model_free(void* m) { delete(Model*)m; }
+
+int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* glob, float* policy, float* value,
+                   float* misc, int mode, int threads) {
+  nnForward(*(Model*)m, X, Y, n, bin, glob, policy, value, misc, mode, threads);
+  return 0;
+}
+
+void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
+                    int nnMode, void* model, int nnThreads) {
+  if(!T.loaded)
+    return nullptr;
+  Selfplay* s = new Selfplay();
+  SelfplayCfg cfg;
+  cfg.g = Geom(X, Y, W);
+  cfg.sp.maxVisits = maxVisits;
+  cfg.nodeCap = nodeCap;
+  cfg.seed = seed;
+  cfg.slotBase = slotBase;
+  cfg.nnMode = nnMode;
+  cfg.model = (const Model*)model;
+  cfg.nnThreads = nnThreads;
+  selfplayInit(*s, cfg, games);
+  return s;
+}
+void ora_sp_free(void* h) { delete(Selfplay*)h; }
+
+int ora_sp_rounds(void* h, int n) {
+  Selfplay* s = (Selfplay*)h;
+  for(int i = 0; i < n; i++)
+    selfplayRound(*s);
+  return 0;
+}
+
+// info[16]: phase, rootK, nodeCount, rootIdx, turn, pla, gameNum, playouts, nnEvals,
+//           movesMade, gamesFinished, rngCtr, leafKind, rootVisits, lastCell, lastDir
+int ora_sp_game_info(void* h, int slot, int64_t* info) {
+  Selfplay* s = (Selfplay*)h;
+  Game& gm = s->games[slot];
+  int64_t v[16] = {gm.phase, gm.rootK, gm.nodeCount, gm.rootIdx, gm.root.turn, gm.root.pla, gm.gameNum,
+                   (int64_t)gm.playouts, (int64_t)gm.nnEvals, (int64_t)gm.movesMade, (int64_t)gm.gamesFinished,
+                   (int64_t)gm.rng.ctr, gm.leafKind, gm.rootIdx >= 0 ? (int64_t)gm.nodes[gm.rootIdx].visits : 0,
+                   gm.root.lastCell, gm.root.lastDir};
+  memcpy(info, v, sizeof(v));
+  return 0;
+}
+
+// Copies the node pool of a game: nodes as raw 64-byte records (see ora::Node),
+// and edges child/visits/move for the first nodeCount nodes.
+int ora_sp_game_nodes(void* h, int slot, void* nodes, uint32_t* edgeChild, uint32_t* edgeVisits, uint16_t* edgeMove,
+                      float* policy) {
+  Selfplay* s = (Selfplay*)h;
+  Game& gm = s->games[slot];
+  const int P = s->cfg.g.P;
+  memcpy(nodes, gm.nodes.data(), sizeof(Node) * gm.nodeCount);
+  memcpy(edgeChild, gm.edgeChild.data(), sizeof(uint32_t) * (size_t)gm.nodeCount * P);
+  memcpy(edgeVisits, gm.edgeVisits.data(), sizeof(uint32_t) * (size_t)gm.nodeCount * P);
+  memcpy(edgeMove, gm.edgeMove.data(), sizeof(uint16_t) * (size_t)gm.nodeCount * P);
+  memcpy(policy, gm.policy.data(), sizeof(float) * (size_t)gm.nodeCount * P);
+  return gm.nodeCount;
+}
+
+int ora_sp_root_noised(void* h, int slot, float* out) {
+  Selfplay* s = (Selfplay*)h;
+  memcpy(out, s->games[slot].rootNoised.data(), sizeof(float) * s->cfg.g.P);
+  return 0;
+}
+
+int ora_sp_rows_count(void* h) { return ((Selfplay*)h)->rows.n; }
+int ora_sp_rows(void* h, uint8_t* bin, float* globIn, int16_t* policy, float* globT, int8_t* value) {
+  Rows& R = ((Selfplay*)h)->rows;
+  memcpy(bin, R.bin.data(), R.bin.size());
+  memcpy(globIn, R.globIn.data(), R.globIn.size() * 4);
+  memcpy(policy, R.policy.data(), R.policy.size() * 2);
+  memcpy(globT, R.globT.data(), R.globT.size() * 4);
+  memcpy(value, R.value.data(), R.value.size());
+  return R.n;
+}
+int ora_sizeof_node() { return (int)sizeof(Node); }
+
+}  // extern "C"

@@ -1,0 +1,1317 @@
+// ORACLE (test infrastructure only) — MCTS and self-play restatement.
+// Semantics follow the reference search with Coffee utility (win/loss only):
+//   playoutDescend            search.cpp:936-1165
+//   allocateOrFindNode        search.cpp:704-759   (graph search, SVB attach)
+//   maybeCatchUpEdgeVisits    search.cpp:1169-1207
+//   selectBestChildToDescend  searchexplorehelpers.cpp:304-451
+//   getExploreSelectionValue* searchexplorehelpers.cpp:27-207
+//   getFpuValueForChildren... searchexplorehelpers.cpp:245-301
+//   addLeafValue / recompute  searchupdatehelpers.cpp:12-328
+//   downweightBadChildren...  searchupdatehelpers.cpp:330-419
+//   maybeAddPolicyNoiseAndTemp searchhelpers.cpp:51-222
+//   getPlaySelectionValues    searchresults.cpp:63-309, LCB searchhelpers.cpp:469-521
+//   getChosenMoveLoc          searchresults.cpp:435-453, chooseIndexWithTemperature searchhelpers.cpp:11-49
+//   makeMove (tree reuse)     search.cpp:262-330, beginSearch :514-694
+//   Play::runGame targets     play.cpp:635-704, :1262-1460
+//   TrainingWriteBuffers::addRow trainingwrite.cpp:316-565
+// plus SPEC decisions.  Reductions over children use treeSum64.
+#include "ora_search.h"
+
+#include <algorithm>
+#include <cassert>
+#include <cstdio>
+#include <cstring>
+
+namespace ora {
+
+static const int SVB_CAP = 4096;
+static const uint64_t SVB_SEED = 0x5b5b5b5b5b5b5b5bULL;
+
+// ---------------------------------------------------------------------------
+// Fake network: a deterministic function of the (symmetrised) input planes.
+void packPlanes(const Geom& g, const float* bin, uint64_t* words) {
+  int nbits = NUM_SPATIAL * g.A, nw = (nbits + 63) / 64;
+  for(int i = 0; i < nw; i++)
+    words[i] = 0;
+  for(int i = 0; i < nbits; i++)
+    if(bin[i] != 0.0f)
+      words[i >> 6] |= 1ULL << (i & 63);
+}
+
+void fakeNet(const Geom& g, const float* bin, float* policy, float* value, float* misc) {
+  uint64_t w[32];
+  packPlanes(g, bin, w);
+  int nw = (NUM_SPATIAL * g.A + 63) / 64;
+  uint64_t h = 0x243f6a8885a308d3ULL;
+  for(int i = 0; i < nw; i++)
+    h = mix64(h ^ w[i]);
+  for(int j = 0; j < g.P + 4; j++) {
+    uint64_t v = mix64(h + (uint64_t)j * 0x9e3779b97f4a7c15ULL);
+    int q = (int)((v >> 40) & 0xffffu);
+    if(j < g.P)
+      policy[j] = ((float)q - 32768.0f) * (1.0f / 8192.0f);
+    else if(j < g.P + 2)
+      value[j - g.P] = ((float)q - 32768.0f) * (1.0f / 16384.0f);
+    else
+      misc[j - g.P - 2] = ((float)q - 32768.0f) * (1.0f / 16384.0f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+namespace {
+
+inline int svbIdxMove0(int pos) { return pos; }
+inline int svbIdxMove1(int pos) { return (MAX_P + 1) + pos; }
+inline int svbIdxPla(int pla) { return 2 * (MAX_P + 1) + pla; }
+inline int svbIdxPat(int color, int wy, int wx) { return 2 * (MAX_P + 1) + 3 + color * 25 + wy * 5 + wx; }
+
+struct Ctx {
+  Selfplay& s;
+  Game& gm;
+  const Geom& g;
+  const SearchParams& sp;
+  Ctx(Selfplay& s_, Game& gm_) : s(s_), gm(gm_), g(s_.cfg.g), sp(s_.cfg.sp) {}
+
+  Node& N(int i) { return gm.nodes[i]; }
+  uint32_t& EC(int n, int i) { return gm.edgeChild[(size_t)n * g.P + i]; }
+  uint32_t& EV(int n, int i) { return gm.edgeVisits[(size_t)n * g.P + i]; }
+  uint16_t& EM(int n, int i) { return gm.edgeMove[(size_t)n * g.P + i]; }
+  float* POL(int n) { return &gm.policy[(size_t)n * g.P]; }
+
+  // --- transposition table (SearchNodeTable, searchnodetable.h) ---
+  int ttCap() const { return (int)gm.ttNode.size(); }
+  int ttFind(uint64_t k0, uint64_t k1) {
+    int mask = ttCap() - 1;
+    for(int i = (int)(k0 & (uint64_t)mask);; i = (i + 1) & mask) {
+      if(gm.ttNode[i] < 0)
+        return -1;
+      if(gm.ttKey0[i] == k0 && gm.ttKey1[i] == k1)
+        return gm.ttNode[i];
+    }
+  }
+  void ttInsert(uint64_t k0, uint64_t k1, int node) {
+    int mask = ttCap() - 1;
+    int i = (int)(k0 & (uint64_t)mask);
+    while(gm.ttNode[i] >= 0)
+      i = (i + 1) & mask;
+    gm.ttKey0[i] = k0;
+    gm.ttKey1[i] = k1;
+    gm.ttNode[i] = node;
+  }
+  void ttClear() { std::fill(gm.ttNode.begin(), gm.ttNode.end(), -1); }
+
+  // --- subtree value bias table (subtreevaluebiastable.cpp:61-78) ---
+  int svbFindOrInsert(std::vector<uint64_t>& key, std::vector<float>& d, std::vector<float>& w,
+                      std::vector<uint8_t>& used, uint64_t k) {
+    int mask = SVB_CAP - 1;
+    for(int i = (int)(k & (uint64_t)mask);; i = (i + 1) & mask) {
+      if(!used[i]) {
+        used[i] = 1;
+        key[i] = k;
+        d[i] = 0.0f;
+        w[i] = 0.0f;
+        return i;
+      }
+      if(key[i] == k)
+        return i;
+    }
+  }
+  // Key (SPEC a19): ZOBRIST_MOVE_LOCS[parentPrev][0] ^ [prev][1] ^ 5x5 local
+  // pattern around `prev` on the board BEFORE it was played ^ mover.
+  uint64_t svbKey(const Board& before, int parentPrevPos, int movePos, int mover) {
+    const std::vector<uint64_t>& Z = s.svbZ;
+    uint64_t h = Z[svbIdxMove0(parentPrevPos)] ^ Z[svbIdxMove1(movePos)] ^ Z[svbIdxPla(mover)];
+    int cell = movePos % g.A;
+    int x = cell % g.X, y = cell / g.X;
+    for(int wy = 0; wy < 5; wy++)
+      for(int wx = 0; wx < 5; wx++) {
+        int xx = x + wx - 2, yy = y + wy - 2;
+        int col = (xx >= 0 && xx < g.X && yy >= 0 && yy < g.Y) ? before.c[yy * g.X + xx] : 3;
+        h ^= Z[svbIdxPat(col, wy, wx)];
+      }
+    return h;
+  }
+
+  int allocNode(uint8_t nextPla, H128 key, bool terminal) {
+    int i = gm.nodeCount++;
+    if(i >= (int)gm.nodes.size()) {
+      fprintf(stderr, "oracle: node pool overflow\n");
+      abort();
+    }
+    Node& n = N(i);
+    memset(&n, 0, sizeof(Node));
+    n.svbEntry = -1;
+    n.nextPla = nextPla;
+    n.flags = terminal ? 2 : 0;
+    n.key0 = key.h0;
+    n.key1 = key.h1;
+    return i;
+  }
+
+  static float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeight) {
+    // NodeStats::childWeight searchnode.h:59-61
+    return rawWeight * ((float)edgeVisits / (float)std::max(childVisits, 1u));
+  }
+
+  // --- addLeafValue searchupdatehelpers.cpp:12-82 (weight 1, Coffee utility = winLoss) ---
+  void addLeafValue(int ni, float wl, bool isTerminal, bool assumeNoExisting) {
+    Node& n = N(ni);
+    float utility = wl;
+    if(sp.subtreeValueBiasFactor != 0.0f && !isTerminal && n.svbEntry >= 0) {
+      float d = gm.svbDelta[n.svbEntry], w = gm.svbWeight[n.svbEntry];
+      if(w > 0.001f)
+        utility = utility + (sp.subtreeValueBiasFactor * d) / w;
+    }
+    float usq = utility * utility;
+    if(assumeNoExisting) {
+      n.winLossAvg = wl;
+      n.utilityAvg = utility;
+      n.utilitySqAvg = usq;
+      n.weightSqSum = 1.0f;
+      n.weightSum = 1.0f;
+      n.visits += 1;
+    } else {
+      float oldW = n.weightSum, newW = oldW + 1.0f;
+      n.winLossAvg = (n.winLossAvg * oldW + wl) / newW;
+      n.utilityAvg = (n.utilityAvg * oldW + utility) / newW;
+      n.utilitySqAvg = (n.utilitySqAvg * oldW + usq) / newW;
+      n.weightSqSum = n.weightSqSum + 1.0f;
+      n.weightSum = newW;
+      n.visits += 1;
+    }
+  }
+
+  float cdf(float z) {
+    // DistributionTable::getCdf distributiontable.h (size 2000, [-50,50])
+    float d = (1999.0f * (z - (-50.0f))) / 100.0f;
+    if(d <= 0.0f)
+      return 0.0f;
+    int idx = (int)d;
+    if(idx >= 1999)
+      return 1.0f;
+    float lambda = d - (float)idx;
+    float y0 = T.cdf[idx], y1 = T.cdf[idx + 1];
+    return y0 + lambda * (y1 - y0);
+  }
+
+  // --- recomputeNodeStats searchupdatehelpers.cpp:151-328 ---
+  void recompute(int ni, int numVisitsToAdd, bool isRoot) {
+    Node& n = N(ni);
+    const int k = n.numChildren;
+    float wAdj[MAX_P], selfU[MAX_P], wlv[MAX_P], uv[MAX_P], usqv[MAX_P], wsqv[MAX_P], tmp[MAX_P];
+    bool good[MAX_P];
+    int numGood = 0;
+    float maxW = 0.0f;
+    for(int i = 0; i < k; i++) {
+      const Node& c = N((int)EC(ni, i));
+      uint32_t ev = EV(ni, i);
+      good[i] = c.visits > 0 && c.weightSum > 0.0f && ev > 0;
+      if(good[i]) {
+        numGood++;
+        selfU[i] = n.nextPla == 2 ? c.utilityAvg : -c.utilityAvg;
+        wAdj[i] = childWeight(ev, c.visits, c.weightSum);
+        if(wAdj[i] > maxW)
+          maxW = wAdj[i];
+      } else {
+        selfU[i] = 0.0f;
+        wAdj[i] = 0.0f;
+      }
+    }
+    float origTotal = treeSum64(wAdj, k);
+    float currentTotal = origTotal;
+    float amountToSubtract = 0.0f, amountToPrune = 0.0f;
+    if(isRoot && sp.rootNoiseEnabled) {
+      amountToSubtract = std::min(sp.chosenMoveSubtract, maxW / 64.0f);
+      amountToPrune = std::min(sp.chosenMovePrune, maxW / 64.0f);
+    }
+    // downweightBadChildrenAndNormalizeWeight (valueWeightExponent != 0 branch)
+    if(numGood > 0 && currentTotal > 0.0f) {
+      float stdev[MAX_P];
+      for(int i = 0; i < k; i++) {
+        stdev[i] = good[i] ? sqrtf(1e-8f + 1.0f / (1.5f * sqrtf(wAdj[i]))) : 0.0f;
+        tmp[i] = good[i] ? selfU[i] * wAdj[i] : 0.0f;
+      }
+      float simpleValue = treeSum64(tmp, k) / currentTotal;
+      for(int i = 0; i < k; i++) {
+        if(!good[i]) {
+          tmp[i] = 0.0f;
+          continue;
+        }
+        if(wAdj[i] < amountToPrune) {
+          tmp[i] = 0.0f;
+          continue;
+        }
+        float nw = wAdj[i] - amountToSubtract;
+        if(nw <= 0.0f)
+          nw = 0.0f;
+        float z = (selfU[i] - simpleValue) / stdev[i];
+        float p = cdf(z) + 0.0001f;
+        float f = sp.valueWeightExponent == 0.5f ? sqrtf(p) : kPowf(p, sp.valueWeightExponent);
+        tmp[i] = nw * f;
+      }
+      float totalNew = treeSum64(tmp, k);
+      float factor = currentTotal / totalNew;
+      for(int i = 0; i < k; i++)
+        wAdj[i] = tmp[i] * factor;
+    }
+    for(int i = 0; i < k; i++) {
+      if(!good[i]) {
+        wlv[i] = uv[i] = usqv[i] = wsqv[i] = 0.0f;
+        continue;
+      }
+      const Node& c = N((int)EC(ni, i));
+      float ws = wAdj[i] / c.weightSum;
+      wlv[i] = wAdj[i] * c.winLossAvg;
+      uv[i] = wAdj[i] * c.utilityAvg;
+      usqv[i] = wAdj[i] * c.utilitySqAvg;
+      wsqv[i] = (ws * ws) * c.weightSqSum;
+    }
+    float winLossSum = treeSum64(wlv, k);
+    float utilitySum = treeSum64(uv, k);
+    float utilitySqSum = treeSum64(usqv, k);
+    float weightSqSum = treeSum64(wsqv, k);
+    float weightSum = currentTotal;
+    float wl = n.nnWin - n.nnLoss;
+    float utility = wl;
+    if(sp.subtreeValueBiasFactor != 0.0f && n.svbEntry >= 0) {
+      int e = n.svbEntry;
+      if(currentTotal > 1e-10f) {
+        float utilityChildren = utilitySum / currentTotal;
+        float svbW = kPowf(origTotal, sp.subtreeValueBiasWeightExponent);
+        float svbD = (utilityChildren - utility) * svbW;
+        gm.svbDelta[e] = gm.svbDelta[e] + (svbD - n.lastSvbDelta);
+        gm.svbWeight[e] = gm.svbWeight[e] + (svbW - n.lastSvbWeight);
+        n.lastSvbDelta = svbD;
+        n.lastSvbWeight = svbW;
+      }
+      float d = gm.svbDelta[e], w = gm.svbWeight[e];
+      if(w > 0.001f)
+        utility = utility + (sp.subtreeValueBiasFactor * d) / w;
+    }
+    winLossSum = winLossSum + wl;
+    utilitySum = utilitySum + utility;
+    utilitySqSum = utilitySqSum + utility * utility;
+    weightSqSum = weightSqSum + 1.0f;
+    weightSum = weightSum + 1.0f;
+    n.winLossAvg = winLossSum / weightSum;
+    n.utilityAvg = utilitySum / weightSum;
+    n.utilitySqAvg = utilitySqSum / weightSum;
+    n.weightSqSum = weightSqSum;
+    n.weightSum = weightSum;
+    n.visits += (uint32_t)numVisitsToAdd;
+  }
+
+  // --- getFpuValueForChildrenAssumeVisited searchexplorehelpers.cpp:245-301 ---
+  float fpuValue(int ni, int pla, bool isRoot, float probMass) {
+    const Node& n = N(ni);
+    float parentUtility = n.utilityAvg;
+    float forFpu = parentUtility;
+    if(sp.fpuParentWeightByVisitedPolicy) {
+      float pw = sp.fpuParentWeightByVisitedPolicyPow == 2.0f ? probMass * probMass
+                                                              : kPowf(probMass, sp.fpuParentWeightByVisitedPolicyPow);
+      float avgWeight = std::min(1.0f, pw);
+      forFpu = avgWeight * parentUtility + (1.0f - avgWeight) * (n.nnWin - n.nnLoss);
+    }
+    float redMax = isRoot ? sp.rootFpuReductionMax : sp.fpuReductionMax;
+    float lossProp = isRoot ? sp.rootFpuLossProp : sp.fpuLossProp;
+    float reduction = redMax * sqrtf(probMass);
+    float fpu = pla == 2 ? forFpu - reduction : forFpu + reduction;
+    float lossValue = pla == 2 ? -1.0f : 1.0f;
+    fpu = fpu + (lossValue - fpu) * lossProp;
+    return fpu;
+  }
+
+  float exploreScaling(float totalChildWeight) {
+    float c = sp.cpuctExploration;
+    if(sp.cpuctExplorationLog != 0.0f)
+      c = c + sp.cpuctExplorationLog * kLogf((totalChildWeight + sp.cpuctExplorationBase) / sp.cpuctExplorationBase);
+    return c * sqrtf(totalChildWeight + 0.01f);
+  }
+
+  // --- selectBestChildToDescend searchexplorehelpers.cpp:304-451 ---
+  // returns slot (k = new child), sets newPos; -1 if nothing selectable.
+  int selectBest(int ni, const float* pol, bool isRoot, int& newPos) {
+    const Node& n = N(ni);
+    const int k = n.numChildren;
+    int pla = n.nextPla;
+    float probs[MAX_P], cw[MAX_P];
+    bool hasChild[MAX_P];
+    memset(hasChild, 0, sizeof(hasChild));
+    for(int i = 0; i < k; i++) {
+      const Node& c = N((int)EC(ni, i));
+      float p = pol[EM(ni, i)];
+      probs[i] = p < 0.0f ? 0.0f : p;
+      cw[i] = p < 0.0f ? 0.0f : childWeight(EV(ni, i), c.visits, c.weightSum);
+      hasChild[EM(ni, i)] = true;
+    }
+    float probMass = treeSum64(probs, k);
+    float total = treeSum64(cw, k);
+    float fpu = fpuValue(ni, pla, isRoot, probMass);
+    float scaling = exploreScaling(total);
+    float best = -INFINITY;
+    int bestSlot = -1;
+    for(int i = 0; i < k; i++) {
+      const Node& c = N((int)EC(ni, i));
+      float p = pol[EM(ni, i)];
+      float v;
+      if(p < 0.0f)
+        v = -INFINITY;  // POLICY_ILLEGAL_SELECTION_VALUE
+      else {
+        float w = cw[i];
+        float u = (c.visits == 0 || w <= 0.0f) ? fpu : c.utilityAvg;
+        if(isRoot && sp.rootDesiredPerChildVisitsCoeff > 0.0f && p > 0.0f &&
+           w < sqrtf((p * total) * sp.rootDesiredPerChildVisitsCoeff))
+          v = 1e20f;
+        else
+          v = (scaling * p) / (1.0f + w) + (pla == 2 ? u : -u);
+      }
+      if(v > best) {
+        best = v;
+        bestSlot = i;
+      }
+    }
+    float bestNewProb = -1.0f;
+    int bestNew = -1;
+    for(int pos = 0; pos < g.P; pos++) {
+      if(hasChild[pos])
+        continue;
+      float p = pol[pos];
+      if(p < 0.0f)
+        continue;
+      if(p > bestNewProb) {
+        bestNewProb = p;
+        bestNew = pos;
+      }
+    }
+    newPos = -1;
+    if(bestNew >= 0) {
+      float v = (scaling * bestNewProb) / 1.0f + (pla == 2 ? fpu : -fpu);
+      if(v > best) {
+        best = v;
+        bestSlot = k;
+        newPos = bestNew;
+      }
+    }
+    return bestSlot;
+  }
+
+  // --- playoutDescend (select half) ---
+  void descend() {
+    gm.pathNode.clear();
+    gm.pathSlot.clear();
+    Board b = gm.root;
+    int ni = gm.rootIdx;
+    while(true) {
+      Node& n = N(ni);
+      if(n.flags & 2) {
+        gm.leafKind = LEAF_TERMINAL;
+        gm.leafNode = ni;
+        gm.leafBoard = b;
+        break;
+      }
+      bool isRoot = ni == gm.rootIdx;
+      const float* pol = isRoot ? gm.rootNoised.data() : POL(ni);
+      int newPos = -1;
+      int slot = selectBest(ni, pol, isRoot, newPos);
+      if(slot < 0) {
+        gm.leafKind = LEAF_NOCHILD;
+        gm.leafNode = ni;
+        break;
+      }
+      if(slot == n.numChildren) {
+        int cell = newPos % g.A, dir = newPos / g.A;
+        Board before = b;
+        playMove(g, b, cell, dir);
+        H128 key = stateHash(g, b);
+        int child = sp.useGraphSearch ? ttFind(key.h0, key.h1) : -1;
+        if(child < 0) {
+          child = allocNode(b.pla, key, b.finished != 0);
+          if(sp.subtreeValueBiasFactor != 0.0f && before.histCell[0] >= 0) {
+            int ppos = before.histDir[0] * g.A + before.histCell[0];
+            uint64_t k = svbKey(before, ppos, newPos, before.pla);
+            N(child).svbEntry = svbFindOrInsert(gm.svbKey, gm.svbDelta, gm.svbWeight, gm.svbUsed, k);
+          }
+          if(sp.useGraphSearch)
+            ttInsert(key.h0, key.h1, child);
+        }
+        Node& nn = N(ni);  // (re-fetch: vector storage is fixed-size, no realloc)
+        EC(ni, slot) = (uint32_t)child;
+        EV(ni, slot) = 0;
+        EM(ni, slot) = (uint16_t)newPos;
+        nn.numChildren++;
+        gm.pathNode.push_back(ni);
+        gm.pathSlot.push_back(slot);
+        if(N(child).visits > 0) {  // maybeCatchUpEdgeVisits: edgeVisits 0 < childVisits
+          gm.leafKind = LEAF_CATCHUP;
+          gm.leafNode = child;
+          break;
+        }
+        gm.leafNode = child;
+        gm.leafBoard = b;
+        gm.leafKind = (N(child).flags & 2) ? LEAF_TERMINAL : LEAF_NN;
+        break;
+      }
+      int child = (int)EC(ni, slot);
+      gm.pathNode.push_back(ni);
+      gm.pathSlot.push_back(slot);
+      if(EV(ni, slot) < N(child).visits) {
+        gm.leafKind = LEAF_CATCHUP;
+        gm.leafNode = child;
+        break;
+      }
+      int mv = EM(ni, slot);
+      playMove(g, b, mv % g.A, mv / g.A);
+      ni = child;
+    }
+  }
+
+  // NNEvaluator::evaluate post-processing nneval.cpp:702-815 + inverse symmetry
+  // (copyOutputsWithSymmetry nninputs.cpp:349-357).
+  void postprocess(const Board& b, int sym, const float* out, float* pol, float& whiteWin, float& whiteLoss) {
+    if(g.X != g.Y)
+      sym &= 3;
+    float logit[MAX_P];
+    bool legal[MAX_P];
+    float mx = -1e25f;  // maxPolicy init nneval.cpp:709
+    for(int pos = 0; pos < g.P; pos++) {
+      int d = pos / g.A, cell = pos % g.A;
+      legal[pos] = isLegal(g, b, cell, d);
+      float v = legal[pos] ? out[symDir(d, sym) * g.A + symCell(g, cell, sym)] : -1e30f;
+      logit[pos] = v;
+      if(v > mx)
+        mx = v;
+    }
+    float e[MAX_P];
+    for(int pos = 0; pos < g.P; pos++)
+      e[pos] = kExpf(logit[pos] - mx);
+    float sum = treeSum64(e, g.P);
+    int legalCount = 0;
+    for(int pos = 0; pos < g.P; pos++)
+      legalCount += legal[pos] ? 1 : 0;
+    if(sum <= 0.0f) {
+      float uniform = 1.0f / (float)legalCount;
+      for(int pos = 0; pos < g.P; pos++)
+        pol[pos] = legal[pos] ? uniform : -1.0f;
+    } else {
+      for(int pos = 0; pos < g.P; pos++)
+        pol[pos] = legal[pos] ? e[pos] / sum : -1.0f;
+    }
+    float wlg = out[g.P], llg = out[g.P + 1];
+    float m = std::max(wlg, llg);
+    float wp = kExpf(wlg - m), lp = kExpf(llg - m);
+    float ps = wp + lp;
+    wp = wp / ps;
+    lp = lp / ps;
+    if(b.pla == 2) {
+      whiteWin = wp;
+      whiteLoss = lp;
+    } else {
+      whiteWin = lp;
+      whiteLoss = wp;
+    }
+  }
+
+  float interpolateEarly(float halflife, float earlyValue, float value) {
+    // Search::interpolateEarly searchhelpers.cpp:463-467
+    float rawHalflives = (float)gm.root.turn / halflife;
+    float halflives = rawHalflives * (19.0f / sqrtf((float)(g.X * g.Y)));
+    return value + (earlyValue - value) * kPowf(0.5f, halflives);
+  }
+
+  // maybeAddPolicyNoiseAndTemp searchhelpers.cpp:122-222 (root only)
+  void noiseAndTemp(const float* raw, float* out) {
+    for(int pos = 0; pos < g.P; pos++)
+      out[pos] = raw[pos];
+    if(sp.rootPolicyTemperature != 1.0f || sp.rootPolicyTemperatureEarly != 1.0f) {
+      float t = interpolateEarly(sp.chosenMoveTemperatureHalflife, sp.rootPolicyTemperatureEarly, sp.rootPolicyTemperature);
+      float mx = 0.0f;
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] > mx)
+          mx = out[pos];
+      float logMax = kLogf(mx);
+      float invTemp = 1.0f / t;
+      float sum = 0.0f;
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] > 0.0f) {
+          float p = kExpf((kLogf(out[pos]) - logMax) * invTemp);
+          out[pos] = p;
+          sum = sum + p;
+        }
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] >= 0.0f)
+          out[pos] = out[pos] / sum;
+    }
+    if(sp.rootNoiseEnabled) {
+      // computeDirichletAlphaDistribution searchhelpers.cpp:51-91
+      float alpha[MAX_P];
+      int legalCount = 0;
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] >= 0.0f)
+          legalCount++;
+      float logSum = 0.0f;
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] >= 0.0f) {
+          alpha[pos] = kLogf(std::min(0.01f, out[pos]) + 1e-20f);
+          logSum = logSum + alpha[pos];
+        }
+      float logMean = logSum / (float)legalCount;
+      float propSum = 0.0f;
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] >= 0.0f) {
+          alpha[pos] = std::max(0.0f, alpha[pos] - logMean);
+          propSum = propSum + alpha[pos];
+        }
+      float uniform = 1.0f / (float)legalCount;
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] >= 0.0f)
+          alpha[pos] = propSum <= 0.0f ? uniform : 0.5f * (alpha[pos] / propSum + uniform);
+      // addDirichletNoise searchhelpers.cpp:93-120
+      float r[MAX_P];
+      float rSum = 0.0f;
+      for(int pos = 0; pos < g.P; pos++) {
+        if(out[pos] >= 0.0f) {
+          r[pos] = gm.rng.gamma(alpha[pos] * sp.rootDirichletNoiseTotalConcentration);
+          rSum = rSum + r[pos];
+        } else
+          r[pos] = 0.0f;
+      }
+      for(int pos = 0; pos < g.P; pos++)
+        r[pos] = r[pos] / rSum;
+      float w = sp.rootDirichletNoiseWeight;
+      for(int pos = 0; pos < g.P; pos++)
+        if(out[pos] >= 0.0f)
+          out[pos] = r[pos] * w + out[pos] * (1.0f - w);
+    }
+  }
+
+  // getSelfUtilityLCBAndRadius searchhelpers.cpp:469-521 (utilityRangeRadius = 1)
+  void lcbAndRadius(int pla, int ci, uint32_t ev, float& lcb, float& radius) {
+    const Node& c = N(ci);
+    radius = 2.0f * 1.0f * sp.lcbStdevs;
+    lcb = -radius;
+    float ws = childWeight(ev, c.visits, c.weightSum);
+    float wsq = childWeight(ev, c.visits, c.weightSqSum);
+    if(c.visits == 0 || ws <= 0.0f || wsq <= 0.0f)
+      return;
+    float u = c.utilityAvg, usq = c.utilitySqAvg;
+    float ess = (ws * ws) / wsq;
+    float priorWeight = ws / ((ess * ess) * ess);
+    usq = std::max(usq, u * u + 1e-8f);
+    usq = (usq * ws + (usq + 1.0f) * priorWeight) / (ws + priorWeight);
+    ws = ws + priorWeight;
+    wsq = wsq + priorWeight * priorWeight;
+    ess = (ws * ws) / wsq;
+    float selfU = pla == 2 ? u : -u;
+    float variance = usq - u * u;
+    float stdev = sqrtf(variance / ess);
+    radius = stdev * sp.lcbStdevs;
+    lcb = selfU - radius;
+  }
+
+  // getPlaySelectionValues searchresults.cpp:63-309 on the root.
+  // Fills pos[] and vals[]; returns count (0 = failure).
+  int playSelectionValues(float scaleMaxToAtLeast, bool allowDirectPolicyMoves, int* posOut, float* vals) {
+    int ri = gm.rootIdx;
+    const Node& n = N(ri);
+    const int k = n.numChildren;
+    const float* pol = gm.rootNoised.data();
+    int pla = n.nextPla;
+    float cw[MAX_P];
+    for(int i = 0; i < k; i++) {
+      const Node& c = N((int)EC(ri, i));
+      cw[i] = childWeight(EV(ri, i), c.visits, c.weightSum);
+      posOut[i] = EM(ri, i);
+      vals[i] = cw[i];
+    }
+    float total = treeSum64(cw, k);
+    int numChildren = k;
+    int bestIdx = 0;
+    float bestWeight = -1e30f;
+    {
+      float maxGood = -1e30f;
+      for(int i = 0; i < k; i++) {
+        float ev = (float)EV(ri, i);
+        float gdn = vals[i] * std::max(0.0f, ev - 1.0f) / std::max(1.0f, ev) + 2.0f * pol[posOut[i]];
+        if(gdn > maxGood) {
+          maxGood = gdn;
+          bestWeight = vals[i];
+          bestIdx = i;
+        }
+      }
+    }
+    if(k > 0) {
+      float fpu = fpuValue(ri, pla, true, 1.0f);
+      float scaling = exploreScaling(total);
+      // getExploreSelectionValueOfChild for the best child, isDuringSearch = false
+      const Node& bc = N((int)EC(ri, bestIdx));
+      float bp = pol[posOut[bestIdx]];
+      float bw = cw[bestIdx];
+      float bu = (bc.visits == 0 || bw <= 0.0f) ? fpu : bc.utilityAvg;
+      float bestValue = bp < 0.0f ? -INFINITY : (scaling * bp) / (1.0f + bw) + (pla == 2 ? bu : -bu);
+      for(int i = 0; i < k; i++) {
+        if(i == bestIdx)
+          continue;
+        // getReducedPlaySelectionWeight searchexplorehelpers.cpp:209-243
+        const Node& c = N((int)EC(ri, i));
+        float w = cw[i];
+        float reduced;
+        if(c.visits == 0 || w <= 0.0f)
+          reduced = 0.0f;
+        else {
+          float p = pol[posOut[i]];
+          float wanted;
+          if(p < 0.0f)
+            wanted = 0.0f;
+          else {
+            float valueComponent = pla == 2 ? c.utilityAvg : -c.utilityAvg;
+            float exploreComponent = bestValue - valueComponent;
+            float exploreComponentScaling = scaling * p;
+            if(exploreComponent <= 0.0f)
+              wanted = INFINITY;
+            else {
+              wanted = exploreComponentScaling / exploreComponent - 1.0f;
+              if(wanted < 0.0f)
+                wanted = 0.0f;
+            }
+          }
+          reduced = w > wanted ? wanted : w;
+        }
+        vals[i] = ceilf(reduced);
+      }
+    }
+    if(sp.useLcbForSelection && k > 0) {
+      float lcb[MAX_P], rad[MAX_P];
+      float bestLcb = -1e10f;
+      int bestLcbIdx = -1;
+      for(int i = 0; i < k; i++) {
+        lcbAndRadius(pla, (int)EC(ri, i), EV(ri, i), lcb[i], rad[i]);
+        float w = vals[i];
+        if(w > 0.0f && w >= sp.minVisitPropForLCB * bestWeight && lcb[i] > bestLcb) {
+          bestLcb = lcb[i];
+          bestLcbIdx = i;
+        }
+      }
+      if(bestLcbIdx >= 0) {
+        float adjusted = vals[bestLcbIdx];
+        for(int i = 0; i < k; i++) {
+          if(i == bestLcbIdx)
+            continue;
+          float excess = bestLcb - lcb[i];
+          if(excess < 0.0f)
+            continue;
+          float rf = (rad[i] + excess) / (rad[i] + 0.20f * excess);
+          float lbound = (rf * rf) * vals[i];
+          if(lbound > adjusted)
+            adjusted = lbound;
+        }
+        vals[bestLcbIdx] = adjusted;
+      }
+    }
+    if(numChildren == 0) {
+      if(!allowDirectPolicyMoves)
+        return 0;
+      for(int p = 0; p < g.P; p++) {
+        if(!isLegal(g, gm.root, p % g.A, p / g.A) || pol[p] < 0.0f)
+          continue;
+        posOut[numChildren] = p;
+        vals[numChildren] = pol[p];
+        numChildren++;
+      }
+      if(numChildren == 0)
+        return 0;
+    }
+    float mx = 0.0f;
+    for(int i = 0; i < numChildren; i++)
+      if(vals[i] > mx)
+        mx = vals[i];
+    if(mx <= 0.0f)
+      return 0;
+    float amountToSubtract = std::min(sp.chosenMoveSubtract, mx / 64.0f);
+    float amountToPrune = std::min(sp.chosenMovePrune, mx / 64.0f);
+    float newMax = mx - amountToSubtract;
+    for(int i = 0; i < numChildren; i++) {
+      if(vals[i] < amountToPrune)
+        vals[i] = 0.0f;
+      else {
+        vals[i] = vals[i] - amountToSubtract;
+        if(vals[i] <= 0.0f)
+          vals[i] = 0.0f;
+      }
+    }
+    if(newMax < scaleMaxToAtLeast)
+      for(int i = 0; i < numChildren; i++)
+        vals[i] = vals[i] * (scaleMaxToAtLeast / newMax);
+    return numChildren;
+  }
+
+  // chooseIndexWithTemperature searchhelpers.cpp:11-49 with our stream.
+  int chooseIndex(const float* vals, int n, float temperature) {
+    float mx = 0.0f;
+    for(int i = 0; i < n; i++)
+      if(vals[i] > mx)
+        mx = vals[i];
+    if(temperature <= 1.0e-4f) {
+      float best = vals[0];
+      int bi = 0;
+      for(int i = 1; i < n; i++)
+        if(vals[i] > best) {
+          best = vals[i];
+          bi = i;
+        }
+      return bi;
+    }
+    float pr[MAX_P];
+    float logMax = kLogf(mx);
+    float sum = 0.0f;
+    for(int i = 0; i < n; i++) {
+      pr[i] = vals[i] <= 0.0f ? 0.0f : kExpf((kLogf(vals[i]) - logMax) / temperature);
+      sum = sum + pr[i];
+    }
+    float d = gm.rng.uni() * sum;  // Rand::nextUInt(relProbs) rand.h:244-262
+    float acc = 0.0f;
+    for(int i = 0; i < n; i++) {
+      acc = acc + pr[i];
+      if(acc > d)
+        return i;
+    }
+    return n - 1;
+  }
+
+  void mark(int root, std::vector<uint8_t>& live) {
+    std::vector<int> st;
+    st.push_back(root);
+    live[root] = 1;
+    while(!st.empty()) {
+      int v = st.back();
+      st.pop_back();
+      for(int i = 0; i < N(v).numChildren; i++) {
+        int c = (int)EC(v, i);
+        if(!live[c]) {
+          live[c] = 1;
+          st.push_back(c);
+        }
+      }
+    }
+  }
+
+  void clearTree() {
+    gm.nodeCount = 0;
+    gm.rootIdx = -1;
+    ttClear();
+    std::fill(gm.svbUsed.begin(), gm.svbUsed.end(), 0);
+  }
+
+  // Search::makeMove search.cpp:262-330 + deleteAllOld... :790-810 +
+  // SubtreeValueBiasTable::clearUnusedSynchronous :47-59, as an in-place,
+  // order-preserving compaction of the node pool (SPEC: GC).
+  void reuseTree(int chosenPos) {
+    int ri = gm.rootIdx;
+    int child = -1;
+    if(ri >= 0)
+      for(int i = 0; i < N(ri).numChildren; i++)
+        if(EM(ri, i) == chosenPos) {
+          child = (int)EC(ri, i);
+          break;
+        }
+    if(child < 0 || !(N(child).flags & 1)) {
+      clearTree();
+      return;
+    }
+    std::vector<uint8_t> live(gm.nodeCount, 0);
+    mark(child, live);
+    int liveCount = 0;
+    for(int i = 0; i < gm.nodeCount; i++)
+      liveCount += live[i];
+    if(liveCount + sp.maxVisits + 2 > (int)gm.nodes.size()) {
+      clearTree();
+      return;
+    }
+    // removeSubtreeValueBias for every deleted table node and for the promoted
+    // child (whose copy becomes the root without an SVB entry), in index order.
+    for(int i = 0; i < gm.nodeCount; i++) {
+      Node& n = N(i);
+      if((live[i] && i != child) || n.svbEntry < 0)
+        continue;
+      int e = n.svbEntry;
+      gm.svbDelta[e] = gm.svbDelta[e] - n.lastSvbDelta * sp.subtreeValueBiasFreeProp;
+      gm.svbWeight[e] = gm.svbWeight[e] - n.lastSvbWeight * sp.subtreeValueBiasFreeProp;
+    }
+    N(child).svbEntry = -1;
+    N(child).lastSvbDelta = 0.0f;
+    N(child).lastSvbWeight = 0.0f;
+    std::vector<int> newIdx(gm.nodeCount, -1);
+    int j = 0;
+    for(int i = 0; i < gm.nodeCount; i++)
+      if(live[i])
+        newIdx[i] = j++;
+    for(int i = 0; i < gm.nodeCount; i++) {
+      if(!live[i])
+        continue;
+      int d = newIdx[i];
+      if(d != i) {
+        gm.nodes[d] = gm.nodes[i];
+        memcpy(&gm.edgeChild[(size_t)d * g.P], &gm.edgeChild[(size_t)i * g.P], sizeof(uint32_t) * g.P);
+        memcpy(&gm.edgeVisits[(size_t)d * g.P], &gm.edgeVisits[(size_t)i * g.P], sizeof(uint32_t) * g.P);
+        memcpy(&gm.edgeMove[(size_t)d * g.P], &gm.edgeMove[(size_t)i * g.P], sizeof(uint16_t) * g.P);
+        memcpy(&gm.policy[(size_t)d * g.P], &gm.policy[(size_t)i * g.P], sizeof(float) * g.P);
+      }
+      for(int e = 0; e < N(d).numChildren; e++)
+        EC(d, e) = (uint32_t)newIdx[EC(d, e)];
+    }
+    gm.nodeCount = liveCount;
+    gm.rootIdx = newIdx[child];
+    ttClear();
+    for(int i = 0; i < gm.nodeCount; i++)
+      if(i != gm.rootIdx)
+        ttInsert(N(i).key0, N(i).key1, i);
+    std::vector<uint64_t> k2(SVB_CAP, 0);
+    std::vector<float> d2(SVB_CAP, 0.0f), w2(SVB_CAP, 0.0f);
+    std::vector<uint8_t> u2(SVB_CAP, 0);
+    for(int i = 0; i < gm.nodeCount; i++) {
+      Node& n = N(i);
+      if(n.svbEntry < 0)
+        continue;
+      int oe = n.svbEntry;
+      int mask = SVB_CAP - 1;
+      int slot = (int)(gm.svbKey[oe] & (uint64_t)mask);
+      while(u2[slot] && k2[slot] != gm.svbKey[oe])
+        slot = (slot + 1) & mask;
+      if(!u2[slot]) {
+        u2[slot] = 1;
+        k2[slot] = gm.svbKey[oe];
+        d2[slot] = gm.svbDelta[oe];
+        w2[slot] = gm.svbWeight[oe];
+      }
+      n.svbEntry = slot;
+    }
+    gm.svbKey.swap(k2);
+    gm.svbDelta.swap(d2);
+    gm.svbWeight.swap(w2);
+    gm.svbUsed.swap(u2);
+  }
+
+  // Search::recursivelyRecomputeStats search.cpp:834-910, post-order in child order.
+  void recursiveRecompute() {
+    if(gm.rootIdx < 0)
+      return;
+    std::vector<uint8_t> seen(gm.nodeCount, 0);
+    std::vector<std::pair<int, int>> st;
+    st.push_back({gm.rootIdx, 0});
+    seen[gm.rootIdx] = 1;
+    while(!st.empty()) {
+      int v = st.back().first;
+      int& next = st.back().second;
+      if(next < N(v).numChildren) {
+        int c = (int)EC(v, next);
+        next++;
+        if(!seen[c]) {
+          seen[c] = 1;
+          st.push_back({c, 0});
+        }
+        continue;
+      }
+      st.pop_back();
+      Node& n = N(v);
+      if(n.numChildren == 0) {
+        if(n.weightSum > 0.0f) {
+          n.utilityAvg = n.winLossAvg;
+          n.utilitySqAvg = n.winLossAvg * n.winLossAvg;
+        }
+      } else
+        recompute(v, 0, v == gm.rootIdx);
+    }
+  }
+
+  void startGame() {
+    gm.rng.seed = mix64(s.cfg.seed ^ mix64(((uint64_t)(s.cfg.slotBase + gm.slot) << 32) | gm.gameNum));
+    gm.rng.ctr = 0;
+    boardInit(g, gm.root);
+    clearTree();
+    gm.turns.clear();
+    gm.gameHash0 = gm.rng.next();
+    gm.gameHash1 = gm.rng.next();
+    gm.phase = PH_ROOTEVAL;
+    gm.rootK = 0;
+  }
+
+  void finishGame();
+  void commitMove();
+};
+
+void Ctx::commitMove() {
+  int posv[MAX_P];
+  float vals[MAX_P];
+  TurnRec tr;
+  // getChosenMoveLoc (searchresults.cpp:435-453)
+  int n = playSelectionValues(0.0f, true, posv, vals);
+  if(n <= 0) {
+    fprintf(stderr, "oracle: no move selectable\n");
+    abort();
+  }
+  float temp = interpolateEarly(sp.chosenMoveTemperatureHalflife, sp.chosenMoveTemperatureEarly, sp.chosenMoveTemperature);
+  int chosen = posv[chooseIndex(vals, n, temp)];
+  const Node& r = N(gm.rootIdx);
+  // extractValueTargets play.cpp:674-682 via ReportedSearchValues reportedsearchvalues.cpp:10-50
+  float wl = std::max(-1.0f, std::min(1.0f, r.winLossAvg));
+  tr.whiteWin = std::max(0.0f, std::min(1.0f, 0.5f * (wl + 1.0f)));
+  tr.whiteLoss = std::max(0.0f, std::min(1.0f, 0.5f * (-wl + 1.0f)));
+  tr.visits = r.visits;
+  // extractPolicyTarget play.cpp:635-672
+  tr.policyTarget.assign(g.P, 0);
+  {
+    int m = playSelectionValues(10.0f, false, posv, vals);
+    float mx = 0.0f;
+    for(int i = 0; i < m; i++)
+      if(vals[i] > mx)
+        mx = vals[i];
+    float factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
+    for(int i = 0; i < m; i++)
+      tr.policyTarget[posv[i]] = (int16_t)roundf(vals[i] * factor);
+  }
+  // computeNNRawStats play.cpp:684-704 (first root-symmetry eval)
+  tr.rawWhiteWL = gm.rawWin - gm.rawLoss;
+  {
+    float ent = 0.0f;
+    for(int p = 0; p < g.P; p++) {
+      float q = gm.rawPolicy[p];
+      if(q >= 1e-30f)
+        ent = ent + (-q * kLogf(q));
+    }
+    tr.rawPolicyEntropy = ent;
+  }
+  // getPolicySurpriseAndEntropy searchresults.cpp:486-550
+  {
+    int m = playSelectionValues(1.0f, true, posv, vals);
+    const float* pol = gm.rootNoised.data();
+    float sumV = 0.0f;
+    for(int i = 0; i < m; i++)
+      sumV = sumV + vals[i];
+    float surprise = 0.0f, searchEnt = 0.0f, polEnt = 0.0f;
+    for(int i = 0; i < m; i++) {
+      float p = std::max(pol[posv[i]], 1e-30f);
+      float t = vals[i] / sumV;
+      if(t > 1e-30f) {
+        float lt = kLogf(t), lp = kLogf(p);
+        surprise = surprise + t * (lt - lp);
+        searchEnt = searchEnt + (-t * lt);
+      }
+    }
+    for(int p = 0; p < g.P; p++)
+      if(pol[p] > 1e-30f)
+        polEnt = polEnt + (-pol[p] * kLogf(pol[p]));
+    tr.policySurprise = std::max(0.0f, surprise);
+    tr.searchEntropy = std::max(0.0f, searchEnt);
+    tr.policyEntropy = std::max(0.0f, polEnt);
+  }
+  tr.cell = (int8_t)(chosen % g.A);
+  tr.dir = (int8_t)(chosen / g.A);
+  gm.turns.push_back(tr);
+  reuseTree(chosen);
+  playMove(g, gm.root, chosen % g.A, chosen / g.A);
+  gm.movesMade++;
+  if(gm.root.finished) {
+    finishGame();
+    gm.gamesFinished++;
+    gm.gameNum++;
+    startGame();
+    return;
+  }
+  if(sp.subtreeValueBiasFactor != 0.0f)
+    recursiveRecompute();
+  gm.phase = PH_ROOTEVAL;
+  gm.rootK = 0;
+}
+
+static void packBitsBE(const float* v, int len, uint8_t* out) {
+  // packBits trainingwrite.cpp:218-232 (big-endian within each byte)
+  for(int i = 0; i < (len + 7) / 8; i++)
+    out[i] = 0;
+  for(int i = 0; i < len; i++)
+    if(v[i] != 0.0f)
+      out[i >> 3] |= (uint8_t)(1u << (7 - (i & 7)));
+}
+
+// Play::runGame finalisation play.cpp:1431-1460 + TrainingDataWriter::writeGame
+// trainingwrite.cpp:774-890 + addRow :316-565 (benchmark mode: weight 1 per turn).
+void Ctx::finishGame() {
+  const int numMoves = (int)gm.turns.size();
+  const int A = g.A, P = g.P, pb = (A + 7) / 8;
+  float finalWin = gm.root.winner == 2 ? 1.0f : (gm.root.winner == 1 ? 0.0f : 0.5f);
+  std::vector<float> tWin(numMoves + 1), tLoss(numMoves + 1);
+  for(int t = 0; t < numMoves; t++) {
+    tWin[t] = gm.turns[t].whiteWin;
+    tLoss[t] = gm.turns[t].whiteLoss;
+  }
+  tWin[numMoves] = finalWin;
+  tLoss[numMoves] = 1.0f - finalWin;
+  std::vector<Board> boards(numMoves + 1);
+  boardInit(g, boards[0]);
+  for(int t = 0; t < numMoves; t++) {
+    boards[t + 1] = boards[t];
+    playMove(g, boards[t + 1], gm.turns[t].cell, gm.turns[t].dir);
+  }
+  const Board& fin = boards[numMoves];
+  // finalMaxLength (SPEC: per-cell longest same-colour run through the cell, 0 if empty)
+  int8_t finalMaxLen[MAX_AREA];
+  for(int c = 0; c < A; c++)
+    finalMaxLen[c] = fin.c[c] == 0 ? 0 : (int8_t)maxRun(g, fin, c);
+  Rows& R = s.rows;
+  for(int t = 0; t < numMoves; t++) {
+    const Board& b = boards[t];
+    int pla = b.pla, opp = 3 - pla;
+    float bin[NUM_SPATIAL * MAX_AREA], glob[1];
+    encodeV1(g, b, 0, bin, glob);
+    size_t r = (size_t)R.n;
+    R.n++;
+    R.bin.resize((size_t)R.n * NUM_SPATIAL * pb);
+    R.globIn.resize((size_t)R.n);
+    R.policy.resize((size_t)R.n * 2 * P);
+    R.globT.resize((size_t)R.n * 64);
+    R.value.resize((size_t)R.n * 5 * A);
+    for(int ch = 0; ch < NUM_SPATIAL; ch++)
+      packBitsBE(bin + ch * A, A, &R.bin[(r * NUM_SPATIAL + ch) * pb]);
+    R.globIn[r] = glob[0];
+    int16_t* pol = &R.policy[r * 2 * P];
+    for(int p = 0; p < P; p++) {
+      pol[p] = gm.turns[t].policyTarget[p];
+      pol[P + p] = t + 1 < numMoves ? gm.turns[t + 1].policyTarget[p] : (int16_t)1;
+    }
+    float* gt = &R.globT[r * 64];
+    for(int i = 0; i < 64; i++)
+      gt[i] = 0.0f;
+    // fillValueTDTargets trainingwrite.cpp:286-314
+    const float nowFactors[5] = {0.0f, 1.0f / (1.0f + (float)A * 0.176f), 1.0f / (1.0f + (float)A * 0.056f),
+                                 1.0f / (1.0f + (float)A * 0.016f), 1.0f};
+    for(int f = 0; f < 5; f++) {
+      float win = 0.0f, loss = 0.0f, left = 1.0f;
+      for(int i = t; i <= numMoves; i++) {
+        float now;
+        if(i == numMoves) {
+          now = left;
+          left = 0.0f;
+        } else {
+          now = left * nowFactors[f];
+          left = left * (1.0f - nowFactors[f]);
+        }
+        win = win + now * (pla == 2 ? tWin[i] : tLoss[i]);
+        loss = loss + now * (pla == 2 ? tLoss[i] : tWin[i]);
+      }
+      gt[2 * f] = win;
+      gt[2 * f + 1] = loss;
+    }
+    {
+      float sum = 0.0f;
+      for(int i = t + 1; i <= numMoves; i++) {
+        float prevWL = tWin[i - 1] - tLoss[i - 1], nextWL = tWin[i] - tLoss[i];
+        float var = (nextWL - prevWL) * (nextWL - prevWL);
+        sum = sum + (float)(i - t) * var;
+      }
+      gt[22] = sum;
+    }
+    gt[25] = 1.0f;
+    gt[26] = 1.0f;
+    gt[27] = 1.0f;
+    gt[28] = t + 1 < numMoves ? 1.0f : 0.0f;
+    gt[30] = gm.turns[t].policySurprise;
+    gt[31] = gm.turns[t].policyEntropy;
+    gt[32] = gm.turns[t].searchEntropy;
+    gt[33] = 1.0f;
+    bool h = true;
+    for(int i = 0; i < 5; i++) {
+      h = h && gm.rng.uni() < 0.98f;
+      gt[36 + i] = h ? 1.0f : 0.0f;
+    }
+    gt[41] = (float)(gm.gameHash0 & 0x3FFFFF);
+    gt[42] = (float)((gm.gameHash0 >> 22) & 0x3FFFFF);
+    gt[43] = (float)((gm.gameHash0 >> 44) & 0xFFFFF);
+    gt[44] = (float)(gm.gameHash1 & 0x3FFFFF);
+    gt[45] = (float)((gm.gameHash1 >> 22) & 0x3FFFFF);
+    gt[46] = (float)((gm.gameHash1 >> 44) & 0xFFFFF);
+    gt[51] = (float)t;
+    gt[57] = pla == 2 ? gm.turns[t].rawWhiteWL : -gm.turns[t].rawWhiteWL;
+    gt[59] = gm.turns[t].rawPolicyEntropy;
+    gt[60] = (float)gm.turns[t].visits;
+    gt[63] = 1.0f;
+    int8_t* vt = &R.value[r * 5 * A];
+    const Board& b2 = boards[std::min(t + 2, numMoves)];
+    const Board& b3 = boards[std::min(t + 6, numMoves)];
+    for(int c = 0; c < A; c++) {
+      vt[c] = fin.c[c] == pla ? 1 : (fin.c[c] == opp ? -1 : 0);
+      vt[A + c] = 0;
+      vt[2 * A + c] = b2.c[c] == pla ? 1 : (b2.c[c] == opp ? -1 : 0);
+      vt[3 * A + c] = b3.c[c] == pla ? 1 : (b3.c[c] == opp ? -1 : 0);
+      vt[4 * A + c] = finalMaxLen[c];
+    }
+  }
+}
+
+}  // namespace
+
+void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames) {
+  s.cfg = cfg;
+  const Geom& g = s.cfg.g;
+  Rng zr;
+  zr.seed = SVB_SEED;
+  s.svbZ.resize(2 * (MAX_P + 1) + 3 + 4 * 25);
+  for(auto& z : s.svbZ)
+    z = zr.next();
+  s.games.resize(numGames);
+  for(int i = 0; i < numGames; i++) {
+    Game& gm = s.games[i];
+    gm.slot = i;
+    gm.gameNum = 0;
+    gm.nodes.resize(cfg.nodeCap);
+    gm.edgeChild.assign((size_t)cfg.nodeCap * g.P, 0);
+    gm.edgeVisits.assign((size_t)cfg.nodeCap * g.P, 0);
+    gm.edgeMove.assign((size_t)cfg.nodeCap * g.P, 0);
+    gm.policy.assign((size_t)cfg.nodeCap * g.P, 0.0f);
+    gm.rootNoised.assign(g.P, 0.0f);
+    gm.accPolicy.assign(g.P, 0.0f);
+    gm.rawPolicy.assign(g.P, 0.0f);
+    gm.ttKey0.assign(2 * cfg.nodeCap, 0);
+    gm.ttKey1.assign(2 * cfg.nodeCap, 0);
+    gm.ttNode.assign(2 * cfg.nodeCap, -1);
+    gm.svbKey.assign(SVB_CAP, 0);
+    gm.svbDelta.assign(SVB_CAP, 0.0f);
+    gm.svbWeight.assign(SVB_CAP, 0.0f);
+    gm.svbUsed.assign(SVB_CAP, 0);
+    Ctx(s, gm).startGame();
+  }
+}
+
+void selfplayRound(Selfplay& s) {
+  const Geom& g = s.cfg.g;
+  const int G = (int)s.games.size();
+  const int A = g.A;
+  std::vector<float> bin((size_t)G * NUM_SPATIAL * A), glob((size_t)G);
+  std::vector<int> need(G, 0);
+  // ---- select ----
+  for(int i = 0; i < G; i++) {
+    Game& gm = s.games[i];
+    Ctx cx(s, gm);
+    if(gm.phase == PH_ROOTEVAL) {
+      if(gm.rootK == 0) {
+        int idx[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+        for(int k = 0; k < 4; k++) {
+          int j = k + (int)gm.rng.below((uint32_t)(8 - k));
+          std::swap(idx[k], idx[j]);
+          gm.syms[k] = idx[k];
+        }
+      }
+      gm.leafKind = LEAF_ROOTEVAL;
+      gm.leafSym = gm.syms[gm.rootK];
+      gm.leafBoard = gm.root;
+    } else {
+      cx.descend();
+      if(gm.leafKind == LEAF_NN)
+        gm.leafSym = (int)gm.rng.below(8);
+    }
+    if(gm.leafKind == LEAF_NN || gm.leafKind == LEAF_ROOTEVAL) {
+      encodeV1(g, gm.leafBoard, gm.leafSym, &bin[(size_t)i * NUM_SPATIAL * A], &glob[i]);
+      need[i] = 1;
+      gm.nnEvals++;
+    }
+  }
+  // ---- NN ----
+  std::vector<float> out((size_t)G * (g.P + 4));
+  std::vector<int> idx;
+  for(int i = 0; i < G; i++)
+    if(need[i])
+      idx.push_back(i);
+  if(s.cfg.nnMode == 0) {
+    for(int i : idx)
+      fakeNet(g, &bin[(size_t)i * NUM_SPATIAL * A], &out[(size_t)i * (g.P + 4)], &out[(size_t)i * (g.P + 4) + g.P],
+              &out[(size_t)i * (g.P + 4) + g.P + 2]);
+  } else if(!idx.empty()) {
+    int n = (int)idx.size();
+    std::vector<float> cb((size_t)n * NUM_SPATIAL * A), cg(n), pol((size_t)n * 4 * A), val((size_t)n * 2), misc((size_t)n * 2);
+    for(int j = 0; j < n; j++) {
+      memcpy(&cb[(size_t)j * NUM_SPATIAL * A], &bin[(size_t)idx[j] * NUM_SPATIAL * A], sizeof(float) * NUM_SPATIAL * A);
+      cg[j] = glob[idx[j]];
+    }
+    nnForward(*s.cfg.model, g.X, g.Y, n, cb.data(), cg.data(), pol.data(), val.data(), misc.data(),
+              s.cfg.nnMode == 2 ? 1 : 0, s.cfg.nnThreads);
+    for(int j = 0; j < n; j++) {
+      float* o = &out[(size_t)idx[j] * (g.P + 4)];
+      memcpy(o, &pol[(size_t)j * 4 * A], sizeof(float) * g.P);
+      o[g.P] = val[2 * j];
+      o[g.P + 1] = val[2 * j + 1];
+      o[g.P + 2] = misc[2 * j];
+      o[g.P + 3] = misc[2 * j + 1];
+    }
+  }
+  // ---- backup ----
+  for(int i = 0; i < G; i++) {
+    Game& gm = s.games[i];
+    Ctx cx(s, gm);
+    const float* o = &out[(size_t)i * (g.P + 4)];
+    if(gm.leafKind == LEAF_ROOTEVAL) {
+      float pol[MAX_P], w, l;
+      cx.postprocess(gm.root, gm.leafSym, o, pol, w, l);
+      if(gm.rootK == 0) {
+        for(int p = 0; p < g.P; p++) {
+          gm.rawPolicy[p] = pol[p];
+          gm.accPolicy[p] = 0.0f + pol[p];
+        }
+        gm.rawWin = w;
+        gm.rawLoss = l;
+        gm.accWin = 0.0f + w;
+        gm.accLoss = 0.0f + l;
+      } else {
+        for(int p = 0; p < g.P; p++)
+          gm.accPolicy[p] = gm.accPolicy[p] + pol[p];
+        gm.accWin = gm.accWin + w;
+        gm.accLoss = gm.accLoss + l;
+      }
+      gm.rootK++;
+      if(gm.rootK == s.cfg.sp.rootNumSymmetriesToSample) {
+        float fl = (float)s.cfg.sp.rootNumSymmetriesToSample;
+        bool fresh = gm.rootIdx < 0;
+        if(fresh)
+          gm.rootIdx = cx.allocNode(gm.root.pla, stateHash(g, gm.root), false);
+        Node& r = cx.N(gm.rootIdx);
+        float* rp = cx.POL(gm.rootIdx);
+        for(int p = 0; p < g.P; p++)
+          rp[p] = gm.accPolicy[p] / fl;
+        r.nnWin = gm.accWin / fl;
+        r.nnLoss = gm.accLoss / fl;
+        r.flags |= 1;
+        if(fresh)
+          cx.addLeafValue(gm.rootIdx, r.nnWin - r.nnLoss, false, true);
+        cx.noiseAndTemp(rp, gm.rootNoised.data());
+        gm.phase = PH_SEARCH;
+        if(cx.N(gm.rootIdx).visits >= (uint32_t)s.cfg.sp.maxVisits)
+          cx.commitMove();
+      }
+      continue;
+    }
+    // PH_SEARCH leaf
+    if(gm.leafKind == LEAF_NN) {
+      Node& n = cx.N(gm.leafNode);
+      float w, l;
+      cx.postprocess(gm.leafBoard, gm.leafSym, o, cx.POL(gm.leafNode), w, l);
+      n.nnWin = w;
+      n.nnLoss = l;
+      n.flags |= 1;
+      cx.addLeafValue(gm.leafNode, w - l, false, true);
+    } else if(gm.leafKind == LEAF_TERMINAL) {
+      // search.cpp:943-953: value = 2*whiteWinsOfWinner - 1 (SPEC B16: draw = 0)
+      float v = gm.leafBoard.winner == 2 ? 1.0f : (gm.leafBoard.winner == 1 ? -1.0f : 0.0f);
+      cx.addLeafValue(gm.leafNode, v, true, false);
+    } else if(gm.leafKind == LEAF_NOCHILD) {
+      Node& n = cx.N(gm.leafNode);
+      cx.addLeafValue(gm.leafNode, n.nnWin - n.nnLoss, false, false);
+    }
+    for(int j = (int)gm.pathNode.size() - 1; j >= 0; j--) {
+      int pn = gm.pathNode[j];
+      cx.EV(pn, gm.pathSlot[j]) += 1;
+      cx.recompute(pn, 1, pn == gm.rootIdx);
+    }
+    gm.playouts++;
+    if(cx.N(gm.rootIdx).visits >= (uint32_t)s.cfg.sp.maxVisits)
+      cx.commitMove();
+  }
+  s.rounds++;
+}
+
+}  // namespace ora

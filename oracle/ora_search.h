@@ -1,0 +1,127 @@
+// ORACLE (test infrastructure only) — MCTS + self-play restatement.  See ora.h.
+#pragma once
+#include <vector>
+
+#include "ora.h"
+#include "ora_math.h"
+
+namespace ora {
+
+// SearchParams (searchparams.h) restricted to what Coffee self-play reads, with
+// the values of cpp/configs/training/selfplay1.cfg (SURVEY §8d benchmark mode).
+struct SearchParams {
+  int maxVisits = 600;
+  float cpuctExploration = 1.1f, cpuctExplorationLog = 0.0f, cpuctExplorationBase = 500.0f;
+  float fpuReductionMax = 0.2f, rootFpuReductionMax = 0.0f, fpuLossProp = 0.0f, rootFpuLossProp = 0.0f;
+  int fpuParentWeightByVisitedPolicy = 1;
+  float fpuParentWeightByVisitedPolicyPow = 2.0f;
+  float valueWeightExponent = 0.5f;
+  int rootNoiseEnabled = 1;
+  float rootDirichletNoiseTotalConcentration = 10.83f, rootDirichletNoiseWeight = 0.25f;
+  float rootPolicyTemperature = 1.1f, rootPolicyTemperatureEarly = 1.25f;
+  float rootDesiredPerChildVisitsCoeff = 2.0f;
+  int rootNumSymmetriesToSample = 4;
+  float chosenMoveTemperature = 0.15f, chosenMoveTemperatureEarly = 0.75f, chosenMoveTemperatureHalflife = 19.0f;
+  float chosenMoveSubtract = 0.0f, chosenMovePrune = 1.0f;
+  int useLcbForSelection = 1;
+  float lcbStdevs = 5.0f, minVisitPropForLCB = 0.15f;
+  float subtreeValueBiasFactor = 0.30f, subtreeValueBiasWeightExponent = 0.8f, subtreeValueBiasFreeProp = 0.8f;
+  int useGraphSearch = 1;
+};
+
+// Node record; identical fields and pool layout to the HIP engine so whole
+// pools can be compared bit-for-bit.
+struct Node {
+  uint32_t visits;
+  float weightSum, weightSqSum, utilityAvg, utilitySqAvg, winLossAvg;
+  float nnWin, nnLoss;             // white-perspective NN probs (NNOutput::whiteWinProb/LossProb)
+  float lastSvbDelta, lastSvbWeight;
+  int32_t svbEntry;                // -1 none
+  uint16_t numChildren;
+  uint8_t nextPla;
+  uint8_t flags;                   // 1 = expanded (has NN output), 2 = terminal
+  uint64_t key0, key1;             // transposition key (stateHash)
+};
+
+enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1 };
+
+struct TurnRec {
+  int8_t cell, dir;
+  std::vector<int16_t> policyTarget;  // [P]
+  float whiteWin, whiteLoss;          // extractValueTargets (play.cpp:674-682)
+  float rawWhiteWL, rawPolicyEntropy; // computeNNRawStats (play.cpp:684-704)
+  float policySurprise, policyEntropy, searchEntropy;
+  uint32_t visits;
+};
+
+struct Rows {
+  int n = 0;
+  std::vector<uint8_t> bin;      // [n][15][(A+7)/8]
+  std::vector<float> globIn;     // [n][1]
+  std::vector<int16_t> policy;   // [n][2][P]
+  std::vector<float> globT;      // [n][64]
+  std::vector<int8_t> value;     // [n][5][A]
+};
+
+struct SelfplayCfg {
+  Geom g;
+  SearchParams sp;
+  int nodeCap = 2048;
+  uint64_t seed = 1;
+  int slotBase = 0;        // global index of this engine's first game slot (rank * games)
+  int nnMode = 0;          // 0 fake deterministic net, 1 model fp32, 2 model bf16-emulation
+  const Model* model = nullptr;
+  int nnThreads = 1;
+};
+
+struct Game {
+  int slot = 0;
+  uint32_t gameNum = 0;
+  Rng rng;
+  Board root;
+  int phase = PH_ROOTEVAL, rootK = 0;
+  int syms[4];
+  std::vector<float> accPolicy;  // [P]
+  float accWin = 0, accLoss = 0;
+  std::vector<float> rawPolicy;  // first root eval (raw stats)
+  float rawWin = 0, rawLoss = 0;
+  // tree
+  int nodeCount = 0, rootIdx = -1;
+  std::vector<Node> nodes;
+  std::vector<uint32_t> edgeChild, edgeVisits;
+  std::vector<uint16_t> edgeMove;
+  std::vector<float> policy;     // [cap][P]
+  std::vector<float> rootNoised; // [P]
+  std::vector<uint64_t> ttKey0, ttKey1;
+  std::vector<int32_t> ttNode;
+  std::vector<uint64_t> svbKey;
+  std::vector<float> svbDelta, svbWeight;
+  std::vector<uint8_t> svbUsed;
+  // playout scratch
+  int leafKind = LEAF_NONE, leafNode = -1, leafSym = 0;
+  Board leafBoard;
+  std::vector<int> pathNode, pathSlot;
+  // game record
+  std::vector<TurnRec> turns;
+  uint64_t gameHash0 = 0, gameHash1 = 0;
+  // counters
+  uint64_t playouts = 0, nnEvals = 0, movesMade = 0, gamesFinished = 0;
+};
+
+struct Selfplay {
+  SelfplayCfg cfg;
+  std::vector<Game> games;
+  std::vector<uint64_t> svbZ;  // SVB pattern zobrist (SPEC a19)
+  Rows rows;
+  uint64_t rounds = 0;
+};
+
+void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames);
+// One round = select for every game, one batched NN eval, backup for every game.
+void selfplayRound(Selfplay& s);
+// The deterministic stand-in network (analogue of nneval.cpp:442-500 debugSkipNeuralNet).
+void fakeNet(const Geom& g, const float* bin, float* policy, float* value, float* misc);
+void packPlanes(const Geom& g, const float* bin, uint64_t* words);
+
+}  // namespace ora

@@ -1,0 +1,188 @@
+"""ORACLE (test infrastructure only): ctypes wrapper over oracle/_build/liboracle.so.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  The product package (katacoffee_amd) never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+_lib = None
+
+P = ctypes.c_void_p
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.ora_model_load.restype = P
+        L.ora_sp_create.restype = P
+        L.ora_sp_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
+        L.ora_nn_forward.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P, ctypes.c_int, ctypes.c_int]
+        L.ora_sp_rounds.argtypes = [P, ctypes.c_int]
+        L.ora_sp_game_info.argtypes = [P, ctypes.c_int, P]
+        L.ora_sp_game_nodes.argtypes = [P, ctypes.c_int, P, P, P, P, P]
+        L.ora_sp_root_noised.argtypes = [P, ctypes.c_int, P]
+        L.ora_sp_rows_count.argtypes = [P]
+        L.ora_sp_rows.argtypes = [P, P, P, P, P, P]
+        L.ora_sp_free.argtypes = [P]
+        L.ora_model_free.argtypes = [P]
+        _load_tables(L)
+        _lib = L
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _load_tables(L):
+    z = np.load(os.path.join(GOLDEN, "zobrist.npz"))
+    t = np.load(os.path.join(GOLDEN, "tdist3.npz"))
+    arrs = [np.ascontiguousarray(z[k], np.uint64) for k in ["board", "board2", "player", "size_x", "size_y"]]
+    go = np.ascontiguousarray(z["game_over"], np.uint64)
+    cdf = np.ascontiguousarray(t["cdf"].astype(np.float32))
+    L.ora_load_tables(*[ptr(a) for a in arrs], ptr(go), ptr(cdf))
+    _load_tables.keep = arrs + [go, cdf]
+
+
+NODE_DTYPE = np.dtype([
+    ("visits", "<u4"), ("weightSum", "<f4"), ("weightSqSum", "<f4"), ("utilityAvg", "<f4"),
+    ("utilitySqAvg", "<f4"), ("winLossAvg", "<f4"), ("nnWin", "<f4"), ("nnLoss", "<f4"),
+    ("lastSvbDelta", "<f4"), ("lastSvbWeight", "<f4"), ("svbEntry", "<i4"), ("numChildren", "<u2"),
+    ("nextPla", "u1"), ("flags", "u1"), ("key0", "<u8"), ("key1", "<u8"),
+])
+assert NODE_DTYPE.itemsize == 64
+
+
+def rules_batch(X, Y, W, colors, last_cell, last_dir, pla):
+    n = len(pla)
+    A = X * Y
+    legal = np.zeros((n, 4 * A), np.uint8)
+    has = np.zeros(n, np.uint8)
+    lib().ora_rules_batch(X, Y, W, n, ptr(np.ascontiguousarray(colors, np.uint8)),
+                          ptr(np.ascontiguousarray(last_cell, np.int8)), ptr(np.ascontiguousarray(last_dir, np.int8)),
+                          ptr(np.ascontiguousarray(pla, np.uint8)), ptr(legal), ptr(has))
+    return legal, has
+
+
+def play_batch(X, Y, W, colors, last_cell, last_dir, pla, move):
+    n = len(pla)
+    A = X * Y
+    out = dict(colors=np.zeros((n, A), np.uint8), finished=np.zeros(n, np.uint8), winner=np.zeros(n, np.uint8),
+               max_run=np.zeros(n, np.int32), pos_hash=np.zeros((n, 2), np.uint64), state_hash=np.zeros((n, 2), np.uint64))
+    lib().ora_play_batch(X, Y, W, n, ptr(np.ascontiguousarray(colors, np.uint8)),
+                         ptr(np.ascontiguousarray(last_cell, np.int8)), ptr(np.ascontiguousarray(last_dir, np.int8)),
+                         ptr(np.ascontiguousarray(pla, np.uint8)), ptr(np.ascontiguousarray(move, np.int32)),
+                         ptr(out["colors"]), ptr(out["finished"]), ptr(out["winner"]), ptr(out["max_run"]),
+                         ptr(out["pos_hash"]), ptr(out["state_hash"]))
+    return out
+
+
+def encode_batch(X, Y, W, colors, hist_cell, hist_dir, pla, sym):
+    n = len(pla)
+    A = X * Y
+    binp = np.zeros((n, 15, A), np.float32)
+    glob = np.zeros(n, np.float32)
+    lib().ora_encode_batch(X, Y, W, n, ptr(np.ascontiguousarray(colors, np.uint8)),
+                           ptr(np.ascontiguousarray(hist_cell, np.int8)), ptr(np.ascontiguousarray(hist_dir, np.int8)),
+                           ptr(np.ascontiguousarray(pla, np.uint8)), ptr(np.ascontiguousarray(sym, np.int32)),
+                           ptr(binp), ptr(glob))
+    return binp, glob
+
+
+def fake_net(X, Y, W, binp):
+    n = binp.shape[0]
+    out = np.zeros((n, 4 * X * Y + 4), np.float32)
+    lib().ora_fake_net(X, Y, W, n, ptr(np.ascontiguousarray(binp, np.float32)), ptr(out))
+    return out
+
+
+class Model:
+    def __init__(self, path):
+        self.h = lib().ora_model_load(path.encode())
+        if not self.h:
+            raise RuntimeError("oracle: cannot load model " + path)
+
+    def forward(self, X, Y, binp, glob, mode=0, threads=1):
+        n = binp.shape[0]
+        A = X * Y
+        pol = np.zeros((n, 4, A), np.float32)
+        val = np.zeros((n, 2), np.float32)
+        misc = np.zeros((n, 2), np.float32)
+        lib().ora_nn_forward(self.h, X, Y, n, ptr(np.ascontiguousarray(binp, np.float32)),
+                             ptr(np.ascontiguousarray(glob, np.float32)), ptr(pol), ptr(val), ptr(misc), mode, threads)
+        return pol, val, misc
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_model_free(self.h)
+
+
+class Selfplay:
+    """Round-synchronous self-play engine (select -> batched NN -> backup per round)."""
+
+    def __init__(self, X, Y, W, games, max_visits, node_cap=2048, seed=1, slot_base=0, nn_mode=0, model=None,
+                 nn_threads=1):
+        self.X, self.Y, self.W, self.games = X, Y, W, games
+        self.A, self.P = X * Y, 4 * X * Y
+        self.model = model
+        self.h = lib().ora_sp_create(X, Y, W, games, max_visits, node_cap, seed, slot_base, nn_mode,
+                                     model.h if model is not None else None, nn_threads)
+        if not self.h:
+            raise RuntimeError("oracle selfplay create failed")
+
+    def rounds(self, n):
+        lib().ora_sp_rounds(self.h, n)
+
+    def info(self, slot):
+        a = np.zeros(16, np.int64)
+        lib().ora_sp_game_info(self.h, slot, ptr(a))
+        keys = ["phase", "rootK", "nodeCount", "rootIdx", "turn", "pla", "gameNum", "playouts", "nnEvals",
+                "movesMade", "gamesFinished", "rngCtr", "leafKind", "rootVisits", "lastCell", "lastDir"]
+        return dict(zip(keys, a.tolist()))
+
+    def nodes(self, slot, cap=4096):
+        nodes = np.zeros(cap, NODE_DTYPE)
+        ec = np.zeros(cap * self.P, np.uint32)
+        ev = np.zeros(cap * self.P, np.uint32)
+        em = np.zeros(cap * self.P, np.uint16)
+        pol = np.zeros(cap * self.P, np.float32)
+        n = lib().ora_sp_game_nodes(self.h, slot, ptr(nodes), ptr(ec), ptr(ev), ptr(em), ptr(pol))
+        P = self.P
+        return dict(nodes=nodes[:n], edge_child=ec[:n * P].reshape(n, P), edge_visits=ev[:n * P].reshape(n, P),
+                    edge_move=em[:n * P].reshape(n, P), policy=pol[:n * P].reshape(n, P))
+
+    def root_noised(self, slot):
+        out = np.zeros(self.P, np.float32)
+        lib().ora_sp_root_noised(self.h, slot, ptr(out))
+        return out
+
+    def rows(self):
+        n = lib().ora_sp_rows_count(self.h)
+        A, P = self.A, self.P
+        pb = (A + 7) // 8
+        r = dict(binaryInputNCHWPacked=np.zeros((n, 15, pb), np.uint8), globalInputNC=np.zeros((n, 1), np.float32),
+                 policyTargetsNCMove=np.zeros((n, 2, P), np.int16), globalTargetsNC=np.zeros((n, 64), np.float32),
+                 valueTargetsNCHW=np.zeros((n, 5, self.Y, self.X), np.int8))
+        lib().ora_sp_rows(self.h, ptr(r["binaryInputNCHWPacked"]), ptr(r["globalInputNC"]),
+                          ptr(r["policyTargetsNCMove"]), ptr(r["globalTargetsNC"]), ptr(r["valueTargetsNCHW"]))
+        return r
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_sp_free(self.h)
