@@ -1,0 +1,213 @@
+// Device-side Coffee rules over bitboards (DBoard), wave-cooperative where the
+// work is per-move.  Semantics restated from the reference:
+//   Board::isLegal           board.cpp:185-227  (line constraint + "other empty cell on the line")
+//   Board::playMoveAssumeLegal board.cpp:427-435, BoardHistory::makeBoardMoveAssumeLegal
+//                            boardhistory.cpp:157-176 (+ SPEC B16 draw when stuck, B18 history)
+//   Board::maxConsecutives   board.cpp:315-335
+//   NNInputs::fillRowV1      nninputs.cpp:508-657 (SPEC a6 15-plane V1)
+#pragma once
+#include "detmath.h"
+#include "kc_common.h"
+
+namespace kc {
+
+KC_HD BB occupied(const DBoard& b) { return bbOr(b.stones[0], b.stones[1]); }
+KC_HD int colorAt(const DBoard& b, int c) {
+  return bbTest(b.stones[0], c) ? 1 : (bbTest(b.stones[1], c) ? 2 : 0);
+}
+
+KC_HD bool isLegal(const DTables& T, const DBoard& b, int cell, int dir) {
+  BB occ = occupied(b);
+  if(bbTest(occ, cell))
+    return false;
+  if(b.lastCell >= 0 && b.lastDir < 4 && !bbTest(T.lineMask[b.lastCell][b.lastDir], cell))
+    return false;
+  return bbAny(bbAndNot(T.lineMask[cell][dir], occ));
+}
+
+KC_HD int maxRun(const DTables& T, const DBoard& b, int cell) {
+  const int X = T.X, Y = T.Y;
+  const BB& own = b.stones[colorAt(b, cell) == 2 ? 1 : 0];
+  const int dxs[4] = {0, -1, -1, 1}, dys[4] = {-1, 0, -1, -1};
+  int x = cell % X, y = cell / X, best = 1;
+  for(int d = 0; d < 4; d++) {
+    int n = 1;
+    for(int s = -1; s <= 1; s += 2) {
+      int cx = x + s * dxs[d], cy = y + s * dys[d];
+      while(cx >= 0 && cx < X && cy >= 0 && cy < Y && bbTest(own, cy * X + cx)) {
+        n++;
+        cx += s * dxs[d];
+        cy += s * dys[d];
+      }
+    }
+    best = n > best ? n : best;
+  }
+  return best;
+}
+
+// Longest run of the cell's colour along axis d through the cell (0 if empty).
+KC_HD int runAlong(const DTables& T, const DBoard& b, int cell, int d) {
+  int col = colorAt(b, cell);
+  if(col == 0)
+    return 0;
+  const BB& own = b.stones[col - 1];
+  const int dxs[4] = {0, -1, -1, 1}, dys[4] = {-1, 0, -1, -1};
+  int x = cell % T.X, y = cell / T.X, n = 1;
+  for(int s = -1; s <= 1; s += 2) {
+    int cx = x + s * dxs[d], cy = y + s * dys[d];
+    while(cx >= 0 && cx < T.X && cy >= 0 && cy < T.Y && bbTest(own, cy * T.X + cx)) {
+      n++;
+      cx += s * dxs[d];
+      cy += s * dys[d];
+    }
+  }
+  return n;
+}
+
+KC_HD void boardInit(const DTables& T, DBoard& b) {
+  b.stones[0] = BB{0, 0};
+  b.stones[1] = BB{0, 0};
+  b.h0 = T.zInit[0];
+  b.h1 = T.zInit[1];
+  b.lastCell = -1;
+  b.lastDir = 4;
+  b.pla = 1;
+  b.finished = 0;
+  b.winner = 0;
+  b.pad0 = 0;
+  b.turn = 0;
+  for(int i = 0; i < HIST; i++) {
+    b.histCell[i] = -1;
+    b.histDir[i] = 4;
+  }
+  for(int i = 0; i < 6; i++)
+    b.pad1[i] = 0;
+}
+
+// State part of playMove (everything except the end-of-game test).
+KC_HD void applyMove(const DTables& T, DBoard& b, int cell, int dir) {
+  int pla = b.pla;
+  bbSet(b.stones[pla - 1], cell);
+  b.h0 ^= T.zBoard[cell][pla][0];
+  b.h1 ^= T.zBoard[cell][pla][1];
+  b.lastCell = (int8_t)cell;
+  b.lastDir = (int8_t)dir;
+  for(int i = HIST - 1; i > 0; i--) {
+    b.histCell[i] = b.histCell[i - 1];
+    b.histDir[i] = b.histDir[i - 1];
+  }
+  b.histCell[0] = (int8_t)cell;
+  b.histDir[0] = (int8_t)dir;
+  b.turn++;
+  b.pla = (int8_t)(3 - pla);
+  b.finished = 0;
+  b.winner = 0;
+}
+
+KC_HD bool hasAnyLegalSerial(const DTables& T, const DBoard& b) {
+  for(int c = 0; c < T.A; c++)
+    for(int d = 0; d < 4; d++)
+      if(isLegal(T, b, c, d))
+        return true;
+  return false;
+}
+
+// Serial (single-thread) full move: host tools and per-lane use.
+KC_HD void playMoveSerial(const DTables& T, DBoard& b, int cell, int dir) {
+  int mover = b.pla;
+  applyMove(T, b, cell, dir);
+  if(maxRun(T, b, cell) >= T.W) {
+    b.finished = 1;
+    b.winner = (int8_t)mover;
+  } else if(!hasAnyLegalSerial(T, b)) {
+    b.finished = 1;
+    b.winner = 0;
+  }
+}
+
+// GraphHash::getStateHash graphhash.cpp:3-12 + last-move term (SPEC a20).
+KC_HD void stateHash(const DTables& T, const DBoard& b, uint64_t& k0, uint64_t& k1) {
+  k0 = b.h0 ^ T.zPlayer[b.pla][0];
+  k1 = b.h1 ^ T.zPlayer[b.pla][1];
+  if(b.lastCell >= 0) {
+    k0 ^= T.zBoard2[b.lastCell][b.lastDir][0];
+    k1 ^= T.zBoard2[b.lastCell][b.lastDir][1];
+  }
+  if(b.finished) {
+    k0 ^= T.zGameOver[0];
+    k1 ^= T.zGameOver[1];
+  }
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// Wave-cooperative: every lane calls with the same board; result is uniform.
+KC_D bool hasAnyLegalWave(const DTables& T, const DBoard& b) {
+  bool any = false;
+  for(int pos = laneId(); pos < T.P; pos += 64)
+    any = any || isLegal(T, b, pos % T.A, pos / T.A);
+  return ballot(any) != 0;
+}
+
+KC_D void playMoveWave(const DTables& T, DBoard& b, int cell, int dir) {
+  int mover = b.pla;
+  applyMove(T, b, cell, dir);
+  if(maxRun(T, b, cell) >= T.W) {
+    b.finished = 1;
+    b.winner = (int8_t)mover;
+  } else if(!hasAnyLegalWave(T, b)) {
+    b.finished = 1;
+    b.winner = 0;
+  }
+}
+
+// Feature bit of V1 plane `plane` at ORIGINAL cell c, for symmetry sym (the bit
+// is stored at symCell[sym][c]).
+KC_D bool v1Bit(const DTables& T, const DBoard& b, int plane, int c, int sym) {
+  int pla = b.pla;
+  switch(plane) {
+    case 0: return true;
+    case 1: return colorAt(b, c) == pla;
+    case 2: return colorAt(b, c) == 3 - pla;
+    case 3: case 4: case 5: case 6:
+      return b.histCell[0] == c && T.symDir[sym][b.histDir[0]] == plane - 3;
+    case 7: case 8: case 9: case 10:
+      return b.histCell[plane - 6] == c;
+    case 11: {
+      for(int d = 0; d < 4; d++)
+        if(isLegal(T, b, c, d))
+          return true;
+      return false;
+    }
+    default: {
+      int len = T.W - 1 - (plane - 12);
+      if(len < 1)
+        return false;
+      for(int d = 0; d < 4; d++)
+        if(runAlong(T, b, c, d) == len)
+          return true;
+      return false;
+    }
+  }
+}
+
+// Packs the 15 V1 planes (symmetric frame) into T.inWords words: bit i of the
+// flat [plane][cell] index lands in word i>>6, bit i&63 (oracle packPlanes).
+KC_D void encodePackedWave(const DTables& T, const DBoard& b, int sym, uint64_t* out) {
+  if(T.X != T.Y)
+    sym &= 3;
+  const int A = T.A;
+  for(int w = 0; w < T.inWords; w++) {
+    int i = w * 64 + laneId();
+    bool bit = false;
+    if(i < NUM_SPATIAL * A) {
+      int plane = i / A, s = i % A;
+      bit = v1Bit(T, b, plane, T.invSymCell[sym][s], sym);
+    }
+    uint64_t word = ballot(bit);
+    if(laneId() == 0)
+      out[w] = word;
+  }
+}
+#endif
+
+}  // namespace kc

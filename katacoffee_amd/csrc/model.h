@@ -1,0 +1,55 @@
+// Coffee network weights: the "CFNN" v1 file format and a seeded initializer.
+//
+// The reference has no Coffee model format (desc.cpp:800-914 only reads
+// KataGo Go nets).  This format carries exactly the tensors of the Coffee head
+// contract (NNOutput, nninputs.h:75-118) on a KataGo-style trunk
+// (model_pytorch.py:678-1152; eigenbackend.cpp:888-1377):
+//
+//   "CFNN" u32 version=1
+//   i32 cin gin C Cg p1 g1 v1 v2 nblocks, i32 kinds[nblocks] (0 regular, 1 gpool)
+//   f32 tensors, in this order:
+//     convInit[C][cin][3][3]  globInit[C][gin]
+//     per block: bn1s[C] bn1b[C]
+//        regular: conv1[C][C][3][3] bn2s[C] bn2b[C] conv2[C][C][3][3]
+//        gpool  : conv1r[C-Cg][C][3][3] conv1g[Cg][C][3][3] bngs[Cg] bngb[Cg]
+//                 linG[C-Cg][3Cg] bn2s[C-Cg] bn2b[C-Cg] conv2[C][C-Cg][3][3]
+//     tips[C] tipb[C]
+//     pConv1[p1][C] pConvG[g1][C] pBiasG[g1] pLinG[p1][3g1] pBias2[p1] pConv2[4][p1]
+//     vConv1[v1][C] vBias1[v1] vLin2[v2][3v1] vB2[v2] vLin3[2][v2] vB3[2] vLinM[2][v2] vBM[2]
+// BatchNorm layers are stored merged (scale = gamma/sqrt(var+eps), bias = beta -
+// scale*mean, eigenbackend.cpp:684-734).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace kc {
+
+struct ModelCfg {
+  int cin = 15, gin = 1, C = 96, Cg = 32, p1 = 32, g1 = 32, v1 = 32, v2 = 64;
+  std::vector<int> kinds;  // per block
+};
+
+struct ModelBlock {
+  int kind = 0;
+  std::vector<float> bn1s, bn1b, conv1, conv1g, bngs, bngb, linG, bn2s, bn2b, conv2;
+};
+
+struct ModelHost {
+  ModelCfg cfg;
+  std::vector<float> convInit, globInit;
+  std::vector<ModelBlock> blocks;
+  std::vector<float> tips, tipb;
+  std::vector<float> pConv1, pConvG, pBiasG, pLinG, pBias2, pConv2;
+  std::vector<float> vConv1, vBias1, vLin2, vB2, vLin3, vB3, vLinM, vBM;
+};
+
+// Named architectures: "b6c96" (BASELINE C1/C2), "b10c128" (C3/C4).
+ModelCfg modelCfgByName(const std::string& name);
+ModelHost randomModel(const ModelCfg& cfg, uint64_t seed);
+void saveModel(const std::string& path, const ModelHost& m);
+ModelHost loadModel(const std::string& path);
+// FLOPs per evaluation at area A (2 x MACs of every conv / matmul).
+double modelFlopsPerEval(const ModelCfg& cfg, int A);
+
+}  // namespace kc

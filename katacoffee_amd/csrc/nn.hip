@@ -1,0 +1,617 @@
+// Fused residual-network forward for Coffee leaf batches (one launch per batch).
+//
+// Semantics: eigenbackend.cpp (ConvLayer :270-680, BatchNormLayer :684-734,
+// poolRowsGPool :141-166, poolRowsValueHead :168-186, ResidualBlock :888-931,
+// GlobalPoolingResidualBlock :935-1015, Trunk :1169-1227, PolicyHead :1229-1299,
+// ValueHead :1301-1377), Coffee head contract nninputs.h:75-118.
+//
+// MI355X design (DESIGN.md "NN forward"):
+//  * one 512-thread workgroup (8 waves) per 8 boards = 200 rows (positions),
+//    204 VGPRs -> 2 waves/SIMD, one resident workgroup per CU (LDS ~80 KB);
+//  * 3x3 convolutions are implicit GEMMs on v_mfma_f32_16x16x32_bf16:
+//    A = activations gathered from LDS by neighbour offset (bf16, NHWC, padded
+//    rows -> conflict-free ds_read_b128), B = weights pre-swizzled on the host
+//    into per-lane 16-byte fragments streamed from L2 (one dwordx4 per lane);
+//  * the residual trunk x lives in registers (f32, accumulator layout) for the
+//    whole network; only the bf16 conv input is staged through LDS, so HBM sees
+//    the 48-byte packed input and the 416-byte output per board and nothing else;
+//  * BN + ReLU, global pooling, the gpool bias and both heads are fused epilogues.
+// Waves: rg = wave>>1 owns a contiguous range of 16-row tiles, cg = wave&1 owns
+// half of the output channels.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <vector>
+
+#include "detmath.h"
+#include "engine.h"
+
+namespace kc {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int X_, int Y_, int C_>
+struct NNGeo {
+  static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
+  static constexpr int NB = 8;
+  static constexpr int ROWS = NB * A;
+  static constexpr int RT = (ROWS + 15) / 16;
+  // rows [ROWS, RT*16) are tile padding (computed, never read as neighbours);
+  // ZROW is the all-zero row that out-of-board neighbour taps read.
+  static constexpr int ZROW = RT * 16;
+  static constexpr int TBASE = RT / 4, TREM = RT % 4, MAXT = TBASE + (TREM > 0 ? 1 : 0);
+  static constexpr int ASTR = C + 8;     // bf16 per activation row (+16 B pad: conflict-free b128 reads)
+  static constexpr int NCT = C / 32;     // 16-col tiles per wave
+  static constexpr int NCT_ALL = C / 16;
+  static constexpr int P = 4 * A;
+  static constexpr int OFF_SCR = (((ZROW + 1) * ASTR * 2) + 15) / 16 * 16;
+  static constexpr int OFF_POOL = OFF_SCR + ZROW * 32 * 4;
+  static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
+  static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
+  static constexpr int LDS = OFF_VH + NB * 64 * 4;
+  static_assert(C % 32 == 0, "C must be a multiple of 32");
+  static_assert(ZROW * 32 * 4 <= (ZROW + 1) * ASTR * 2, "value-branch f32 scratch must fit in act");
+  static_assert(LDS <= 163840, "LDS budget");
+};
+
+KC_D uint16_t bf16bits(float f) {
+  uint32_t u = __builtin_bit_cast(uint32_t, f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+// First accumulator row owned by this lane in tile tstart.  The empty asm makes
+// the value opaque so the compiler recomputes per-row LDS addresses at each use
+// instead of hoisting dozens of them out of the block loop (register spills).
+KC_D int laneRow(int tstart, int lane) {
+  int r = tstart * 16 + 4 * (lane >> 4);
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
+// Implicit-GEMM convolution over the wave's tiles: acc[t][ct] += A(t, K) * B(K, ct).
+template <class G, int NTAPS, int NCB>
+KC_D void convTiles(const uint16_t* __restrict__ act, const bf16x8* __restrict__ w, f32x4 (&acc)[G::MAXT][G::NCT],
+                    int tstart, int ntiles, int cg, int lane) {
+  const int kq = 8 * (lane >> 4);
+  const int r0 = tstart * 16 + (lane & 15);
+#pragma unroll 1
+  for(int tap = 0; tap < NTAPS; tap++) {
+    const int dy = NTAPS == 9 ? tap / 3 - 1 : 0;
+    const int dx = NTAPS == 9 ? tap % 3 - 1 : 0;
+    // neighbour row (or the zero row) per tile, as an LDS element offset
+    int roff[G::MAXT];
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++) {
+      int r = r0 + t * 16;
+      int b = r / G::A;
+      int p = r - b * G::A;
+      int yy = p / G::X + dy;
+      int xx = p - (p / G::X) * G::X + dx;
+      bool ok = r < G::ROWS && yy >= 0 && yy < G::Y && xx >= 0 && xx < G::X;
+      roff[t] = (ok ? (r + dy * G::X + dx) : G::ZROW) * G::ASTR + kq;
+    }
+#pragma unroll 1
+    for(int cb = 0; cb < NCB; cb++) {
+      const int s = tap * NCB + cb;
+      bf16x8 bcur[G::NCT];
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++)
+        bcur[ct] = w[((size_t)s * G::NCT_ALL + cg * G::NCT + ct) * 64 + lane];
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++) {
+        if(t < ntiles) {
+          bf16x8 a = *reinterpret_cast<const bf16x8*>(act + roff[t] + cb * 32);
+#pragma unroll
+          for(int ct = 0; ct < G::NCT; ct++)
+            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bcur[ct], acc[t][ct], 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// The residual trunk is kept in registers as fp16 (RNE) between blocks; the
+// oracle's GPU-emulation mode rounds at the same points.
+template <class G>
+KC_D void packX(f16x4 (&xh)[G::MAXT][G::NCT], const f32x4 (&a)[G::MAXT][G::NCT]) {
+#pragma unroll
+  for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++)
+      xh[t][ct] = __builtin_convertvector(a[t][ct], f16x4);
+}
+template <class G>
+KC_D void unpackX(f32x4 (&a)[G::MAXT][G::NCT], const f16x4 (&xh)[G::MAXT][G::NCT]) {
+#pragma unroll
+  for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++)
+      a[t][ct] = __builtin_convertvector(xh[t][ct], f32x4);
+}
+
+template <class G>
+KC_D void zeroAcc(f32x4 (&a)[G::MAXT][G::NCT]) {
+#pragma unroll
+  for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++)
+      a[t][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+// act[row][col] = bf16(relu(v * s[col] + b[col])) for cols in [c0, c1).
+template <class G, class V>
+KC_D void storeBnRelu(uint16_t* act, const V (&v)[G::MAXT][G::NCT], const float* __restrict__ s,
+                      const float* __restrict__ bb, int tstart, int ntiles, int cg, int lane, int c0, int c1) {
+  const int rl = laneRow(tstart, lane);
+#pragma unroll
+  for(int ct = 0; ct < G::NCT; ct++) {
+    const int col = cg * (G::C / 2) + ct * 16 + (lane & 15);
+    if(cg * (G::C / 2) + ct * 16 < c0 || cg * (G::C / 2) + ct * 16 >= c1)
+      continue;
+    const float sc = s[col], bi = bb[col];
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++) {
+      if(t >= ntiles)
+        continue;
+#pragma unroll
+      for(int j = 0; j < 4; j++) {
+        int row = rl + t * 16 + j;
+        float x = (float)v[t][ct][j] * sc + bi;
+        x = x > 0.0f ? x : 0.0f;
+        act[row * G::ASTR + col] = bf16bits(x);
+      }
+    }
+  }
+}
+
+template <int X, int Y, int C>
+__global__ void __launch_bounds__(512, 2)
+    kNNForward(const NNLayout* __restrict__ L, const bf16x8* __restrict__ WB, const float* __restrict__ WF, int n,
+               const int* __restrict__ countDev, int inWords, float winLen, const uint64_t* __restrict__ in,
+               float* __restrict__ out) {
+  using G = NNGeo<X, Y, C>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int count = countDev ? min(*countDev, n) : n;
+  const int base = blockIdx.x * G::NB;
+  if(base >= count)
+    return;
+  const int nb = min(G::NB, count - base);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rg = wave >> 1, cg = wave & 1;
+  const int tstart = rg * G::TBASE + min(rg, G::TREM);
+  const int ntiles = G::TBASE + (rg < G::TREM ? 1 : 0);
+  uint16_t* act = reinterpret_cast<uint16_t*>(smem);
+  float* actF = reinterpret_cast<float*>(smem);
+  float* scr = reinterpret_cast<float*>(smem + G::OFF_SCR);
+  float* poolP = reinterpret_cast<float*>(smem + G::OFF_POOL);
+  float* poolV = poolP + G::NB * 96;
+  float* biasS = reinterpret_cast<float*>(smem + G::OFF_BIAS);
+  float* vh = reinterpret_cast<float*>(smem + G::OFF_VH);
+  const float sqOff = sqrtf((float)G::A) - 14.0f;
+
+  // ---- unpack the packed V1 planes: act[row][0..31] (15 planes + zero pad), zero row ----
+  for(int idx = tid; idx < (G::ZROW + 1) * 32; idx += 512) {
+    int row = idx >> 5, c = idx & 31;
+    uint16_t v = 0;
+    if(row < nb * G::A && c < NUM_SPATIAL) {
+      int b = row / G::A, p = row - b * G::A;
+      int i = c * G::A + p;
+      uint64_t word = in[(size_t)(base + b) * inWords + (i >> 6)];
+      v = ((word >> (i & 63)) & 1ULL) ? (uint16_t)0x3f80 : (uint16_t)0;
+    }
+    act[row * G::ASTR + c] = v;
+  }
+  for(int c = 32 + tid; c < G::C; c += 512)
+    act[G::ZROW * G::ASTR + c] = 0;
+  __syncthreads();
+
+  f16x4 x[G::MAXT][G::NCT];
+  f32x4 acc[G::MAXT][G::NCT];
+  zeroAcc<G>(acc);
+  convTiles<G, 9, 1>(act, WB + L->wInit, acc, tstart, ntiles, cg, lane);
+  {
+    // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++) {
+      const int col = cg * (G::C / 2) + ct * 16 + (lane & 15);
+      const float gb = WF[L->globInit + col] * winLen;
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+        for(int j = 0; j < 4; j++)
+          acc[t][ct][j] += gb;
+    }
+  }
+  packX<G>(x, acc);
+  const int Cr = G::C - L->Cg;
+  for(int blk = 0; blk < L->nblocks; blk++) {
+    __syncthreads();  // previous conv finished reading act
+    storeBnRelu<G>(act, x, WF + L->bn1s[blk], WF + L->bn1b[blk], tstart, ntiles, cg, lane, 0, G::C);
+    __syncthreads();
+    zeroAcc<G>(acc);
+    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], acc, tstart, ntiles, cg, lane);
+    __syncthreads();
+    if(L->kinds[blk] == 0) {
+      storeBnRelu<G>(act, acc, WF + L->bn2s[blk], WF + L->bn2b[blk], tstart, ntiles, cg, lane, 0, G::C);
+      __syncthreads();
+      unpackX<G>(acc, x);
+      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], acc, tstart, ntiles, cg, lane);
+      packX<G>(x, acc);
+    } else {
+      // g branch: BN-ReLU into scr (f32), then KataGPool per board (model_pytorch.py:326-352)
+      const float* gs = WF + L->bngs[blk];
+      const float* gbias = WF + L->bngb[blk];
+      const int rl = laneRow(tstart, lane);
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++) {
+        const int c0 = cg * (G::C / 2) + ct * 16;
+        if(c0 < Cr)
+          continue;
+        const int gc = c0 - Cr + (lane & 15);
+        const float sc = gs[gc], bi = gbias[gc];
+#pragma unroll
+        for(int t = 0; t < G::MAXT; t++) {
+          if(t >= ntiles)
+            continue;
+#pragma unroll
+          for(int j = 0; j < 4; j++) {
+            int row = rl + t * 16 + j;
+            float v = acc[t][ct][j] * sc + bi;
+            scr[row * 32 + gc] = v > 0.0f ? v : 0.0f;
+          }
+        }
+      }
+      __syncthreads();
+      for(int idx = tid; idx < G::NB * 32; idx += 512) {
+        const int b = idx >> 5, c = idx & 31;
+        float s = 0.0f, m = 0.0f;
+#pragma unroll 1
+        for(int p = 0; p < G::A; p++) {
+          float v = scr[(b * G::A + p) * 32 + c];
+          s += v;
+          m = v > m ? v : m;
+        }
+        float mean = s / (float)G::A;
+        poolP[b * 96 + c] = mean;
+        poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
+        poolP[b * 96 + 64 + c] = m;
+      }
+      __syncthreads();
+      {
+        const float* lg = WF + L->linG[blk];
+        for(int idx = tid; idx < G::NB * Cr; idx += 512) {
+          const int b = idx / Cr, o = idx - b * Cr;
+          float s = 0.0f;
+#pragma unroll 4
+          for(int i = 0; i < 96; i++)
+            s += lg[o * 96 + i] * poolP[b * 96 + i];
+          biasS[b * Cr + o] = s;
+        }
+      }
+      __syncthreads();
+      {
+        // r branch + gpool bias -> BN2-ReLU -> bf16 act (cols < Cr)
+        const float* s2 = WF + L->bn2s[blk];
+        const float* b2 = WF + L->bn2b[blk];
+        const int rl = laneRow(tstart, lane);
+#pragma unroll
+        for(int ct = 0; ct < G::NCT; ct++) {
+          const int c0 = cg * (G::C / 2) + ct * 16;
+          if(c0 >= Cr)
+            continue;
+          const int col = c0 + (lane & 15);
+          const float sc = s2[col], bi = b2[col];
+#pragma unroll
+          for(int t = 0; t < G::MAXT; t++) {
+            if(t >= ntiles)
+              continue;
+#pragma unroll
+            for(int j = 0; j < 4; j++) {
+              int row = rl + t * 16 + j;
+              int brd = row / G::A;
+              brd = brd < G::NB ? brd : G::NB - 1;
+              float v = (acc[t][ct][j] + biasS[brd * Cr + col]) * sc + bi;
+              act[row * G::ASTR + col] = bf16bits(v > 0.0f ? v : 0.0f);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      unpackX<G>(acc, x);
+      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], acc, tstart, ntiles, cg, lane);
+      packX<G>(x, acc);
+    }
+  }
+  // ---- trunk tip ----
+  __syncthreads();
+  storeBnRelu<G>(act, x, WF + L->tips, WF + L->tipb, tstart, ntiles, cg, lane, 0, G::C);
+  __syncthreads();
+  // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
+  zeroAcc<G>(acc);
+  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, acc, tstart, ntiles, cg, lane);
+  __syncthreads();  // act dead from here; reuse it as f32 [ROWS][32] for the value branch
+  {
+    const float* pbg = WF + L->pBiasG;
+    const float* vb1 = WF + L->vBias1;
+    const int rl = laneRow(tstart, lane);
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++) {
+      const int c0 = cg * (G::C / 2) + ct * 16;
+      if(c0 < 32)
+        continue;
+      const bool isG = c0 < 64;
+      const int hc = (c0 - (isG ? 32 : 64)) + (lane & 15);
+      const float bi = isG ? pbg[hc] : vb1[hc];
+      float* dst = isG ? scr : actF;
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++) {
+        if(t >= ntiles)
+          continue;
+#pragma unroll
+        for(int j = 0; j < 4; j++) {
+          int row = rl + t * 16 + j;
+          float v = acc[t][ct][j] + bi;
+          dst[row * 32 + hc] = v > 0.0f ? v : 0.0f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for(int idx = tid; idx < G::NB * 32; idx += 512) {
+    const int b = idx >> 5, c = idx & 31;
+    float s = 0.0f, m = 0.0f, sv = 0.0f;
+#pragma unroll 1
+    for(int p = 0; p < G::A; p++) {
+      float v = scr[(b * G::A + p) * 32 + c];
+      s += v;
+      m = v > m ? v : m;
+      sv += actF[(b * G::A + p) * 32 + c];
+    }
+    float mean = s / (float)G::A, meanv = sv / (float)G::A;
+    poolP[b * 96 + c] = mean;
+    poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
+    poolP[b * 96 + 64 + c] = m;
+    poolV[b * 96 + c] = meanv;
+    poolV[b * 96 + 32 + c] = meanv * (sqOff / 10.0f);
+    poolV[b * 96 + 64 + c] = meanv * ((sqOff * sqOff) / 100.0f - 0.1f);
+  }
+  __syncthreads();
+  {
+    const float* plg = WF + L->pLinG;
+    for(int idx = tid; idx < G::NB * 32; idx += 512) {
+      const int b = idx >> 5, o = idx & 31;
+      float s = 0.0f;
+#pragma unroll 4
+      for(int i = 0; i < 96; i++)
+        s += plg[o * 96 + i] * poolP[b * 96 + i];
+      biasS[b * 32 + o] = s;
+    }
+    const int v2 = L->v2;
+    const float* l2 = WF + L->vLin2;
+    const float* b2 = WF + L->vB2;
+    for(int idx = tid; idx < G::NB * v2; idx += 512) {
+      const int b = idx / v2, oo = idx - b * v2;
+      float t = b2[oo];
+#pragma unroll 4
+      for(int i = 0; i < 96; i++)
+        t += l2[oo * 96 + i] * poolV[b * 96 + i];
+      vh[b * 64 + oo] = t > 0.0f ? t : 0.0f;
+    }
+  }
+  __syncthreads();
+  if(tid < G::NB * 4) {
+    const int b = tid >> 2, o = tid & 3;
+    if(b < nb) {
+      const int v2 = L->v2;
+      const float* w = o < 2 ? WF + L->vLin3 + o * v2 : WF + L->vLinM + (o - 2) * v2;
+      float s = o < 2 ? WF[L->vB3 + o] : WF[L->vBM + o - 2];
+#pragma unroll 4
+      for(int i = 0; i < v2; i++)
+        s += w[i] * vh[b * 64 + i];
+      out[(size_t)(base + b) * (G::P + 4) + G::P + o] = s;
+    }
+  }
+  if(cg == 0) {
+    // policy: relu(p + gpool bias + bias2) -> 1x1 conv p1 -> 4 direction logits
+    const float* pb2 = WF + L->pBias2;
+    const float* w2 = WF + L->pConv2;
+    const int c0 = lane & 15, c1 = 16 + (lane & 15);
+    const int rl = laneRow(tstart, lane);
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++) {
+      if(t >= ntiles)
+        continue;
+#pragma unroll
+      for(int j = 0; j < 4; j++) {
+        int row = rl + t * 16 + j;
+        int brd = row / G::A;
+        int bclamp = brd < G::NB ? brd : G::NB - 1;
+        float p0 = acc[t][0][j] + biasS[bclamp * 32 + c0] + pb2[c0];
+        float p1 = acc[t][1][j] + biasS[bclamp * 32 + c1] + pb2[c1];
+        p0 = p0 > 0.0f ? p0 : 0.0f;
+        p1 = p1 > 0.0f ? p1 : 0.0f;
+        float part[4];
+#pragma unroll
+        for(int d = 0; d < 4; d++) {
+          float s = p0 * w2[d * 32 + c0] + p1 * w2[d * 32 + c1];
+#pragma unroll
+          for(int off = 1; off < 16; off <<= 1)
+            s += __shfl_xor(s, off, 64);
+          part[d] = s;
+        }
+        if((lane & 15) == 0 && row < nb * G::A) {
+          int pp = row - brd * G::A;
+          float* o = out + (size_t)(base + brd) * (G::P + 4);
+#pragma unroll
+          for(int d = 0; d < 4; d++)
+            o[d * G::A + pp] = part[d];
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host: pack weights into B-fragment order and launch.
+
+static uint16_t f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+// B fragment order for one conv: [kstep = tap*NCB + cb][coltile][lane][8],
+// element = W(co = ct*16 + (lane&15), cin = cb*32 + 8*(lane>>4) + j, tap).
+static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout,
+                     const std::function<float(int, int, int)>& W) {
+  const int ncb = cinPad / 32, nct = cout / 16;
+  for(int tap = 0; tap < ntaps; tap++)
+    for(int cb = 0; cb < ncb; cb++)
+      for(int ct = 0; ct < nct; ct++)
+        for(int l = 0; l < 64; l++)
+          for(int j = 0; j < 8; j++) {
+            int co = ct * 16 + (l & 15), ci = cb * 32 + 8 * (l >> 4) + j;
+            dst.push_back(f2bf(W(co, ci, tap)));
+          }
+}
+
+bool NNEngine::supported(const ModelCfg& c, int X, int Y) {
+  return X == 5 && Y == 5 && c.C == 96 && c.Cg == 32 && c.p1 == 32 && c.g1 == 32 && c.v1 == 32 && c.v2 <= 64 &&
+         c.cin == NUM_SPATIAL && c.gin == 1 && (int)c.kinds.size() <= NN_MAX_BLOCKS;
+}
+
+NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W) : cfg_(m.cfg), X_(X), Y_(Y), W_(W) {
+  if(!supported(m.cfg, X, Y))
+    throw std::invalid_argument("NNEngine: unsupported architecture/geometry (round 1 ships b6c96 @ 5x5)");
+  flops_ = modelFlopsPerEval(cfg_, X * Y);
+  const int C = cfg_.C, Cr = C - cfg_.Cg;
+  std::vector<uint16_t> wb;
+  std::vector<float> wf;
+  NNLayout& L = layout_;
+  memset(&L, 0, sizeof(L));
+  L.nblocks = (int)cfg_.kinds.size();
+  L.C = C; L.Cg = cfg_.Cg; L.p1 = cfg_.p1; L.g1 = cfg_.g1; L.v1 = cfg_.v1; L.v2 = cfg_.v2;
+  auto f32 = [&](const std::vector<float>& v) {
+    int off = (int)wf.size();
+    wf.insert(wf.end(), v.begin(), v.end());
+    while(wf.size() % 4)
+      wf.push_back(0.0f);
+    return off;
+  };
+  auto bfOff = [&]() { return (int)(wb.size() / 8); };
+  L.wInit = bfOff();
+  packConv(wb, 9, 32, C, [&](int co, int ci, int tap) {
+    return ci < cfg_.cin ? m.convInit[((size_t)co * cfg_.cin + ci) * 9 + tap] : 0.0f;
+  });
+  L.globInit = f32(m.globInit);
+  for(int i = 0; i < L.nblocks; i++) {
+    const ModelBlock& b = m.blocks[i];
+    L.kinds[i] = b.kind;
+    L.bn1s[i] = f32(b.bn1s);
+    L.bn1b[i] = f32(b.bn1b);
+    L.wConv1[i] = bfOff();
+    if(b.kind == 0) {
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv1[((size_t)co * C + ci) * 9 + tap]; });
+      L.bn2s[i] = f32(b.bn2s);
+      L.bn2b[i] = f32(b.bn2b);
+      L.wConv2[i] = bfOff();
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * C + ci) * 9 + tap]; });
+    } else {
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) {
+        return co < Cr ? b.conv1[((size_t)co * C + ci) * 9 + tap] : b.conv1g[((size_t)(co - Cr) * C + ci) * 9 + tap];
+      });
+      L.bngs[i] = f32(b.bngs);
+      L.bngb[i] = f32(b.bngb);
+      L.linG[i] = f32(b.linG);
+      L.bn2s[i] = f32(b.bn2s);
+      L.bn2b[i] = f32(b.bn2b);
+      L.wConv2[i] = bfOff();
+      packConv(wb, 9, Cr, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * Cr + ci) * 9 + tap]; });
+    }
+  }
+  L.tips = f32(m.tips);
+  L.tipb = f32(m.tipb);
+  L.wHead = bfOff();
+  packConv(wb, 1, C, C, [&](int co, int ci, int) {
+    if(co < 32)
+      return m.pConv1[(size_t)co * C + ci];
+    if(co < 64)
+      return m.pConvG[(size_t)(co - 32) * C + ci];
+    return m.vConv1[(size_t)(co - 64) * C + ci];
+  });
+  L.pBiasG = f32(m.pBiasG);
+  L.pLinG = f32(m.pLinG);
+  L.pBias2 = f32(m.pBias2);
+  L.pConv2 = f32(m.pConv2);
+  L.vBias1 = f32(m.vBias1);
+  L.vLin2 = f32(m.vLin2);
+  L.vB2 = f32(m.vB2);
+  L.vLin3 = f32(m.vLin3);
+  L.vB3 = f32(m.vB3);
+  L.vLinM = f32(m.vLinM);
+  L.vBM = f32(m.vBM);
+  KC_HIP(hipMalloc(&wBf16_, wb.size() * 2));
+  KC_HIP(hipMemcpy(wBf16_, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
+  KC_HIP(hipMalloc(&wF32_, wf.size() * 4));
+  KC_HIP(hipMemcpy(wF32_, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+  KC_HIP(hipMalloc(&layoutDev_, sizeof(NNLayout)));
+  KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
+  using G = NNGeo<5, 5, 96>;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+  });
+}
+
+NNEngine::~NNEngine() {
+  (void)hipFree(wBf16_);
+  (void)hipFree(wF32_);
+  (void)hipFree(layoutDev_);
+}
+
+void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev) {
+  if(n <= 0)
+    return;
+  using G = NNGeo<5, 5, 96>;
+  const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
+  int grid = (n + G::NB - 1) / G::NB;
+  hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(512), G::LDS, st, layoutDev_,
+                     (const bf16x8*)wBf16_, wF32_, n, countDev, inWords, (float)W_, in, out);
+  KC_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic stand-in network (oracle fakeNet).
+__global__ void __launch_bounds__(64) kFakeNet(const DTables* __restrict__ Tp, int n, const int* countDev,
+                                               const uint64_t* __restrict__ in, float* __restrict__ out) {
+  const DTables& T = *Tp;
+  const int count = countDev ? min(*countDev, n) : n;
+  int i = blockIdx.x;
+  if(i >= count)
+    return;
+  uint64_t h = 0x243f6a8885a308d3ULL;
+  for(int w = 0; w < T.inWords; w++)
+    h = mix64(h ^ in[(size_t)i * T.inWords + w]);
+  float* o = out + (size_t)i * (T.P + 4);
+  for(int j = threadIdx.x; j < T.P + 4; j += 64) {
+    uint64_t v = mix64(h + (uint64_t)j * 0x9e3779b97f4a7c15ULL);
+    int q = (int)((v >> 40) & 0xffffu);
+    float scale = j < T.P ? (1.0f / 8192.0f) : (1.0f / 16384.0f);
+    o[j] = ((float)q - 32768.0f) * scale;
+  }
+}
+
+void launchFakeNet(const DTables* T, int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev) {
+  if(n <= 0)
+    return;
+  hipLaunchKernelGGL(kFakeNet, dim3(n), dim3(64), 0, st, T, n, countDev, in, out);
+  KC_HIP(hipGetLastError());
+}
+
+}  // namespace kc

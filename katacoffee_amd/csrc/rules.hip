@@ -1,0 +1,127 @@
+// Batched Coffee rules and V1 encoder kernels (the C-ABI's coffee_rules_batch,
+// coffee_play_batch, coffee_encode_batch).  The self-play engine calls the same
+// device functions (kc_board.h) from its select/backup kernels.
+#include "engine.h"
+#include "kc_board.h"
+
+namespace kc {
+
+KC_D DBoard boardFromCells(const DTables& T, const uint8_t* cells, int lastCell, int lastDir, int pla,
+                           const int8_t* histCell, const int8_t* histDir) {
+  DBoard b;
+  boardInit(T, b);
+  for(int c = 0; c < T.A; c++) {
+    int col = cells[c];
+    if(col == 1 || col == 2) {
+      bbSet(b.stones[col - 1], c);
+      b.h0 ^= T.zBoard[c][col][0];
+      b.h1 ^= T.zBoard[c][col][1];
+    }
+  }
+  b.lastCell = (int8_t)lastCell;
+  b.lastDir = (int8_t)lastDir;
+  b.pla = (int8_t)pla;
+  for(int i = 0; i < HIST; i++) {
+    b.histCell[i] = histCell ? histCell[i] : (i == 0 ? (int8_t)lastCell : (int8_t)-1);
+    b.histDir[i] = histDir ? histDir[i] : (i == 0 ? (int8_t)lastDir : (int8_t)4);
+  }
+  return b;
+}
+
+// One wave per position; lanes enumerate the 4A moves (wave-ballot enumeration).
+__global__ void __launch_bounds__(64) kRulesBatch(const DTables* __restrict__ Tp, int n, const uint8_t* cells,
+                                                  const int8_t* lastCell, const int8_t* lastDir, const uint8_t* pla,
+                                                  uint8_t* legal, uint8_t* hasLegal) {
+  const DTables& T = *Tp;
+  int i = blockIdx.x;
+  if(i >= n)
+    return;
+  DBoard b = boardFromCells(T, cells + (size_t)i * T.A, lastCell[i], lastDir[i], pla[i], nullptr, nullptr);
+  bool any = false;
+  for(int pos = laneId(); pos < T.P; pos += 64) {
+    bool ok = (b.pla == 1 || b.pla == 2) && isLegal(T, b, pos % T.A, pos / T.A);
+    legal[(size_t)i * T.P + pos] = ok ? 1 : 0;
+    any = any || ok;
+  }
+  uint64_t m = ballot(any);
+  if(laneId() == 0)
+    hasLegal[i] = m != 0 ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(64) kPlayBatch(const DTables* __restrict__ Tp, int n, const uint8_t* cells,
+                                                 const int8_t* lastCell, const int8_t* lastDir, const uint8_t* pla,
+                                                 const int32_t* move, uint8_t* outCells, uint8_t* finished,
+                                                 uint8_t* winner, int32_t* maxRunOut, uint64_t* posHash,
+                                                 uint64_t* stHash) {
+  const DTables& T = *Tp;
+  int i = blockIdx.x;
+  if(i >= n)
+    return;
+  DBoard b = boardFromCells(T, cells + (size_t)i * T.A, lastCell[i], lastDir[i], pla[i], nullptr, nullptr);
+  int mv = move[i];
+  int cell = mv % T.A, dir = mv / T.A;
+  playMoveWave(T, b, cell, dir);
+  for(int c = laneId(); c < T.A; c += 64)
+    outCells[(size_t)i * T.A + c] = (uint8_t)colorAt(b, c);
+  if(laneId() == 0) {
+    finished[i] = (uint8_t)b.finished;
+    winner[i] = (uint8_t)b.winner;
+    maxRunOut[i] = maxRun(T, b, cell);
+    posHash[2 * i] = b.h0;
+    posHash[2 * i + 1] = b.h1;
+    uint64_t k0, k1;
+    stateHash(T, b, k0, k1);
+    stHash[2 * i] = k0;
+    stHash[2 * i + 1] = k1;
+  }
+}
+
+__global__ void __launch_bounds__(64) kEncodeBatch(const DTables* __restrict__ Tp, int n, const uint8_t* cells,
+                                                   const int8_t* histCell, const int8_t* histDir, const uint8_t* pla,
+                                                   const int32_t* sym, uint64_t* packed, float* planes) {
+  const DTables& T = *Tp;
+  int i = blockIdx.x;
+  if(i >= n)
+    return;
+  const int8_t* hc = histCell + (size_t)i * HIST;
+  const int8_t* hd = histDir + (size_t)i * HIST;
+  DBoard b = boardFromCells(T, cells + (size_t)i * T.A, hc[0], hd[0], pla[i], hc, hd);
+  uint64_t* out = packed + (size_t)i * T.inWords;
+  encodePackedWave(T, b, sym[i], out);
+  if(planes) {
+    __syncthreads();
+    for(int j = laneId(); j < NUM_SPATIAL * T.A; j += 64) {
+      uint64_t w = out[j >> 6];
+      planes[(size_t)i * NUM_SPATIAL * T.A + j] = ((w >> (j & 63)) & 1ULL) ? 1.0f : 0.0f;
+    }
+  }
+}
+
+void launchRulesBatch(const DTables* T, int n, const uint8_t* cells, const int8_t* lastCell, const int8_t* lastDir,
+                      const uint8_t* pla, uint8_t* legal, uint8_t* hasLegal, hipStream_t st) {
+  if(n <= 0)
+    return;
+  hipLaunchKernelGGL(kRulesBatch, dim3(n), dim3(64), 0, st, T, n, cells, lastCell, lastDir, pla, legal, hasLegal);
+  KC_HIP(hipGetLastError());
+}
+
+void launchPlayBatch(const DTables* T, int n, const uint8_t* cells, const int8_t* lastCell, const int8_t* lastDir,
+                     const uint8_t* pla, const int32_t* move, uint8_t* outCells, uint8_t* finished, uint8_t* winner,
+                     int32_t* maxRunOut, uint64_t* posHash, uint64_t* stHash, hipStream_t st) {
+  if(n <= 0)
+    return;
+  hipLaunchKernelGGL(kPlayBatch, dim3(n), dim3(64), 0, st, T, n, cells, lastCell, lastDir, pla, move, outCells,
+                     finished, winner, maxRunOut, posHash, stHash);
+  KC_HIP(hipGetLastError());
+}
+
+void launchEncodeBatch(const DTables* T, int n, const uint8_t* cells, const int8_t* histCell, const int8_t* histDir,
+                       const uint8_t* pla, const int32_t* sym, uint64_t* packed, float* planes, hipStream_t st) {
+  if(n <= 0)
+    return;
+  hipLaunchKernelGGL(kEncodeBatch, dim3(n), dim3(64), 0, st, T, n, cells, histCell, histDir, pla, sym, packed,
+                     planes);
+  KC_HIP(hipGetLastError());
+}
+
+}  // namespace kc

@@ -77,13 +77,15 @@ inline float kPowf(float x, float y) {
   return kExpf(y * kLogf(x));
 }
 
-// 64-lane xor butterfly over up to 128 values (lane l holds v[l] + v[l+64]).
+// 64-lane xor butterfly: lane l first accumulates v[l], v[l+64], v[l+128], ...
+// in order (lanes with l >= n start from +0), then xor-butterfly 32,16,..,1.
 inline float treeSum64(const float* v, int n) {
   float s[64];
   for(int l = 0; l < 64; l++) {
     float a = l < n ? v[l] : 0.0f;
-    float b = l + 64 < n ? v[l + 64] : 0.0f;
-    s[l] = a + b;
+    for(int j = l + 64; j < n; j += 64)
+      a = a + v[j];
+    s[l] = a;
   }
   for(int off = 32; off >= 1; off >>= 1) {
     float t[64];
@@ -122,11 +124,14 @@ struct Rng {
   // Rand::nextGamma, rand.cpp:335-363 (Marsaglia & Tsang), restated in f32.
   float gamma(float a) {
     if(a <= 1.0f) {
-      float r = gamma(a + 1.0f);
+      float r = gammaGt1(a + 1.0f);
       float inva = 1.0f / a;
       float u = uni();
       return r * kPowf(u, inva);
     }
+    return gammaGt1(a);
+  }
+  float gammaGt1(float a) {
     float d = a - 0.333333343f;
     float c = 0.333333343f / sqrtf(d);
     while(true) {
