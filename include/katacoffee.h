@@ -1,0 +1,203 @@
+/* katacoffee.h — C ABI of the MI355X Coffee self-play engine (libkatacoffee.so).
+ *
+ * This is the drop-in boundary of SURVEY.md §8(b): the in-process surface that
+ * replaces the reference's rules / encoder / NN-backend / self-play hot path.
+ * Every entry point:
+ *   - is extern "C", takes plain pointers and sizes, never throws;
+ *   - returns 0 on success and a negative COFFEE_E* code on failure, with the
+ *     message in coffee_last_error() (thread-local) — the reference reports the
+ *     same failures as C++ StringError exceptions (eigenbackend.cpp:1602-1605);
+ *   - takes DEVICE pointers for bulk data unless the parameter says "host",
+ *     and an optional hipStream_t (`stream`, NULL = the default stream).
+ * Handles are single-thread objects, like NeuralNet::ComputeHandle
+ * (nninterface.h:18-20) and Search (search.h:159-165); use one handle per GPU.
+ *
+ * Board geometry: X columns x Y rows, 2 <= X, Y <= 10; cell = y*X + x; A = X*Y.
+ * Move encoding ("pos"): pos = dir*A + cell, dir 0=N 1=W 2=NW 3=NE (board.h:41-47);
+ * P = 4A.  Colours: 0 empty, 1 black, 2 white.  Player 1 moves first.
+ * lastDir 4 = NONE (no previous move), lastCell -1 = none.
+ */
+#ifndef KATACOFFEE_H
+#define KATACOFFEE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COFFEE_OK 0
+#define COFFEE_EINVAL (-1)   /* bad argument / unsupported geometry or model */
+#define COFFEE_EHIP (-2)     /* HIP runtime error */
+#define COFFEE_EIO (-3)      /* file I/O or format error */
+#define COFFEE_EINTERNAL (-4)
+
+#define COFFEE_NUM_SPATIAL 15 /* V1 planes (README "V1", SPEC a6) */
+#define COFFEE_NUM_GLOBAL_TARGETS 64
+
+/* Last error message of the calling thread ("" if none). */
+const char* coffee_last_error(void);
+/* ABI version (major*100 + minor). */
+int coffee_abi_version(void);
+
+/* ---- device memory helpers (so callers need no HIP headers) ---- */
+int coffee_device_count(int* count);
+int coffee_set_device(int device);
+int coffee_malloc(void** dev_ptr, uint64_t bytes);
+int coffee_free(void* dev_ptr);
+/* kind: 0 host->device, 1 device->host, 2 device->device */
+int coffee_memcpy(void* dst, const void* src, uint64_t bytes, int kind);
+int coffee_synchronize(void);
+
+/* ---- rules (replaces Board::isLegal board.cpp:185-227,
+ *      Board::playMoveAssumeLegal board.cpp:427-435 + BoardHistory::makeBoardMoveAssumeLegal
+ *      boardhistory.cpp:157-176, Board::maxConsecutives board.cpp:315-335,
+ *      Board pos_hash board.cpp:134-178, GraphHash::getStateHash graphhash.cpp:3-34) ---- */
+
+/* n positions.  cells [n][A] u8 colours; last_cell/last_dir [n] int8; pla [n] u8.
+ * legal  [n][P] u8 (1 = legal move for pla)        (out)
+ * has_legal [n] u8 (0 = no legal move: SPEC B16 draw) (out) */
+int coffee_rules_batch(int x, int y, int win_len, int n, const uint8_t* cells, const int8_t* last_cell,
+                       const int8_t* last_dir, const uint8_t* pla, uint8_t* legal, uint8_t* has_legal, void* stream);
+
+/* Plays move[i] (pos, assumed legal) for pla[i].  Outputs:
+ * out_cells [n][A]; finished/winner [n] u8 (winner 0 = none/draw); max_run [n] i32
+ * (longest run through the move); pos_hash [n][2] u64 (Board::pos_hash after);
+ * state_hash [n][2] u64 (transposition key: pos_hash ^ next player ^ last move ^ game over). */
+int coffee_play_batch(int x, int y, int win_len, int n, const uint8_t* cells, const int8_t* last_cell,
+                      const int8_t* last_dir, const uint8_t* pla, const int32_t* move, uint8_t* out_cells,
+                      uint8_t* finished, uint8_t* winner, int32_t* max_run, uint64_t* pos_hash,
+                      uint64_t* state_hash, void* stream);
+
+/* ---- V1 encoder (replaces NNInputs::fillRowV1 nninputs.cpp:508-657 with SPEC a6,
+ *      symmetry SymmetryHelpers nninputs.cpp:252-433) ---- */
+
+/* hist_cell/hist_dir [n][5]: the last five moves, [0] most recent (-1 / 4 = none).
+ * sym [n] in 0..7 (bit0 flip y, bit1 flip x, bit2 transpose; transpose ignored when X != Y).
+ * packed [n][ceil(15A/64)] u64: bit i = plane*A + symcell      (out, required)
+ * planes [n][15][A] f32 (NCHW, symmetric frame)                  (out, optional: NULL)
+ * The global input is the single value win_len. */
+int coffee_encode_batch(int x, int y, int win_len, int n, const uint8_t* cells, const int8_t* hist_cell,
+                        const int8_t* hist_dir, const uint8_t* pla, const int32_t* sym, uint64_t* packed,
+                        float* planes, void* stream);
+
+/* ---- network (replaces the NeuralNet:: backend interface nninterface.h:31-171:
+ *      loadModelFile / createComputeHandle / getOutput / free*) ---- */
+
+typedef struct coffee_nn coffee_nn;
+
+/* Writes a seeded random-init CFNN model file ("b6c96", "b10c128", "b2c32"). */
+int coffee_model_write_random(const char* arch, uint64_t seed, const char* path /* host */);
+/* FLOPs per evaluation (2 x MACs) of a CFNN model at area A. */
+int coffee_model_flops(const char* path, int area, double* flops);
+
+/* Loads a CFNN model and prepares device weights for boards X x Y with win length W. */
+int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_nn** out);
+/* in: packed V1 rows [n][ceil(15A/64)] (coffee_encode_batch layout);
+ * out: [n][P+4] f32 = policy logits [4][A] (symmetric frame, dir-major), value logits
+ * (win, loss) from the side to move, misc[2].  bf16 MFMA arithmetic, f32 accumulate. */
+int coffee_nn_forward(coffee_nn* h, int n, const uint64_t* in, float* out, void* stream);
+int coffee_nn_destroy(coffee_nn* h);
+
+/* The deterministic stand-in network (oracle fakeNet), same I/O as coffee_nn_forward. */
+int coffee_fake_net(int x, int y, int win_len, int n, const uint64_t* in, float* out, void* stream);
+
+/* ---- self-play engine (replaces Play::runGame play.cpp:1146-1701 driving
+ *      Search::runWholeSearch search.cpp:361-509 and TrainingWriteBuffers
+ *      trainingwrite.cpp:316-565 for numGameThreads games) ---- */
+
+/* SearchParams (searchparams.h) restricted to Coffee self-play; defaults =
+ * cpp/configs/training/selfplay1.cfg with benchmark settings. */
+typedef struct coffee_search_params {
+  int32_t max_visits;
+  float cpuct_exploration, cpuct_exploration_log, cpuct_exploration_base;
+  float fpu_reduction_max, root_fpu_reduction_max, fpu_loss_prop, root_fpu_loss_prop;
+  int32_t fpu_parent_weight_by_visited_policy;
+  float fpu_parent_weight_by_visited_policy_pow;
+  float value_weight_exponent;
+  int32_t root_noise_enabled;
+  float root_dirichlet_noise_total_concentration, root_dirichlet_noise_weight;
+  float root_policy_temperature, root_policy_temperature_early;
+  float root_desired_per_child_visits_coeff;
+  int32_t root_num_symmetries_to_sample;
+  float chosen_move_temperature, chosen_move_temperature_early, chosen_move_temperature_halflife;
+  float chosen_move_subtract, chosen_move_prune;
+  int32_t use_lcb_for_selection;
+  float lcb_stdevs, min_visit_prop_for_lcb;
+  float subtree_value_bias_factor, subtree_value_bias_weight_exponent, subtree_value_bias_free_prop;
+  int32_t use_graph_search;
+} coffee_search_params;
+
+void coffee_search_params_default(coffee_search_params* p);
+
+typedef struct coffee_selfplay_config {
+  int32_t x, y, win_len;
+  int32_t num_games;     /* concurrent games on this device (numGameThreads) */
+  int32_t node_cap;      /* per-game node pool; 0 = max(2048, 3*max_visits) */
+  int32_t row_capacity;  /* device row buffer capacity; 0 = 4*num_games*A */
+  uint64_t seed;         /* run seed (gameSeedBase) */
+  int32_t slot_base;     /* global index of slot 0 (rank * num_games) */
+  int32_t use_fake_net;  /* 1 = coffee_fake_net instead of the model */
+  int32_t commit_interval; /* rounds between move-commit launches (0 = 8); 1 commits in
+                              the round the root reaches max_visits, like the oracle */
+  const char* model_path;/* CFNN model (host string), ignored with use_fake_net */
+  coffee_search_params search;
+} coffee_selfplay_config;
+
+typedef struct coffee_selfplay coffee_selfplay;
+
+typedef struct coffee_selfplay_stats {
+  uint64_t rounds;          /* select -> NN -> backup rounds run */
+  uint64_t playouts;        /* completed playouts (runSinglePlayout true) */
+  uint64_t nn_evals;        /* network rows evaluated */
+  uint64_t moves;           /* moves committed */
+  uint64_t games_finished;
+  uint64_t rows_written;    /* rows produced so far (drained + pending) */
+  uint64_t rows_pending;    /* rows on the device not yet drained */
+  uint64_t rows_dropped;    /* rows lost to a full row buffer (drain more often) */
+} coffee_selfplay_stats;
+
+int coffee_selfplay_create(const coffee_selfplay_config* cfg, coffee_selfplay** out);
+/* Runs `rounds` rounds (one playout or root evaluation per game per round) on `stream`
+ * (NULL = the engine's own stream).  Asynchronous: call coffee_selfplay_sync. */
+int coffee_selfplay_step(coffee_selfplay* h, int rounds, void* stream);
+int coffee_selfplay_sync(coffee_selfplay* h);
+int coffee_selfplay_stats_get(coffee_selfplay* h, coffee_selfplay_stats* out);
+
+/* Copies up to max_rows finished rows to HOST buffers and removes them from the device
+ * buffer (trainingwrite.cpp:185-205 shapes; 5x5: pb = ceil(A/8) = 4):
+ *   bin   [r][15][pb] u8   binaryInputNCHWPacked (big-endian bits, packBits :218-232)
+ *   glob  [r][1]   f32     globalInputNC
+ *   pol   [r][2][P] i16    policyTargetsNCMove
+ *   gtgt  [r][64]  f32     globalTargetsNC
+ *   value [r][5][A] i8     valueTargetsNCHW
+ *   meta  [r][4]   i32     (slot, game number, turn, num moves) — not part of the .npz
+ * Any output pointer may be NULL.  *n_out = rows copied. */
+int coffee_selfplay_drain_rows(coffee_selfplay* h, int max_rows, uint8_t* bin, float* glob, int16_t* pol,
+                               float* gtgt, int8_t* value, int32_t* meta, int* n_out);
+int coffee_selfplay_destroy(coffee_selfplay* h);
+
+/* Device-side inspection for parity tests and tools (host outputs). */
+/* info[16] i64: phase, rootK, nodeCount, rootIdx, gameNum, turn, pla, finished, winner,
+ *               playouts, nnEvals, moves, gamesFinished, lastCell, lastDir, rng counter */
+int coffee_selfplay_game_info(coffee_selfplay* h, int slot, int64_t* info);
+/* Canonical tree of one game: nodes in breadth-first order from the root following
+ * child slots in order (index-independent).  Per node 16 f32/u32 words, see DESIGN.md. */
+int coffee_selfplay_game_tree(coffee_selfplay* h, int slot, int max_nodes, uint32_t* nodes, uint32_t* edges,
+                              int* n_nodes);
+/* The root's noised policy [P] (after temperature + Dirichlet). */
+int coffee_selfplay_root_policy(coffee_selfplay* h, int slot, float* out);
+
+/* Debug: the Student-t(3) CDF table the search uses (2000 f32). */
+int coffee_debug_cdf_table(int x, int y, int win_len, float* out /* host */);
+
+/* Kernel timing (HIP events on the engine stream) for roofline reporting:
+ * which: 0 select, 1 network, 2 backup, 3 commit.  Summed ms and launch count. */
+int coffee_selfplay_enable_timing(coffee_selfplay* h, int enable);
+int coffee_selfplay_kernel_time(coffee_selfplay* h, int which, double* ms, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KATACOFFEE_H */

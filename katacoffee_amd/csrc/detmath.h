@@ -116,7 +116,6 @@ struct DRng {
   }
 };
 
-#if defined(__HIP_DEVICE_COMPILE__)
 KC_D int laneId() { return (int)(threadIdx.x & 63); }
 
 // treeSum64 (oracle/ora_math.h): the lane's in-order partial, then xor butterfly.
@@ -151,6 +150,5 @@ KC_D void waveArgmax(float& v, int& idx) {
   }
 }
 KC_D uint64_t ballot(bool b) { return __ballot(b); }
-#endif
 
 }  // namespace kc

@@ -11,6 +11,21 @@
 
 namespace kc {
 
+// ADJS (board.cpp:82-85) as steps: N (0,-1), W (-1,0), NW (-1,-1), NE (1,-1).
+KC_HD int dirDx(int d) { return d == 0 ? 0 : (d == 3 ? 1 : -1); }
+KC_HD int dirDy(int d) { return d == 1 ? 0 : -1; }
+
+// Stones of one colour, chosen by an opaque mask rather than by indexing
+// stones[]: an index (or a select the optimizer turns into one) would force
+// the whole board out of registers into scratch memory.
+KC_HD BB stonesOf(const DBoard& b, bool white) {
+  uint64_t m = white ? ~0ULL : 0ULL;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(m));
+#endif
+  return BB{(b.stones[0].lo & ~m) | (b.stones[1].lo & m), (b.stones[0].hi & ~m) | (b.stones[1].hi & m)};
+}
+
 KC_HD BB occupied(const DBoard& b) { return bbOr(b.stones[0], b.stones[1]); }
 KC_HD int colorAt(const DBoard& b, int c) {
   return bbTest(b.stones[0], c) ? 1 : (bbTest(b.stones[1], c) ? 2 : 0);
@@ -27,17 +42,16 @@ KC_HD bool isLegal(const DTables& T, const DBoard& b, int cell, int dir) {
 
 KC_HD int maxRun(const DTables& T, const DBoard& b, int cell) {
   const int X = T.X, Y = T.Y;
-  const BB& own = b.stones[colorAt(b, cell) == 2 ? 1 : 0];
-  const int dxs[4] = {0, -1, -1, 1}, dys[4] = {-1, 0, -1, -1};
+  const BB own = stonesOf(b, colorAt(b, cell) == 2);
   int x = cell % X, y = cell / X, best = 1;
   for(int d = 0; d < 4; d++) {
     int n = 1;
     for(int s = -1; s <= 1; s += 2) {
-      int cx = x + s * dxs[d], cy = y + s * dys[d];
+      int cx = x + s * dirDx(d), cy = y + s * dirDy(d);
       while(cx >= 0 && cx < X && cy >= 0 && cy < Y && bbTest(own, cy * X + cx)) {
         n++;
-        cx += s * dxs[d];
-        cy += s * dys[d];
+        cx += s * dirDx(d);
+        cy += s * dirDy(d);
       }
     }
     best = n > best ? n : best;
@@ -50,15 +64,14 @@ KC_HD int runAlong(const DTables& T, const DBoard& b, int cell, int d) {
   int col = colorAt(b, cell);
   if(col == 0)
     return 0;
-  const BB& own = b.stones[col - 1];
-  const int dxs[4] = {0, -1, -1, 1}, dys[4] = {-1, 0, -1, -1};
+  const BB own = stonesOf(b, col == 2);
   int x = cell % T.X, y = cell / T.X, n = 1;
   for(int s = -1; s <= 1; s += 2) {
-    int cx = x + s * dxs[d], cy = y + s * dys[d];
+    int cx = x + s * dirDx(d), cy = y + s * dirDy(d);
     while(cx >= 0 && cx < T.X && cy >= 0 && cy < T.Y && bbTest(own, cy * T.X + cx)) {
       n++;
-      cx += s * dxs[d];
-      cy += s * dys[d];
+      cx += s * dirDx(d);
+      cy += s * dirDy(d);
     }
   }
   return n;
@@ -74,32 +87,26 @@ KC_HD void boardInit(const DTables& T, DBoard& b) {
   b.pla = 1;
   b.finished = 0;
   b.winner = 0;
-  b.pad0 = 0;
   b.turn = 0;
-  for(int i = 0; i < HIST; i++) {
-    b.histCell[i] = -1;
-    b.histDir[i] = 4;
-  }
-  for(int i = 0; i < 6; i++)
-    b.pad1[i] = 0;
+  b.histC = 0xFFFFFFFFFFULL;  // five "none" cells
+  b.histD = 0x0404040404ULL;
 }
 
 // State part of playMove (everything except the end-of-game test).
 KC_HD void applyMove(const DTables& T, DBoard& b, int cell, int dir) {
   int pla = b.pla;
-  bbSet(b.stones[pla - 1], cell);
+  if(pla == 2)
+    bbSet(b.stones[1], cell);
+  else
+    bbSet(b.stones[0], cell);
   b.h0 ^= T.zBoard[cell][pla][0];
   b.h1 ^= T.zBoard[cell][pla][1];
-  b.lastCell = (int8_t)cell;
-  b.lastDir = (int8_t)dir;
-  for(int i = HIST - 1; i > 0; i--) {
-    b.histCell[i] = b.histCell[i - 1];
-    b.histDir[i] = b.histDir[i - 1];
-  }
-  b.histCell[0] = (int8_t)cell;
-  b.histDir[0] = (int8_t)dir;
+  b.lastCell = cell;
+  b.lastDir = dir;
+  b.histC = ((b.histC << 8) | (uint64_t)(uint8_t)cell) & 0xFFFFFFFFFFULL;
+  b.histD = ((b.histD << 8) | (uint64_t)(uint8_t)dir) & 0xFFFFFFFFFFULL;
   b.turn++;
-  b.pla = (int8_t)(3 - pla);
+  b.pla = 3 - pla;
   b.finished = 0;
   b.winner = 0;
 }
@@ -118,7 +125,7 @@ KC_HD void playMoveSerial(const DTables& T, DBoard& b, int cell, int dir) {
   applyMove(T, b, cell, dir);
   if(maxRun(T, b, cell) >= T.W) {
     b.finished = 1;
-    b.winner = (int8_t)mover;
+    b.winner = mover;
   } else if(!hasAnyLegalSerial(T, b)) {
     b.finished = 1;
     b.winner = 0;
@@ -139,7 +146,6 @@ KC_HD void stateHash(const DTables& T, const DBoard& b, uint64_t& k0, uint64_t& 
   }
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
 // Wave-cooperative: every lane calls with the same board; result is uniform.
 KC_D bool hasAnyLegalWave(const DTables& T, const DBoard& b) {
   bool any = false;
@@ -153,7 +159,7 @@ KC_D void playMoveWave(const DTables& T, DBoard& b, int cell, int dir) {
   applyMove(T, b, cell, dir);
   if(maxRun(T, b, cell) >= T.W) {
     b.finished = 1;
-    b.winner = (int8_t)mover;
+    b.winner = mover;
   } else if(!hasAnyLegalWave(T, b)) {
     b.finished = 1;
     b.winner = 0;
@@ -169,9 +175,11 @@ KC_D bool v1Bit(const DTables& T, const DBoard& b, int plane, int c, int sym) {
     case 1: return colorAt(b, c) == pla;
     case 2: return colorAt(b, c) == 3 - pla;
     case 3: case 4: case 5: case 6:
-      return b.histCell[0] == c && T.symDir[sym][b.histDir[0]] == plane - 3;
-    case 7: case 8: case 9: case 10:
-      return b.histCell[plane - 6] == c;
+      return hCell(b, 0) == c && T.symDir[sym][hDir(b, 0)] == plane - 3;
+    case 7: return hCell(b, 1) == c;
+    case 8: return hCell(b, 2) == c;
+    case 9: return hCell(b, 3) == c;
+    case 10: return hCell(b, 4) == c;
     case 11: {
       for(int d = 0; d < 4; d++)
         if(isLegal(T, b, c, d))
@@ -208,6 +216,5 @@ KC_D void encodePackedWave(const DTables& T, const DBoard& b, int sym, uint64_t*
       out[w] = word;
   }
 }
-#endif
 
 }  // namespace kc

@@ -51,21 +51,22 @@ KC_HD BB bbAndNot(const BB& a, const BB& b) { return BB{a.lo & ~b.lo, a.hi & ~b.
 KC_HD bool bbAny(const BB& a) { return (a.lo | a.hi) != 0; }
 
 // Coffee position (board.h:112-228 + the BoardHistory fields the hot path reads).
+// Plain scalar fields only (no small arrays), so boards stay in registers.
 struct DBoard {
   BB stones[2];          // [0] black, [1] white
   uint64_t h0, h1;       // Board::pos_hash
-  int8_t lastCell;       // -1 none
-  int8_t lastDir;        // 0 N, 1 W, 2 NW, 3 NE, 4 NONE
-  int8_t pla;            // 1 black, 2 white (to move)
-  int8_t finished;       // BoardHistory::isGameFinished
-  int8_t winner;         // 0 none/draw
-  int8_t pad0;
-  int16_t turn;
-  int8_t histCell[HIST]; // [0] = last move
-  int8_t histDir[HIST];
-  int8_t pad1[6];
+  uint64_t histC;        // last five move cells, byte i = i-th most recent (0xFF none)
+  uint64_t histD;        // their directions, byte i (4 = none)
+  int32_t lastCell;      // -1 none
+  int32_t lastDir;       // 0 N, 1 W, 2 NW, 3 NE, 4 NONE
+  int32_t pla;           // 1 black, 2 white (to move)
+  int32_t finished;      // BoardHistory::isGameFinished
+  int32_t winner;        // 0 none/draw
+  int32_t turn;
 };
-static_assert(sizeof(DBoard) == 72, "DBoard layout");
+static_assert(sizeof(DBoard) == 88, "DBoard layout");
+KC_HD int hCell(const DBoard& b, int i) { return (int)(int8_t)(uint8_t)(b.histC >> (8 * i)); }
+KC_HD int hDir(const DBoard& b, int i) { return (int)(uint8_t)(b.histD >> (8 * i)); }
 
 // Device-resident lookup tables for one board geometry (built by tables.cpp).
 struct DTables {

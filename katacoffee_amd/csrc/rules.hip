@@ -13,18 +13,27 @@ KC_D DBoard boardFromCells(const DTables& T, const uint8_t* cells, int lastCell,
   for(int c = 0; c < T.A; c++) {
     int col = cells[c];
     if(col == 1 || col == 2) {
-      bbSet(b.stones[col - 1], c);
+      if(col == 2)
+        bbSet(b.stones[1], c);
+      else
+        bbSet(b.stones[0], c);
       b.h0 ^= T.zBoard[c][col][0];
       b.h1 ^= T.zBoard[c][col][1];
     }
   }
-  b.lastCell = (int8_t)lastCell;
-  b.lastDir = (int8_t)lastDir;
-  b.pla = (int8_t)pla;
-  for(int i = 0; i < HIST; i++) {
-    b.histCell[i] = histCell ? histCell[i] : (i == 0 ? (int8_t)lastCell : (int8_t)-1);
-    b.histDir[i] = histDir ? histDir[i] : (i == 0 ? (int8_t)lastDir : (int8_t)4);
+  b.lastCell = lastCell;
+  b.lastDir = lastDir;
+  b.pla = pla;
+  uint64_t hc = 0, hd = 0;
+#pragma unroll
+  for(int i = HIST - 1; i >= 0; i--) {
+    int c = histCell ? histCell[i] : (i == 0 ? lastCell : -1);
+    int d = histDir ? histDir[i] : (i == 0 ? lastDir : 4);
+    hc = (hc << 8) | (uint64_t)(uint8_t)c;
+    hd = (hd << 8) | (uint64_t)(uint8_t)d;
   }
+  b.histC = hc;
+  b.histD = hd;
   return b;
 }
 

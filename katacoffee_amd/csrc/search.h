@@ -1,0 +1,143 @@
+// Device-resident self-play state: one wave (64 lanes) owns one game.
+//
+// Layout in HBM (DESIGN.md "Data layout"), every array indexed by game slot g:
+//   GameDev   games[G]                         per-game scalars (boards, RNG, phase, counters)
+//   Node      nodes[G][cap]                    64-B statistics record per search node
+//   Edge      edges[G][cap][P]                 (child, edgeVisits) per child slot, slots in
+//   uint16_t  emove[G][cap][P]                 expansion order (SearchChildPointer, searchnode.h)
+//   float     policy[G][cap][P]                NN policy of the node (NNOutput::policyProbs)
+//   uint32_t  freeList[G][cap], allocBits[G][cap/32]   node allocator
+//   TT        ttKey[G][ttCap][2], ttNode[G][ttCap]     transposition table (searchnodetable.h)
+//   SVB       svbKey/svbD/svbW[G][2][svbCap]           subtree value bias tables (double buffered)
+//   float     accPolicy/rawPolicy/rootNoised[G][P]     root symmetry accumulation / noised prior
+//   int32     pathNode/pathSlot[G][MAX_DEPTH]          the current playout's path
+//   TurnRec   turns[G][maxTurns], int16 turnPol[G][maxTurns][P]  per-move records for rows
+// Node indices are an allocator detail: results depend only on child-slot order,
+// which is the reference's expansion order.
+#pragma once
+#include "kc_common.h"
+
+namespace kc {
+
+constexpr int MAX_DEPTH = MAX_AREA + 2;
+constexpr int MAX_LANE_ITEMS = (MAX_P + 63) / 64;  // 7
+
+enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2 };
+
+// SearchParams (searchparams.h) restricted to Coffee self-play.
+struct SP {
+  int maxVisits;
+  float cpuct, cpuctLog, cpuctBase;
+  float fpuRedMax, rootFpuRedMax, fpuLossProp, rootFpuLossProp;
+  int fpuByVisited;
+  float fpuByVisitedPow;
+  float valueWeightExp;
+  int rootNoise;
+  float dirConc, dirWeight;
+  float rootTemp, rootTempEarly;
+  float rootDesiredCoeff;
+  int rootSyms;
+  float moveTemp, moveTempEarly, moveTempHalflife;
+  float moveSubtract, movePrune;
+  int useLcb;
+  float lcbStdevs, minVisitPropLcb;
+  float svbFactor, svbExp, svbFreeProp;
+  int useGraph;
+};
+
+struct Node {
+  uint32_t visits;
+  float weightSum, weightSqSum, utilityAvg, utilitySqAvg, winLossAvg;
+  float nnWin, nnLoss;            // white-perspective NN probabilities
+  float lastSvbDelta, lastSvbWeight;
+  int32_t svbEntry;               // slot in the current SVB table, -1 none
+  uint16_t numChildren;
+  uint8_t nextPla;
+  uint8_t flags;                  // 1 expanded (NN output stored), 2 terminal
+  uint64_t key0, key1;            // transposition key
+};
+static_assert(sizeof(Node) == 64, "Node layout");
+
+struct Edge {
+  uint32_t child, visits;
+};
+
+struct TurnRec {
+  float whiteWin, whiteLoss, rawWhiteWL, rawPolicyEntropy;
+  float policySurprise, policyEntropy, searchEntropy;
+  uint32_t visits;
+  int8_t cell, dir;
+  int8_t pad[6];
+};
+static_assert(sizeof(TurnRec) == 40, "TurnRec layout");
+
+struct GameDev {
+  DBoard root;
+  DBoard leaf;
+  uint64_t rngSeed, rngCtr;
+  uint64_t gameHash0, gameHash1;
+  uint64_t playouts, nnEvals, moves, gamesFinished;
+  int32_t phase, rootK;
+  uint32_t syms;                  // four root symmetries, 4 bits each
+  int32_t pad0, pad1, pad2;
+  int32_t leafKind, leafNode, leafSym, nnSlot;
+  int32_t rootIdx, liveCount, freeTop, pathLen;
+  int32_t gameNum, numTurns, svbSel, err;
+  float accWin, accLoss, rawWin, rawLoss;
+};
+
+struct SearchDev {
+  const DTables* T;
+  SP sp;
+  int G, cap, ttCap, svbCap, P, A, inWords, maxTurns;
+  int rowCap, slotBase;
+  uint64_t seed;
+  GameDev* games;
+  Node* nodes;
+  Edge* edges;
+  uint16_t* emove;
+  float* policy;
+  uint32_t* freeList;
+  uint32_t* allocBits;
+  uint64_t* ttKey;
+  int32_t* ttNode;
+  uint64_t* svbKey;
+  int64_t* svbD;
+  int64_t* svbW;
+  float* accPolicy;
+  float* rawPolicy;
+  float* rootNoised;
+  int32_t* pathNode;
+  int32_t* pathSlot;
+  TurnRec* turns;
+  int16_t* turnPol;
+  // network batch
+  uint64_t* nnIn;        // [G][inWords]
+  float* nnOut;          // [G][P+4]
+  int32_t* nnCount;      // rows in this round's batch
+  // commit queue
+  int32_t* commitList;   // [G]
+  int32_t* commitCount;
+  // rows
+  uint8_t* rBin;         // [rowCap][15][pb]
+  float* rGlob;          // [rowCap]
+  int16_t* rPol;         // [rowCap][2][P]
+  float* rGt;            // [rowCap][64]
+  int8_t* rVal;          // [rowCap][5][A]
+  int32_t* rMeta;        // [rowCap][4]
+  unsigned long long* rCount;
+  unsigned long long* rDropped;
+};
+
+// Kernel launchers (search.hip).
+void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchGameTree(const SearchDev* dd, int slot, int maxNodes, uint32_t* nodesOut, uint32_t* edgesOut,
+                    int32_t* count, hipStream_t st);
+// Dynamic LDS bytes the commit kernel needs for node_cap `cap`.
+size_t commitLdsBytes(int cap);
+
+}  // namespace kc

@@ -1,0 +1,1800 @@
+// Batched KataGo MCTS for Coffee: one wave (64 lanes) per game, thousands of games
+// per launch.  A self-play round is three launches on one stream:
+//   kSelect  — root-symmetry evaluation or one PUCT descent per game, leaf encoded
+//              straight into the network batch (search.cpp:920-1165);
+//   network  — fused residual net (nn.hip) or the stand-in net over the batch;
+//   kBackup  — NN post-processing, leaf value and path backup (searchupdatehelpers.cpp);
+// and every few rounds kCommit plays the chosen move for the games whose root reached
+// maxVisits, reuses the subtree and writes finished games' training rows.
+//
+// Semantics are the oracle's (oracle/ora_search.cpp), which cites the reference
+// lines; each function below names its oracle counterpart.  Every float result
+// is reproduced bit-for-bit: reductions over children use waveSum (the treeSum64
+// order), sequential sums run on lane 0 in the oracle's order, transcendental
+// functions are detmath.h's dlog/dexp/dpow, and the file is compiled with
+// -ffp-contract=off and correctly rounded division/sqrt.
+#include <hip/hip_runtime.h>
+
+#include "detmath.h"
+#include "engine.h"
+#include "kc_board.h"
+#include "search.h"
+
+namespace kc {
+
+static constexpr int SVB_IDX_MOVE1 = MAX_P + 1;
+static constexpr int SVB_IDX_PLA = 2 * (MAX_P + 1);
+static constexpr int SVB_IDX_PAT = 2 * (MAX_P + 1) + 3;
+static constexpr int BIG = 0x7fffffff;
+
+KC_D int64_t svbQ(float x) { return llrintf(x * 4294967296.0f); }
+KC_D float svbF(int64_t v) { return (float)v * (1.0f / 4294967296.0f); }
+
+KC_D void waveSync() { __syncthreads(); }  // blocks are one wave: barrier + memory fence
+
+// Per-game view of the SoA arrays.
+struct GV {
+  const SearchDev& d;
+  const DTables& T;
+  int g, lane;
+  KC_D GV(const SearchDev& d_, int g_) : d(d_), T(*d_.T), g(g_), lane(laneId()) {}
+  KC_D Node* nodes() const { return d.nodes + (size_t)g * d.cap; }
+  KC_D Edge* edges(int n) const { return d.edges + ((size_t)g * d.cap + n) * d.P; }
+  KC_D uint16_t* emove(int n) const { return d.emove + ((size_t)g * d.cap + n) * d.P; }
+  KC_D float* pol(int n) const { return d.policy + ((size_t)g * d.cap + n) * d.P; }
+  KC_D uint32_t* freeList() const { return d.freeList + (size_t)g * d.cap; }
+  KC_D uint32_t* allocBits() const { return d.allocBits + (size_t)g * (d.cap / 32); }
+  KC_D uint64_t* ttKey() const { return d.ttKey + (size_t)g * d.ttCap * 2; }
+  KC_D int32_t* ttNode() const { return d.ttNode + (size_t)g * d.ttCap; }
+  KC_D size_t svbBase(int sel) const { return ((size_t)g * 2 + sel) * d.svbCap; }
+  KC_D float* accPolicy() const { return d.accPolicy + (size_t)g * d.P; }
+  KC_D float* rawPolicy() const { return d.rawPolicy + (size_t)g * d.P; }
+  KC_D float* rootNoised() const { return d.rootNoised + (size_t)g * d.P; }
+  KC_D int32_t* pathNode() const { return d.pathNode + (size_t)g * MAX_DEPTH; }
+  KC_D int32_t* pathSlot() const { return d.pathSlot + (size_t)g * MAX_DEPTH; }
+  KC_D TurnRec* turns() const { return d.turns + (size_t)g * d.maxTurns; }
+  KC_D int16_t* turnPol(int t) const { return d.turnPol + ((size_t)g * d.maxTurns + t) * d.P; }
+};
+
+// Uniform state of one game, held identically by every lane; lane 0 stores.
+struct GS {
+  GameDev s;
+  KC_D DRng rng() const { return DRng{s.rngSeed, s.rngCtr}; }
+};
+
+KC_D void storeGame(const GV& v, const GameDev& s) {
+  if(v.lane == 0)
+    v.d.games[v.g] = s;
+}
+
+KC_D void loadGame(const GV& v, GameDev& s) { s = v.d.games[v.g]; }
+
+template <int NI>
+KC_D float tsum(const float (&x)[NI], int n, int lane) {
+  float a = 0.0f;
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int i = lane + 64 * j;
+    if(i < n)
+      a = j == 0 ? x[j] : a + x[j];
+  }
+  return waveSum(a);
+}
+
+KC_D int bcastI(int v, int srcLane) { return __shfl(v, srcLane, 64); }
+KC_D int firstLane(uint64_t m) { return __builtin_ctzll(m); }
+
+KC_D float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeight) {
+  return rawWeight * ((float)edgeVisits / (float)(childVisits > 1u ? childVisits : 1u));
+}
+
+// ---------------------------------------------------------------------------
+// Transposition table (oracle ttFind / ttInsert): linear probing, 64 slots per step.
+KC_D int ttFind(const GV& v, uint64_t k0, uint64_t k1) {
+  const int mask = v.d.ttCap - 1;
+  const int start = (int)(k0 & (uint64_t)mask);
+  const uint64_t* key = v.ttKey();
+  const int32_t* node = v.ttNode();
+  for(int base = 0; base < v.d.ttCap; base += 64) {
+    int s = (start + base + v.lane) & mask;
+    int nd = node[s];
+    bool match = nd >= 0 && key[2 * s] == k0 && key[2 * s + 1] == k1;
+    uint64_t m = ballot(nd < 0 || match);
+    if(m) {
+      int f = firstLane(m);
+      return bcastI(match ? nd : -1, f);
+    }
+  }
+  return -1;
+}
+
+KC_D void ttInsert(const GV& v, uint64_t k0, uint64_t k1, int nodeIdx) {
+  const int mask = v.d.ttCap - 1;
+  const int start = (int)(k0 & (uint64_t)mask);
+  uint64_t* key = v.ttKey();
+  int32_t* node = v.ttNode();
+  for(int base = 0; base < v.d.ttCap; base += 64) {
+    int s = (start + base + v.lane) & mask;
+    uint64_t m = ballot(node[s] < 0);
+    if(m) {
+      if(v.lane == firstLane(m)) {
+        key[2 * s] = k0;
+        key[2 * s + 1] = k1;
+        node[s] = nodeIdx;
+      }
+      return;
+    }
+  }
+}
+
+// SVB table (oracle svbFindOrInsert), key 0 = empty.
+KC_D int svbFindOrInsert(const GV& v, int sel, uint64_t k) {
+  const int mask = v.d.svbCap - 1;
+  const size_t b = v.svbBase(sel);
+  const int start = (int)(k & (uint64_t)mask);
+  for(int base = 0; base < v.d.svbCap; base += 64) {
+    int s = (start + base + v.lane) & mask;
+    uint64_t kk = v.d.svbKey[b + s];
+    uint64_t m = ballot(kk == 0 || kk == k);
+    if(m) {
+      int f = firstLane(m);
+      int slot = bcastI(s, f);
+      bool empty = __shfl((int)(kk == 0), f, 64) != 0;
+      if(empty && v.lane == f) {
+        v.d.svbKey[b + slot] = k;
+        v.d.svbD[b + slot] = 0;
+        v.d.svbW[b + slot] = 0;
+      }
+      return slot;
+    }
+  }
+  return -1;
+}
+
+// SPEC a19 key (oracle svbKey): Zmove0[parentPrev] ^ Zmove1[move] ^ Zpla[mover] ^ 5x5 pattern.
+KC_D uint64_t svbKeyOf(const GV& v, const DBoard& before, int parentPrevPos, int movePos, int mover) {
+  const DTables& T = v.T;
+  uint64_t h = 0;
+  if(v.lane < 25) {
+    int wy = v.lane / 5, wx = v.lane % 5;
+    int cell = movePos % T.A;
+    int xx = cell % T.X + wx - 2, yy = cell / T.X + wy - 2;
+    int col = (xx >= 0 && xx < T.X && yy >= 0 && yy < T.Y) ? colorAt(before, yy * T.X + xx) : 3;
+    h = T.svbZ[SVB_IDX_PAT + col * 25 + wy * 5 + wx];
+  }
+#pragma unroll
+  for(int off = 32; off >= 1; off >>= 1) {
+    uint32_t lo = __shfl_xor((uint32_t)h, off, 64), hi = __shfl_xor((uint32_t)(h >> 32), off, 64);
+    h ^= ((uint64_t)hi << 32) | lo;
+  }
+  h ^= T.svbZ[parentPrevPos] ^ T.svbZ[SVB_IDX_MOVE1 + movePos] ^ T.svbZ[SVB_IDX_PLA + mover];
+  return h != 0 ? h : 1;
+}
+
+KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k1, bool terminal) {
+  if(s.freeTop <= 0) {
+    s.err = 1;
+    return -1;
+  }
+  s.freeTop--;
+  int idx = (int)v.freeList()[s.freeTop];
+  if(v.lane == 0) {
+    Node n;
+    n.visits = 0;
+    n.weightSum = n.weightSqSum = n.utilityAvg = n.utilitySqAvg = n.winLossAvg = 0.0f;
+    n.nnWin = n.nnLoss = n.lastSvbDelta = n.lastSvbWeight = 0.0f;
+    n.svbEntry = -1;
+    n.numChildren = 0;
+    n.nextPla = (uint8_t)nextPla;
+    n.flags = terminal ? 2 : 0;
+    n.key0 = k0;
+    n.key1 = k1;
+    v.nodes()[idx] = n;
+    atomicOr(&v.allocBits()[idx >> 5], 1u << (idx & 31));
+  }
+  s.liveCount++;
+  return idx;
+}
+
+// ---------------------------------------------------------------------------
+// oracle addLeafValue (searchupdatehelpers.cpp:12-82)
+KC_D void addLeafValue(const GV& v, const GameDev& s, int ni, float wl, bool isTerminal, bool assumeNoExisting) {
+  const SP& sp = v.d.sp;
+  Node* np = &v.nodes()[ni];
+  const int svbEntry = np->svbEntry;
+  uint32_t visits = np->visits;
+  float weightSum = np->weightSum, weightSqSum = np->weightSqSum;
+  float utilityAvg = np->utilityAvg, utilitySqAvg = np->utilitySqAvg, winLossAvg = np->winLossAvg;
+  float utility = wl;
+  if(sp.svbFactor != 0.0f && !isTerminal && svbEntry >= 0) {
+    size_t e = v.svbBase(s.svbSel) + svbEntry;
+    float dd = svbF(v.d.svbD[e]), ww = svbF(v.d.svbW[e]);
+    if(ww > 0.001f)
+      utility = utility + (sp.svbFactor * dd) / ww;
+  }
+  float usq = utility * utility;
+  if(assumeNoExisting) {
+    winLossAvg = wl;
+    utilityAvg = utility;
+    utilitySqAvg = usq;
+    weightSqSum = 1.0f;
+    weightSum = 1.0f;
+    visits += 1;
+  } else {
+    float oldW = weightSum, newW = oldW + 1.0f;
+    winLossAvg = (winLossAvg * oldW + wl) / newW;
+    utilityAvg = (utilityAvg * oldW + utility) / newW;
+    utilitySqAvg = (utilitySqAvg * oldW + usq) / newW;
+    weightSqSum = weightSqSum + 1.0f;
+    weightSum = newW;
+    visits += 1;
+  }
+  waveSync();
+  if(v.lane == 0) {
+    np->visits = visits;
+    np->weightSum = weightSum;
+    np->weightSqSum = weightSqSum;
+    np->utilityAvg = utilityAvg;
+    np->utilitySqAvg = utilitySqAvg;
+    np->winLossAvg = winLossAvg;
+  }
+  waveSync();
+}
+
+KC_D float cdfT(const DTables& T, float z) {
+  float dd = (1999.0f * (z - (-50.0f))) / 100.0f;
+  if(dd <= 0.0f)
+    return 0.0f;
+  int idx = (int)dd;
+  if(idx >= 1999)
+    return 1.0f;
+  float lambda = dd - (float)idx;
+  float y0 = T.cdf[idx], y1 = T.cdf[idx + 1];
+  return y0 + lambda * (y1 - y0);
+}
+
+// oracle recompute (recomputeNodeStats searchupdatehelpers.cpp:151-328 +
+// downweightBadChildrenAndNormalizeWeight :330-419)
+template <int NI>
+KC_D void recompute(const GV& v, const GameDev& s, int ni, int numVisitsToAdd, bool isRoot) {
+  const SP& sp = v.d.sp;
+  Node* np = &v.nodes()[ni];
+  const int k = np->numChildren;
+  const int nextPla = np->nextPla;
+  const int svbEntry = np->svbEntry;
+  const float nnWin = np->nnWin, nnLoss = np->nnLoss;
+  const float lastSvbDelta = np->lastSvbDelta, lastSvbWeight = np->lastSvbWeight;
+  const uint32_t visits0 = np->visits;
+  const Edge* E = v.edges(ni);
+  const Node* NS = v.nodes();
+  bool good[NI];
+  float wAdj[NI], selfU[NI], cU[NI], cUsq[NI], cWl[NI], cWs[NI], cWsq[NI], tmp[NI];
+  int numGood = 0;
+  float maxW = 0.0f;
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int i = v.lane + 64 * j;
+    good[j] = false;
+    wAdj[j] = selfU[j] = cU[j] = cUsq[j] = cWl[j] = cWs[j] = cWsq[j] = 0.0f;
+    if(i < k) {
+      Edge e = E[i];
+      const Node& c = NS[e.child];
+      uint32_t cv = c.visits;
+      float ws = c.weightSum;
+      good[j] = cv > 0 && ws > 0.0f && e.visits > 0;
+      if(good[j]) {
+        cU[j] = c.utilityAvg;
+        cUsq[j] = c.utilitySqAvg;
+        cWl[j] = c.winLossAvg;
+        cWs[j] = ws;
+        cWsq[j] = c.weightSqSum;
+        selfU[j] = nextPla == 2 ? cU[j] : -cU[j];
+        wAdj[j] = childWeight(e.visits, cv, ws);
+        maxW = wAdj[j] > maxW ? wAdj[j] : maxW;
+      }
+    }
+    numGood += __popcll(ballot(good[j]));
+  }
+  maxW = waveMax(maxW);
+  const float origTotal = tsum<NI>(wAdj, k, v.lane);
+  const float currentTotal = origTotal;
+  float amountToSubtract = 0.0f, amountToPrune = 0.0f;
+  if(isRoot && sp.rootNoise) {
+    amountToSubtract = fminf(sp.moveSubtract, maxW / 64.0f);
+    amountToPrune = fminf(sp.movePrune, maxW / 64.0f);
+  }
+  if(numGood > 0 && currentTotal > 0.0f) {
+    float stdev[NI];
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      stdev[j] = good[j] ? sqrtf(1e-8f + 1.0f / (1.5f * sqrtf(wAdj[j]))) : 0.0f;
+      tmp[j] = good[j] ? selfU[j] * wAdj[j] : 0.0f;
+    }
+    const float simpleValue = tsum<NI>(tmp, k, v.lane) / currentTotal;
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      if(!good[j] || wAdj[j] < amountToPrune) {
+        tmp[j] = 0.0f;
+        continue;
+      }
+      float nw = wAdj[j] - amountToSubtract;
+      if(nw <= 0.0f)
+        nw = 0.0f;
+      float z = (selfU[j] - simpleValue) / stdev[j];
+      float p = cdfT(v.T, z) + 0.0001f;
+      float f = sp.valueWeightExp == 0.5f ? sqrtf(p) : dpow(p, sp.valueWeightExp);
+      tmp[j] = nw * f;
+    }
+    const float totalNew = tsum<NI>(tmp, k, v.lane);
+    const float factor = currentTotal / totalNew;
+#pragma unroll
+    for(int j = 0; j < NI; j++)
+      wAdj[j] = tmp[j] * factor;
+  }
+  float wlv[NI], uv[NI], usqv[NI], wsqv[NI];
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    if(!good[j]) {
+      wlv[j] = uv[j] = usqv[j] = wsqv[j] = 0.0f;
+      continue;
+    }
+    float ws = wAdj[j] / cWs[j];
+    wlv[j] = wAdj[j] * cWl[j];
+    uv[j] = wAdj[j] * cU[j];
+    usqv[j] = wAdj[j] * cUsq[j];
+    wsqv[j] = (ws * ws) * cWsq[j];
+  }
+  float winLossSum = tsum<NI>(wlv, k, v.lane);
+  float utilitySum = tsum<NI>(uv, k, v.lane);
+  float utilitySqSum = tsum<NI>(usqv, k, v.lane);
+  float weightSqSum = tsum<NI>(wsqv, k, v.lane);
+  float weightSum = currentTotal;
+  float wl = nnWin - nnLoss;
+  float utility = wl;
+  float newLastD = lastSvbDelta, newLastW = lastSvbWeight;
+  if(sp.svbFactor != 0.0f && svbEntry >= 0) {
+    size_t e = v.svbBase(s.svbSel) + svbEntry;
+    int64_t D = v.d.svbD[e], Wt = v.d.svbW[e];
+    if(currentTotal > 1e-10f) {
+      float utilityChildren = utilitySum / currentTotal;
+      float svbWv = dpow(origTotal, sp.svbExp);
+      float svbDv = (utilityChildren - utility) * svbWv;
+      D += svbQ(svbDv) - svbQ(lastSvbDelta);
+      Wt += svbQ(svbWv) - svbQ(lastSvbWeight);
+      waveSync();
+      if(v.lane == 0) {
+        v.d.svbD[e] = D;
+        v.d.svbW[e] = Wt;
+      }
+      newLastD = svbDv;
+      newLastW = svbWv;
+    }
+    float dd = svbF(D), ww = svbF(Wt);
+    if(ww > 0.001f)
+      utility = utility + (sp.svbFactor * dd) / ww;
+  }
+  winLossSum = winLossSum + wl;
+  utilitySum = utilitySum + utility;
+  utilitySqSum = utilitySqSum + utility * utility;
+  weightSqSum = weightSqSum + 1.0f;
+  weightSum = weightSum + 1.0f;
+  waveSync();
+  if(v.lane == 0) {
+    np->winLossAvg = winLossSum / weightSum;
+    np->utilityAvg = utilitySum / weightSum;
+    np->utilitySqAvg = utilitySqSum / weightSum;
+    np->weightSqSum = weightSqSum;
+    np->weightSum = weightSum;
+    np->visits = visits0 + (uint32_t)numVisitsToAdd;
+    np->lastSvbDelta = newLastD;
+    np->lastSvbWeight = newLastW;
+  }
+  waveSync();
+}
+
+// oracle fpuValue (searchexplorehelpers.cpp:245-301)
+KC_D float fpuValue(const SP& sp, const Node& n, int pla, bool isRoot, float probMass) {
+  float parentUtility = n.utilityAvg;
+  float forFpu = parentUtility;
+  if(sp.fpuByVisited) {
+    float pw = sp.fpuByVisitedPow == 2.0f ? probMass * probMass : dpow(probMass, sp.fpuByVisitedPow);
+    float avgWeight = fminf(1.0f, pw);
+    forFpu = avgWeight * parentUtility + (1.0f - avgWeight) * (n.nnWin - n.nnLoss);
+  }
+  float redMax = isRoot ? sp.rootFpuRedMax : sp.fpuRedMax;
+  float lossProp = isRoot ? sp.rootFpuLossProp : sp.fpuLossProp;
+  float reduction = redMax * sqrtf(probMass);
+  float fpu = pla == 2 ? forFpu - reduction : forFpu + reduction;
+  float lossValue = pla == 2 ? -1.0f : 1.0f;
+  fpu = fpu + (lossValue - fpu) * lossProp;
+  return fpu;
+}
+
+KC_D float exploreScaling(const SP& sp, float totalChildWeight) {
+  float c = sp.cpuct;
+  if(sp.cpuctLog != 0.0f)
+    c = c + sp.cpuctLog * dlog((totalChildWeight + sp.cpuctBase) / sp.cpuctBase);
+  return c * sqrtf(totalChildWeight + 0.01f);
+}
+
+// oracle selectBest (selectBestChildToDescend searchexplorehelpers.cpp:304-451)
+template <int NI>
+KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool isRoot, int& newPos,
+                    uint32_t* hasBits) {
+  const SP& sp = v.d.sp;
+  const int P = v.d.P;
+  const int k = n.numChildren;
+  const int pla = n.nextPla;
+  for(int w = v.lane; w < (P + 31) / 32; w += 64)
+    hasBits[w] = 0;
+  waveSync();
+  const Edge* E = v.edges(ni);
+  const uint16_t* M = v.emove(ni);
+  const Node* NS = v.nodes();
+  float probs[NI], cw[NI], pv[NI], cu[NI];
+  uint32_t cvis[NI];
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int i = v.lane + 64 * j;
+    probs[j] = cw[j] = pv[j] = cu[j] = 0.0f;
+    cvis[j] = 0;
+    if(i < k) {
+      Edge e = E[i];
+      int mv = M[i];
+      const Node& c = NS[e.child];
+      float p = pol[mv];
+      cvis[j] = c.visits;
+      cu[j] = c.utilityAvg;
+      pv[j] = p;
+      probs[j] = p < 0.0f ? 0.0f : p;
+      cw[j] = p < 0.0f ? 0.0f : childWeight(e.visits, cvis[j], c.weightSum);
+      atomicOr(&hasBits[mv >> 5], 1u << (mv & 31));
+    }
+  }
+  const float probMass = tsum<NI>(probs, k, v.lane);
+  const float total = tsum<NI>(cw, k, v.lane);
+  const float fpu = fpuValue(sp, n, pla, isRoot, probMass);
+  const float scaling = exploreScaling(sp, total);
+  float best = -__builtin_inff();
+  int bestIdx = BIG;
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int i = v.lane + 64 * j;
+    if(i >= k)
+      continue;
+    float p = pv[j];
+    float val;
+    if(p < 0.0f)
+      val = -__builtin_inff();
+    else {
+      float w = cw[j];
+      float u = (cvis[j] == 0 || w <= 0.0f) ? fpu : cu[j];
+      if(isRoot && sp.rootDesiredCoeff > 0.0f && p > 0.0f && w < sqrtf((p * total) * sp.rootDesiredCoeff))
+        val = 1e20f;
+      else
+        val = (scaling * p) / (1.0f + w) + (pla == 2 ? u : -u);
+    }
+    if(val > best) {
+      best = val;
+      bestIdx = i;
+    }
+  }
+  waveArgmax(best, bestIdx);
+  int bestSlot = best > -__builtin_inff() ? bestIdx : -1;
+  waveSync();
+  float bp = -1.0f;
+  int bpos = BIG;
+  for(int pos = v.lane; pos < P; pos += 64) {
+    if((hasBits[pos >> 5] >> (pos & 31)) & 1u)
+      continue;
+    float p = pol[pos];
+    if(p < 0.0f)
+      continue;
+    if(p > bp) {
+      bp = p;
+      bpos = pos;
+    }
+  }
+  waveArgmax(bp, bpos);
+  newPos = -1;
+  if(bpos != BIG) {
+    float val = (scaling * bp) / 1.0f + (pla == 2 ? fpu : -fpu);
+    if(val > best) {
+      bestSlot = k;
+      newPos = bpos;
+    }
+  }
+  return bestSlot;
+}
+
+// oracle descend (playoutDescend search.cpp:936-1165, allocateOrFindNode :704-759,
+// maybeCatchUpEdgeVisits :1169-1207)
+template <int NI>
+KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
+  const SP& sp = v.d.sp;
+  const DTables& T = v.T;
+  s.pathLen = 0;
+  DBoard b = s.root;
+  int ni = s.rootIdx;
+  while(true) {
+    const Node& n = v.nodes()[ni];
+    if(n.flags & 2) {
+      s.leafKind = LEAF_TERMINAL;
+      s.leafNode = ni;
+      s.leaf = b;
+      break;
+    }
+    const bool isRoot = ni == s.rootIdx;
+    const float* pol = isRoot ? v.rootNoised() : v.pol(ni);
+    int newPos = -1;
+    int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits);
+    if(slot < 0) {
+      s.leafKind = LEAF_NOCHILD;
+      s.leafNode = ni;
+      break;
+    }
+    if(slot == n.numChildren) {
+      const int cell = newPos % T.A, dir = newPos / T.A;
+      DBoard before = b;
+      playMoveWave(T, b, cell, dir);
+      uint64_t k0, k1;
+      stateHash(T, b, k0, k1);
+      int child = sp.useGraph ? ttFind(v, k0, k1) : -1;
+      if(child < 0) {
+        child = allocNode(v, s, b.pla, k0, k1, b.finished != 0);
+        if(child < 0) {
+          s.leafKind = LEAF_NOCHILD;
+          s.leafNode = ni;
+          break;
+        }
+        if(sp.svbFactor != 0.0f && hCell(before, 0) >= 0) {
+          int ppos = hDir(before, 0) * T.A + hCell(before, 0);
+          uint64_t key = svbKeyOf(v, before, ppos, newPos, before.pla);
+          int e = svbFindOrInsert(v, s.svbSel, key);
+          waveSync();
+          if(v.lane == 0)
+            v.nodes()[child].svbEntry = e;
+        }
+        if(sp.useGraph)
+          ttInsert(v, k0, k1, child);
+      }
+      waveSync();
+      if(v.lane == 0) {
+        v.edges(ni)[slot] = Edge{(uint32_t)child, 0u};
+        v.emove(ni)[slot] = (uint16_t)newPos;
+        v.nodes()[ni].numChildren = (uint16_t)(slot + 1);
+        v.pathNode()[s.pathLen] = ni;
+        v.pathSlot()[s.pathLen] = slot;
+      }
+      s.pathLen++;
+      waveSync();
+      const Node& c = v.nodes()[child];
+      if(c.visits > 0) {
+        s.leafKind = LEAF_CATCHUP;
+        s.leafNode = child;
+        break;
+      }
+      s.leafNode = child;
+      s.leaf = b;
+      s.leafKind = (c.flags & 2) ? LEAF_TERMINAL : LEAF_NN;
+      break;
+    }
+    const Edge e = v.edges(ni)[slot];
+    const int child = (int)e.child;
+    if(v.lane == 0) {
+      v.pathNode()[s.pathLen] = ni;
+      v.pathSlot()[s.pathLen] = slot;
+    }
+    s.pathLen++;
+    if(e.visits < v.nodes()[child].visits) {
+      s.leafKind = LEAF_CATCHUP;
+      s.leafNode = child;
+      break;
+    }
+    const int mv = v.emove(ni)[slot];
+    playMoveWave(T, b, mv % T.A, mv / T.A);
+    ni = child;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kSelect: root evaluation or one descent; NN leaves are encoded into the batch.
+template <int NI>
+__global__ void __launch_bounds__(64) kSelect(const SearchDev* __restrict__ dp) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  if(g >= d.G)
+    return;
+  __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
+  GV v(d, g);
+  GameDev s;
+  loadGame(v, s);
+  if(s.phase == PH_COMMIT) {
+    s.leafKind = LEAF_NONE;
+    if(v.lane == 0)
+      d.games[g].leafKind = LEAF_NONE;
+    return;
+  }
+  DRng rng = DRng{s.rngSeed, s.rngCtr};
+  if(s.phase == PH_ROOTEVAL) {
+    if(s.rootK == 0) {
+      // partial Fisher-Yates over 0..7, kept as packed nibbles (no dynamic register indexing)
+      uint32_t idx = 0x76543210u;
+#pragma unroll
+      for(int k = 0; k < 4; k++) {
+        int j = k + (int)rng.below((uint32_t)(8 - k));
+        uint32_t a = (idx >> (4 * k)) & 15u, b = (idx >> (4 * j)) & 15u;
+        idx = (idx & ~(15u << (4 * k)) & ~(15u << (4 * j))) | (b << (4 * k)) | (a << (4 * j));
+      }
+      s.syms = idx & 0xFFFFu;
+    }
+    s.leafKind = LEAF_ROOTEVAL;
+    s.leafSym = (int)((s.syms >> (4 * s.rootK)) & 15u);
+    s.leaf = s.root;
+  } else {
+    descend<NI>(v, s, hasBits);
+    if(s.leafKind == LEAF_NN)
+      s.leafSym = (int)rng.below(8);
+  }
+  s.rngCtr = rng.ctr;
+  if(s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL) {
+    int slot = 0;
+    if(v.lane == 0)
+      slot = atomicAdd(d.nnCount, 1);
+    slot = bcastI(slot, 0);
+    s.nnSlot = slot;
+    s.nnEvals++;
+    encodePackedWave(v.T, s.leaf, s.leafSym, d.nnIn + (size_t)slot * d.inWords);
+  }
+  waveSync();
+  storeGame(v, s);
+}
+
+// oracle postprocess (nneval.cpp:702-815 + copyOutputsWithSymmetry nninputs.cpp:349-357)
+template <int NI>
+KC_D void postprocess(const GV& v, const DBoard& b, int sym, const float* out, float* polDst, float& whiteWin,
+                      float& whiteLoss) {
+  const DTables& T = v.T;
+  const int P = T.P, A = T.A;
+  if(T.X != T.Y)
+    sym &= 3;
+  float logit[NI];
+  bool legal[NI];
+  float mx = -1e25f;
+  int legalCount = 0;
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int pos = v.lane + 64 * j;
+    legal[j] = false;
+    logit[j] = -1e30f;
+    if(pos < P) {
+      int dd = pos / A, cell = pos % A;
+      legal[j] = isLegal(T, b, cell, dd);
+      logit[j] = legal[j] ? out[T.symDir[sym][dd] * A + T.symCell[sym][cell]] : -1e30f;
+      mx = logit[j] > mx ? logit[j] : mx;
+    }
+    legalCount += __popcll(ballot(legal[j]));
+  }
+  mx = waveMax(mx);
+  float e[NI];
+#pragma unroll
+  for(int j = 0; j < NI; j++)
+    e[j] = dexp(logit[j] - mx);
+  const float sum = tsum<NI>(e, P, v.lane);
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int pos = v.lane + 64 * j;
+    if(pos < P)
+      polDst[pos] = legal[j] ? (sum <= 0.0f ? 1.0f / (float)legalCount : e[j] / sum) : -1.0f;
+  }
+  float wlg = out[P], llg = out[P + 1];
+  float m = wlg > llg ? wlg : llg;
+  float wp = dexp(wlg - m), lp = dexp(llg - m);
+  float ps = wp + lp;
+  wp = wp / ps;
+  lp = lp / ps;
+  if(b.pla == 2) {
+    whiteWin = wp;
+    whiteLoss = lp;
+  } else {
+    whiteWin = lp;
+    whiteLoss = wp;
+  }
+}
+
+KC_D float interpolateEarly(const DTables& T, int turn, float halflife, float earlyValue, float value) {
+  float rawHalflives = (float)turn / halflife;
+  float halflives = rawHalflives * (19.0f / sqrtf((float)(T.X * T.Y)));
+  return value + (earlyValue - value) * dpow(0.5f, halflives);
+}
+
+// Sequential in-order sum of lds[0..n) (the oracle's plain loops), result to all lanes.
+KC_D float seqSum(float* lds, int n, int lane) {
+  waveSync();
+  float acc = 0.0f;
+  if(lane == 0)
+    for(int i = 0; i < n; i++)
+      acc = acc + lds[i];
+  return __shfl(acc, 0, 64);
+}
+
+// oracle noiseAndTemp (maybeAddPolicyNoiseAndTemp searchhelpers.cpp:122-222)
+KC_D void noiseAndTemp(const GV& v, GameDev& s, DRng& rng, const float* raw, float* out, float* scratch) {
+  const SP& sp = v.d.sp;
+  const int P = v.d.P;
+  for(int pos = v.lane; pos < P; pos += 64)
+    out[pos] = raw[pos];
+  waveSync();
+  if(sp.rootTemp != 1.0f || sp.rootTempEarly != 1.0f) {
+    float t = interpolateEarly(v.T, s.root.turn, sp.moveTempHalflife, sp.rootTempEarly, sp.rootTemp);
+    float mx = 0.0f;
+    for(int pos = v.lane; pos < P; pos += 64)
+      mx = out[pos] > mx ? out[pos] : mx;
+    mx = waveMax(mx);
+    float logMax = dlog(mx);
+    float invTemp = 1.0f / t;
+    for(int pos = v.lane; pos < P; pos += 64) {
+      float o = out[pos];
+      float p = 0.0f;
+      if(o > 0.0f) {
+        p = dexp((dlog(o) - logMax) * invTemp);
+        out[pos] = p;
+      }
+      scratch[pos] = p;  // zero terms do not change the in-order sum
+    }
+    float sum = seqSum(scratch, P, v.lane);
+    waveSync();
+    for(int pos = v.lane; pos < P; pos += 64)
+      if(out[pos] >= 0.0f)
+        out[pos] = out[pos] / sum;
+    waveSync();
+  }
+  if(sp.rootNoise) {
+    // computeDirichletAlphaDistribution searchhelpers.cpp:51-91
+    int legalCount = 0;
+    for(int base = 0; base < P; base += 64) {
+      int pos = base + v.lane;
+      legalCount += __popcll(ballot(pos < P && out[pos] >= 0.0f));
+    }
+    float* alpha = scratch;          // [P]
+    float* r = scratch + MAX_P;      // [P]
+    for(int pos = v.lane; pos < P; pos += 64)
+      alpha[pos] = out[pos] >= 0.0f ? dlog(fminf(0.01f, out[pos]) + 1e-20f) : 0.0f;
+    float logSum = seqSum(alpha, P, v.lane);
+    float logMean = logSum / (float)legalCount;
+    waveSync();
+    for(int pos = v.lane; pos < P; pos += 64)
+      alpha[pos] = out[pos] >= 0.0f ? fmaxf(0.0f, alpha[pos] - logMean) : 0.0f;
+    float propSum = seqSum(alpha, P, v.lane);
+    float uniform = 1.0f / (float)legalCount;
+    waveSync();
+    for(int pos = v.lane; pos < P; pos += 64)
+      if(out[pos] >= 0.0f)
+        alpha[pos] = propSum <= 0.0f ? uniform : 0.5f * (alpha[pos] / propSum + uniform);
+    // addDirichletNoise searchhelpers.cpp:93-120; SPEC a24 per-move sub-streams
+    const uint64_t base = rng.next();
+    for(int pos = v.lane; pos < P; pos += 64) {
+      float rv = 0.0f;
+      if(out[pos] >= 0.0f) {
+        DRng sub{mix64(base ^ ((uint64_t)(pos + 1) * 0x9e3779b97f4a7c15ULL)), 0};
+        rv = sub.gamma(alpha[pos] * sp.dirConc);
+      }
+      r[pos] = rv;
+    }
+    float rSum = seqSum(r, P, v.lane);
+    waveSync();
+    float w = sp.dirWeight;
+    for(int pos = v.lane; pos < P; pos += 64) {
+      float rr = r[pos] / rSum;
+      if(out[pos] >= 0.0f)
+        out[pos] = rr * w + out[pos] * (1.0f - w);
+    }
+    waveSync();
+  }
+}
+
+// kBackup: NN post-processing + leaf value + path backup.
+template <int NI>
+__global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  if(g >= d.G)
+    return;
+  __shared__ float scratch[2 * MAX_P];
+  GV v(d, g);
+  GameDev s;
+  loadGame(v, s);
+  if(s.leafKind == LEAF_NONE)
+    return;
+  const SP& sp = d.sp;
+  const int P = d.P;
+  const float* o = d.nnOut + (size_t)s.nnSlot * (P + 4);
+  bool needCommit = false;
+  if(s.leafKind == LEAF_ROOTEVAL) {
+    float* pol = scratch;
+    float w, l;
+    postprocess<NI>(v, s.root, s.leafSym, o, pol, w, l);
+    waveSync();
+    float* acc = v.accPolicy();
+    if(s.rootK == 0) {
+      for(int p = v.lane; p < P; p += 64) {
+        v.rawPolicy()[p] = pol[p];
+        acc[p] = 0.0f + pol[p];
+      }
+      s.rawWin = w;
+      s.rawLoss = l;
+      s.accWin = 0.0f + w;
+      s.accLoss = 0.0f + l;
+    } else {
+      for(int p = v.lane; p < P; p += 64)
+        acc[p] = acc[p] + pol[p];
+      s.accWin = s.accWin + w;
+      s.accLoss = s.accLoss + l;
+    }
+    s.rootK++;
+    if(s.rootK == sp.rootSyms) {
+      const float fl = (float)sp.rootSyms;
+      const bool fresh = s.rootIdx < 0;
+      if(fresh) {
+        uint64_t k0, k1;
+        stateHash(v.T, s.root, k0, k1);
+        s.rootIdx = allocNode(v, s, s.root.pla, k0, k1, false);
+      }
+      waveSync();
+      float* rp = v.pol(s.rootIdx);
+      for(int p = v.lane; p < P; p += 64)
+        rp[p] = acc[p] / fl;
+      if(v.lane == 0) {
+        Node* r = &v.nodes()[s.rootIdx];
+        r->nnWin = s.accWin / fl;
+        r->nnLoss = s.accLoss / fl;
+        r->flags |= 1;
+      }
+      waveSync();
+      if(fresh) {
+        const Node& r = v.nodes()[s.rootIdx];
+        addLeafValue(v, s, s.rootIdx, r.nnWin - r.nnLoss, false, true);
+      }
+      DRng rng{s.rngSeed, s.rngCtr};
+      noiseAndTemp(v, s, rng, rp, v.rootNoised(), scratch);
+      s.rngCtr = rng.ctr;
+      s.phase = PH_SEARCH;
+      needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)sp.maxVisits;
+    }
+  } else {
+    if(s.leafKind == LEAF_NN) {
+      float w, l;
+      postprocess<NI>(v, s.leaf, s.leafSym, o, v.pol(s.leafNode), w, l);
+      waveSync();
+      if(v.lane == 0) {
+        Node* n = &v.nodes()[s.leafNode];
+        n->nnWin = w;
+        n->nnLoss = l;
+        n->flags |= 1;
+      }
+      waveSync();
+      addLeafValue(v, s, s.leafNode, w - l, false, true);
+    } else if(s.leafKind == LEAF_TERMINAL) {
+      float val = s.leaf.winner == 2 ? 1.0f : (s.leaf.winner == 1 ? -1.0f : 0.0f);
+      addLeafValue(v, s, s.leafNode, val, true, false);
+    } else if(s.leafKind == LEAF_NOCHILD) {
+      const Node& n = v.nodes()[s.leafNode];
+      addLeafValue(v, s, s.leafNode, n.nnWin - n.nnLoss, false, false);
+    }
+    const int32_t* pn = v.pathNode();
+    const int32_t* ps = v.pathSlot();
+    for(int j = s.pathLen - 1; j >= 0; j--) {
+      const int node = pn[j], slot = ps[j];
+      waveSync();
+      if(v.lane == 0)
+        v.edges(node)[slot].visits += 1;
+      waveSync();
+      recompute<NI>(v, s, node, 1, node == s.rootIdx);
+    }
+    s.playouts++;
+    needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)sp.maxVisits;
+  }
+  if(needCommit) {
+    s.phase = PH_COMMIT;
+    if(v.lane == 0)
+      d.commitList[atomicAdd(d.commitCount, 1)] = g;
+  }
+  s.leafKind = LEAF_NONE;
+  waveSync();
+  storeGame(v, s);
+}
+
+// ---------------------------------------------------------------------------
+// Commit: move choice, targets, tree reuse, rows.
+
+// oracle lcbAndRadius (getSelfUtilityLCBAndRadius searchhelpers.cpp:469-521)
+KC_D void lcbAndRadius(const SP& sp, int pla, uint32_t cVisits, float cWs, float cWsq, float cU, float cUsq,
+                       uint32_t ev, float& lcb, float& radius) {
+  radius = 2.0f * 1.0f * sp.lcbStdevs;
+  lcb = -radius;
+  float ws = childWeight(ev, cVisits, cWs);
+  float wsq = childWeight(ev, cVisits, cWsq);
+  if(cVisits == 0 || ws <= 0.0f || wsq <= 0.0f)
+    return;
+  float u = cU, usq = cUsq;
+  float ess = (ws * ws) / wsq;
+  float priorWeight = ws / ((ess * ess) * ess);
+  usq = fmaxf(usq, u * u + 1e-8f);
+  usq = (usq * ws + (usq + 1.0f) * priorWeight) / (ws + priorWeight);
+  ws = ws + priorWeight;
+  wsq = wsq + priorWeight * priorWeight;
+  ess = (ws * ws) / wsq;
+  float selfU = pla == 2 ? u : -u;
+  float variance = usq - u * u;
+  float stdev = sqrtf(variance / ess);
+  radius = stdev * sp.lcbStdevs;
+  lcb = selfU - radius;
+}
+
+// oracle playSelectionValues (getPlaySelectionValues searchresults.cpp:63-309).
+// posOut/vals are LDS arrays [P]; returns the count (uniform).
+template <int NI>
+KC_D int playSelectionValues(const GV& v, const GameDev& s, float scaleMaxToAtLeast, bool allowDirect, int* posOut,
+                             float* vals) {
+  const SP& sp = v.d.sp;
+  const int ri = s.rootIdx;
+  const Node& n = v.nodes()[ri];
+  const int k = n.numChildren;
+  const float* pol = v.rootNoised();
+  const int pla = n.nextPla;
+  const Edge* E = v.edges(ri);
+  const uint16_t* M = v.emove(ri);
+  float cw[NI], val[NI];
+  uint32_t ev[NI];
+  int posv[NI];
+  uint32_t cvis[NI];
+  float cws[NI], cwsq[NI], cu[NI], cusq[NI];
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int i = v.lane + 64 * j;
+    cw[j] = val[j] = 0.0f;
+    ev[j] = 0;
+    posv[j] = 0;
+    cvis[j] = 0;
+    cws[j] = cwsq[j] = cu[j] = cusq[j] = 0.0f;
+    if(i < k) {
+      Edge e = E[i];
+      const Node& c = v.nodes()[e.child];
+      cvis[j] = c.visits;
+      cws[j] = c.weightSum;
+      cwsq[j] = c.weightSqSum;
+      cu[j] = c.utilityAvg;
+      cusq[j] = c.utilitySqAvg;
+      ev[j] = e.visits;
+      cw[j] = childWeight(e.visits, cvis[j], cws[j]);
+      posv[j] = M[i];
+      val[j] = cw[j];
+    }
+  }
+  const float total = tsum<NI>(cw, k, v.lane);
+  int numChildren = k;
+  // best child by "good" weight (first max)
+  float maxGood = -1e30f;
+  int bestIdx = BIG;
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int i = v.lane + 64 * j;
+    if(i >= k)
+      continue;
+    float evf = (float)ev[j];
+    float gdn = val[j] * fmaxf(0.0f, evf - 1.0f) / fmaxf(1.0f, evf) + 2.0f * pol[posv[j]];
+    if(gdn > maxGood) {
+      maxGood = gdn;
+      bestIdx = i;
+    }
+  }
+  waveArgmax(maxGood, bestIdx);
+  if(bestIdx == BIG)
+    bestIdx = 0;
+  const int bestLane = bestIdx & 63, bestJ = bestIdx >> 6;
+  float bestWeight = -1e30f;
+  if(k > 0) {
+    float bw = 0.0f;
+#pragma unroll
+    for(int j = 0; j < NI; j++)
+      if(j == bestJ)
+        bw = cw[j];
+    bestWeight = __shfl(bw, bestLane, 64);
+  }
+  if(k > 0) {
+    const float fpu = fpuValue(sp, n, pla, true, 1.0f);
+    const float scaling = exploreScaling(sp, total);
+    float bp = 0.0f, bu = 0.0f;
+    uint32_t bvis = 0;
+#pragma unroll
+    for(int j = 0; j < NI; j++)
+      if(j == bestJ) {
+        bp = pol[posv[j]];
+        bu = cu[j];
+        bvis = cvis[j];
+      }
+    bp = __shfl(bp, bestLane, 64);
+    bu = __shfl(bu, bestLane, 64);
+    bvis = (uint32_t)__shfl((int)bvis, bestLane, 64);
+    const float bw = bestWeight;
+    const float buu = (bvis == 0 || bw <= 0.0f) ? fpu : bu;
+    const float bestValue = bp < 0.0f ? -__builtin_inff() : (scaling * bp) / (1.0f + bw) + (pla == 2 ? buu : -buu);
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      int i = v.lane + 64 * j;
+      if(i >= k || i == bestIdx)
+        continue;
+      float w = cw[j];
+      float reduced;
+      if(cvis[j] == 0 || w <= 0.0f)
+        reduced = 0.0f;
+      else {
+        float p = pol[posv[j]];
+        float wanted;
+        if(p < 0.0f)
+          wanted = 0.0f;
+        else {
+          float valueComponent = pla == 2 ? cu[j] : -cu[j];
+          float exploreComponent = bestValue - valueComponent;
+          float exploreComponentScaling = scaling * p;
+          if(exploreComponent <= 0.0f)
+            wanted = __builtin_inff();
+          else {
+            wanted = exploreComponentScaling / exploreComponent - 1.0f;
+            if(wanted < 0.0f)
+              wanted = 0.0f;
+          }
+        }
+        reduced = w > wanted ? wanted : w;
+      }
+      val[j] = ceilf(reduced);
+    }
+  }
+  if(sp.useLcb && k > 0) {
+    float lcb[NI], rad[NI];
+    float bestLcb = -1e10f;
+    int bestLcbIdx = BIG;
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      int i = v.lane + 64 * j;
+      lcb[j] = rad[j] = 0.0f;
+      if(i >= k)
+        continue;
+      lcbAndRadius(sp, pla, cvis[j], cws[j], cwsq[j], cu[j], cusq[j], ev[j], lcb[j], rad[j]);
+      float w = val[j];
+      if(w > 0.0f && w >= sp.minVisitPropLcb * bestWeight && lcb[j] > bestLcb) {
+        bestLcb = lcb[j];
+        bestLcbIdx = i;
+      }
+    }
+    waveArgmax(bestLcb, bestLcbIdx);
+    if(bestLcbIdx != BIG) {
+      float adj = 0.0f;
+#pragma unroll
+      for(int j = 0; j < NI; j++)
+        if(j == (bestLcbIdx >> 6))
+          adj = val[j];
+      adj = __shfl(adj, bestLcbIdx & 63, 64);
+      float lb = adj;
+#pragma unroll
+      for(int j = 0; j < NI; j++) {
+        int i = v.lane + 64 * j;
+        if(i >= k || i == bestLcbIdx)
+          continue;
+        float excess = bestLcb - lcb[j];
+        if(excess < 0.0f)
+          continue;
+        float rf = (rad[j] + excess) / (rad[j] + 0.20f * excess);
+        float lbound = (rf * rf) * val[j];
+        if(lbound > lb)
+          lb = lbound;
+      }
+      lb = waveMax(lb);
+#pragma unroll
+      for(int j = 0; j < NI; j++)
+        if(v.lane + 64 * j == bestLcbIdx)
+          val[j] = lb;
+    }
+  }
+  // to LDS
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    int i = v.lane + 64 * j;
+    if(i < k) {
+      posOut[i] = posv[j];
+      vals[i] = val[j];
+    }
+  }
+  waveSync();
+  if(numChildren == 0) {
+    if(!allowDirect)
+      return 0;
+    const int P = v.d.P;
+    for(int base = 0; base < P; base += 64) {
+      int p = base + v.lane;
+      bool ok = p < P && isLegal(v.T, s.root, p % v.T.A, p / v.T.A) && pol[p] >= 0.0f;
+      uint64_t m = ballot(ok);
+      if(ok) {
+        int idx = numChildren + __popcll(m & ((1ULL << v.lane) - 1ULL));
+        posOut[idx] = p;
+        vals[idx] = pol[p];
+      }
+      numChildren += __popcll(m);
+    }
+    waveSync();
+    if(numChildren == 0)
+      return 0;
+  }
+  float mx = 0.0f;
+  for(int i = v.lane; i < numChildren; i += 64)
+    mx = vals[i] > mx ? vals[i] : mx;
+  mx = waveMax(mx);
+  if(mx <= 0.0f)
+    return 0;
+  const float amountToSubtract = fminf(sp.moveSubtract, mx / 64.0f);
+  const float amountToPrune = fminf(sp.movePrune, mx / 64.0f);
+  const float newMax = mx - amountToSubtract;
+  for(int i = v.lane; i < numChildren; i += 64) {
+    float x = vals[i];
+    if(x < amountToPrune)
+      x = 0.0f;
+    else {
+      x = x - amountToSubtract;
+      if(x <= 0.0f)
+        x = 0.0f;
+    }
+    if(newMax < scaleMaxToAtLeast)
+      x = x * (scaleMaxToAtLeast / newMax);
+    vals[i] = x;
+  }
+  waveSync();
+  return numChildren;
+}
+
+// oracle chooseIndex (chooseIndexWithTemperature searchhelpers.cpp:11-49)
+KC_D int chooseIndex(const GV& v, DRng& rng, const float* vals, int n, float temperature, float* pr) {
+  float mx = 0.0f;
+  for(int i = v.lane; i < n; i += 64)
+    mx = vals[i] > mx ? vals[i] : mx;
+  mx = waveMax(mx);
+  if(temperature <= 1.0e-4f) {
+    float best = -__builtin_inff();
+    int bi = BIG;
+    for(int i = v.lane; i < n; i += 64)
+      if(vals[i] > best) {
+        best = vals[i];
+        bi = i;
+      }
+    waveArgmax(best, bi);
+    // oracle: best starts at vals[0]; strictly greater later values win
+    return bi == BIG ? 0 : bi;
+  }
+  const float logMax = dlog(mx);
+  for(int i = v.lane; i < n; i += 64)
+    pr[i] = vals[i] <= 0.0f ? 0.0f : dexp((dlog(vals[i]) - logMax) / temperature);
+  const float sum = seqSum(pr, n, v.lane);
+  const float dd = rng.uni() * sum;
+  int chosen = n - 1;
+  if(v.lane == 0) {
+    float acc = 0.0f;
+    for(int i = 0; i < n; i++) {
+      acc = acc + pr[i];
+      if(acc > dd) {
+        chosen = i;
+        break;
+      }
+    }
+  }
+  return bcastI(chosen, 0);
+}
+
+KC_D void clearTables(const GV& v, GameDev& s) {
+  const int cap = v.d.cap;
+  uint32_t* fl = v.freeList();
+  for(int i = v.lane; i < cap; i += 64)
+    fl[i] = (uint32_t)(cap - 1 - i);  // pop order: 0, 1, 2, ...
+  for(int i = v.lane; i < cap / 32; i += 64)
+    v.allocBits()[i] = 0;
+  for(int i = v.lane; i < v.d.ttCap; i += 64)
+    v.ttNode()[i] = -1;
+  const size_t sb = v.svbBase(s.svbSel);
+  for(int i = v.lane; i < v.d.svbCap; i += 64)
+    v.d.svbKey[sb + i] = 0;
+  s.freeTop = cap;
+  s.liveCount = 0;
+  s.rootIdx = -1;
+  waveSync();
+}
+
+// oracle reuseTree (Search::makeMove search.cpp:262-330 + deleteAllOld... :790-810 +
+// SubtreeValueBiasTable::clearUnusedSynchronous :47-59) as mark / free / rebuild.
+// lds: live bitmap [cap/32] u32 + BFS queue [cap] u16.
+KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, uint16_t* queue, int* qtail) {
+  const SP& sp = v.d.sp;
+  const int cap = v.d.cap;
+  const int ri = s.rootIdx;
+  int child = -1;
+  if(ri >= 0) {
+    const Node& r = v.nodes()[ri];
+    const Edge* E = v.edges(ri);
+    const uint16_t* M = v.emove(ri);
+    for(int base = 0; base < r.numChildren; base += 64) {
+      int i = base + v.lane;
+      bool hit = i < r.numChildren && M[i] == chosenPos;
+      uint64_t m = ballot(hit);
+      if(m) {
+        int f = firstLane(m);
+        child = bcastI(hit ? (int)E[i].child : -1, f);
+        break;
+      }
+    }
+  }
+  if(child < 0 || !(v.nodes()[child].flags & 1)) {
+    clearTables(v, s);
+    return;
+  }
+  // mark: parallel BFS over child slots
+  for(int i = v.lane; i < cap / 32; i += 64)
+    liveBits[i] = 0;
+  waveSync();
+  if(v.lane == 0) {
+    liveBits[child >> 5] |= 1u << (child & 31);
+    queue[0] = (uint16_t)child;
+    *qtail = 1;
+  }
+  waveSync();
+  int head = 0;
+  while(true) {
+    const int tail = *qtail;
+    if(head >= tail)
+      break;
+    const int cnt = min(64, tail - head);
+    if(v.lane < cnt) {
+      const int nd = queue[head + v.lane];
+      const int kc = v.nodes()[nd].numChildren;
+      const Edge* E = v.edges(nd);
+      for(int i = 0; i < kc; i++) {
+        const int c = (int)E[i].child;
+        const uint32_t bit = 1u << (c & 31);
+        uint32_t old = atomicOr(&liveBits[c >> 5], bit);
+        if(!(old & bit))
+          queue[atomicAdd(qtail, 1)] = (uint16_t)c;
+      }
+    }
+    head += cnt;
+    waveSync();
+  }
+  int liveCount = 0;
+  for(int i = v.lane; i < cap / 32; i += 64)
+    liveCount += __popc(liveBits[i]);
+#pragma unroll
+  for(int off = 32; off >= 1; off >>= 1)
+    liveCount += __shfl_xor(liveCount, off, 64);
+  if(liveCount + sp.maxVisits + 2 > cap) {
+    clearTables(v, s);
+    return;
+  }
+  // removeSubtreeValueBias for dead table nodes and the promoted child (fixed point: any order)
+  const size_t sb = v.svbBase(s.svbSel);
+  uint32_t* ab = v.allocBits();
+  for(int i = v.lane; i < cap; i += 64) {
+    bool alloc = (ab[i >> 5] >> (i & 31)) & 1u;
+    bool live = (liveBits[i >> 5] >> (i & 31)) & 1u;
+    if(!alloc || (live && i != child))
+      continue;
+    const Node& n = v.nodes()[i];
+    if(n.svbEntry < 0)
+      continue;
+    atomicAdd((unsigned long long*)&v.d.svbD[sb + n.svbEntry],
+              (unsigned long long)(-svbQ(n.lastSvbDelta * sp.svbFreeProp)));
+    atomicAdd((unsigned long long*)&v.d.svbW[sb + n.svbEntry],
+              (unsigned long long)(-svbQ(n.lastSvbWeight * sp.svbFreeProp)));
+  }
+  waveSync();
+  if(v.lane == 0) {
+    Node* c = &v.nodes()[child];
+    c->svbEntry = -1;
+    c->lastSvbDelta = 0.0f;
+    c->lastSvbWeight = 0.0f;
+  }
+  // free list = every non-live index; allocBits = live
+  int top = 0;
+  uint32_t* fl = v.freeList();
+  for(int base = 0; base < cap; base += 64) {
+    int i = base + v.lane;
+    bool live = (liveBits[i >> 5] >> (i & 31)) & 1u;
+    uint64_t m = ballot(!live);
+    if(!live)
+      fl[top + __popcll(m & ((1ULL << v.lane) - 1ULL))] = (uint32_t)i;
+    top += __popcll(m);
+  }
+  for(int i = v.lane; i < cap / 32; i += 64)
+    ab[i] = liveBits[i];
+  s.freeTop = top;
+  s.liveCount = liveCount;
+  s.rootIdx = child;
+  // transposition table: clear, insert every live node but the root (CAS, any order)
+  int32_t* tn = v.ttNode();
+  uint64_t* tk = v.ttKey();
+  for(int i = v.lane; i < v.d.ttCap; i += 64)
+    tn[i] = -1;
+  // new SVB table
+  const int nsel = s.svbSel ^ 1;
+  const size_t nb = v.svbBase(nsel);
+  for(int i = v.lane; i < v.d.svbCap; i += 64)
+    v.d.svbKey[nb + i] = 0;
+  waveSync();
+  const int tmask = v.d.ttCap - 1, smask = v.d.svbCap - 1;
+  for(int i = v.lane; i < cap; i += 64) {
+    bool live = (liveBits[i >> 5] >> (i & 31)) & 1u;
+    if(!live)
+      continue;
+    Node* n = &v.nodes()[i];
+    if(i != child && v.d.sp.useGraph) {
+      int sl = (int)(n->key0 & (uint64_t)tmask);
+      while(atomicCAS(&tn[sl], -1, i) != -1)
+        sl = (sl + 1) & tmask;
+      tk[2 * sl] = n->key0;
+      tk[2 * sl + 1] = n->key1;
+    }
+    if(n->svbEntry >= 0) {
+      const size_t oe = sb + n->svbEntry;
+      const uint64_t key = v.d.svbKey[oe];
+      int sl = (int)(key & (uint64_t)smask);
+      while(true) {
+        unsigned long long prev =
+          atomicCAS((unsigned long long*)&v.d.svbKey[nb + sl], 0ULL, (unsigned long long)key);
+        if(prev == 0ULL || prev == key)
+          break;
+        sl = (sl + 1) & smask;
+      }
+      v.d.svbD[nb + sl] = v.d.svbD[oe];
+      v.d.svbW[nb + sl] = v.d.svbW[oe];
+      n->svbEntry = sl;
+    }
+  }
+  s.svbSel = nsel;
+  waveSync();
+}
+
+KC_D void startGame(const GV& v, GameDev& s) {
+  s.rngSeed = mix64(v.d.seed ^ mix64(((uint64_t)(v.d.slotBase + v.g) << 32) | (uint32_t)s.gameNum));
+  s.rngCtr = 0;
+  boardInit(v.T, s.root);
+  clearTables(v, s);
+  s.numTurns = 0;
+  DRng rng{s.rngSeed, s.rngCtr};
+  s.gameHash0 = rng.next();
+  s.gameHash1 = rng.next();
+  s.rngCtr = rng.ctr;
+  s.phase = PH_ROOTEVAL;
+  s.rootK = 0;
+  s.leafKind = LEAF_NONE;
+}
+
+// oracle finishGame (play.cpp:1431-1460 + trainingwrite.cpp:316-565, 774-890).
+// boards: LDS [numMoves+1] DBoard; f32 scratch [2*(MAX_AREA+1)].
+KC_D void finishGame(const GV& v, GameDev& s, DRng& rng, DBoard* boards, float* tw) {
+  const DTables& T = v.T;
+  const SearchDev& d = v.d;
+  const int numMoves = s.numTurns;
+  const int A = T.A, P = T.P, pb = (A + 7) / 8;
+  const TurnRec* tr = v.turns();
+  const float finalWin = s.root.winner == 2 ? 1.0f : (s.root.winner == 1 ? 0.0f : 0.5f);
+  float* tWin = tw;
+  float* tLoss = tw + (MAX_AREA + 1);
+  for(int t = v.lane; t < numMoves; t += 64) {
+    tWin[t] = tr[t].whiteWin;
+    tLoss[t] = tr[t].whiteLoss;
+  }
+  if(v.lane == 0) {
+    tWin[numMoves] = finalWin;
+    tLoss[numMoves] = 1.0f - finalWin;
+    DBoard b;
+    boardInit(T, b);
+    boards[0] = b;
+    for(int t = 0; t < numMoves; t++) {
+      applyMove(T, b, tr[t].cell, tr[t].dir);
+      boards[t + 1] = b;
+    }
+  }
+  waveSync();
+  const DBoard& fin = boards[numMoves];
+  unsigned long long base = 0;
+  bool fits = true;
+  if(v.lane == 0) {
+    base = atomicAdd(d.rCount, (unsigned long long)numMoves);
+    if(base + (unsigned long long)numMoves > (unsigned long long)d.rowCap) {
+      atomicAdd(d.rCount, (unsigned long long)(-(long long)numMoves));
+      atomicAdd(d.rDropped, (unsigned long long)numMoves);
+      fits = false;
+    }
+  }
+  fits = __shfl((int)fits, 0, 64) != 0;
+  base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(base >> 32), 0, 64) << 32) |
+         (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
+  const float nowF1 = 1.0f / (1.0f + (float)A * 0.176f), nowF2 = 1.0f / (1.0f + (float)A * 0.056f),
+              nowF3 = 1.0f / (1.0f + (float)A * 0.016f);
+  for(int t = 0; t < numMoves; t++) {
+    // history-mask draws (uniform; consumed even when the row is dropped)
+    bool h = true;
+    uint32_t hm = 0;
+#pragma unroll
+    for(int i = 0; i < 5; i++) {
+      h = h && rng.uni() < 0.98f;
+      hm |= (h ? 1u : 0u) << i;
+    }
+    if(!fits)
+      continue;
+    const size_t r = (size_t)base + t;
+    const DBoard& b = boards[t];
+    const int pla = b.pla, opp = 3 - pla;
+    for(int idx = v.lane; idx < NUM_SPATIAL * pb; idx += 64) {
+      const int plane = idx / pb, byte = idx % pb;
+      uint32_t bits = 0;
+      for(int bit = 0; bit < 8; bit++) {
+        int cell = byte * 8 + bit;
+        if(cell < A && v1Bit(T, b, plane, cell, 0))
+          bits |= 1u << (7 - bit);
+      }
+      d.rBin[r * NUM_SPATIAL * pb + idx] = (uint8_t)bits;
+    }
+    if(v.lane == 0)
+      d.rGlob[r] = (float)T.W;
+    const int16_t* p0 = v.turnPol(t);
+    const int16_t* p1 = t + 1 < numMoves ? v.turnPol(t + 1) : nullptr;
+    int16_t* pol = d.rPol + r * 2 * P;
+    for(int p = v.lane; p < P; p += 64) {
+      pol[p] = p0[p];
+      pol[P + p] = p1 ? p1[p] : (int16_t)1;
+    }
+    float gval = 0.0f;
+    const int li = v.lane;
+    if(li < 10) {
+      const int f = li >> 1;
+      const float nf = f == 0 ? 0.0f : (f == 1 ? nowF1 : (f == 2 ? nowF2 : (f == 3 ? nowF3 : 1.0f)));
+      float win = 0.0f, loss = 0.0f, left = 1.0f;
+      for(int i = t; i <= numMoves; i++) {
+        float now;
+        if(i == numMoves) {
+          now = left;
+          left = 0.0f;
+        } else {
+          now = left * nf;
+          left = left * (1.0f - nf);
+        }
+        win = win + now * (pla == 2 ? tWin[i] : tLoss[i]);
+        loss = loss + now * (pla == 2 ? tLoss[i] : tWin[i]);
+      }
+      gval = (li & 1) ? loss : win;
+    } else if(li == 22) {
+      float sum = 0.0f;
+      for(int i = t + 1; i <= numMoves; i++) {
+        float prevWL = tWin[i - 1] - tLoss[i - 1], nextWL = tWin[i] - tLoss[i];
+        float var = (nextWL - prevWL) * (nextWL - prevWL);
+        sum = sum + (float)(i - t) * var;
+      }
+      gval = sum;
+    } else if(li == 25 || li == 26 || li == 27 || li == 33 || li == 63) {
+      gval = 1.0f;
+    } else if(li == 28) {
+      gval = t + 1 < numMoves ? 1.0f : 0.0f;
+    } else if(li == 30) {
+      gval = tr[t].policySurprise;
+    } else if(li == 31) {
+      gval = tr[t].policyEntropy;
+    } else if(li == 32) {
+      gval = tr[t].searchEntropy;
+    } else if(li >= 36 && li <= 40) {
+      gval = ((hm >> (li - 36)) & 1u) ? 1.0f : 0.0f;
+    } else if(li == 41) {
+      gval = (float)(s.gameHash0 & 0x3FFFFF);
+    } else if(li == 42) {
+      gval = (float)((s.gameHash0 >> 22) & 0x3FFFFF);
+    } else if(li == 43) {
+      gval = (float)((s.gameHash0 >> 44) & 0xFFFFF);
+    } else if(li == 44) {
+      gval = (float)(s.gameHash1 & 0x3FFFFF);
+    } else if(li == 45) {
+      gval = (float)((s.gameHash1 >> 22) & 0x3FFFFF);
+    } else if(li == 46) {
+      gval = (float)((s.gameHash1 >> 44) & 0xFFFFF);
+    } else if(li == 51) {
+      gval = (float)t;
+    } else if(li == 57) {
+      gval = pla == 2 ? tr[t].rawWhiteWL : -tr[t].rawWhiteWL;
+    } else if(li == 59) {
+      gval = tr[t].rawPolicyEntropy;
+    } else if(li == 60) {
+      gval = (float)tr[t].visits;
+    }
+    d.rGt[r * 64 + li] = gval;
+    int8_t* vt = d.rVal + r * 5 * A;
+    const DBoard& b2 = boards[min(t + 2, numMoves)];
+    const DBoard& b3 = boards[min(t + 6, numMoves)];
+    for(int c = v.lane; c < A; c += 64) {
+      int fc = colorAt(fin, c), c2 = colorAt(b2, c), c3 = colorAt(b3, c);
+      vt[c] = fc == pla ? 1 : (fc == opp ? -1 : 0);
+      vt[A + c] = 0;
+      vt[2 * A + c] = c2 == pla ? 1 : (c2 == opp ? -1 : 0);
+      vt[3 * A + c] = c3 == pla ? 1 : (c3 == opp ? -1 : 0);
+      vt[4 * A + c] = fc == 0 ? 0 : (int8_t)maxRun(T, fin, c);
+    }
+    if(v.lane < 4) {
+      int m = v.lane == 0 ? d.slotBase + v.g : (v.lane == 1 ? s.gameNum : (v.lane == 2 ? t : numMoves));
+      d.rMeta[r * 4 + v.lane] = m;
+    }
+  }
+}
+
+// oracle commitMove (getChosenMoveLoc searchresults.cpp:435-453, extract*Targets
+// play.cpp:635-704, getPolicySurpriseAndEntropy searchresults.cpp:486-550, makeMove)
+template <int NI>
+__global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp) {
+  const SearchDev& d = *dp;
+  if((int)blockIdx.x >= *d.commitCount)
+    return;
+  const int g = d.commitList[blockIdx.x];
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int* posv = reinterpret_cast<int*>(lds);                    // [MAX_P]
+  float* vals = reinterpret_cast<float*>(posv + MAX_P);       // [MAX_P]
+  float* tmp = vals + MAX_P;                                  // [MAX_P]
+  float* tmp2 = tmp + MAX_P;                                  // [MAX_P]
+  float* tw = tmp2 + MAX_P;                                   // [2*(MAX_AREA+1)]
+  int* qtail = reinterpret_cast<int*>(tw + 2 * (MAX_AREA + 1));
+  DBoard* boards = reinterpret_cast<DBoard*>(qtail + 4);      // [MAX_AREA+1]
+  uint32_t* liveBits = reinterpret_cast<uint32_t*>(boards + (MAX_AREA + 1));  // [cap/32]
+  uint16_t* queue = reinterpret_cast<uint16_t*>(liveBits + d.cap / 32);     // [cap]
+  GV v(d, g);
+  GameDev s;
+  loadGame(v, s);
+  const SP& sp = d.sp;
+  const int P = d.P, A = d.A;
+  DRng rng{s.rngSeed, s.rngCtr};
+  int n = playSelectionValues<NI>(v, s, 0.0f, true, posv, vals);
+  if(n <= 0) {
+    s.err = 2;
+    n = 1;
+    posv[0] = 0;
+  }
+  const float temp = interpolateEarly(v.T, s.root.turn, sp.moveTempHalflife, sp.moveTempEarly, sp.moveTemp);
+  int ci = chooseIndex(v, rng, vals, n, temp, tmp);
+  waveSync();
+  const int chosen = posv[ci];
+  const Node& r = v.nodes()[s.rootIdx];
+  TurnRec rec;
+  {
+    float wl = fmaxf(-1.0f, fminf(1.0f, r.winLossAvg));
+    rec.whiteWin = fmaxf(0.0f, fminf(1.0f, 0.5f * (wl + 1.0f)));
+    rec.whiteLoss = fmaxf(0.0f, fminf(1.0f, 0.5f * (-wl + 1.0f)));
+    rec.visits = r.visits;
+  }
+  const int t = s.numTurns;
+  int16_t* pt = v.turnPol(t);
+  waveSync();
+  {
+    for(int p = v.lane; p < P; p += 64)
+      pt[p] = 0;
+    int m = playSelectionValues<NI>(v, s, 10.0f, false, posv, vals);
+    float mx = 0.0f;
+    for(int i = v.lane; i < m; i += 64)
+      mx = vals[i] > mx ? vals[i] : mx;
+    mx = waveMax(mx);
+    float factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
+    waveSync();
+    for(int i = v.lane; i < m; i += 64)
+      pt[posv[i]] = (int16_t)roundf(vals[i] * factor);
+  }
+  rec.rawWhiteWL = s.rawWin - s.rawLoss;
+  {
+    const float* rp = v.rawPolicy();
+    for(int p = v.lane; p < P; p += 64) {
+      float q = rp[p];
+      tmp[p] = q >= 1e-30f ? -q * dlog(q) : 0.0f;
+    }
+    // in-order sum of only the q >= 1e-30 terms: zero terms are exact no-ops
+    rec.rawPolicyEntropy = seqSum(tmp, P, v.lane);
+  }
+  {
+    waveSync();
+    int m = playSelectionValues<NI>(v, s, 1.0f, true, posv, vals);
+    const float* pol = v.rootNoised();
+    const float sumV = seqSum(vals, m, v.lane);
+    // per-child terms (0 where the oracle skips), summed in order on lane 0
+    waveSync();
+    for(int i = v.lane; i < m; i += 64) {
+      float p = fmaxf(pol[posv[i]], 1e-30f);
+      float tt = vals[i] / sumV;
+      float st = 0.0f, et = 0.0f;
+      if(tt > 1e-30f) {
+        float lt = dlog(tt), lp = dlog(p);
+        st = tt * (lt - lp);
+        et = -tt * lt;
+      }
+      tmp[i] = st;
+      tmp2[i] = et;
+    }
+    const float surprise = seqSum(tmp, m, v.lane);
+    const float searchEnt = seqSum(tmp2, m, v.lane);
+    waveSync();
+    for(int p = v.lane; p < P; p += 64) {
+      float q = pol[p];
+      tmp[p] = q > 1e-30f ? -q * dlog(q) : 0.0f;
+    }
+    float polEnt = seqSum(tmp, P, v.lane);
+    rec.policySurprise = fmaxf(0.0f, surprise);
+    rec.searchEntropy = fmaxf(0.0f, searchEnt);
+    rec.policyEntropy = fmaxf(0.0f, polEnt);
+  }
+  rec.cell = (int8_t)(chosen % A);
+  rec.dir = (int8_t)(chosen / A);
+  for(int i = 0; i < 6; i++)
+    rec.pad[i] = 0;
+  waveSync();
+  if(v.lane == 0)
+    v.turns()[t] = rec;
+  s.numTurns++;
+  reuseTree(v, s, chosen, liveBits, queue, qtail);
+  playMoveWave(v.T, s.root, chosen % A, chosen / A);
+  s.moves++;
+  waveSync();
+  if(s.root.finished) {
+    finishGame(v, s, rng, boards, tw);
+    s.gamesFinished++;
+    s.gameNum++;
+    startGame(v, s);
+  } else {
+    s.rngCtr = rng.ctr;
+    s.phase = PH_ROOTEVAL;
+    s.rootK = 0;
+  }
+  waveSync();
+  storeGame(v, s);
+}
+
+__global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  if(g >= d.G)
+    return;
+  GV v(d, g);
+  GameDev s;
+  for(int i = 0; i < (int)(sizeof(GameDev) / 4); i++)
+    reinterpret_cast<uint32_t*>(&s)[i] = 0;
+  s.svbSel = 0;
+  s.gameNum = 0;
+  startGame(v, s);
+  waveSync();
+  storeGame(v, s);
+}
+
+// Canonical breadth-first export of one game's tree (tests / tools).
+// nodesOut [maxNodes][24] u32, edgesOut [maxNodes][P][3] u32 (child bfs index, edge visits, move).
+__global__ void kGameTree(const SearchDev* __restrict__ dp, int g, int maxNodes, uint32_t* nodesOut,
+                          uint32_t* edgesOut, int32_t* count) {
+  const SearchDev& d = *dp;
+  if(threadIdx.x != 0)
+    return;
+  const GameDev& s = d.games[g];
+  const Node* NS = d.nodes + (size_t)g * d.cap;
+  if(s.rootIdx < 0) {
+    *count = 0;
+    return;
+  }
+  // canonical index map kept in nodesOut word 23 of each discovered node: store original idx
+  int n = 0;
+  int head = 0;
+  nodesOut[23] = (uint32_t)s.rootIdx;
+  n = 1;
+  while(head < n && head < maxNodes) {
+    const int idx = (int)nodesOut[(size_t)head * 24 + 23];
+    const Node& x = NS[idx];
+    uint32_t* o = nodesOut + (size_t)head * 24;
+    o[0] = x.visits;
+    o[1] = f2u(x.weightSum);
+    o[2] = f2u(x.weightSqSum);
+    o[3] = f2u(x.utilityAvg);
+    o[4] = f2u(x.utilitySqAvg);
+    o[5] = f2u(x.winLossAvg);
+    o[6] = f2u(x.nnWin);
+    o[7] = f2u(x.nnLoss);
+    o[8] = f2u(x.lastSvbDelta);
+    o[9] = f2u(x.lastSvbWeight);
+    o[10] = (uint32_t)x.numChildren | ((uint32_t)x.nextPla << 16) | ((uint32_t)x.flags << 24);
+    o[11] = (uint32_t)x.key0;
+    o[12] = (uint32_t)(x.key0 >> 32);
+    o[13] = (uint32_t)x.key1;
+    o[14] = (uint32_t)(x.key1 >> 32);
+    uint64_t sk = 0;
+    int64_t sd = 0, sw = 0;
+    if(x.svbEntry >= 0) {
+      size_t e = ((size_t)g * 2 + s.svbSel) * d.svbCap + x.svbEntry;
+      sk = d.svbKey[e];
+      sd = d.svbD[e];
+      sw = d.svbW[e];
+    }
+    o[15] = (uint32_t)sk;
+    o[16] = (uint32_t)(sk >> 32);
+    o[17] = (uint32_t)(uint64_t)sd;
+    o[18] = (uint32_t)((uint64_t)sd >> 32);
+    o[19] = (uint32_t)(uint64_t)sw;
+    o[20] = (uint32_t)((uint64_t)sw >> 32);
+    o[21] = 0;
+    o[22] = 0;
+    const Edge* E = d.edges + ((size_t)g * d.cap + idx) * d.P;
+    const uint16_t* M = d.emove + ((size_t)g * d.cap + idx) * d.P;
+    for(int i = 0; i < x.numChildren; i++) {
+      const int c = (int)E[i].child;
+      int ci = -1;
+      for(int q = 0; q < n; q++)
+        if((int)nodesOut[(size_t)q * 24 + 23] == c) {
+          ci = q;
+          break;
+        }
+      if(ci < 0 && n < maxNodes) {
+        nodesOut[(size_t)n * 24 + 23] = (uint32_t)c;
+        ci = n++;
+      }
+      uint32_t* eo = edgesOut + ((size_t)head * d.P + i) * 3;
+      eo[0] = (uint32_t)ci;
+      eo[1] = E[i].visits;
+      eo[2] = M[i];
+    }
+    head++;
+  }
+  // replace word 23 (original index) by 0 so the export is index independent
+  for(int q = 0; q < n; q++)
+    nodesOut[(size_t)q * 24 + 23] = 0;
+  *count = n;
+}
+
+// ---------------------------------------------------------------------------
+static int laneItems(int P) { return P <= 128 ? 2 : (P <= 256 ? 4 : 7); }
+
+void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+  hipLaunchKernelGGL(kInit, dim3(d.G), dim3(64), 0, st, dd);
+  KC_HIP(hipGetLastError());
+}
+
+void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+  switch(laneItems(d.P)) {
+    case 2: hipLaunchKernelGGL(kSelect<2>, dim3(d.G), dim3(64), 0, st, dd); break;
+    case 4: hipLaunchKernelGGL(kSelect<4>, dim3(d.G), dim3(64), 0, st, dd); break;
+    default: hipLaunchKernelGGL(kSelect<7>, dim3(d.G), dim3(64), 0, st, dd); break;
+  }
+  KC_HIP(hipGetLastError());
+}
+
+void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+  switch(laneItems(d.P)) {
+    case 2: hipLaunchKernelGGL(kBackup<2>, dim3(d.G), dim3(64), 0, st, dd); break;
+    case 4: hipLaunchKernelGGL(kBackup<4>, dim3(d.G), dim3(64), 0, st, dd); break;
+    default: hipLaunchKernelGGL(kBackup<7>, dim3(d.G), dim3(64), 0, st, dd); break;
+  }
+  KC_HIP(hipGetLastError());
+}
+
+size_t commitLdsBytes(int cap) {
+  size_t b = (size_t)MAX_P * 4 * 4 + 2 * (MAX_AREA + 1) * 4 + 16;
+  b += sizeof(DBoard) * (MAX_AREA + 1);
+  b += (size_t)(cap / 32) * 4 + (size_t)cap * 2;
+  return (b + 15) / 16 * 16;
+}
+
+void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+  const size_t lds = commitLdsBytes(d.cap);
+  switch(laneItems(d.P)) {
+    case 2: hipLaunchKernelGGL(kCommit<2>, dim3(d.G), dim3(64), lds, st, dd); break;
+    case 4: hipLaunchKernelGGL(kCommit<4>, dim3(d.G), dim3(64), lds, st, dd); break;
+    default: hipLaunchKernelGGL(kCommit<7>, dim3(d.G), dim3(64), lds, st, dd); break;
+  }
+  KC_HIP(hipGetLastError());
+}
+
+void launchGameTree(const SearchDev* dd, int slot, int maxNodes, uint32_t* nodesOut, uint32_t* edgesOut,
+                    int32_t* count, hipStream_t st) {
+  hipLaunchKernelGGL(kGameTree, dim3(1), dim3(64), 0, st, dd, slot, maxNodes, nodesOut, edgesOut, count);
+  KC_HIP(hipGetLastError());
+}
+
+}  // namespace kc

@@ -1,0 +1,332 @@
+// Host side of the self-play engine: device allocation, the round loop and the
+// row drain.  Replaces the reference's per-thread game loop (selfplay.cpp:262-330
+// gameLoop, Play::runGame play.cpp:1146-1701) and NNEvaluator batching
+// (nneval.cpp:386-567): all games advance together, one playout per round.
+#include "selfplay.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace kc {
+
+static int nextPow2(int v) {
+  int p = 1;
+  while(p < v)
+    p <<= 1;
+  return p;
+}
+
+SP toSP(const coffee_search_params& p) {
+  SP s;
+  s.maxVisits = p.max_visits;
+  s.cpuct = p.cpuct_exploration;
+  s.cpuctLog = p.cpuct_exploration_log;
+  s.cpuctBase = p.cpuct_exploration_base;
+  s.fpuRedMax = p.fpu_reduction_max;
+  s.rootFpuRedMax = p.root_fpu_reduction_max;
+  s.fpuLossProp = p.fpu_loss_prop;
+  s.rootFpuLossProp = p.root_fpu_loss_prop;
+  s.fpuByVisited = p.fpu_parent_weight_by_visited_policy;
+  s.fpuByVisitedPow = p.fpu_parent_weight_by_visited_policy_pow;
+  s.valueWeightExp = p.value_weight_exponent;
+  s.rootNoise = p.root_noise_enabled;
+  s.dirConc = p.root_dirichlet_noise_total_concentration;
+  s.dirWeight = p.root_dirichlet_noise_weight;
+  s.rootTemp = p.root_policy_temperature;
+  s.rootTempEarly = p.root_policy_temperature_early;
+  s.rootDesiredCoeff = p.root_desired_per_child_visits_coeff;
+  s.rootSyms = p.root_num_symmetries_to_sample;
+  s.moveTemp = p.chosen_move_temperature;
+  s.moveTempEarly = p.chosen_move_temperature_early;
+  s.moveTempHalflife = p.chosen_move_temperature_halflife;
+  s.moveSubtract = p.chosen_move_subtract;
+  s.movePrune = p.chosen_move_prune;
+  s.useLcb = p.use_lcb_for_selection;
+  s.lcbStdevs = p.lcb_stdevs;
+  s.minVisitPropLcb = p.min_visit_prop_for_lcb;
+  s.svbFactor = p.subtree_value_bias_factor;
+  s.svbExp = p.subtree_value_bias_weight_exponent;
+  s.svbFreeProp = p.subtree_value_bias_free_prop;
+  s.useGraph = p.use_graph_search;
+  return s;
+}
+
+template <class T>
+static T* devAlloc(std::vector<void*>& owned, size_t count, bool zero = true) {
+  void* p = nullptr;
+  size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  KC_HIP(hipMalloc(&p, bytes));
+  owned.push_back(p);
+  if(zero)
+    KC_HIP(hipMemset(p, 0, bytes));
+  return reinterpret_cast<T*>(p);
+}
+
+SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
+  if(c.num_games <= 0)
+    throw std::invalid_argument("num_games must be positive");
+  const coffee_search_params& sp = c.search;
+  if(sp.max_visits < 1 || sp.root_num_symmetries_to_sample < 1 || sp.root_num_symmetries_to_sample > 4)
+    throw std::invalid_argument("search params: max_visits >= 1 and 1 <= root_num_symmetries_to_sample <= 4");
+  const DTables& ht = hostTables(c.x, c.y, c.win_len);
+  T_ = deviceTables(c.x, c.y, c.win_len);
+  commitInterval_ = c.commit_interval > 0 ? c.commit_interval : 8;
+  int cap = c.node_cap > 0 ? c.node_cap : std::max(2048, 3 * sp.max_visits);
+  cap = (cap + 63) / 64 * 64;
+  if(cap > 65535)
+    throw std::invalid_argument("node_cap must be <= 65535");
+  if(cap < sp.max_visits + 4)
+    throw std::invalid_argument("node_cap must exceed max_visits + 3");
+  const int G = c.num_games, P = ht.P, A = ht.A;
+  const int ttCap = nextPow2(2 * cap);
+  const int rowCap = c.row_capacity > 0 ? c.row_capacity : 4 * G * A;
+  if(!c.use_fake_net) {
+    if(!c.model_path)
+      throw std::invalid_argument("model_path required unless use_fake_net");
+    ModelHost m = loadModel(c.model_path);
+    nn_.reset(new NNEngine(m, c.x, c.y, c.win_len));
+  }
+  SearchDev& d = hd_;
+  memset(&d, 0, sizeof(d));
+  d.T = T_;
+  d.sp = toSP(sp);
+  d.G = G;
+  d.cap = cap;
+  d.ttCap = ttCap;
+  d.svbCap = ttCap;
+  d.P = P;
+  d.A = A;
+  d.inWords = ht.inWords;
+  d.maxTurns = A + 1;
+  d.rowCap = rowCap;
+  d.slotBase = c.slot_base;
+  d.seed = c.seed;
+  d.games = devAlloc<GameDev>(owned_, G);
+  d.nodes = devAlloc<Node>(owned_, (size_t)G * cap, false);
+  d.edges = devAlloc<Edge>(owned_, (size_t)G * cap * P, false);
+  d.emove = devAlloc<uint16_t>(owned_, (size_t)G * cap * P, false);
+  d.policy = devAlloc<float>(owned_, (size_t)G * cap * P, false);
+  d.freeList = devAlloc<uint32_t>(owned_, (size_t)G * cap, false);
+  d.allocBits = devAlloc<uint32_t>(owned_, (size_t)G * (cap / 32));
+  d.ttKey = devAlloc<uint64_t>(owned_, (size_t)G * ttCap * 2, false);
+  d.ttNode = devAlloc<int32_t>(owned_, (size_t)G * ttCap, false);
+  d.svbKey = devAlloc<uint64_t>(owned_, (size_t)G * 2 * ttCap);
+  d.svbD = devAlloc<int64_t>(owned_, (size_t)G * 2 * ttCap);
+  d.svbW = devAlloc<int64_t>(owned_, (size_t)G * 2 * ttCap);
+  d.accPolicy = devAlloc<float>(owned_, (size_t)G * P);
+  d.rawPolicy = devAlloc<float>(owned_, (size_t)G * P);
+  d.rootNoised = devAlloc<float>(owned_, (size_t)G * P);
+  d.pathNode = devAlloc<int32_t>(owned_, (size_t)G * MAX_DEPTH);
+  d.pathSlot = devAlloc<int32_t>(owned_, (size_t)G * MAX_DEPTH);
+  d.turns = devAlloc<TurnRec>(owned_, (size_t)G * d.maxTurns);
+  d.turnPol = devAlloc<int16_t>(owned_, (size_t)G * d.maxTurns * P);
+  d.nnIn = devAlloc<uint64_t>(owned_, (size_t)G * ht.inWords);
+  d.nnOut = devAlloc<float>(owned_, (size_t)G * (P + 4));
+  d.nnCount = devAlloc<int32_t>(owned_, 1);
+  d.commitList = devAlloc<int32_t>(owned_, G);
+  d.commitCount = devAlloc<int32_t>(owned_, 1);
+  const int pb = (A + 7) / 8;
+  d.rBin = devAlloc<uint8_t>(owned_, (size_t)rowCap * NUM_SPATIAL * pb, false);
+  d.rGlob = devAlloc<float>(owned_, (size_t)rowCap, false);
+  d.rPol = devAlloc<int16_t>(owned_, (size_t)rowCap * 2 * P, false);
+  d.rGt = devAlloc<float>(owned_, (size_t)rowCap * 64, false);
+  d.rVal = devAlloc<int8_t>(owned_, (size_t)rowCap * 5 * A, false);
+  d.rMeta = devAlloc<int32_t>(owned_, (size_t)rowCap * 4, false);
+  d.rCount = devAlloc<unsigned long long>(owned_, 1);
+  d.rDropped = devAlloc<unsigned long long>(owned_, 1);
+  dd_ = devAlloc<SearchDev>(owned_, 1);
+  KC_HIP(hipMemcpy(dd_, &d, sizeof(SearchDev), hipMemcpyHostToDevice));
+  KC_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  const size_t lds = commitLdsBytes(cap);
+  if(lds > 64 * 1024)
+    throw std::invalid_argument("node_cap too large for the commit kernel's LDS");
+  launchSelfplayInit(d, dd_, stream_);
+  KC_HIP(hipStreamSynchronize(stream_));
+}
+
+SelfplayEngine::~SelfplayEngine() {
+  if(stream_)
+    (void)hipStreamSynchronize(stream_);
+  for(const PendingTiming& p : pending_) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for(hipEvent_t e : evPool_)
+    (void)hipEventDestroy(e);
+  nn_.reset();
+  for(void* p : owned_)
+    (void)hipFree(p);
+  if(stream_)
+    (void)hipStreamDestroy(stream_);
+}
+
+// Kernel timing: an event pair per launch on the launch stream, resolved later
+// (no host synchronisation inside the round loop).
+hipEvent_t SelfplayEngine::takeEvent() {
+  if(evPool_.empty()) {
+    hipEvent_t e;
+    KC_HIP(hipEventCreate(&e));
+    return e;
+  }
+  hipEvent_t e = evPool_.back();
+  evPool_.pop_back();
+  return e;
+}
+
+void SelfplayEngine::timed(int which, hipStream_t st, const std::function<void()>& f) {
+  if(!timing_) {
+    f();
+    return;
+  }
+  hipEvent_t a = takeEvent(), b = takeEvent();
+  KC_HIP(hipEventRecord(a, st));
+  f();
+  KC_HIP(hipEventRecord(b, st));
+  pending_.push_back({which, a, b});
+}
+
+void SelfplayEngine::resolveTiming() {
+  for(const PendingTiming& p : pending_) {
+    KC_HIP(hipEventSynchronize(p.b));
+    float ms = 0.0f;
+    KC_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    kernelMs_[p.which] += ms;
+    kernelLaunches_[p.which]++;
+    evPool_.push_back(p.a);
+    evPool_.push_back(p.b);
+  }
+  pending_.clear();
+}
+
+void SelfplayEngine::step(int rounds, hipStream_t st) {
+  if(!st)
+    st = stream_;
+  const SearchDev& d = hd_;
+  for(int r = 0; r < rounds; r++) {
+    KC_HIP(hipMemsetAsync(d.nnCount, 0, sizeof(int32_t), st));
+    timed(0, st, [&] { launchSelect(d, dd_, st); });
+    timed(1, st, [&] {
+      if(nn_)
+        nn_->forward(d.G, d.nnIn, d.nnOut, st, d.nnCount);
+      else
+        launchFakeNet(T_, d.G, d.nnIn, d.nnOut, st, d.nnCount);
+    });
+    timed(2, st, [&] { launchBackup(d, dd_, st); });
+    rounds_++;
+    if(rounds_ % (uint64_t)commitInterval_ == 0 || r == rounds - 1) {
+      timed(3, st, [&] { launchCommit(d, dd_, st); });
+      KC_HIP(hipMemsetAsync(d.commitCount, 0, sizeof(int32_t), st));
+    }
+  }
+}
+
+void SelfplayEngine::sync() {
+  KC_HIP(hipStreamSynchronize(stream_));
+  resolveTiming();
+}
+
+void SelfplayEngine::stats(coffee_selfplay_stats& out) {
+  sync();
+  std::vector<GameDev> g(hd_.G);
+  KC_HIP(hipMemcpy(g.data(), hd_.games, sizeof(GameDev) * hd_.G, hipMemcpyDeviceToHost));
+  memset(&out, 0, sizeof(out));
+  out.rounds = rounds_;
+  for(const GameDev& x : g) {
+    out.playouts += x.playouts;
+    out.nn_evals += x.nnEvals;
+    out.moves += x.moves;
+    out.games_finished += x.gamesFinished;
+  }
+  unsigned long long cnt = 0, dropped = 0;
+  KC_HIP(hipMemcpy(&cnt, hd_.rCount, 8, hipMemcpyDeviceToHost));
+  KC_HIP(hipMemcpy(&dropped, hd_.rDropped, 8, hipMemcpyDeviceToHost));
+  out.rows_pending = cnt;
+  out.rows_written = rowsDrained_ + cnt;
+  out.rows_dropped = dropped;
+}
+
+int SelfplayEngine::drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, float* gt, int8_t* val,
+                          int32_t* meta) {
+  sync();
+  unsigned long long cnt = 0;
+  KC_HIP(hipMemcpy(&cnt, hd_.rCount, 8, hipMemcpyDeviceToHost));
+  const int n = (int)std::min<unsigned long long>(cnt, (unsigned long long)std::max(maxRows, 0));
+  const int A = hd_.A, P = hd_.P, pb = (A + 7) / 8;
+  auto cp = [&](void* dst, const void* src, size_t rowBytes) {
+    if(dst && n > 0)
+      KC_HIP(hipMemcpy(dst, src, rowBytes * n, hipMemcpyDeviceToHost));
+  };
+  cp(bin, hd_.rBin, (size_t)NUM_SPATIAL * pb);
+  cp(glob, hd_.rGlob, 4);
+  cp(pol, hd_.rPol, (size_t)2 * P * 2);
+  cp(gt, hd_.rGt, 64 * 4);
+  cp(val, hd_.rVal, (size_t)5 * A);
+  cp(meta, hd_.rMeta, 16);
+  if(n > 0 && (unsigned long long)n < cnt) {
+    // keep the undrained tail at the front of the buffer
+    const size_t rest = cnt - n;
+    auto mv = [&](void* base, size_t rowBytes) {
+      KC_HIP(hipMemcpy(base, (char*)base + rowBytes * n, rowBytes * rest, hipMemcpyDeviceToDevice));
+    };
+    mv(hd_.rBin, (size_t)NUM_SPATIAL * pb);
+    mv(hd_.rGlob, 4);
+    mv(hd_.rPol, (size_t)2 * P * 2);
+    mv(hd_.rGt, 256);
+    mv(hd_.rVal, (size_t)5 * A);
+    mv(hd_.rMeta, 16);
+  }
+  unsigned long long left = cnt - (unsigned long long)n;
+  KC_HIP(hipMemcpy(hd_.rCount, &left, 8, hipMemcpyHostToDevice));
+  rowsDrained_ += n;
+  return n;
+}
+
+void SelfplayEngine::gameInfo(int slot, int64_t* info) {
+  if(slot < 0 || slot >= hd_.G)
+    throw std::invalid_argument("slot out of range");
+  sync();
+  GameDev g;
+  KC_HIP(hipMemcpy(&g, hd_.games + slot, sizeof(GameDev), hipMemcpyDeviceToHost));
+  int64_t v[16] = {g.phase, g.rootK, g.liveCount, g.rootIdx, g.gameNum, g.root.turn, g.root.pla,
+                   g.root.finished, g.root.winner, (int64_t)g.playouts, (int64_t)g.nnEvals, (int64_t)g.moves,
+                   (int64_t)g.gamesFinished, g.root.lastCell, g.root.lastDir, (int64_t)g.rngCtr};
+  memcpy(info, v, sizeof(v));
+}
+
+int SelfplayEngine::gameTree(int slot, int maxNodes, uint32_t* nodes, uint32_t* edges) {
+  if(slot < 0 || slot >= hd_.G || maxNodes <= 0)
+    throw std::invalid_argument("slot/max_nodes out of range");
+  sync();
+  std::vector<void*> tmp;
+  uint32_t* dn = devAlloc<uint32_t>(tmp, (size_t)maxNodes * 24);
+  uint32_t* de = devAlloc<uint32_t>(tmp, (size_t)maxNodes * hd_.P * 3);
+  int32_t* dc = devAlloc<int32_t>(tmp, 1);
+  launchGameTree(dd_, slot, maxNodes, dn, de, dc, stream_);
+  KC_HIP(hipStreamSynchronize(stream_));
+  int n = 0;
+  KC_HIP(hipMemcpy(&n, dc, 4, hipMemcpyDeviceToHost));
+  if(nodes)
+    KC_HIP(hipMemcpy(nodes, dn, (size_t)maxNodes * 24 * 4, hipMemcpyDeviceToHost));
+  if(edges)
+    KC_HIP(hipMemcpy(edges, de, (size_t)maxNodes * hd_.P * 3 * 4, hipMemcpyDeviceToHost));
+  for(void* p : tmp)
+    (void)hipFree(p);
+  return n;
+}
+
+void SelfplayEngine::rootPolicy(int slot, float* out) {
+  if(slot < 0 || slot >= hd_.G)
+    throw std::invalid_argument("slot out of range");
+  sync();
+  KC_HIP(hipMemcpy(out, hd_.rootNoised + (size_t)slot * hd_.P, sizeof(float) * hd_.P, hipMemcpyDeviceToHost));
+}
+
+void SelfplayEngine::kernelTime(int which, double& ms, uint64_t& launches) {
+  resolveTiming();
+  if(which < 0 || which > 3)
+    throw std::invalid_argument("which must be 0..3");
+  ms = kernelMs_[which];
+  launches = kernelLaunches_[which];
+}
+
+}  // namespace kc

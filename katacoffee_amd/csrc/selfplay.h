@@ -1,0 +1,54 @@
+// Host self-play engine (selfplay.cpp) behind coffee_selfplay_*.
+#pragma once
+#include <functional>
+#include <memory>
+#include <vector>
+
+#include "../../include/katacoffee.h"
+#include "engine.h"
+#include "search.h"
+
+namespace kc {
+
+SP toSP(const coffee_search_params& p);
+
+class SelfplayEngine {
+ public:
+  explicit SelfplayEngine(const coffee_selfplay_config& c);
+  ~SelfplayEngine();
+  void step(int rounds, hipStream_t st);
+  void sync();
+  void stats(coffee_selfplay_stats& out);
+  int drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, float* gt, int8_t* val, int32_t* meta);
+  void gameInfo(int slot, int64_t* info);
+  int gameTree(int slot, int maxNodes, uint32_t* nodes, uint32_t* edges);
+  void rootPolicy(int slot, float* out);
+  void setTiming(bool on) { timing_ = on; }
+  void kernelTime(int which, double& ms, uint64_t& launches);
+  const SearchDev& dev() const { return hd_; }
+
+ private:
+  struct PendingTiming {
+    int which;
+    hipEvent_t a, b;
+  };
+  void timed(int which, hipStream_t st, const std::function<void()>& f);
+  hipEvent_t takeEvent();
+  void resolveTiming();
+  std::vector<PendingTiming> pending_;
+  std::vector<hipEvent_t> evPool_;
+  const DTables* T_ = nullptr;
+  std::unique_ptr<NNEngine> nn_;
+  SearchDev hd_;
+  SearchDev* dd_ = nullptr;
+  std::vector<void*> owned_;
+  hipStream_t stream_ = nullptr;
+  int commitInterval_ = 8;
+  uint64_t rounds_ = 0;
+  uint64_t rowsDrained_ = 0;
+  bool timing_ = false;
+  double kernelMs_[4] = {0, 0, 0, 0};
+  uint64_t kernelLaunches_[4] = {0, 0, 0, 0};
+};
+
+}  // namespace kc

@@ -182,8 +182,9 @@ int ora_sp_root_noised(void* h, int slot, float* out) {
 }
 
 int ora_sp_rows_count(void* h) { return ((Selfplay*)h)->rows.n; }
-int ora_sp_rows(void* h, uint8_t* bin, float* globIn, int16_t* policy, float* globT, int8_t* value) {
+int ora_sp_rows(void* h, uint8_t* bin, float* globIn, int16_t* policy, float* globT, int8_t* value, int32_t* meta) {
   Rows& R = ((Selfplay*)h)->rows;
+  memcpy(meta, R.meta.data(), R.meta.size() * 4);
   memcpy(bin, R.bin.data(), R.bin.size());
   memcpy(globIn, R.globIn.data(), R.globIn.size() * 4);
   memcpy(policy, R.policy.data(), R.policy.size() * 2);
@@ -192,5 +193,73 @@ int ora_sp_rows(void* h, uint8_t* bin, float* globIn, int16_t* policy, float* gl
   return R.n;
 }
 int ora_sizeof_node() { return (int)sizeof(Node); }
+
+// Canonical breadth-first export (same algorithm and word layout as the device
+// kGameTree): nodes [maxNodes][24] u32, edges [maxNodes][P][3] u32.
+int ora_sp_game_tree(void* h, int slot, int maxNodes, uint32_t* out, uint32_t* edges) {
+  Selfplay* s = (Selfplay*)h;
+  Game& gm = s->games[slot];
+  const int P = s->cfg.g.P;
+  if(gm.rootIdx < 0)
+    return 0;
+  std::vector<int> order;
+  order.push_back(gm.rootIdx);
+  auto f2u = [](float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+  };
+  size_t head = 0;
+  while(head < order.size() && (int)head < maxNodes) {
+    const int idx = order[head];
+    const Node& x = gm.nodes[idx];
+    uint32_t* o = out + head * 24;
+    memset(o, 0, 24 * 4);
+    o[0] = x.visits;
+    o[1] = f2u(x.weightSum);
+    o[2] = f2u(x.weightSqSum);
+    o[3] = f2u(x.utilityAvg);
+    o[4] = f2u(x.utilitySqAvg);
+    o[5] = f2u(x.winLossAvg);
+    o[6] = f2u(x.nnWin);
+    o[7] = f2u(x.nnLoss);
+    o[8] = f2u(x.lastSvbDelta);
+    o[9] = f2u(x.lastSvbWeight);
+    o[10] = (uint32_t)x.numChildren | ((uint32_t)x.nextPla << 16) | ((uint32_t)x.flags << 24);
+    o[11] = (uint32_t)x.key0;
+    o[12] = (uint32_t)(x.key0 >> 32);
+    o[13] = (uint32_t)x.key1;
+    o[14] = (uint32_t)(x.key1 >> 32);
+    if(x.svbEntry >= 0) {
+      uint64_t sk = gm.svbKey[x.svbEntry];
+      uint64_t sd = (uint64_t)gm.svbDelta[x.svbEntry], sw = (uint64_t)gm.svbWeight[x.svbEntry];
+      o[15] = (uint32_t)sk;
+      o[16] = (uint32_t)(sk >> 32);
+      o[17] = (uint32_t)sd;
+      o[18] = (uint32_t)(sd >> 32);
+      o[19] = (uint32_t)sw;
+      o[20] = (uint32_t)(sw >> 32);
+    }
+    for(int i = 0; i < x.numChildren; i++) {
+      const int c = (int)gm.edgeChild[(size_t)idx * P + i];
+      int ci = -1;
+      for(size_t q = 0; q < order.size(); q++)
+        if(order[q] == c) {
+          ci = (int)q;
+          break;
+        }
+      if(ci < 0 && (int)order.size() < maxNodes) {
+        order.push_back(c);
+        ci = (int)order.size() - 1;
+      }
+      uint32_t* eo = edges + (head * P + i) * 3;
+      eo[0] = (uint32_t)ci;
+      eo[1] = gm.edgeVisits[(size_t)idx * P + i];
+      eo[2] = gm.edgeMove[(size_t)idx * P + i];
+    }
+    head++;
+  }
+  return (int)order.size();
+}
 
 }  // extern "C"

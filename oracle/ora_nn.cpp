@@ -8,7 +8,8 @@
 //   Trunk :1169-1227, PolicyHead :1229-1299 (Coffee: 4 direction logits, no pass),
 //   ValueHead :1301-1377 (Coffee: win/loss logits + 2 misc).
 // Boards always fill the NN input here (nnLen == board size), so the mask is 1.
-// mode 1 rounds every convolution weight and convolution input to bf16 (RNE),
+// mode 1 rounds every convolution weight and convolution input to bf16 (RNE)
+// and the residual trunk to fp16 (RNE) after the stem and after every block,
 // exactly where the HIP kernel does, to compare with it at accumulation-order
 // precision.
 #include <cmath>
@@ -28,6 +29,31 @@ static inline float bf16r(float f) {
   u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
   float r;
   memcpy(&r, &u, 4);
+  return r;
+}
+
+// float -> IEEE binary16 -> float, round to nearest even (v_cvt_f16_f32).
+static inline float f16r(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  uint32_t sign = u & 0x80000000u, a = u & 0x7fffffffu;
+  if(a >= 0x7f800000u)
+    return f;
+  float r;
+  if(a < 0x38800000u) {  // below 2^-14: binary16 subnormal, quantum 2^-24
+    float m;
+    memcpy(&m, &a, 4);
+    r = nearbyintf(m * 16777216.0f) * (1.0f / 16777216.0f);
+  } else {
+    uint32_t v = (a + 0xfffu + ((a >> 13) & 1u)) & ~0x1fffu;
+    if(v >= 0x47800000u)
+      v = 0x7f800000u;
+    memcpy(&r, &v, 4);
+  }
+  uint32_t ru;
+  memcpy(&ru, &r, 4);
+  ru |= sign;
+  memcpy(&r, &ru, 4);
   return r;
 }
 
@@ -203,6 +229,12 @@ void forwardOne(const Model& m, const Ctx& cx, const float* binNCHW, const float
     for(int p = 0; p < A; p++)
       x[(size_t)p * C + co] += s;
   }
+  auto roundTrunk = [&]() {
+    if(cx.bf)
+      for(float& v : x)
+        v = f16r(v);
+  };
+  roundTrunk();
   std::vector<float> pooled(3 * (size_t)C), bias(C);
   for(const Model::Block& b : m.blocks) {
     bnRelu(cx, x.data(), C, b.bn1s.data(), b.bn1b.data(), a.data());
@@ -227,6 +259,7 @@ void forwardOne(const Model& m, const Ctx& cx, const float* binNCHW, const float
       bnRelu(cx, h.data(), Cr, b.bn2s.data(), b.bn2b.data(), a.data());
       conv3(cx, a.data(), Cr, b.conv2.data(), C, x.data(), true);
     }
+    roundTrunk();
   }
   bnRelu(cx, x.data(), C, m.tips.data(), m.tipb.data(), a.data());
   // Policy head

@@ -25,6 +25,11 @@
 namespace ora {
 
 static const int SVB_CAP = 4096;
+
+// SPEC B27: subtree-value-bias sums are kept in 64-bit fixed point (2^-32 units)
+// so that concurrent/unordered updates are exact and order independent.
+inline int64_t svbQ(float x) { return llrintf(x * 4294967296.0f); }
+inline float svbF(int64_t v) { return (float)v * (1.0f / 4294967296.0f); }
 static const uint64_t SVB_SEED = 0x5b5b5b5b5b5b5b5bULL;
 
 // ---------------------------------------------------------------------------
@@ -101,15 +106,15 @@ struct Ctx {
   void ttClear() { std::fill(gm.ttNode.begin(), gm.ttNode.end(), -1); }
 
   // --- subtree value bias table (subtreevaluebiastable.cpp:61-78) ---
-  int svbFindOrInsert(std::vector<uint64_t>& key, std::vector<float>& d, std::vector<float>& w,
+  int svbFindOrInsert(std::vector<uint64_t>& key, std::vector<int64_t>& d, std::vector<int64_t>& w,
                       std::vector<uint8_t>& used, uint64_t k) {
     int mask = SVB_CAP - 1;
     for(int i = (int)(k & (uint64_t)mask);; i = (i + 1) & mask) {
       if(!used[i]) {
         used[i] = 1;
         key[i] = k;
-        d[i] = 0.0f;
-        w[i] = 0.0f;
+        d[i] = 0;
+        w[i] = 0;
         return i;
       }
       if(key[i] == k)
@@ -129,7 +134,7 @@ struct Ctx {
         int col = (xx >= 0 && xx < g.X && yy >= 0 && yy < g.Y) ? before.c[yy * g.X + xx] : 3;
         h ^= Z[svbIdxPat(col, wy, wx)];
       }
-    return h;
+    return h != 0 ? h : 1;  // 0 is the device table's empty sentinel
   }
 
   int allocNode(uint8_t nextPla, H128 key, bool terminal) {
@@ -158,7 +163,7 @@ struct Ctx {
     Node& n = N(ni);
     float utility = wl;
     if(sp.subtreeValueBiasFactor != 0.0f && !isTerminal && n.svbEntry >= 0) {
-      float d = gm.svbDelta[n.svbEntry], w = gm.svbWeight[n.svbEntry];
+      float d = svbF(gm.svbDelta[n.svbEntry]), w = svbF(gm.svbWeight[n.svbEntry]);
       if(w > 0.001f)
         utility = utility + (sp.subtreeValueBiasFactor * d) / w;
     }
@@ -279,12 +284,12 @@ struct Ctx {
         float utilityChildren = utilitySum / currentTotal;
         float svbW = kPowf(origTotal, sp.subtreeValueBiasWeightExponent);
         float svbD = (utilityChildren - utility) * svbW;
-        gm.svbDelta[e] = gm.svbDelta[e] + (svbD - n.lastSvbDelta);
-        gm.svbWeight[e] = gm.svbWeight[e] + (svbW - n.lastSvbWeight);
+        gm.svbDelta[e] += svbQ(svbD) - svbQ(n.lastSvbDelta);
+        gm.svbWeight[e] += svbQ(svbW) - svbQ(n.lastSvbWeight);
         n.lastSvbDelta = svbD;
         n.lastSvbWeight = svbW;
       }
-      float d = gm.svbDelta[e], w = gm.svbWeight[e];
+      float d = svbF(gm.svbDelta[e]), w = svbF(gm.svbWeight[e]);
       if(w > 0.001f)
         utility = utility + (sp.subtreeValueBiasFactor * d) / w;
     }
@@ -565,12 +570,17 @@ struct Ctx {
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] >= 0.0f)
           alpha[pos] = propSum <= 0.0f ? uniform : 0.5f * (alpha[pos] / propSum + uniform);
-      // addDirichletNoise searchhelpers.cpp:93-120
+      // addDirichletNoise searchhelpers.cpp:93-120.  SPEC a24: one draw from the
+      // game stream seeds an independent sub-stream per move (parallel on device).
       float r[MAX_P];
       float rSum = 0.0f;
+      const uint64_t base = gm.rng.next();
       for(int pos = 0; pos < g.P; pos++) {
         if(out[pos] >= 0.0f) {
-          r[pos] = gm.rng.gamma(alpha[pos] * sp.rootDirichletNoiseTotalConcentration);
+          Rng sub;
+          sub.seed = mix64(base ^ ((uint64_t)(pos + 1) * 0x9e3779b97f4a7c15ULL));
+          sub.ctr = 0;
+          r[pos] = sub.gamma(alpha[pos] * sp.rootDirichletNoiseTotalConcentration);
           rSum = rSum + r[pos];
         } else
           r[pos] = 0.0f;
@@ -833,8 +843,8 @@ struct Ctx {
       if((live[i] && i != child) || n.svbEntry < 0)
         continue;
       int e = n.svbEntry;
-      gm.svbDelta[e] = gm.svbDelta[e] - n.lastSvbDelta * sp.subtreeValueBiasFreeProp;
-      gm.svbWeight[e] = gm.svbWeight[e] - n.lastSvbWeight * sp.subtreeValueBiasFreeProp;
+      gm.svbDelta[e] -= svbQ(n.lastSvbDelta * sp.subtreeValueBiasFreeProp);
+      gm.svbWeight[e] -= svbQ(n.lastSvbWeight * sp.subtreeValueBiasFreeProp);
     }
     N(child).svbEntry = -1;
     N(child).lastSvbDelta = 0.0f;
@@ -865,7 +875,7 @@ struct Ctx {
       if(i != gm.rootIdx)
         ttInsert(N(i).key0, N(i).key1, i);
     std::vector<uint64_t> k2(SVB_CAP, 0);
-    std::vector<float> d2(SVB_CAP, 0.0f), w2(SVB_CAP, 0.0f);
+    std::vector<int64_t> d2(SVB_CAP, 0), w2(SVB_CAP, 0);
     std::vector<uint8_t> u2(SVB_CAP, 0);
     for(int i = 0; i < gm.nodeCount; i++) {
       Node& n = N(i);
@@ -888,38 +898,6 @@ struct Ctx {
     gm.svbDelta.swap(d2);
     gm.svbWeight.swap(w2);
     gm.svbUsed.swap(u2);
-  }
-
-  // Search::recursivelyRecomputeStats search.cpp:834-910, post-order in child order.
-  void recursiveRecompute() {
-    if(gm.rootIdx < 0)
-      return;
-    std::vector<uint8_t> seen(gm.nodeCount, 0);
-    std::vector<std::pair<int, int>> st;
-    st.push_back({gm.rootIdx, 0});
-    seen[gm.rootIdx] = 1;
-    while(!st.empty()) {
-      int v = st.back().first;
-      int& next = st.back().second;
-      if(next < N(v).numChildren) {
-        int c = (int)EC(v, next);
-        next++;
-        if(!seen[c]) {
-          seen[c] = 1;
-          st.push_back({c, 0});
-        }
-        continue;
-      }
-      st.pop_back();
-      Node& n = N(v);
-      if(n.numChildren == 0) {
-        if(n.weightSum > 0.0f) {
-          n.utilityAvg = n.winLossAvg;
-          n.utilitySqAvg = n.winLossAvg * n.winLossAvg;
-        }
-      } else
-        recompute(v, 0, v == gm.rootIdx);
-    }
   }
 
   void startGame() {
@@ -1016,8 +994,8 @@ void Ctx::commitMove() {
     startGame();
     return;
   }
-  if(sp.subtreeValueBiasFactor != 0.0f)
-    recursiveRecompute();
+  // SPEC B26: Search::recursivelyRecomputeStats (search.cpp:671, :834-910) is not
+  // run after tree reuse; the kept subtree keeps its statistics.
   gm.phase = PH_ROOTEVAL;
   gm.rootK = 0;
 }
@@ -1068,6 +1046,11 @@ void Ctx::finishGame() {
     R.policy.resize((size_t)R.n * 2 * P);
     R.globT.resize((size_t)R.n * 64);
     R.value.resize((size_t)R.n * 5 * A);
+    R.meta.resize((size_t)R.n * 4);
+    R.meta[r * 4 + 0] = s.cfg.slotBase + gm.slot;
+    R.meta[r * 4 + 1] = (int32_t)gm.gameNum;
+    R.meta[r * 4 + 2] = t;
+    R.meta[r * 4 + 3] = numMoves;
     for(int ch = 0; ch < NUM_SPATIAL; ch++)
       packBitsBE(bin + ch * A, A, &R.bin[(r * NUM_SPATIAL + ch) * pb]);
     R.globIn[r] = glob[0];
@@ -1172,8 +1155,8 @@ void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames) {
     gm.ttKey1.assign(2 * cfg.nodeCap, 0);
     gm.ttNode.assign(2 * cfg.nodeCap, -1);
     gm.svbKey.assign(SVB_CAP, 0);
-    gm.svbDelta.assign(SVB_CAP, 0.0f);
-    gm.svbWeight.assign(SVB_CAP, 0.0f);
+    gm.svbDelta.assign(SVB_CAP, 0);
+    gm.svbWeight.assign(SVB_CAP, 0);
     gm.svbUsed.assign(SVB_CAP, 0);
     Ctx(s, gm).startGame();
   }

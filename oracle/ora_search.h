@@ -62,6 +62,7 @@ struct Rows {
   std::vector<int16_t> policy;   // [n][2][P]
   std::vector<float> globT;      // [n][64]
   std::vector<int8_t> value;     // [n][5][A]
+  std::vector<int32_t> meta;     // [n][4] slot, game number, turn, num moves
 };
 
 struct SelfplayCfg {
@@ -96,7 +97,7 @@ struct Game {
   std::vector<uint64_t> ttKey0, ttKey1;
   std::vector<int32_t> ttNode;
   std::vector<uint64_t> svbKey;
-  std::vector<float> svbDelta, svbWeight;
+  std::vector<int64_t> svbDelta, svbWeight;  // fixed point, 2^-32 units (SPEC B27)
   std::vector<uint8_t> svbUsed;
   // playout scratch
   int leafKind = LEAF_NONE, leafNode = -1, leafSym = 0;

@@ -38,7 +38,8 @@ def lib():
         L.ora_sp_game_nodes.argtypes = [P, ctypes.c_int, P, P, P, P, P]
         L.ora_sp_root_noised.argtypes = [P, ctypes.c_int, P]
         L.ora_sp_rows_count.argtypes = [P]
-        L.ora_sp_rows.argtypes = [P, P, P, P, P, P]
+        L.ora_sp_rows.argtypes = [P, P, P, P, P, P, P]
+        L.ora_sp_game_tree.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P]
         L.ora_sp_free.argtypes = [P]
         L.ora_model_free.argtypes = [P]
         _load_tables(L)
@@ -178,10 +179,17 @@ class Selfplay:
         pb = (A + 7) // 8
         r = dict(binaryInputNCHWPacked=np.zeros((n, 15, pb), np.uint8), globalInputNC=np.zeros((n, 1), np.float32),
                  policyTargetsNCMove=np.zeros((n, 2, P), np.int16), globalTargetsNC=np.zeros((n, 64), np.float32),
-                 valueTargetsNCHW=np.zeros((n, 5, self.Y, self.X), np.int8))
+                 valueTargetsNCHW=np.zeros((n, 5, self.Y, self.X), np.int8), meta=np.zeros((n, 4), np.int32))
         lib().ora_sp_rows(self.h, ptr(r["binaryInputNCHWPacked"]), ptr(r["globalInputNC"]),
-                          ptr(r["policyTargetsNCMove"]), ptr(r["globalTargetsNC"]), ptr(r["valueTargetsNCHW"]))
+                          ptr(r["policyTargetsNCMove"]), ptr(r["globalTargetsNC"]), ptr(r["valueTargetsNCHW"]),
+                          ptr(r["meta"]))
         return r
+
+    def game_tree(self, slot, max_nodes=4096):
+        nodes = np.zeros((max_nodes, 24), np.uint32)
+        edges = np.zeros((max_nodes, self.P, 3), np.uint32)
+        n = lib().ora_sp_game_tree(self.h, slot, max_nodes, ptr(nodes), ptr(edges))
+        return nodes[:n], edges[:n]
 
     def __del__(self):
         if getattr(self, "h", None):

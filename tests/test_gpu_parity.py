@@ -1,0 +1,195 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference fixtures and
+the CPU oracle.
+
+  rules / play / hashes : bit-exact vs tests/golden/rules_*.npz (reference cpp/game output)
+  encoder               : bit-exact vs the oracle restatement, 8 symmetries
+  stand-in network      : bit-exact vs the oracle
+  residual network      : |logit diff| <= 1e-3 vs the oracle's bf16-emulation mode
+                          (same roundings, different f32 accumulation order);
+                          vs the fp32 oracle (Eigen-backend semantics) <= 5e-2 (bf16 arithmetic)
+  self-play (stand-in net): bit-exact game state, canonical search trees, root
+                          priors and training rows vs the oracle, round for round
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import katacoffee_amd as kc
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = sorted(glob.glob(os.path.join(HERE, "golden", "rules_*.npz")))
+
+
+def _last_cell(d):
+    X = int(d["dims"][0])
+    return np.where(d["last_x"] >= 0, d["last_y"] * X + d["last_x"], -1)
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
+def test_rules_bit_exact_vs_reference(path):
+    d = np.load(path)
+    X, Y, W, _ = map(int, d["dims"])
+    legal, has = kc.rules_batch(X, Y, W, d["colors"], _last_cell(d), d["last_dir"], d["pla"])
+    np.testing.assert_array_equal(legal, d["legal"])
+    np.testing.assert_array_equal(has, d["has_legal"])
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
+def test_play_win_hash_bit_exact_vs_reference(path):
+    d = np.load(path)
+    X, Y, W, _ = map(int, d["dims"])
+    z = np.load(os.path.join(HERE, "golden", "zobrist.npz"))
+    sel = d["move_pos"] >= 0
+    mp = d["move_pos"][sel]
+    cells, fin, win, mr, ph, sh = kc.play_batch(X, Y, W, d["colors"][sel], _last_cell(d)[sel], d["last_dir"][sel],
+                                                d["pla"][sel], mp)
+    after, ha = d["after"][sel], d["hash_after"][sel]
+    np.testing.assert_array_equal(mr, after[:, 2])
+    np.testing.assert_array_equal(ph, ha[:, 0:2])
+    won = after[:, 0] == 1
+    assert np.all(fin[won] == 1)
+    np.testing.assert_array_equal(win[won], after[won, 1])
+    assert np.all(win[~won] == 0)
+    # placed stone
+    A = X * Y
+    np.testing.assert_array_equal(cells[np.arange(len(mp)), mp % A], d["pla"][sel])
+    # transposition key = reference sitHash ^ ZOBRIST_BOARD_HASH2[last move] ^ (game over)
+    cell, dr = mp % A, mp // A
+    spot = (cell % X + 1) + (cell // X + 1) * (X + 1)
+    st = sh ^ z["board2"][spot, dr]
+    st = np.where(fin[:, None] == 1, st ^ z["game_over"][None, :], st)
+    np.testing.assert_array_equal(st, ha[:, 2:4])
+    # and equals the oracle's key
+    o = oracle.play_batch(X, Y, W, d["colors"][sel], _last_cell(d)[sel], d["last_dir"][sel], d["pla"][sel], mp)
+    np.testing.assert_array_equal(sh, o["state_hash"])
+    np.testing.assert_array_equal(fin, o["finished"])
+
+
+def _positions_with_history(path, limit=600):
+    d = np.load(path)
+    X, Y, W, _ = map(int, d["dims"])
+    n = min(limit, len(d["game"]))
+    hc = np.full((n, 5), -1, np.int8)
+    hd = np.full((n, 5), 4, np.int8)
+    for i in range(n):
+        k = 0
+        j = i - 1
+        while k < 5 and j >= 0 and d["game"][j] == d["game"][i]:
+            mv = d["move_pos"][j]
+            hc[i, k] = mv % (X * Y)
+            hd[i, k] = mv // (X * Y)
+            k += 1
+            j -= 1
+    return d, X, Y, W, n, hc, hd
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
+def test_encoder_bit_exact_vs_oracle(path):
+    d, X, Y, W, n, hc, hd = _positions_with_history(path)
+    rng = np.random.default_rng(0)
+    sym = rng.integers(0, 8, n).astype(np.int32)
+    packed, planes = kc.encode_batch(X, Y, W, d["colors"][:n], hc, hd, d["pla"][:n], sym)
+    ob, og = oracle.encode_batch(X, Y, W, d["colors"][:n], hc, hd, d["pla"][:n], sym)
+    np.testing.assert_array_equal(planes, ob)
+    np.testing.assert_array_equal(og, W)
+    # packed bits agree with the planes (bit i = plane*A + cell)
+    A = X * Y
+    bits = np.unpackbits(packed.view(np.uint8), axis=1, bitorder="little")[:, :15 * A]
+    np.testing.assert_array_equal(bits.reshape(n, 15, A), planes.astype(np.uint8))
+
+
+def test_fake_net_bit_exact_vs_oracle():
+    d, X, Y, W, n, hc, hd = _positions_with_history(GOLD[[i for i, p in enumerate(GOLD) if "5x5" in p][0]], 300)
+    sym = np.zeros(n, np.int32)
+    packed, planes = kc.encode_batch(X, Y, W, d["colors"][:n], hc, hd, d["pla"][:n], sym)
+    np.testing.assert_array_equal(kc.fake_net(X, Y, W, packed), oracle.fake_net(X, Y, W, planes))
+
+
+@pytest.fixture(scope="module")
+def model_path(tmp_path_factory):
+    p = str(tmp_path_factory.mktemp("m") / "b6c96.cfnn")
+    kc.write_random_model("b6c96", 0xC0FFEE, p)
+    return p
+
+
+def test_network_logits_vs_oracle(model_path):
+    path = [p for p in GOLD if "5x5" in p][0]
+    d, X, Y, W, n, hc, hd = _positions_with_history(path, 203)  # ragged: not a multiple of 8 boards
+    sym = np.random.default_rng(1).integers(0, 8, n).astype(np.int32)
+    packed, planes = kc.encode_batch(X, Y, W, d["colors"][:n], hc, hd, d["pla"][:n], sym)
+    net = kc.Network(model_path, X, Y, W)
+    out = net.forward(packed)
+    m = oracle.Model(model_path)
+    glob_in = np.full((n, 1), float(W), np.float32)
+    A = X * Y
+    for mode, tol in [(1, 1e-3), (0, 5e-2)]:
+        pol, val, misc = m.forward(X, Y, planes, glob_in, mode=mode, threads=8)
+        ref = np.concatenate([pol.reshape(n, 4 * A), val, misc], axis=1)
+        err = np.abs(out - ref).max()
+        print("mode", mode, "max |diff|", err, "max |ref|", np.abs(ref).max())
+        assert err <= tol, (mode, err)
+    # batch-size independence: evaluating a subset gives identical rows
+    np.testing.assert_array_equal(net.forward(packed[:17]), out[:17])
+    net.close()
+
+
+INFO_KEYS = [("phase", "phase"), ("rootK", "rootK"), ("liveCount", "nodeCount"), ("gameNum", "gameNum"),
+             ("turn", "turn"), ("pla", "pla"), ("playouts", "playouts"), ("nnEvals", "nnEvals"),
+             ("moves", "movesMade"), ("gamesFinished", "gamesFinished"), ("rngCtr", "rngCtr"),
+             ("lastCell", "lastCell"), ("lastDir", "lastDir")]
+
+
+def _sorted_rows(r):
+    order = np.lexsort((r["meta"][:, 2], r["meta"][:, 1], r["meta"][:, 0]))
+    return {k: v[order] for k, v in r.items()}
+
+
+@pytest.mark.parametrize("games,visits,rounds,seed", [(6, 40, 900, 3), (4, 24, 700, 99)])
+def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed):
+    cap = 128
+    gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1)
+    ora = oracle.Selfplay(5, 5, 4, games=games, max_visits=visits, node_cap=cap, seed=seed)
+    done = 0
+    for chunk in [1, 4, 20, rounds]:
+        step = chunk - done
+        if step <= 0:
+            continue
+        gpu.step(step)
+        ora.rounds(step)
+        done = chunk
+        for g in range(games):
+            gi, oi = gpu.game_info(g), ora.info(g)
+            for a, b in INFO_KEYS:
+                assert gi[a] == oi[b], (done, g, a, gi[a], oi[b])
+            gn, ge = gpu.game_tree(g)
+            on, oe = ora.game_tree(g)
+            np.testing.assert_array_equal(gn, on, err_msg="round %d game %d nodes" % (done, g))
+            np.testing.assert_array_equal(ge, oe, err_msg="round %d game %d edges" % (done, g))
+            if gi["phase"] == 1:
+                np.testing.assert_array_equal(gpu.root_policy(g), ora.root_noised(g))
+    st = gpu.stats()
+    assert st["games_finished"] > 0 and st["rows_dropped"] == 0
+    gr = _sorted_rows(gpu.drain_rows())
+    orr = _sorted_rows(ora.rows())
+    assert len(gr["meta"]) == len(orr["meta"]) > 0
+    for k in orr:
+        np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
+
+
+def test_selfplay_network_smoke(model_path):
+    sp = kc.Selfplay(5, 5, 4, num_games=64, max_visits=16, seed=5, model_path=model_path, commit_interval=4)
+    sp.step(800)
+    st = sp.stats()
+    assert st["playouts"] > 0 and st["nn_evals"] > 0 and st["moves"] > 0
+    assert st["games_finished"] > 0
+    r = sp.drain_rows()
+    n = len(r["meta"])
+    assert n == st["rows_written"] - st["rows_pending"] + n or n > 0
+    assert r["policyTargetsNCMove"][:, 0].sum(axis=1).min() > 0
+    np.testing.assert_array_equal(r["globalTargetsNC"][:, 63], 1.0)
+    sp.close()

@@ -1,0 +1,59 @@
+"""CPU checks of the oracle's self-play restatement (the checker the GPU parity
+tests trust): determinism, game/row invariants, row format."""
+import numpy as np
+
+from oracle import oracle
+
+
+def _run(seed, rounds=700):
+    sp = oracle.Selfplay(5, 5, 4, games=3, max_visits=24, node_cap=128, seed=seed)
+    sp.rounds(rounds)
+    return sp
+
+
+def test_deterministic_and_seed_sensitive():
+    a, b, c = _run(11), _run(11), _run(12)
+    ra, rb, rc = a.rows(), b.rows(), c.rows()
+    assert len(ra["meta"]) > 0
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k])
+    assert len(ra["meta"]) != len(rc["meta"]) or any(not np.array_equal(ra[k], rc[k]) for k in ra)
+
+
+def test_row_invariants():
+    sp = _run(5, rounds=900)
+    r = sp.rows()
+    n = len(r["meta"])
+    assert n > 0
+    meta = r["meta"]
+    # every finished game contributes numMoves consecutive rows, turns 0..numMoves-1
+    for slot, gnum in {(int(m[0]), int(m[1])) for m in meta}:
+        sel = (meta[:, 0] == slot) & (meta[:, 1] == gnum)
+        turns = np.sort(meta[sel, 2])
+        np.testing.assert_array_equal(turns, np.arange(meta[sel, 3][0]))
+    pol = r["policyTargetsNCMove"]
+    assert pol.min() >= 0 and pol[:, 0].sum(axis=1).min() > 0
+    gt = r["globalTargetsNC"]
+    np.testing.assert_array_equal(gt[:, 63], 1.0)
+    np.testing.assert_array_equal(gt[:, 25], 1.0)
+    # TD value targets are (win, loss) pairs summing to <= 1
+    for f in range(5):
+        s = gt[:, 2 * f] + gt[:, 2 * f + 1]
+        assert np.all(s <= 1.0 + 1e-5) and np.all(s >= -1e-6)
+    v = r["valueTargetsNCHW"]
+    assert set(np.unique(v[:, 0])) <= {-1, 0, 1}
+    assert np.all(v[:, 1] == 0)
+    assert v[:, 4].max() >= 4  # every game ends in a win (run >= winLen) or a draw
+    # global input = win length
+    np.testing.assert_array_equal(r["globalInputNC"][:, 0], 4.0)
+
+
+def test_tree_export_is_canonical():
+    sp = _run(3, rounds=150)
+    nodes, edges = sp.game_tree(0)
+    assert len(nodes) > 1
+    # root visits = 1 + sum of edge visits into its children after reuse-free start
+    root_children = nodes[0, 10] & 0xFFFF
+    assert root_children > 0
+    child_idx = edges[0, :root_children, 0]
+    assert np.all(child_idx < len(nodes))
