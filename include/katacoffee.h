@@ -190,6 +190,10 @@ int coffee_selfplay_root_policy(coffee_selfplay* h, int slot, float* out);
 
 /* Debug: the Student-t(3) CDF table the search uses (2000 f32). */
 int coffee_debug_cdf_table(int x, int y, int win_len, float* out /* host */);
+/* Debug: the Zobrist tables by cell (host): board [A][3][2], board2 [A][4][2],
+ * player [3][2], init [2] (size-X ^ size-Y hashes), game_over [2]. */
+int coffee_debug_zobrist(int x, int y, int win_len, uint64_t* board, uint64_t* board2, uint64_t* player,
+                         uint64_t* init, uint64_t* game_over);
 
 /* Kernel timing (HIP events on the engine stream) for roofline reporting:
  * which: 0 select, 1 network, 2 backup, 3 commit.  Summed ms and launch count. */

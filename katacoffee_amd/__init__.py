@@ -86,7 +86,7 @@ EXPORTS = [
     "coffee_nn_forward", "coffee_nn_destroy", "coffee_fake_net", "coffee_search_params_default",
     "coffee_selfplay_create", "coffee_selfplay_step", "coffee_selfplay_sync", "coffee_selfplay_stats_get",
     "coffee_selfplay_drain_rows", "coffee_selfplay_destroy", "coffee_selfplay_game_info",
-    "coffee_selfplay_game_tree", "coffee_selfplay_root_policy", "coffee_debug_cdf_table",
+    "coffee_selfplay_game_tree", "coffee_selfplay_root_policy", "coffee_debug_cdf_table", "coffee_debug_zobrist",
     "coffee_selfplay_enable_timing", "coffee_selfplay_kernel_time",
 ]
 
@@ -127,6 +127,7 @@ def lib():
         L.coffee_selfplay_enable_timing.argtypes = [c_p, c_i]
         L.coffee_selfplay_kernel_time.argtypes = [c_p, c_i, c_p, c_p]
         L.coffee_debug_cdf_table.argtypes = [c_i, c_i, c_i, c_p]
+        L.coffee_debug_zobrist.argtypes = [c_i, c_i, c_i] + [c_p] * 5
         _lib = L
     return _lib
 
@@ -285,6 +286,15 @@ def fake_net(X, Y, W, packed):
 def cdf_table(X=5, Y=5, W=4):
     out = np.zeros(2000, np.float32)
     check(lib().coffee_debug_cdf_table(X, Y, W, _ptr(out)))
+    return out
+
+
+def zobrist_tables(X, Y, W):
+    A = X * Y
+    out = dict(board=np.zeros((A, 3, 2), np.uint64), board2=np.zeros((A, 4, 2), np.uint64),
+               player=np.zeros((3, 2), np.uint64), init=np.zeros(2, np.uint64), game_over=np.zeros(2, np.uint64))
+    check(lib().coffee_debug_zobrist(X, Y, W, *[_ptr(out[k]) for k in ["board", "board2", "player", "init",
+                                                                          "game_over"]]))
     return out
 
 

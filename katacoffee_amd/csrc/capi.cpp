@@ -339,6 +339,20 @@ int coffee_debug_cdf_table(int x, int y, int win_len, float* out) {
   });
 }
 
+int coffee_debug_zobrist(int x, int y, int win_len, uint64_t* board, uint64_t* board2, uint64_t* player,
+                         uint64_t* init, uint64_t* game_over) {
+  return guarded([&] {
+    need(board && board2 && player && init && game_over, "NULL argument");
+    checkGeom(x, y, win_len);
+    DTables t = buildTables(x, y, win_len);
+    memcpy(board, t.zBoard, sizeof(uint64_t) * t.A * 3 * 2);
+    memcpy(board2, t.zBoard2, sizeof(uint64_t) * t.A * 4 * 2);
+    memcpy(player, t.zPlayer, sizeof(t.zPlayer));
+    memcpy(init, t.zInit, sizeof(t.zInit));
+    memcpy(game_over, t.zGameOver, sizeof(t.zGameOver));
+  });
+}
+
 int coffee_selfplay_enable_timing(coffee_selfplay* h, int enable) {
   return guarded([&] {
     need(h && h->eng, "NULL handle");

@@ -54,7 +54,7 @@ class NNEngine {
   int X_, Y_, W_;
   double flops_;
   NNLayout layout_;
-  void* wBf16_ = nullptr;  // device
+  void* wHalf_ = nullptr;  // device
   float* wF32_ = nullptr;  // device
   NNLayout* layoutDev_ = nullptr;
 };

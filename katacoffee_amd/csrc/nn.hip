@@ -8,12 +8,14 @@
 // MI355X design (DESIGN.md "NN forward"):
 //  * one 512-thread workgroup (8 waves) per 8 boards = 200 rows (positions),
 //    204 VGPRs -> 2 waves/SIMD, one resident workgroup per CU (LDS ~80 KB);
-//  * 3x3 convolutions are implicit GEMMs on v_mfma_f32_16x16x32_bf16:
-//    A = activations gathered from LDS by neighbour offset (bf16, NHWC, padded
+//  * 3x3 convolutions are implicit GEMMs on v_mfma_f32_16x16x32_f16 (fp16
+//    operands, f32 accumulation; same rate as bf16 on gfx950, 3 more mantissa
+//    bits, so logits stay within 1e-3 of the fp32 reference):
+//    A = activations gathered from LDS by neighbour offset (fp16, NHWC, padded
 //    rows -> conflict-free ds_read_b128), B = weights pre-swizzled on the host
 //    into per-lane 16-byte fragments streamed from L2 (one dwordx4 per lane);
-//  * the residual trunk x lives in registers (f32, accumulator layout) for the
-//    whole network; only the bf16 conv input is staged through LDS, so HBM sees
+//  * the residual trunk x lives in registers (fp16, accumulator layout) for the
+//    whole network; only the fp16 conv input is staged through LDS, so HBM sees
 //    the 48-byte packed input and the 416-byte output per board and nothing else;
 //  * BN + ReLU, global pooling, the gpool bias and both heads are fused epilogues.
 // Waves: rg = wave>>1 owns a contiguous range of 16-row tiles, cg = wave&1 owns
@@ -31,7 +33,7 @@
 
 namespace kc {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int X_, int Y_, int C_>
@@ -58,10 +60,7 @@ struct NNGeo {
   static_assert(LDS <= 163840, "LDS budget");
 };
 
-KC_D uint16_t bf16bits(float f) {
-  uint32_t u = __builtin_bit_cast(uint32_t, f);
-  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
+KC_D uint16_t f16bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }  // v_cvt_f16_f32, RNE
 
 // First accumulator row owned by this lane in tile tstart.  The empty asm makes
 // the value opaque so the compiler recomputes per-row LDS addresses at each use
@@ -74,7 +73,7 @@ KC_D int laneRow(int tstart, int lane) {
 
 // Implicit-GEMM convolution over the wave's tiles: acc[t][ct] += A(t, K) * B(K, ct).
 template <class G, int NTAPS, int NCB>
-KC_D void convTiles(const uint16_t* __restrict__ act, const bf16x8* __restrict__ w, f32x4 (&acc)[G::MAXT][G::NCT],
+KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, f32x4 (&acc)[G::MAXT][G::NCT],
                     int tstart, int ntiles, int cg, int lane) {
   const int kq = 8 * (lane >> 4);
   const int r0 = tstart * 16 + (lane & 15);
@@ -97,17 +96,17 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const bf16x8* __restrict__
 #pragma unroll 1
     for(int cb = 0; cb < NCB; cb++) {
       const int s = tap * NCB + cb;
-      bf16x8 bcur[G::NCT];
+      h16x8 bcur[G::NCT];
 #pragma unroll
       for(int ct = 0; ct < G::NCT; ct++)
         bcur[ct] = w[((size_t)s * G::NCT_ALL + cg * G::NCT + ct) * 64 + lane];
 #pragma unroll
       for(int t = 0; t < G::MAXT; t++) {
         if(t < ntiles) {
-          bf16x8 a = *reinterpret_cast<const bf16x8*>(act + roff[t] + cb * 32);
+          h16x8 a = *reinterpret_cast<const h16x8*>(act + roff[t] + cb * 32);
 #pragma unroll
           for(int ct = 0; ct < G::NCT; ct++)
-            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bcur[ct], acc[t][ct], 0, 0, 0);
+            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bcur[ct], acc[t][ct], 0, 0, 0);
         }
       }
     }
@@ -164,7 +163,7 @@ KC_D void storeBnRelu(uint16_t* act, const V (&v)[G::MAXT][G::NCT], const float*
         int row = rl + t * 16 + j;
         float x = (float)v[t][ct][j] * sc + bi;
         x = x > 0.0f ? x : 0.0f;
-        act[row * G::ASTR + col] = bf16bits(x);
+        act[row * G::ASTR + col] = f16bits(x);
       }
     }
   }
@@ -172,7 +171,7 @@ KC_D void storeBnRelu(uint16_t* act, const V (&v)[G::MAXT][G::NCT], const float*
 
 template <int X, int Y, int C>
 __global__ void __launch_bounds__(512, 2)
-    kNNForward(const NNLayout* __restrict__ L, const bf16x8* __restrict__ WB, const float* __restrict__ WF, int n,
+    kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF, int n,
                const int* __restrict__ countDev, int inWords, float winLen, const uint64_t* __restrict__ in,
                float* __restrict__ out) {
   using G = NNGeo<X, Y, C>;
@@ -203,7 +202,7 @@ __global__ void __launch_bounds__(512, 2)
       int b = row / G::A, p = row - b * G::A;
       int i = c * G::A + p;
       uint64_t word = in[(size_t)(base + b) * inWords + (i >> 6)];
-      v = ((word >> (i & 63)) & 1ULL) ? (uint16_t)0x3f80 : (uint16_t)0;
+      v = ((word >> (i & 63)) & 1ULL) ? (uint16_t)0x3c00 : (uint16_t)0;
     }
     act[row * G::ASTR + c] = v;
   }
@@ -317,7 +316,7 @@ __global__ void __launch_bounds__(512, 2)
               int brd = row / G::A;
               brd = brd < G::NB ? brd : G::NB - 1;
               float v = (acc[t][ct][j] + biasS[brd * Cr + col]) * sc + bi;
-              act[row * G::ASTR + col] = bf16bits(v > 0.0f ? v : 0.0f);
+              act[row * G::ASTR + col] = f16bits(v > 0.0f ? v : 0.0f);
             }
           }
         }
@@ -460,10 +459,22 @@ __global__ void __launch_bounds__(512, 2)
 // ---------------------------------------------------------------------------
 // Host: pack weights into B-fragment order and launch.
 
-static uint16_t f2bf(float f) {
+// float -> IEEE binary16 bits, round to nearest even (weights; saturates to inf).
+static uint16_t f2h(float f) {
   uint32_t u;
   memcpy(&u, &f, 4);
-  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  const uint32_t sign = (u >> 16) & 0x8000u, a = u & 0x7fffffffu;
+  if(a >= 0x7f800000u)
+    return (uint16_t)(sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u));
+  if(a < 0x38800000u) {  // subnormal half: quantum 2^-24
+    float m;
+    memcpy(&m, &a, 4);
+    return (uint16_t)(sign | (uint32_t)nearbyintf(m * 16777216.0f));
+  }
+  uint32_t r = a + 0xfffu + ((a >> 13) & 1u);
+  if(r >= 0x47800000u)
+    return (uint16_t)(sign | 0x7c00u);
+  return (uint16_t)(sign | (((r >> 23) - 112u) << 10) | ((r >> 13) & 0x3ffu));
 }
 
 // B fragment order for one conv: [kstep = tap*NCB + cb][coltile][lane][8],
@@ -477,7 +488,7 @@ static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout
         for(int l = 0; l < 64; l++)
           for(int j = 0; j < 8; j++) {
             int co = ct * 16 + (l & 15), ci = cb * 32 + 8 * (l >> 4) + j;
-            dst.push_back(f2bf(W(co, ci, tap)));
+            dst.push_back(f2h(W(co, ci, tap)));
           }
 }
 
@@ -556,8 +567,8 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W) : cfg_(m.cfg), X_(X)
   L.vB3 = f32(m.vB3);
   L.vLinM = f32(m.vLinM);
   L.vBM = f32(m.vBM);
-  KC_HIP(hipMalloc(&wBf16_, wb.size() * 2));
-  KC_HIP(hipMemcpy(wBf16_, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
+  KC_HIP(hipMalloc(&wHalf_, wb.size() * 2));
+  KC_HIP(hipMemcpy(wHalf_, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&wF32_, wf.size() * 4));
   KC_HIP(hipMemcpy(wF32_, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&layoutDev_, sizeof(NNLayout)));
@@ -570,7 +581,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W) : cfg_(m.cfg), X_(X)
 }
 
 NNEngine::~NNEngine() {
-  (void)hipFree(wBf16_);
+  (void)hipFree(wHalf_);
   (void)hipFree(wF32_);
   (void)hipFree(layoutDev_);
 }
@@ -582,7 +593,7 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
   int grid = (n + G::NB - 1) / G::NB;
   hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(512), G::LDS, st, layoutDev_,
-                     (const bf16x8*)wBf16_, wF32_, n, countDev, inWords, (float)W_, in, out);
+                     (const h16x8*)wHalf_, wF32_, n, countDev, inWords, (float)W_, in, out);
   KC_HIP(hipGetLastError());
 }
 

@@ -182,6 +182,7 @@ uint64_t murmurMix(uint64_t x) {
 }
 
 uint64_t splitMix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ULL;
   x ^= x >> 30;
   x *= 0xbf58476d1ce4e5b9ULL;
   x ^= x >> 27;

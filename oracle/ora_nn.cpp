@@ -8,7 +8,7 @@
 //   Trunk :1169-1227, PolicyHead :1229-1299 (Coffee: 4 direction logits, no pass),
 //   ValueHead :1301-1377 (Coffee: win/loss logits + 2 misc).
 // Boards always fill the NN input here (nnLen == board size), so the mask is 1.
-// mode 1 rounds every convolution weight and convolution input to bf16 (RNE)
+// mode 1 rounds every convolution weight and convolution input to fp16 (RNE)
 // and the residual trunk to fp16 (RNE) after the stem and after every block,
 // exactly where the HIP kernel does, to compare with it at accumulation-order
 // precision.
@@ -20,17 +20,6 @@
 #include "ora.h"
 
 namespace ora {
-
-static inline float bf16r(float f) {
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  if((u & 0x7f800000u) == 0x7f800000u)
-    return f;
-  u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
-  float r;
-  memcpy(&r, &u, 4);
-  return r;
-}
 
 // float -> IEEE binary16 -> float, round to nearest even (v_cvt_f16_f32).
 static inline float f16r(float f) {
@@ -143,7 +132,7 @@ void conv3(const Ctx& cx, const float* in, int cin, const float* w, int cout, fl
     for(int ci = 0; ci < cin; ci++)
       for(int t = 0; t < 9; t++) {
         float v = w[((size_t)co * cin + ci) * 9 + t];
-        wt[((size_t)t * cin + ci) * cout + co] = cx.bf ? bf16r(v) : v;
+        wt[((size_t)t * cin + ci) * cout + co] = cx.bf ? f16r(v) : v;
       }
   std::vector<float> acc((size_t)cout);
   for(int y = 0; y < cx.Y; y++)
@@ -158,7 +147,7 @@ void conv3(const Ctx& cx, const float* in, int cin, const float* w, int cout, fl
         for(int ci = 0; ci < cin; ci++) {
           float v = ip[ci];
           if(cx.bf)
-            v = bf16r(v);
+            v = f16r(v);
           const float* wr = wp + (size_t)ci * cout;
           for(int co = 0; co < cout; co++)
             acc[co] += v * wr[co];
@@ -178,8 +167,8 @@ void conv1(const Ctx& cx, const float* in, int cin, const float* w, int cout, fl
       for(int ci = 0; ci < cin; ci++) {
         float v = in[(size_t)a * cin + ci], ww = w[(size_t)co * cin + ci];
         if(roundBf) {
-          v = bf16r(v);
-          ww = bf16r(ww);
+          v = f16r(v);
+          ww = f16r(ww);
         }
         s += v * ww;
       }

@@ -76,3 +76,18 @@ def test_random_model_roundtrip(L, tmp_path):
     X[0, 0] = 1.0
     pol, val, misc = m.forward(5, 5, X, np.array([[4.0]], np.float32))
     assert np.all(np.isfinite(pol)) and np.all(np.isfinite(val))
+
+
+@pytest.mark.parametrize("X,Y,W", [(5, 5, 4), (7, 7, 5), (9, 9, 5), (10, 10, 5), (6, 4, 3)])
+def test_zobrist_tables_match_reference(L, X, Y, W):
+    # Board::initHash board.cpp:134-178 as the reference computes it (tests/golden/zobrist.npz
+    # was written by oracle/ref/refgen from the reference sources), indexed by our cell order.
+    z = np.load(os.path.join(REPO, "tests", "golden", "zobrist.npz"))
+    t = kc.zobrist_tables(X, Y, W)
+    cells = np.arange(X * Y)
+    spot = (cells % X + 1) + (cells // X + 1) * (X + 1)
+    np.testing.assert_array_equal(t["board"], z["board"][spot, :3])
+    np.testing.assert_array_equal(t["board2"], z["board2"][spot])
+    np.testing.assert_array_equal(t["player"], z["player"][:3])
+    np.testing.assert_array_equal(t["init"], z["size_x"][X] ^ z["size_y"][Y])
+    np.testing.assert_array_equal(t["game_over"], z["game_over"])
