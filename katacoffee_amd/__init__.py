@@ -102,6 +102,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise CoffeeError("libkatacoffee.so not built (run katacoffee_amd.build()); no CPU fallback exists")
+        # One HIP runtime per process: torch's libraries ask for "libamdhip64.so" while
+        # ours asks for the SONAME "libamdhip64.so.7".  Loading torch first lets our
+        # request resolve to torch's already-loaded copy; the reverse order would load
+        # two runtimes, and ours would then see no device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         L.coffee_last_error.restype = ctypes.c_char_p
         L.coffee_model_write_random.argtypes = [ctypes.c_char_p, c_u64, ctypes.c_char_p]

@@ -42,10 +42,11 @@ struct NNGeo {
   static constexpr int NB = 8;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
-  // rows [ROWS, RT*16) are tile padding (computed, never read as neighbours);
-  // ZROW is the all-zero row that out-of-board neighbour taps read.
-  static constexpr int ZROW = RT * 16;
-  static constexpr int TBASE = RT / 4, TREM = RT % 4, MAXT = TBASE + (TREM > 0 ? 1 : 0);
+  // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): rows
+  // [ROWS, 64*MAXT) are padding (computed, never read as neighbours); ZROW is
+  // the all-zero row that out-of-board neighbour taps read.
+  static constexpr int MAXT = (RT + 3) / 4;
+  static constexpr int ZROW = 4 * MAXT * 16;
   static constexpr int ASTR = C + 8;     // bf16 per activation row (+16 B pad: conflict-free b128 reads)
   static constexpr int NCT = C / 32;     // 16-col tiles per wave
   static constexpr int NCT_ALL = C / 16;
@@ -54,11 +55,27 @@ struct NNGeo {
   static constexpr int OFF_POOL = OFF_SCR + ZROW * 32 * 4;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
-  static constexpr int LDS = OFF_VH + NB * 64 * 4;
+  static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap (one buffer)
+  static constexpr int OFF_W = (OFF_VH + NB * 64 * 4 + 15) / 16 * 16;
+  static constexpr int LDS = OFF_W + 2 * WBUF * 16;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
   static_assert(ZROW * 32 * 4 <= (ZROW + 1) * ASTR * 2, "value-branch f32 scratch must fit in act");
   static_assert(LDS <= 163840, "LDS budget");
 };
+
+#ifdef KC_NN_PROFILE
+// Phase timestamps (shader clock) of the first workgroups: tools/nn_phase.hip.
+__device__ unsigned long long g_nnPhase[4][64];
+#define NN_PHASE(i)                                  \
+  do {                                               \
+    if(blockIdx.x < 4 && threadIdx.x == 0)           \
+      g_nnPhase[blockIdx.x][(i)] = clock64();        \
+  } while(0)
+#else
+#define NN_PHASE(i) \
+  do {              \
+  } while(0)
+#endif
 
 KC_D uint16_t f16bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }  // v_cvt_f16_f32, RNE
 
@@ -72,13 +89,39 @@ KC_D int laneRow(int tstart, int lane) {
 }
 
 // Implicit-GEMM convolution over the wave's tiles: acc[t][ct] += A(t, K) * B(K, ct).
+// Weights are staged per tap through a double-buffered LDS slab shared by the
+// workgroup's 8 waves: the next tap's fragments are loaded from L2 into registers
+// while this tap's MFMAs run, then stored to the other buffer (one barrier per tap).
 template <class G, int NTAPS, int NCB>
-KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, f32x4 (&acc)[G::MAXT][G::NCT],
-                    int tstart, int ntiles, int cg, int lane) {
+KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
+                    f32x4 (&acc)[G::MAXT][G::NCT], int tstart, int ntiles, int cg, int lane, int tid) {
+  constexpr int UNITS = NCB * G::NCT_ALL * 64;  // 16-B fragments per tap
+  constexpr int PER = (UNITS + 511) / 512;
+  {
+    h16x8 r[PER];
+#pragma unroll
+    for(int u = 0; u < PER; u++)
+      if(tid + u * 512 < UNITS)
+        r[u] = w[tid + u * 512];
+#pragma unroll
+    for(int u = 0; u < PER; u++)
+      if(tid + u * 512 < UNITS)
+        wl[tid + u * 512] = r[u];
+  }
+  __syncthreads();
   const int kq = 8 * (lane >> 4);
   const int r0 = tstart * 16 + (lane & 15);
 #pragma unroll 1
   for(int tap = 0; tap < NTAPS; tap++) {
+    const bool more = tap + 1 < NTAPS;
+    h16x8 nx[PER];
+    if(more) {
+#pragma unroll
+      for(int u = 0; u < PER; u++)
+        if(tid + u * 512 < UNITS)
+          nx[u] = w[(size_t)(tap + 1) * UNITS + tid + u * 512];
+    }
+    const h16x8* wb = wl + (tap & 1) * G::WBUF;
     const int dy = NTAPS == 9 ? tap / 3 - 1 : 0;
     const int dx = NTAPS == 9 ? tap % 3 - 1 : 0;
     // neighbour row (or the zero row) per tile, as an LDS element offset
@@ -93,13 +136,12 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
       bool ok = r < G::ROWS && yy >= 0 && yy < G::Y && xx >= 0 && xx < G::X;
       roff[t] = (ok ? (r + dy * G::X + dx) : G::ZROW) * G::ASTR + kq;
     }
-#pragma unroll 1
+#pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
-      const int s = tap * NCB + cb;
       h16x8 bcur[G::NCT];
 #pragma unroll
       for(int ct = 0; ct < G::NCT; ct++)
-        bcur[ct] = w[((size_t)s * G::NCT_ALL + cg * G::NCT + ct) * 64 + lane];
+        bcur[ct] = wb[(cb * G::NCT_ALL + cg * G::NCT + ct) * 64 + lane];
 #pragma unroll
       for(int t = 0; t < G::MAXT; t++) {
         if(t < ntiles) {
@@ -110,10 +152,33 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
         }
       }
     }
+    if(more) {
+      h16x8* nb = wl + ((tap + 1) & 1) * G::WBUF;
+#pragma unroll
+      for(int u = 0; u < PER; u++)
+        if(tid + u * 512 < UNITS)
+          nb[tid + u * 512] = nx[u];
+    }
+    __syncthreads();
   }
 }
 
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// Copies a row-major [rows][96] f32 matrix (global, 16-B aligned) into LDS
+// transposed to [96][rows], so that threads of one wave (consecutive output
+// rows) read consecutive banks in the dot-product loops.
+KC_D void stageT96(float* __restrict__ dst, const float* __restrict__ src, int rows, int tid) {
+  const int n4 = rows * 24;
+  for(int q = tid; q < n4; q += 512) {
+    const int o = q / 24, i4 = (q - o * 24) * 4;
+    const float4 v = reinterpret_cast<const float4*>(src)[q];
+    dst[(i4 + 0) * rows + o] = v.x;
+    dst[(i4 + 1) * rows + o] = v.y;
+    dst[(i4 + 2) * rows + o] = v.z;
+    dst[(i4 + 3) * rows + o] = v.w;
+  }
+}
 
 // The residual trunk is kept in registers as fp16 (RNE) between blocks; the
 // oracle's GPU-emulation mode rounds at the same points.
@@ -176,6 +241,7 @@ __global__ void __launch_bounds__(512, 2)
                float* __restrict__ out) {
   using G = NNGeo<X, Y, C>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  NN_PHASE(0);
   const int count = countDev ? min(*countDev, n) : n;
   const int base = blockIdx.x * G::NB;
   if(base >= count)
@@ -183,8 +249,8 @@ __global__ void __launch_bounds__(512, 2)
   const int nb = min(G::NB, count - base);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rg = wave >> 1, cg = wave & 1;
-  const int tstart = rg * G::TBASE + min(rg, G::TREM);
-  const int ntiles = G::TBASE + (rg < G::TREM ? 1 : 0);
+  const int tstart = rg * G::MAXT;
+  const int ntiles = G::MAXT;
   uint16_t* act = reinterpret_cast<uint16_t*>(smem);
   float* actF = reinterpret_cast<float*>(smem);
   float* scr = reinterpret_cast<float*>(smem + G::OFF_SCR);
@@ -192,6 +258,7 @@ __global__ void __launch_bounds__(512, 2)
   float* poolV = poolP + G::NB * 96;
   float* biasS = reinterpret_cast<float*>(smem + G::OFF_BIAS);
   float* vh = reinterpret_cast<float*>(smem + G::OFF_VH);
+  h16x8* wl = reinterpret_cast<h16x8*>(smem + G::OFF_W);
   const float sqOff = sqrtf((float)G::A) - 14.0f;
 
   // ---- unpack the packed V1 planes: act[row][0..31] (15 planes + zero pad), zero row ----
@@ -210,10 +277,11 @@ __global__ void __launch_bounds__(512, 2)
     act[G::ZROW * G::ASTR + c] = 0;
   __syncthreads();
 
+  NN_PHASE(1);
   f16x4 x[G::MAXT][G::NCT];
   f32x4 acc[G::MAXT][G::NCT];
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1>(act, WB + L->wInit, acc, tstart, ntiles, cg, lane);
+  convTiles<G, 9, 1>(act, WB + L->wInit, wl, acc, tstart, ntiles, cg, lane, tid);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
 #pragma unroll
@@ -229,18 +297,23 @@ __global__ void __launch_bounds__(512, 2)
   }
   packX<G>(x, acc);
   const int Cr = G::C - L->Cg;
+  NN_PHASE(2);
   for(int blk = 0; blk < L->nblocks; blk++) {
     __syncthreads();  // previous conv finished reading act
+    NN_PHASE(3 + 4 * blk);
     storeBnRelu<G>(act, x, WF + L->bn1s[blk], WF + L->bn1b[blk], tstart, ntiles, cg, lane, 0, G::C);
     __syncthreads();
     zeroAcc<G>(acc);
-    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], acc, tstart, ntiles, cg, lane);
+    NN_PHASE(4 + 4 * blk);
+    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], wl, acc, tstart, ntiles, cg, lane, tid);
     __syncthreads();
+    NN_PHASE(5 + 4 * blk);
     if(L->kinds[blk] == 0) {
       storeBnRelu<G>(act, acc, WF + L->bn2s[blk], WF + L->bn2b[blk], tstart, ntiles, cg, lane, 0, G::C);
       __syncthreads();
       unpackX<G>(acc, x);
-      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], acc, tstart, ntiles, cg, lane);
+      NN_PHASE(6 + 4 * blk);
+      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], wl, acc, tstart, ntiles, cg, lane, tid);
       packX<G>(x, acc);
     } else {
       // g branch: BN-ReLU into scr (f32), then KataGPool per board (model_pytorch.py:326-352)
@@ -267,6 +340,9 @@ __global__ void __launch_bounds__(512, 2)
         }
       }
       __syncthreads();
+      NN_PHASE(50);
+      float* lgT = reinterpret_cast<float*>(wl);  // weight slab is idle between convs
+      stageT96(lgT, WF + L->linG[blk], Cr, tid);
       for(int idx = tid; idx < G::NB * 32; idx += 512) {
         const int b = idx >> 5, c = idx & 31;
         float s = 0.0f, m = 0.0f;
@@ -282,18 +358,19 @@ __global__ void __launch_bounds__(512, 2)
         poolP[b * 96 + 64 + c] = m;
       }
       __syncthreads();
+      NN_PHASE(51);
       {
-        const float* lg = WF + L->linG[blk];
         for(int idx = tid; idx < G::NB * Cr; idx += 512) {
           const int b = idx / Cr, o = idx - b * Cr;
           float s = 0.0f;
-#pragma unroll 4
+#pragma unroll 8
           for(int i = 0; i < 96; i++)
-            s += lg[o * 96 + i] * poolP[b * 96 + i];
+            s += lgT[i * Cr + o] * poolP[b * 96 + i];
           biasS[b * Cr + o] = s;
         }
       }
       __syncthreads();
+      NN_PHASE(52);
       {
         // r branch + gpool bias -> BN2-ReLU -> bf16 act (cols < Cr)
         const float* s2 = WF + L->bn2s[blk];
@@ -323,18 +400,21 @@ __global__ void __launch_bounds__(512, 2)
       }
       __syncthreads();
       unpackX<G>(acc, x);
-      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], acc, tstart, ntiles, cg, lane);
+      NN_PHASE(6 + 4 * blk);
+      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], wl, acc, tstart, ntiles, cg, lane, tid);
       packX<G>(x, acc);
     }
   }
   // ---- trunk tip ----
   __syncthreads();
+  NN_PHASE(40);
   storeBnRelu<G>(act, x, WF + L->tips, WF + L->tipb, tstart, ntiles, cg, lane, 0, G::C);
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, acc, tstart, ntiles, cg, lane);
+  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, wl, acc, tstart, ntiles, cg, lane, tid);
   __syncthreads();  // act dead from here; reuse it as f32 [ROWS][32] for the value branch
+  NN_PHASE(41);
   {
     const float* pbg = WF + L->pBiasG;
     const float* vb1 = WF + L->vBias1;
@@ -362,6 +442,11 @@ __global__ void __launch_bounds__(512, 2)
     }
   }
   __syncthreads();
+  NN_PHASE(53);
+  float* plgT = reinterpret_cast<float*>(wl);
+  float* l2T = plgT + 32 * 96;
+  stageT96(plgT, WF + L->pLinG, 32, tid);
+  stageT96(l2T, WF + L->vLin2, L->v2, tid);
   for(int idx = tid; idx < G::NB * 32; idx += 512) {
     const int b = idx >> 5, c = idx & 31;
     float s = 0.0f, m = 0.0f, sv = 0.0f;
@@ -381,25 +466,24 @@ __global__ void __launch_bounds__(512, 2)
     poolV[b * 96 + 64 + c] = meanv * ((sqOff * sqOff) / 100.0f - 0.1f);
   }
   __syncthreads();
+  NN_PHASE(54);
   {
-    const float* plg = WF + L->pLinG;
     for(int idx = tid; idx < G::NB * 32; idx += 512) {
       const int b = idx >> 5, o = idx & 31;
       float s = 0.0f;
-#pragma unroll 4
+#pragma unroll 8
       for(int i = 0; i < 96; i++)
-        s += plg[o * 96 + i] * poolP[b * 96 + i];
+        s += plgT[i * 32 + o] * poolP[b * 96 + i];
       biasS[b * 32 + o] = s;
     }
     const int v2 = L->v2;
-    const float* l2 = WF + L->vLin2;
     const float* b2 = WF + L->vB2;
     for(int idx = tid; idx < G::NB * v2; idx += 512) {
       const int b = idx / v2, oo = idx - b * v2;
       float t = b2[oo];
-#pragma unroll 4
+#pragma unroll 8
       for(int i = 0; i < 96; i++)
-        t += l2[oo * 96 + i] * poolV[b * 96 + i];
+        t += l2T[i * v2 + oo] * poolV[b * 96 + i];
       vh[b * 64 + oo] = t > 0.0f ? t : 0.0f;
     }
   }
@@ -416,6 +500,7 @@ __global__ void __launch_bounds__(512, 2)
       out[(size_t)(base + b) * (G::P + 4) + G::P + o] = s;
     }
   }
+  NN_PHASE(42);
   if(cg == 0) {
     // policy: relu(p + gpool bias + bias2) -> 1x1 conv p1 -> 4 direction logits
     const float* pb2 = WF + L->pBias2;

@@ -56,18 +56,26 @@ struct GV {
   KC_D int16_t* turnPol(int t) const { return d.turnPol + ((size_t)g * d.maxTurns + t) * d.P; }
 };
 
-// Uniform state of one game, held identically by every lane; lane 0 stores.
-struct GS {
-  GameDev s;
-  KC_D DRng rng() const { return DRng{s.rngSeed, s.rngCtr}; }
-};
-
+// The game's uniform state lives in LDS for the kernel's duration (one wave per
+// block): every lane executes the same updates, so same-value LDS writes from
+// all lanes are benign and program order keeps them visible to later reads.
+// Keeping it out of registers roughly halves the kernels' VGPR use.
+static_assert(sizeof(GameDev) % 4 == 0, "GameDev copy granularity");
 KC_D void storeGame(const GV& v, const GameDev& s) {
-  if(v.lane == 0)
-    v.d.games[v.g] = s;
+  waveSync();
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&s);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&v.d.games[v.g]);
+  for(int i = v.lane; i < (int)(sizeof(GameDev) / 4); i += 64)
+    dst[i] = src[i];
 }
 
-KC_D void loadGame(const GV& v, GameDev& s) { s = v.d.games[v.g]; }
+KC_D void loadGame(const GV& v, GameDev& s) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&v.d.games[v.g]);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&s);
+  for(int i = v.lane; i < (int)(sizeof(GameDev) / 4); i += 64)
+    dst[i] = src[i];
+  waveSync();
+}
 
 template <int NI>
 KC_D float tsum(const float (&x)[NI], int n, int lane) {
@@ -535,7 +543,12 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
     }
     if(slot == n.numChildren) {
       const int cell = newPos % T.A, dir = newPos / T.A;
-      DBoard before = b;
+      // SVB key of the expansion (needs the board before the move); computed
+      // up front so no second board copy stays live across playMoveWave.
+      const bool svbKeyed = sp.svbFactor != 0.0f && hCell(b, 0) >= 0;
+      uint64_t svbKey = 0;
+      if(svbKeyed)
+        svbKey = svbKeyOf(v, b, hDir(b, 0) * T.A + hCell(b, 0), newPos, b.pla);
       playMoveWave(T, b, cell, dir);
       uint64_t k0, k1;
       stateHash(T, b, k0, k1);
@@ -547,10 +560,8 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
           s.leafNode = ni;
           break;
         }
-        if(sp.svbFactor != 0.0f && hCell(before, 0) >= 0) {
-          int ppos = hDir(before, 0) * T.A + hCell(before, 0);
-          uint64_t key = svbKeyOf(v, before, ppos, newPos, before.pla);
-          int e = svbFindOrInsert(v, s.svbSel, key);
+        if(svbKeyed) {
+          int e = svbFindOrInsert(v, s.svbSel, svbKey);
           waveSync();
           if(v.lane == 0)
             v.nodes()[child].svbEntry = e;
@@ -600,14 +611,14 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
 // ---------------------------------------------------------------------------
 // kSelect: root evaluation or one descent; NN leaves are encoded into the batch.
 template <int NI>
-__global__ void __launch_bounds__(64) kSelect(const SearchDev* __restrict__ dp) {
+__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* __restrict__ dp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
   if(g >= d.G)
     return;
   __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
   GV v(d, g);
-  GameDev s;
+  __shared__ GameDev s;
   loadGame(v, s);
   if(s.phase == PH_COMMIT) {
     s.leafKind = LEAF_NONE;
@@ -802,7 +813,7 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
     return;
   __shared__ float scratch[2 * MAX_P];
   GV v(d, g);
-  GameDev s;
+  __shared__ GameDev s;
   loadGame(v, s);
   if(s.leafKind == LEAF_NONE)
     return;
@@ -1546,7 +1557,7 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp) 
   uint32_t* liveBits = reinterpret_cast<uint32_t*>(boards + (MAX_AREA + 1));  // [cap/32]
   uint16_t* queue = reinterpret_cast<uint16_t*>(liveBits + d.cap / 32);     // [cap]
   GV v(d, g);
-  GameDev s;
+  __shared__ GameDev s;
   loadGame(v, s);
   const SP& sp = d.sp;
   const int P = d.P, A = d.A;
@@ -1658,9 +1669,10 @@ __global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp) {
   if(g >= d.G)
     return;
   GV v(d, g);
-  GameDev s;
-  for(int i = 0; i < (int)(sizeof(GameDev) / 4); i++)
+  __shared__ GameDev s;
+  for(int i = v.lane; i < (int)(sizeof(GameDev) / 4); i += 64)
     reinterpret_cast<uint32_t*>(&s)[i] = 0;
+  waveSync();
   s.svbSel = 0;
   s.gameNum = 0;
   startGame(v, s);
