@@ -85,6 +85,7 @@ def main():
     import torch
 
     import katacoffee_amd as kc
+    from katacoffee_amd import rows as kcrows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -124,19 +125,9 @@ def main():
         n = len(rows["meta"])
         if dist is not None:
             # RCCL gather of this step's finished rows to rank 0 (the writer rank)
-            blob = torch.from_numpy(rows["policyTargetsNCMove"].reshape(n, -1).view("uint8").copy()
-                                    if n else torch.zeros(0, dtype=torch.uint8).numpy()).cuda()
-            cnt = torch.tensor([n], device="cuda")
-            cnts = [torch.zeros_like(cnt) for _ in range(world)]
-            dist.all_gather(cnts, cnt)
-            mx = int(max(c.item() for c in cnts))
-            rowbytes = 2 * 2 * 100
-            pad = torch.zeros((mx, rowbytes), dtype=torch.uint8, device="cuda")
-            if n:
-                pad[:n] = blob.view(n, rowbytes)
-            outs = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
-            dist.gather(pad, outs, dst=0)
-            rows_gathered += sum(int(c.item()) for c in cnts)
+            got = kcrows.gather_to_rank0(rows, 5, 5, dist, torch.device("cuda", local))
+            if rank == 0:
+                rows_gathered += len(got["meta"])
         else:
             rows_gathered += n
     sp.sync()

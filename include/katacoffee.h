@@ -177,6 +177,14 @@ int coffee_selfplay_drain_rows(coffee_selfplay* h, int max_rows, uint8_t* bin, f
                                float* gtgt, int8_t* value, int32_t* meta, int* n_out);
 int coffee_selfplay_destroy(coffee_selfplay* h);
 
+/* Writes n rows (HOST arrays, drain_rows layout) as a training .npz in the reference's
+ * format (TrainingWriteBuffers::writeToZipFile trainingwrite.cpp:566-587): members
+ * binaryInputNCHWPacked, globalInputNC, policyTargetsNCMove, globalTargetsNC,
+ * valueTargetsNCHW, each a v1.0 .npy with a 256-byte header; written to path.tmp
+ * and renamed into place. */
+int coffee_write_npz(const char* path, int n, int x, int y, const uint8_t* bin, const float* glob,
+                     const int16_t* pol, const float* gtgt, const int8_t* value);
+
 /* Device-side inspection for parity tests and tools (host outputs). */
 /* info[16] i64: phase, rootK, nodeCount, rootIdx, gameNum, turn, pla, finished, winner,
  *               playouts, nnEvals, moves, gamesFinished, lastCell, lastDir, rng counter */

@@ -87,7 +87,7 @@ EXPORTS = [
     "coffee_selfplay_create", "coffee_selfplay_step", "coffee_selfplay_sync", "coffee_selfplay_stats_get",
     "coffee_selfplay_drain_rows", "coffee_selfplay_destroy", "coffee_selfplay_game_info",
     "coffee_selfplay_game_tree", "coffee_selfplay_root_policy", "coffee_debug_cdf_table", "coffee_debug_zobrist",
-    "coffee_selfplay_enable_timing", "coffee_selfplay_kernel_time",
+    "coffee_selfplay_enable_timing", "coffee_selfplay_kernel_time", "coffee_write_npz",
 ]
 
 
@@ -136,6 +136,7 @@ def lib():
         L.coffee_selfplay_kernel_time.argtypes = [c_p, c_i, c_p, c_p]
         L.coffee_debug_cdf_table.argtypes = [c_i, c_i, c_i, c_p]
         L.coffee_debug_zobrist.argtypes = [c_i, c_i, c_i] + [c_p] * 5
+        L.coffee_write_npz.argtypes = [ctypes.c_char_p, c_i, c_i, c_i] + [c_p] * 5
         _lib = L
     return _lib
 
@@ -295,6 +296,15 @@ def cdf_table(X=5, Y=5, W=4):
     out = np.zeros(2000, np.float32)
     check(lib().coffee_debug_cdf_table(X, Y, W, _ptr(out)))
     return out
+
+
+def write_npz(path, rows, X, Y):
+    """Training rows -> .npz in the reference's format (native writer)."""
+    n = len(rows["globalInputNC"])
+    arrs = [np.ascontiguousarray(rows[k], dtype=t) for k, t in
+            [("binaryInputNCHWPacked", np.uint8), ("globalInputNC", np.float32), ("policyTargetsNCMove", np.int16),
+             ("globalTargetsNC", np.float32), ("valueTargetsNCHW", np.int8)]]
+    check(lib().coffee_write_npz(path.encode(), n, X, Y, *[_ptr(a) for a in arrs]))
 
 
 def zobrist_tables(X, Y, W):

@@ -10,6 +10,7 @@
 #include "../../include/katacoffee.h"
 #include "engine.h"
 #include "model.h"
+#include "npzwrite.h"
 #include "selfplay.h"
 
 namespace kc {
@@ -305,6 +306,15 @@ int coffee_selfplay_destroy(coffee_selfplay* h) {
       delete h->eng;
       delete h;
     }
+  });
+}
+
+int coffee_write_npz(const char* path, int n, int x, int y, const uint8_t* bin, const float* glob,
+                     const int16_t* pol, const float* gtgt, const int8_t* value) {
+  return guarded([&] {
+    need(path != nullptr, "NULL path");
+    need(n >= 0 && x >= 2 && y >= 2 && x <= MAX_LEN && y <= MAX_LEN, "bad shape");
+    writeNpz(path, n, x, y, bin, glob, pol, gtgt, value);
   });
 }
 

@@ -91,3 +91,25 @@ def test_zobrist_tables_match_reference(L, X, Y, W):
     np.testing.assert_array_equal(t["player"], z["player"][:3])
     np.testing.assert_array_equal(t["init"], z["size_x"][X] ^ z["size_y"][Y])
     np.testing.assert_array_equal(t["game_over"], z["game_over"])
+
+
+def test_npz_writer_roundtrip(L, tmp_path):
+    # rows from the oracle engine, written by the native writer, read back with numpy
+    sp = oracle.Selfplay(5, 5, 4, games=2, max_visits=12, node_cap=64, seed=3)
+    sp.rounds(400)
+    rows = sp.rows()
+    assert len(rows["meta"]) > 0
+    path = str(tmp_path / "rows.npz")
+    kc.write_npz(path, rows, 5, 5)
+    assert not os.path.exists(path + ".tmp")
+    with np.load(path) as z:
+        assert sorted(z.files) == sorted(["binaryInputNCHWPacked", "globalInputNC", "policyTargetsNCMove",
+                                          "globalTargetsNC", "valueTargetsNCHW"])
+        for k in z.files:
+            assert z[k].dtype == rows[k].dtype, k
+            np.testing.assert_array_equal(z[k], rows[k])
+    import zipfile
+    with zipfile.ZipFile(path) as zf:
+        assert zf.testzip() is None
+        raw = zf.read("globalTargetsNC")
+        assert raw[:6] == b"\x93NUMPY" and len(raw) == 256 + rows["globalTargetsNC"].nbytes  # 256-byte header
