@@ -1,0 +1,362 @@
+// `katago selfplay` for Coffee on MI355X: the process-level boundary of the hot path
+// (command/selfplay.cpp:44-72 flags, :83-250 output layout).  Host C++ over the C ABI.
+//
+//   katago selfplay -config <cfg> -models-dir <dir> -output-dir <dir>
+//                   [-max-games-total N] [-override-config k=v,k=v,...]
+//
+// Reads KataGo-style `key = value` config files (selfplay1.cfg keys that apply to this
+// path, plus `winLen`, `numGpus`, `boardXLen`/`boardYLen`; `bSizes` first entry sets a
+// square board).  Uses the newest model file in -models-dir (CFNN v1); writes
+// <output-dir>/<modelName>/tdata/<hex>.npz (maxRowsPerTrainFile rows each, reference
+// layout) and <output-dir>/log<time>.log.  One engine per GPU, each GPU on its own
+// thread with games [gpu*numGameThreads, (gpu+1)*numGameThreads); each writes its own
+// files (SURVEY §8e fallback, no collective).  SIGINT/SIGTERM: flush rows and exit.
+#include <dirent.h>
+#include <sys/stat.h>
+
+#include <atomic>
+#include <cstdarg>
+#include <chrono>
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <random>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/katacoffee.h"
+
+static std::atomic<bool> gStop(false);
+static void onSignal(int) { gStop = true; }
+
+static std::mutex gLogMu;
+static FILE* gLog = nullptr;
+static void logf(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  std::lock_guard<std::mutex> lk(gLogMu);
+  time_t t = time(nullptr);
+  char ts[32];
+  strftime(ts, sizeof(ts), "%Y-%m-%d %H:%M:%S", localtime(&t));
+  fprintf(stdout, "%s: %s\n", ts, buf);
+  fflush(stdout);
+  if(gLog) {
+    fprintf(gLog, "%s: %s\n", ts, buf);
+    fflush(gLog);
+  }
+}
+
+static std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
+  return a == std::string::npos ? "" : s.substr(a, b - a + 1);
+}
+
+static bool readConfig(const std::string& path, std::map<std::string, std::string>& kv) {
+  std::ifstream in(path);
+  if(!in)
+    return false;
+  std::string line;
+  while(std::getline(in, line)) {
+    size_t h = line.find('#');
+    if(h != std::string::npos)
+      line = line.substr(0, h);
+    size_t eq = line.find('=');
+    if(eq == std::string::npos)
+      continue;
+    std::string k = trim(line.substr(0, eq)), v = trim(line.substr(eq + 1));
+    if(!k.empty())
+      kv[k] = v;
+  }
+  return true;
+}
+
+static void die(const std::string& msg) {
+  fprintf(stderr, "katago selfplay: %s\n", msg.c_str());
+  exit(1);
+}
+
+static void check(int rc, const char* what) {
+  if(rc != COFFEE_OK)
+    die(std::string(what) + ": " + coffee_last_error());
+}
+
+static std::string newestModel(const std::string& dir) {
+  DIR* d = opendir(dir.c_str());
+  if(!d)
+    die("cannot open models dir " + dir);
+  std::string best;
+  time_t bestT = 0;
+  while(dirent* e = readdir(d)) {
+    if(e->d_name[0] == '.')
+      continue;
+    std::string p = dir + "/" + e->d_name;
+    struct stat st;
+    if(stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode) && (best.empty() || st.st_mtime > bestT)) {
+      best = p;
+      bestT = st.st_mtime;
+    }
+  }
+  closedir(d);
+  if(best.empty())
+    die("no model file in " + dir);
+  return best;
+}
+
+static void mkdirs(const std::string& path) {
+  std::string cur;
+  std::stringstream ss(path);
+  std::string part;
+  if(!path.empty() && path[0] == '/')
+    cur = "/";
+  while(std::getline(ss, part, '/')) {
+    if(part.empty())
+      continue;
+    cur += part + "/";
+    mkdir(cur.c_str(), 0755);
+  }
+}
+
+struct Settings {
+  int x = 5, y = 5, winLen = 4, games = 4096, gpus = 1, maxRowsPerFile = 10000;
+  int64_t maxGamesTotal = -1;
+  uint64_t seed = 0;
+  coffee_search_params sp;
+};
+
+static void applyConfig(const std::map<std::string, std::string>& kv, Settings& s) {
+  auto geti = [&](const char* k, int& v) {
+    auto it = kv.find(k);
+    if(it != kv.end())
+      v = std::stoi(it->second);
+  };
+  auto getf = [&](const char* k, float& v) {
+    auto it = kv.find(k);
+    if(it != kv.end())
+      v = std::stof(it->second);
+  };
+  auto getb = [&](const char* k, int32_t& v) {
+    auto it = kv.find(k);
+    if(it != kv.end())
+      v = (it->second == "true" || it->second == "True" || it->second == "1") ? 1 : 0;
+  };
+  auto it = kv.find("bSizes");
+  if(it != kv.end()) {
+    s.x = s.y = std::stoi(it->second.substr(0, it->second.find(',')));
+  }
+  geti("boardXLen", s.x);
+  geti("boardYLen", s.y);
+  geti("winLen", s.winLen);
+  geti("numGameThreads", s.games);
+  geti("numGamesPerGpu", s.games);
+  geti("numGpus", s.gpus);
+  geti("maxRowsPerTrainFile", s.maxRowsPerFile);
+  coffee_search_params& p = s.sp;
+  geti("maxVisits", p.max_visits);
+  getf("cpuctExploration", p.cpuct_exploration);
+  getf("cpuctExplorationLog", p.cpuct_exploration_log);
+  getf("cpuctExplorationBase", p.cpuct_exploration_base);
+  getf("fpuReductionMax", p.fpu_reduction_max);
+  getf("rootFpuReductionMax", p.root_fpu_reduction_max);
+  getf("fpuLossProp", p.fpu_loss_prop);
+  getf("rootFpuLossProp", p.root_fpu_loss_prop);
+  getb("fpuParentWeightByVisitedPolicy", p.fpu_parent_weight_by_visited_policy);
+  getf("fpuParentWeightByVisitedPolicyPow", p.fpu_parent_weight_by_visited_policy_pow);
+  getf("valueWeightExponent", p.value_weight_exponent);
+  getb("rootNoiseEnabled", p.root_noise_enabled);
+  getf("rootDirichletNoiseTotalConcentration", p.root_dirichlet_noise_total_concentration);
+  getf("rootDirichletNoiseWeight", p.root_dirichlet_noise_weight);
+  getf("rootPolicyTemperature", p.root_policy_temperature);
+  getf("rootPolicyTemperatureEarly", p.root_policy_temperature_early);
+  getf("rootDesiredPerChildVisitsCoeff", p.root_desired_per_child_visits_coeff);
+  geti("rootNumSymmetriesToSample", p.root_num_symmetries_to_sample);
+  getf("chosenMoveTemperature", p.chosen_move_temperature);
+  getf("chosenMoveTemperatureEarly", p.chosen_move_temperature_early);
+  getf("chosenMoveTemperatureHalflife", p.chosen_move_temperature_halflife);
+  getf("chosenMoveSubtract", p.chosen_move_subtract);
+  getf("chosenMovePrune", p.chosen_move_prune);
+  getb("useLcbForSelection", p.use_lcb_for_selection);
+  getf("lcbStdevs", p.lcb_stdevs);
+  getf("minVisitPropForLCB", p.min_visit_prop_for_lcb);
+  getf("subtreeValueBiasFactor", p.subtree_value_bias_factor);
+  getf("subtreeValueBiasWeightExponent", p.subtree_value_bias_weight_exponent);
+  getf("subtreeValueBiasFreeProp", p.subtree_value_bias_free_prop);
+  getb("useGraphSearch", p.use_graph_search);
+}
+
+struct RowSink {
+  std::string dir;
+  int x, y, maxRows;
+  std::mt19937_64 rng;
+  std::vector<uint8_t> bin;
+  std::vector<float> glob, gt;
+  std::vector<int16_t> pol;
+  std::vector<int8_t> val;
+  int n = 0;
+  int64_t filesWritten = 0, rowsWritten = 0;
+
+  void append(int k, const uint8_t* b, const float* g, const int16_t* p, const float* t, const int8_t* v) {
+    const int A = x * y, pb = (A + 7) / 8;
+    bin.insert(bin.end(), b, b + (size_t)k * 15 * pb);
+    glob.insert(glob.end(), g, g + k);
+    pol.insert(pol.end(), p, p + (size_t)k * 2 * 4 * A);
+    gt.insert(gt.end(), t, t + (size_t)k * 64);
+    val.insert(val.end(), v, v + (size_t)k * 5 * A);
+    n += k;
+  }
+  void flush(bool all) {
+    const int A = x * y, pb = (A + 7) / 8, P = 4 * A;
+    while(n >= maxRows || (all && n > 0)) {
+      int k = n < maxRows ? n : maxRows;
+      char name[64];
+      snprintf(name, sizeof(name), "%016llX.npz", (unsigned long long)rng());
+      std::string path = dir + "/" + name;
+      check(coffee_write_npz(path.c_str(), k, x, y, bin.data(), glob.data(), pol.data(), gt.data(), val.data()),
+            "write npz");
+      bin.erase(bin.begin(), bin.begin() + (size_t)k * 15 * pb);
+      glob.erase(glob.begin(), glob.begin() + k);
+      pol.erase(pol.begin(), pol.begin() + (size_t)k * 2 * P);
+      gt.erase(gt.begin(), gt.begin() + (size_t)k * 64);
+      val.erase(val.begin(), val.begin() + (size_t)k * 5 * A);
+      n -= k;
+      filesWritten++;
+      rowsWritten += k;
+      logf("wrote %s (%d rows)", path.c_str(), k);
+    }
+  }
+};
+
+static std::atomic<int64_t> gGamesDone(0);
+
+static void runGpu(int gpu, const Settings& s, const std::string& model, const std::string& tdata) {
+  check(coffee_set_device(gpu), "set device");
+  coffee_selfplay_config c;
+  memset(&c, 0, sizeof(c));
+  c.x = s.x;
+  c.y = s.y;
+  c.win_len = s.winLen;
+  c.num_games = s.games;
+  c.seed = s.seed;
+  c.slot_base = gpu * s.games;
+  c.use_fake_net = 0;
+  c.commit_interval = 8;
+  c.model_path = model.c_str();
+  c.search = s.sp;
+  coffee_selfplay* h = nullptr;
+  check(coffee_selfplay_create(&c, &h), "create engine");
+  RowSink sink{tdata, s.x, s.y, s.maxRowsPerFile, std::mt19937_64(s.seed ^ (0x9E3779B97F4A7C15ULL * (gpu + 1)))};
+  const int A = s.x * s.y, pb = (A + 7) / 8, P = 4 * A;
+  const int chunk = 65536;
+  std::vector<uint8_t> bin((size_t)chunk * 15 * pb);
+  std::vector<float> glob(chunk), gt((size_t)chunk * 64);
+  std::vector<int16_t> pol((size_t)chunk * 2 * P);
+  std::vector<int8_t> val((size_t)chunk * 5 * A);
+  std::vector<int32_t> meta((size_t)chunk * 4);
+  uint64_t lastGames = 0;
+  auto t0 = std::chrono::steady_clock::now();
+  while(!gStop) {
+    check(coffee_selfplay_step(h, 200, nullptr), "step");
+    int got = 0;
+    do {
+      check(coffee_selfplay_drain_rows(h, chunk, bin.data(), glob.data(), pol.data(), gt.data(), val.data(),
+                                       meta.data(), &got),
+            "drain");
+      if(got > 0)
+        sink.append(got, bin.data(), glob.data(), pol.data(), gt.data(), val.data());
+    } while(got == chunk);
+    sink.flush(false);
+    coffee_selfplay_stats st;
+    check(coffee_selfplay_stats_get(h, &st), "stats");
+    gGamesDone += (int64_t)(st.games_finished - lastGames);
+    lastGames = st.games_finished;
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    logf("gpu %d: %llu games, %llu moves, %.1f rows/s, %.3g playouts/s, %llu rows dropped", gpu,
+         (unsigned long long)st.games_finished, (unsigned long long)st.moves, st.moves / secs, st.playouts / secs,
+         (unsigned long long)st.rows_dropped);
+    if(s.maxGamesTotal >= 0 && gGamesDone >= s.maxGamesTotal)
+      gStop = true;
+  }
+  sink.flush(true);
+  coffee_selfplay_destroy(h);
+  logf("gpu %d done: %lld files, %lld rows", gpu, (long long)sink.filesWritten, (long long)sink.rowsWritten);
+}
+
+int main(int argc, char** argv) {
+  if(argc < 2 || std::string(argv[1]) != "selfplay")
+    die("usage: katago selfplay -config <cfg> -models-dir <dir> -output-dir <dir> [-max-games-total N] "
+        "[-override-config k=v,...]");
+  std::string cfgPath, modelsDir, outDir, overrides;
+  int64_t maxGames = -1;
+  for(int i = 2; i < argc; i++) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if(i + 1 >= argc)
+        die("missing value for " + a);
+      return argv[++i];
+    };
+    if(a == "-config")
+      cfgPath = next();
+    else if(a == "-models-dir")
+      modelsDir = next();
+    else if(a == "-output-dir")
+      outDir = next();
+    else if(a == "-max-games-total")
+      maxGames = std::stoll(next());
+    else if(a == "-override-config")
+      overrides = next();
+    else
+      die("unknown argument " + a);
+  }
+  if(cfgPath.empty() || modelsDir.empty() || outDir.empty())
+    die("-config, -models-dir and -output-dir are required");
+  std::map<std::string, std::string> kv;
+  if(!readConfig(cfgPath, kv))
+    die("cannot read config " + cfgPath);
+  std::stringstream os(overrides);
+  std::string item;
+  while(std::getline(os, item, ',')) {
+    size_t eq = item.find('=');
+    if(eq != std::string::npos)
+      kv[trim(item.substr(0, eq))] = trim(item.substr(eq + 1));
+  }
+  Settings s;
+  coffee_search_params_default(&s.sp);
+  applyConfig(kv, s);
+  s.maxGamesTotal = maxGames;
+  s.seed = std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32);
+  mkdirs(outDir);
+  char lname[64];
+  time_t now = time(nullptr);
+  strftime(lname, sizeof(lname), "log%Y%m%d-%H%M%S.log", localtime(&now));
+  gLog = fopen((outDir + "/" + lname).c_str(), "w");
+  std::signal(SIGINT, onSignal);
+  std::signal(SIGTERM, onSignal);
+  const std::string model = newestModel(modelsDir);
+  std::string modelName = model.substr(model.find_last_of('/') + 1);
+  if(modelName.find('.') != std::string::npos)
+    modelName = modelName.substr(0, modelName.find('.'));
+  const std::string tdata = outDir + "/" + modelName + "/tdata";
+  mkdirs(tdata);
+  int ndev = 0;
+  check(coffee_device_count(&ndev), "device count");
+  if(s.gpus < 1 || s.gpus > ndev)
+    die("numGpus must be in 1.." + std::to_string(ndev));
+  logf("selfplay: model %s, %dx%d win %d, %d games/GPU x %d GPUs, %d visits", model.c_str(), s.x, s.y, s.winLen,
+       s.games, s.gpus, s.sp.max_visits);
+  std::vector<std::thread> th;
+  for(int g = 0; g < s.gpus; g++)
+    th.emplace_back(runGpu, g, std::cref(s), std::cref(model), std::cref(tdata));
+  for(auto& t : th)
+    t.join();
+  if(gLog)
+    fclose(gLog);
+  return 0;
+}
