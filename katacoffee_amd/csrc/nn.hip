@@ -36,6 +36,9 @@ namespace kc {
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+constexpr int NN_WAVES = 8;  // waves per workgroup (4 per SIMD)
+constexpr int NN_NT = NN_WAVES * 64;
+
 template <int X_, int Y_, int C_>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
@@ -45,9 +48,12 @@ struct NNGeo {
   // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): rows
   // [ROWS, 64*MAXT) are padding (computed, never read as neighbours); ZROW is
   // the all-zero row that out-of-board neighbour taps read.
-  static constexpr int MAXT = (RT + 3) / 4;
-  static constexpr int ZROW = 4 * MAXT * 16;
-  static constexpr int ASTR = C + 8;     // bf16 per activation row (+16 B pad: conflict-free b128 reads)
+  static constexpr int RGROUPS = NN_WAVES / 2;  // row groups (x 2 column halves)
+  static constexpr int MAXT = (RT + RGROUPS - 1) / RGROUPS;
+  static constexpr int ZROW = RGROUPS * MAXT * 16;
+  // fp16 per activation row: 56-dword rows make the A-fragment ds_read_b128 (lane
+  // groups {0-3,12-15,20-27}, ... ; 16 rows x 4 k-quarters) bank-conflict free.
+  static constexpr int ASTR = C + 16;
   static constexpr int NCT = C / 32;     // 16-col tiles per wave
   static constexpr int NCT_ALL = C / 16;
   static constexpr int P = 4 * A;
@@ -96,17 +102,17 @@ template <class G, int NTAPS, int NCB>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                     f32x4 (&acc)[G::MAXT][G::NCT], int tstart, int ntiles, int cg, int lane, int tid) {
   constexpr int UNITS = NCB * G::NCT_ALL * 64;  // 16-B fragments per tap
-  constexpr int PER = (UNITS + 511) / 512;
+  constexpr int PER = (UNITS + NN_NT - 1) / NN_NT;
   {
     h16x8 r[PER];
 #pragma unroll
     for(int u = 0; u < PER; u++)
-      if(tid + u * 512 < UNITS)
-        r[u] = w[tid + u * 512];
+      if(tid + u * NN_NT < UNITS)
+        r[u] = w[tid + u * NN_NT];
 #pragma unroll
     for(int u = 0; u < PER; u++)
-      if(tid + u * 512 < UNITS)
-        wl[tid + u * 512] = r[u];
+      if(tid + u * NN_NT < UNITS)
+        wl[tid + u * NN_NT] = r[u];
   }
   __syncthreads();
   const int kq = 8 * (lane >> 4);
@@ -118,8 +124,8 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
     if(more) {
 #pragma unroll
       for(int u = 0; u < PER; u++)
-        if(tid + u * 512 < UNITS)
-          nx[u] = w[(size_t)(tap + 1) * UNITS + tid + u * 512];
+        if(tid + u * NN_NT < UNITS)
+          nx[u] = w[(size_t)(tap + 1) * UNITS + tid + u * NN_NT];
     }
     const h16x8* wb = wl + (tap & 1) * G::WBUF;
     const int dy = NTAPS == 9 ? tap / 3 - 1 : 0;
@@ -136,28 +142,32 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
       bool ok = r < G::ROWS && yy >= 0 && yy < G::Y && xx >= 0 && xx < G::X;
       roff[t] = (ok ? (r + dy * G::X + dx) : G::ZROW) * G::ASTR + kq;
     }
+    // Issue every LDS read of the tap first (all K-chunks' A and B fragments), then
+    // the MFMAs: one exposed LDS latency per tap instead of one per K-chunk.
+    h16x8 bfr[NCB][G::NCT], afr[NCB][G::MAXT];
 #pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
-      h16x8 bcur[G::NCT];
 #pragma unroll
       for(int ct = 0; ct < G::NCT; ct++)
-        bcur[ct] = wb[(cb * G::NCT_ALL + cg * G::NCT + ct) * 64 + lane];
+        bfr[cb][ct] = wb[(cb * G::NCT_ALL + cg * G::NCT + ct) * 64 + lane];
 #pragma unroll
-      for(int t = 0; t < G::MAXT; t++) {
-        if(t < ntiles) {
-          h16x8 a = *reinterpret_cast<const h16x8*>(act + roff[t] + cb * 32);
-#pragma unroll
-          for(int ct = 0; ct < G::NCT; ct++)
-            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bcur[ct], acc[t][ct], 0, 0, 0);
-        }
-      }
+      for(int t = 0; t < G::MAXT; t++)
+        afr[cb][t] = *reinterpret_cast<const h16x8*>(act + roff[t] + cb * 32);
     }
+#pragma unroll
+    for(int cb = 0; cb < NCB; cb++)
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+        for(int ct = 0; ct < G::NCT; ct++)
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afr[cb][t], bfr[cb][ct], acc[t][ct], 0, 0, 0);
+    (void)ntiles;
     if(more) {
       h16x8* nb = wl + ((tap + 1) & 1) * G::WBUF;
 #pragma unroll
       for(int u = 0; u < PER; u++)
-        if(tid + u * 512 < UNITS)
-          nb[tid + u * 512] = nx[u];
+        if(tid + u * NN_NT < UNITS)
+          nb[tid + u * NN_NT] = nx[u];
     }
     __syncthreads();
   }
@@ -170,7 +180,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 // rows) read consecutive banks in the dot-product loops.
 KC_D void stageT96(float* __restrict__ dst, const float* __restrict__ src, int rows, int tid) {
   const int n4 = rows * 24;
-  for(int q = tid; q < n4; q += 512) {
+  for(int q = tid; q < n4; q += NN_NT) {
     const int o = q / 24, i4 = (q - o * 24) * 4;
     const float4 v = reinterpret_cast<const float4*>(src)[q];
     dst[(i4 + 0) * rows + o] = v.x;
@@ -235,7 +245,7 @@ KC_D void storeBnRelu(uint16_t* act, const V (&v)[G::MAXT][G::NCT], const float*
 }
 
 template <int X, int Y, int C>
-__global__ void __launch_bounds__(512, 2)
+__global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF, int n,
                const int* __restrict__ countDev, int inWords, float winLen, const uint64_t* __restrict__ in,
                float* __restrict__ out) {
@@ -262,7 +272,7 @@ __global__ void __launch_bounds__(512, 2)
   const float sqOff = sqrtf((float)G::A) - 14.0f;
 
   // ---- unpack the packed V1 planes: act[row][0..31] (15 planes + zero pad), zero row ----
-  for(int idx = tid; idx < (G::ZROW + 1) * 32; idx += 512) {
+  for(int idx = tid; idx < (G::ZROW + 1) * 32; idx += NN_NT) {
     int row = idx >> 5, c = idx & 31;
     uint16_t v = 0;
     if(row < nb * G::A && c < NUM_SPATIAL) {
@@ -273,7 +283,7 @@ __global__ void __launch_bounds__(512, 2)
     }
     act[row * G::ASTR + c] = v;
   }
-  for(int c = 32 + tid; c < G::C; c += 512)
+  for(int c = 32 + tid; c < G::C; c += NN_NT)
     act[G::ZROW * G::ASTR + c] = 0;
   __syncthreads();
 
@@ -343,7 +353,7 @@ __global__ void __launch_bounds__(512, 2)
       NN_PHASE(50);
       float* lgT = reinterpret_cast<float*>(wl);  // weight slab is idle between convs
       stageT96(lgT, WF + L->linG[blk], Cr, tid);
-      for(int idx = tid; idx < G::NB * 32; idx += 512) {
+      for(int idx = tid; idx < G::NB * 32; idx += NN_NT) {
         const int b = idx >> 5, c = idx & 31;
         float s = 0.0f, m = 0.0f;
 #pragma unroll 1
@@ -360,7 +370,7 @@ __global__ void __launch_bounds__(512, 2)
       __syncthreads();
       NN_PHASE(51);
       {
-        for(int idx = tid; idx < G::NB * Cr; idx += 512) {
+        for(int idx = tid; idx < G::NB * Cr; idx += NN_NT) {
           const int b = idx / Cr, o = idx - b * Cr;
           float s = 0.0f;
 #pragma unroll 8
@@ -447,7 +457,7 @@ __global__ void __launch_bounds__(512, 2)
   float* l2T = plgT + 32 * 96;
   stageT96(plgT, WF + L->pLinG, 32, tid);
   stageT96(l2T, WF + L->vLin2, L->v2, tid);
-  for(int idx = tid; idx < G::NB * 32; idx += 512) {
+  for(int idx = tid; idx < G::NB * 32; idx += NN_NT) {
     const int b = idx >> 5, c = idx & 31;
     float s = 0.0f, m = 0.0f, sv = 0.0f;
 #pragma unroll 1
@@ -468,7 +478,7 @@ __global__ void __launch_bounds__(512, 2)
   __syncthreads();
   NN_PHASE(54);
   {
-    for(int idx = tid; idx < G::NB * 32; idx += 512) {
+    for(int idx = tid; idx < G::NB * 32; idx += NN_NT) {
       const int b = idx >> 5, o = idx & 31;
       float s = 0.0f;
 #pragma unroll 8
@@ -478,7 +488,7 @@ __global__ void __launch_bounds__(512, 2)
     }
     const int v2 = L->v2;
     const float* b2 = WF + L->vB2;
-    for(int idx = tid; idx < G::NB * v2; idx += 512) {
+    for(int idx = tid; idx < G::NB * v2; idx += NN_NT) {
       const int b = idx / v2, oo = idx - b * v2;
       float t = b2[oo];
 #pragma unroll 8
@@ -677,7 +687,7 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   using G = NNGeo<5, 5, 96>;
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
   int grid = (n + G::NB - 1) / G::NB;
-  hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(512), G::LDS, st, layoutDev_,
+  hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_,
                      (const h16x8*)wHalf_, wF32_, n, countDev, inWords, (float)W_, in, out);
   KC_HIP(hipGetLastError());
 }
