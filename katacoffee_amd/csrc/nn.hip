@@ -58,14 +58,15 @@ struct NNGeo {
   static constexpr int NCT_ALL = C / 16;
   static constexpr int P = 4 * A;
   static constexpr int OFF_SCR = (((ZROW + 1) * ASTR * 2) + 15) / 16 * 16;
-  static constexpr int OFF_POOL = OFF_SCR + ZROW * 32 * 4;
+  static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
+  static constexpr int OFF_POOL = OFF_SCR + ZROW * SCR * 4;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
   static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap (one buffer)
   static constexpr int OFF_W = (OFF_VH + NB * 64 * 4 + 15) / 16 * 16;
   static constexpr int LDS = OFF_W + 2 * WBUF * 16;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
-  static_assert(ZROW * 32 * 4 <= (ZROW + 1) * ASTR * 2, "value-branch f32 scratch must fit in act");
+  static_assert(ZROW * SCR * 4 <= (ZROW + 1) * ASTR * 2, "value-branch f32 scratch must fit in act");
   static_assert(LDS <= 163840, "LDS budget");
 };
 
@@ -345,7 +346,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
           for(int j = 0; j < 4; j++) {
             int row = rl + t * 16 + j;
             float v = acc[t][ct][j] * sc + bi;
-            scr[row * 32 + gc] = v > 0.0f ? v : 0.0f;
+            scr[row * G::SCR + gc] = v > 0.0f ? v : 0.0f;
           }
         }
       }
@@ -353,30 +354,41 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       NN_PHASE(50);
       float* lgT = reinterpret_cast<float*>(wl);  // weight slab is idle between convs
       stageT96(lgT, WF + L->linG[blk], Cr, tid);
-      for(int idx = tid; idx < G::NB * 32; idx += NN_NT) {
-        const int b = idx >> 5, c = idx & 31;
+      // pooling: a lane pair per (board, channel), each summing half of the positions
+      for(int idx = tid; idx < G::NB * 64; idx += NN_NT) {
+        const int pr = idx >> 1, half = idx & 1;
+        const int b = pr >> 5, c = pr & 31;
+        const int p0 = half ? (G::A + 1) / 2 : 0, p1 = half ? G::A : (G::A + 1) / 2;
         float s = 0.0f, m = 0.0f;
-#pragma unroll 1
-        for(int p = 0; p < G::A; p++) {
-          float v = scr[(b * G::A + p) * 32 + c];
+#pragma unroll 4
+        for(int p = p0; p < p1; p++) {
+          float v = scr[(b * G::A + p) * G::SCR + c];
           s += v;
           m = v > m ? v : m;
         }
-        float mean = s / (float)G::A;
-        poolP[b * 96 + c] = mean;
-        poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
-        poolP[b * 96 + 64 + c] = m;
+        s = s + __shfl_xor(s, 1, 64);
+        m = fmaxf(m, __shfl_xor(m, 1, 64));
+        if(half == 0) {
+          float mean = s / (float)G::A;
+          poolP[b * 96 + c] = mean;
+          poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
+          poolP[b * 96 + 64 + c] = m;
+        }
       }
       __syncthreads();
       NN_PHASE(51);
       {
         for(int idx = tid; idx < G::NB * Cr; idx += NN_NT) {
           const int b = idx / Cr, o = idx - b * Cr;
-          float s = 0.0f;
-#pragma unroll 8
-          for(int i = 0; i < 96; i++)
-            s += lgT[i * Cr + o] * poolP[b * 96 + i];
-          biasS[b * Cr + o] = s;
+          float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;  // four independent chains
+#pragma unroll 4
+          for(int i = 0; i < 96; i += 4) {
+            s0 += lgT[i * Cr + o] * poolP[b * 96 + i];
+            s1 += lgT[(i + 1) * Cr + o] * poolP[b * 96 + i + 1];
+            s2 += lgT[(i + 2) * Cr + o] * poolP[b * 96 + i + 2];
+            s3 += lgT[(i + 3) * Cr + o] * poolP[b * 96 + i + 3];
+          }
+          biasS[b * Cr + o] = (s0 + s1) + (s2 + s3);
         }
       }
       __syncthreads();
@@ -446,7 +458,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
         for(int j = 0; j < 4; j++) {
           int row = rl + t * 16 + j;
           float v = acc[t][ct][j] + bi;
-          dst[row * 32 + hc] = v > 0.0f ? v : 0.0f;
+          dst[row * G::SCR + hc] = v > 0.0f ? v : 0.0f;
         }
       }
     }
@@ -457,43 +469,59 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   float* l2T = plgT + 32 * 96;
   stageT96(plgT, WF + L->pLinG, 32, tid);
   stageT96(l2T, WF + L->vLin2, L->v2, tid);
-  for(int idx = tid; idx < G::NB * 32; idx += NN_NT) {
-    const int b = idx >> 5, c = idx & 31;
+  for(int idx = tid; idx < G::NB * 64; idx += NN_NT) {
+    const int pr = idx >> 1, half = idx & 1;
+    const int b = pr >> 5, c = pr & 31;
+    const int p0 = half ? (G::A + 1) / 2 : 0, p1 = half ? G::A : (G::A + 1) / 2;
     float s = 0.0f, m = 0.0f, sv = 0.0f;
-#pragma unroll 1
-    for(int p = 0; p < G::A; p++) {
-      float v = scr[(b * G::A + p) * 32 + c];
+#pragma unroll 4
+    for(int p = p0; p < p1; p++) {
+      float v = scr[(b * G::A + p) * G::SCR + c];
       s += v;
       m = v > m ? v : m;
-      sv += actF[(b * G::A + p) * 32 + c];
+      sv += actF[(b * G::A + p) * G::SCR + c];
     }
-    float mean = s / (float)G::A, meanv = sv / (float)G::A;
-    poolP[b * 96 + c] = mean;
-    poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
-    poolP[b * 96 + 64 + c] = m;
-    poolV[b * 96 + c] = meanv;
-    poolV[b * 96 + 32 + c] = meanv * (sqOff / 10.0f);
-    poolV[b * 96 + 64 + c] = meanv * ((sqOff * sqOff) / 100.0f - 0.1f);
+    s = s + __shfl_xor(s, 1, 64);
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    sv = sv + __shfl_xor(sv, 1, 64);
+    if(half == 0) {
+      float mean = s / (float)G::A, meanv = sv / (float)G::A;
+      poolP[b * 96 + c] = mean;
+      poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
+      poolP[b * 96 + 64 + c] = m;
+      poolV[b * 96 + c] = meanv;
+      poolV[b * 96 + 32 + c] = meanv * (sqOff / 10.0f);
+      poolV[b * 96 + 64 + c] = meanv * ((sqOff * sqOff) / 100.0f - 0.1f);
+    }
   }
   __syncthreads();
   NN_PHASE(54);
   {
     for(int idx = tid; idx < G::NB * 32; idx += NN_NT) {
       const int b = idx >> 5, o = idx & 31;
-      float s = 0.0f;
-#pragma unroll 8
-      for(int i = 0; i < 96; i++)
-        s += plgT[i * 32 + o] * poolP[b * 96 + i];
-      biasS[b * 32 + o] = s;
+      float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+#pragma unroll 4
+      for(int i = 0; i < 96; i += 4) {
+        s0 += plgT[i * 32 + o] * poolP[b * 96 + i];
+        s1 += plgT[(i + 1) * 32 + o] * poolP[b * 96 + i + 1];
+        s2 += plgT[(i + 2) * 32 + o] * poolP[b * 96 + i + 2];
+        s3 += plgT[(i + 3) * 32 + o] * poolP[b * 96 + i + 3];
+      }
+      biasS[b * 32 + o] = (s0 + s1) + (s2 + s3);
     }
     const int v2 = L->v2;
     const float* b2 = WF + L->vB2;
     for(int idx = tid; idx < G::NB * v2; idx += NN_NT) {
       const int b = idx / v2, oo = idx - b * v2;
-      float t = b2[oo];
-#pragma unroll 8
-      for(int i = 0; i < 96; i++)
-        t += l2T[i * v2 + oo] * poolV[b * 96 + i];
+      float t0 = 0.0f, t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
+#pragma unroll 4
+      for(int i = 0; i < 96; i += 4) {
+        t0 += l2T[i * v2 + oo] * poolV[b * 96 + i];
+        t1 += l2T[(i + 1) * v2 + oo] * poolV[b * 96 + i + 1];
+        t2 += l2T[(i + 2) * v2 + oo] * poolV[b * 96 + i + 2];
+        t3 += l2T[(i + 3) * v2 + oo] * poolV[b * 96 + i + 3];
+      }
+      const float t = b2[oo] + ((t0 + t1) + (t2 + t3));
       vh[b * 64 + oo] = t > 0.0f ? t : 0.0f;
     }
   }
