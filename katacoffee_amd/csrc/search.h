@@ -3,8 +3,9 @@
 // Layout in HBM (DESIGN.md "Data layout"), every array indexed by game slot g:
 //   GameDev   games[G]                         per-game scalars (boards, RNG, phase, counters)
 //   Node      nodes[G][cap]                    64-B statistics record per search node
-//   Edge      edges[G][cap][P]                 (child, edgeVisits) per child slot, slots in
-//   uint16_t  emove[G][cap][P]                 expansion order (SearchChildPointer, searchnode.h)
+//   Edge      edges[G][cap][P]                 (child, edgeVisits, prior, move) per child slot,
+//                                              slots in expansion order (SearchChildPointer, searchnode.h)
+//   uint16_t  order[G][cap][P]                 legal moves by descending prior (next expansion = order[k])
 //   float     policy[G][cap][P]                NN policy of the node (NNOutput::policyProbs)
 //   uint32_t  freeList[G][cap], allocBits[G][cap/32]   node allocator
 //   TT        ttKey[G][ttCap][2], ttNode[G][ttCap]     transposition table (searchnodetable.h)
@@ -61,6 +62,8 @@ static_assert(sizeof(Node) == 64, "Node layout");
 
 struct Edge {
   uint32_t child, visits;
+  float prior;    // parent's NN prior of the move (root selection reads the noised root policy)
+  uint32_t move;  // policy position dir*A + cell
 };
 
 struct TurnRec {
@@ -96,7 +99,7 @@ struct SearchDev {
   GameDev* games;
   Node* nodes;
   Edge* edges;
-  uint16_t* emove;
+  uint16_t* order;
   float* policy;
   uint32_t* freeList;
   uint32_t* allocBits;

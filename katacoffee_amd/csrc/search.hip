@@ -40,7 +40,7 @@ struct GV {
   KC_D GV(const SearchDev& d_, int g_) : d(d_), T(*d_.T), g(g_), lane(laneId()) {}
   KC_D Node* nodes() const { return d.nodes + (size_t)g * d.cap; }
   KC_D Edge* edges(int n) const { return d.edges + ((size_t)g * d.cap + n) * d.P; }
-  KC_D uint16_t* emove(int n) const { return d.emove + ((size_t)g * d.cap + n) * d.P; }
+  KC_D uint16_t* order(int n) const { return d.order + ((size_t)g * d.cap + n) * d.P; }
   KC_D float* pol(int n) const { return d.policy + ((size_t)g * d.cap + n) * d.P; }
   KC_D uint32_t* freeList() const { return d.freeList + (size_t)g * d.cap; }
   KC_D uint32_t* allocBits() const { return d.allocBits + (size_t)g * (d.cap / 32); }
@@ -433,11 +433,12 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
   const int P = v.d.P;
   const int k = n.numChildren;
   const int pla = n.nextPla;
-  for(int w = v.lane; w < (P + 31) / 32; w += 64)
-    hasBits[w] = 0;
-  waveSync();
+  if(isRoot) {
+    for(int w = v.lane; w < (P + 31) / 32; w += 64)
+      hasBits[w] = 0;
+    waveSync();
+  }
   const Edge* E = v.edges(ni);
-  const uint16_t* M = v.emove(ni);
   const Node* NS = v.nodes();
   float probs[NI], cw[NI], pv[NI], cu[NI];
   uint32_t cvis[NI];
@@ -448,15 +449,15 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
     cvis[j] = 0;
     if(i < k) {
       Edge e = E[i];
-      int mv = M[i];
       const Node& c = NS[e.child];
-      float p = pol[mv];
+      float p = isRoot ? pol[e.move] : e.prior;
       cvis[j] = c.visits;
       cu[j] = c.utilityAvg;
       pv[j] = p;
       probs[j] = p < 0.0f ? 0.0f : p;
       cw[j] = p < 0.0f ? 0.0f : childWeight(e.visits, cvis[j], c.weightSum);
-      atomicOr(&hasBits[mv >> 5], 1u << (mv & 31));
+      if(isRoot)
+        atomicOr(&hasBits[e.move >> 5], 1u << (e.move & 31));
     }
   }
   const float probMass = tsum<NI>(probs, k, v.lane);
@@ -489,21 +490,32 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
   }
   waveArgmax(best, bestIdx);
   int bestSlot = best > -__builtin_inff() ? bestIdx : -1;
-  waveSync();
   float bp = -1.0f;
   int bpos = BIG;
-  for(int pos = v.lane; pos < P; pos += 64) {
-    if((hasBits[pos >> 5] >> (pos & 31)) & 1u)
-      continue;
-    float p = pol[pos];
-    if(p < 0.0f)
-      continue;
-    if(p > bp) {
-      bp = p;
+  if(isRoot) {
+    // root priors carry noise: scan every unexpanded legal move
+    waveSync();
+    for(int pos = v.lane; pos < P; pos += 64) {
+      if((hasBits[pos >> 5] >> (pos & 31)) & 1u)
+        continue;
+      float p = pol[pos];
+      if(p < 0.0f)
+        continue;
+      if(p > bp) {
+        bp = p;
+        bpos = pos;
+      }
+    }
+    waveArgmax(bp, bpos);
+  } else if(k < P) {
+    // non-root: children are always created in prior order, so the best
+    // unexpanded move is the k-th entry of the node's expansion order
+    const int pos = v.order(ni)[k];
+    if(pos != 0xFFFF) {
+      bp = pol[pos];
       bpos = pos;
     }
   }
-  waveArgmax(bp, bpos);
   newPos = -1;
   if(bpos != BIG) {
     float val = (scaling * bp) / 1.0f + (pla == 2 ? fpu : -fpu);
@@ -571,8 +583,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
       }
       waveSync();
       if(v.lane == 0) {
-        v.edges(ni)[slot] = Edge{(uint32_t)child, 0u};
-        v.emove(ni)[slot] = (uint16_t)newPos;
+        v.edges(ni)[slot] = Edge{(uint32_t)child, 0u, v.pol(ni)[newPos], (uint32_t)newPos};
         v.nodes()[ni].numChildren = (uint16_t)(slot + 1);
         v.pathNode()[s.pathLen] = ni;
         v.pathSlot()[s.pathLen] = slot;
@@ -602,8 +613,13 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
       s.leafNode = child;
       break;
     }
-    const int mv = v.emove(ni)[slot];
-    playMoveWave(T, b, mv % T.A, mv / T.A);
+    // existing child: its terminal flag already says whether the move ends the game
+    const int mv = (int)e.move, mover = b.pla;
+    applyMove(T, b, mv % T.A, mv / T.A);
+    if(v.nodes()[child].flags & 2) {
+      b.finished = 1;
+      b.winner = maxRun(T, b, mv % T.A) >= T.W ? mover : 0;
+    }
     ni = child;
   }
 }
@@ -804,6 +820,34 @@ KC_D void noiseAndTemp(const GV& v, GameDev& s, DRng& rng, const float* raw, flo
   }
 }
 
+// Expansion order of a freshly evaluated node: legal moves by descending prior,
+// ties by ascending position (the order selectBest's new-child scan yields),
+// 0xFFFF after the last legal move. Rank by counting; priors staged in LDS.
+KC_D void buildOrder(const GV& v, int ni, const float* pol, float* lds) {
+  const int P = v.d.P;
+  for(int p = v.lane; p < P; p += 64)
+    lds[p] = pol[p];
+  waveSync();
+  uint16_t* ord = v.order(ni);
+  int nLegal = 0;
+  for(int p = v.lane; p < P; p += 64) {
+    const float x = lds[p];
+    if(x < 0.0f)
+      continue;
+    int rank = 0;
+    for(int q = 0; q < P; q++) {
+      const float y = lds[q];
+      rank += (y > x || (y == x && q < p)) ? 1 : 0;
+    }
+    ord[rank] = (uint16_t)p;
+  }
+  for(int base = 0; base < P; base += 64)
+    nLegal += __builtin_popcountll(ballot(base + v.lane < P && lds[base + v.lane] >= 0.0f));
+  for(int r = nLegal + v.lane; r < P; r += 64)
+    ord[r] = 0xFFFF;
+  waveSync();
+}
+
 // kBackup: NN post-processing + leaf value + path backup.
 template <int NI>
 __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) {
@@ -875,8 +919,10 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
   } else {
     if(s.leafKind == LEAF_NN) {
       float w, l;
-      postprocess<NI>(v, s.leaf, s.leafSym, o, v.pol(s.leafNode), w, l);
+      float* pol = v.pol(s.leafNode);
+      postprocess<NI>(v, s.leaf, s.leafSym, o, pol, w, l);
       waveSync();
+      buildOrder(v, s.leafNode, pol, scratch);
       if(v.lane == 0) {
         Node* n = &v.nodes()[s.leafNode];
         n->nnWin = w;
@@ -954,7 +1000,6 @@ KC_D int playSelectionValues(const GV& v, const GameDev& s, float scaleMaxToAtLe
   const float* pol = v.rootNoised();
   const int pla = n.nextPla;
   const Edge* E = v.edges(ri);
-  const uint16_t* M = v.emove(ri);
   float cw[NI], val[NI];
   uint32_t ev[NI];
   int posv[NI];
@@ -978,7 +1023,7 @@ KC_D int playSelectionValues(const GV& v, const GameDev& s, float scaleMaxToAtLe
       cusq[j] = c.utilitySqAvg;
       ev[j] = e.visits;
       cw[j] = childWeight(e.visits, cvis[j], cws[j]);
-      posv[j] = M[i];
+      posv[j] = (int)e.move;
       val[j] = cw[j];
     }
   }
@@ -1228,10 +1273,9 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
   if(ri >= 0) {
     const Node& r = v.nodes()[ri];
     const Edge* E = v.edges(ri);
-    const uint16_t* M = v.emove(ri);
     for(int base = 0; base < r.numChildren; base += 64) {
       int i = base + v.lane;
-      bool hit = i < r.numChildren && M[i] == chosenPos;
+      bool hit = i < r.numChildren && (int)E[i].move == chosenPos;
       uint64_t m = ballot(hit);
       if(m) {
         int f = firstLane(m);
@@ -1734,7 +1778,6 @@ __global__ void kGameTree(const SearchDev* __restrict__ dp, int g, int maxNodes,
     o[21] = 0;
     o[22] = 0;
     const Edge* E = d.edges + ((size_t)g * d.cap + idx) * d.P;
-    const uint16_t* M = d.emove + ((size_t)g * d.cap + idx) * d.P;
     for(int i = 0; i < x.numChildren; i++) {
       const int c = (int)E[i].child;
       int ci = -1;
@@ -1750,7 +1793,7 @@ __global__ void kGameTree(const SearchDev* __restrict__ dp, int g, int maxNodes,
       uint32_t* eo = edgesOut + ((size_t)head * d.P + i) * 3;
       eo[0] = (uint32_t)ci;
       eo[1] = E[i].visits;
-      eo[2] = M[i];
+      eo[2] = E[i].move;
     }
     head++;
   }

@@ -104,7 +104,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.games = devAlloc<GameDev>(owned_, G);
   d.nodes = devAlloc<Node>(owned_, (size_t)G * cap, false);
   d.edges = devAlloc<Edge>(owned_, (size_t)G * cap * P, false);
-  d.emove = devAlloc<uint16_t>(owned_, (size_t)G * cap * P, false);
+  d.order = devAlloc<uint16_t>(owned_, (size_t)G * cap * P, false);
   d.policy = devAlloc<float>(owned_, (size_t)G * cap * P, false);
   d.freeList = devAlloc<uint32_t>(owned_, (size_t)G * cap, false);
   d.allocBits = devAlloc<uint32_t>(owned_, (size_t)G * (cap / 32));
