@@ -57,6 +57,7 @@ class NNEngine {
   void* wHalf_ = nullptr;  // device
   float* wF32_ = nullptr;  // device
   NNLayout* layoutDev_ = nullptr;
+  uint16_t* tabDev_ = nullptr;  // device row tables (nn.hip rowTables)
 };
 
 // Deterministic stand-in network (see oracle fakeNet); same I/O as NNEngine.

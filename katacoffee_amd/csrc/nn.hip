@@ -45,28 +45,43 @@ struct NNGeo {
   static constexpr int NB = 8;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
-  // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): rows
-  // [ROWS, 64*MAXT) are padding (computed, never read as neighbours); ZROW is
-  // the all-zero row that out-of-board neighbour taps read.
+  // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): output
+  // rows [ROWS, 64*MAXT) are padding (computed from arbitrary data, never stored).
   static constexpr int RGROUPS = NN_WAVES / 2;  // row groups (x 2 column halves)
   static constexpr int MAXT = (RT + RGROUPS - 1) / RGROUPS;
-  static constexpr int ZROW = RGROUPS * MAXT * 16;
+  static constexpr int MROWS = RGROUPS * MAXT * 16;  // computed output rows
+  // Activations in LDS are stored per board with a one-cell zero border
+  // ((Y+2) x (X+2) cells), so every 3x3 neighbour of an on-board cell is a fixed
+  // row offset away and the implicit-GEMM A reads need no bounds checks.
+  static constexpr int PX = X + 2, PY = Y + 2, PA = PX * PY;
+  static constexpr int PROWS = NB * PA;
   // fp16 per activation row: 56-dword rows make the A-fragment ds_read_b128 (lane
   // groups {0-3,12-15,20-27}, ... ; 16 rows x 4 k-quarters) bank-conflict free.
   static constexpr int ASTR = C + 16;
+  static constexpr int ROWB = ASTR * 2;  // bytes per activation row
   static constexpr int NCT = C / 32;     // 16-col tiles per wave
   static constexpr int NCT_ALL = C / 16;
   static constexpr int P = 4 * A;
-  static constexpr int OFF_SCR = (((ZROW + 1) * ASTR * 2) + 15) / 16 * 16;
+  static constexpr int ACT_BYTES = (PROWS * ROWB + 15) / 16 * 16;
+  // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
-  static constexpr int OFF_POOL = OFF_SCR + ZROW * SCR * 4;
+  static constexpr int OFF_SCR = MROWS * SCR * 4;
+  static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
-  static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap (one buffer)
-  static constexpr int OFF_W = (OFF_VH + NB * 64 * 4 + 15) / 16 * 16;
-  static constexpr int LDS = OFF_W + 2 * WBUF * 16;
+  static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap (one slot)
+  // row tables (u16): rowPa[MROWS], rowBP[MROWS], bpRow[ROWS] -- built on the host
+  static constexpr int NTAB = 2 * MROWS + ROWS;
+  static constexpr int OFF_TAB = OFF_VH + NB * 64 * 4;
+  // per-block f32 parameter slabs (double buffered, filled one block ahead)
+  static constexpr int NPRM = 448;
+  static constexpr int OFF_PRM = (OFF_TAB + NTAB * 2 + 15) / 16 * 16;
+  static constexpr int OFF_W = OFF_PRM + 2 * NPRM * 4;
+  static constexpr int LDS = OFF_W + 3 * WBUF * 16;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
-  static_assert(ZROW * SCR * 4 <= (ZROW + 1) * ASTR * 2, "value-branch f32 scratch must fit in act");
+  static_assert(2 * MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
+  static_assert(96 * 64 * 4 <= MROWS * SCR * 4, "gpool linear weights must fit below scr");
+  static_assert(2 * PA * ROWB + 2 * 64 < 65536, "A-read offsets must fit the ds_read immediate");
   static_assert(LDS <= 163840, "LDS budget");
 };
 
@@ -75,8 +90,12 @@ struct NNGeo {
 __device__ unsigned long long g_nnPhase[4][64];
 #define NN_PHASE(i)                                  \
   do {                                               \
-    if(blockIdx.x < 4 && threadIdx.x == 0)           \
+    if(blockIdx.x < 4 && threadIdx.x == 0) {         \
       g_nnPhase[blockIdx.x][(i)] = clock64();        \
+      if((i) == 0 || (i) == 42)                      \
+        g_nnPhase[blockIdx.x][(i) == 0 ? 62 : 63] =  \
+            __builtin_amdgcn_s_memrealtime();        \
+    }                                                \
   } while(0)
 #else
 #define NN_PHASE(i) \
@@ -86,91 +105,108 @@ __device__ unsigned long long g_nnPhase[4][64];
 
 KC_D uint16_t f16bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }  // v_cvt_f16_f32, RNE
 
-// First accumulator row owned by this lane in tile tstart.  The empty asm makes
-// the value opaque so the compiler recomputes per-row LDS addresses at each use
-// instead of hoisting dozens of them out of the block loop (register spills).
-KC_D int laneRow(int tstart, int lane) {
-  int r = tstart * 16 + 4 * (lane >> 4);
-  asm volatile("" : "+v"(r));
-  return r;
+// Padded LDS row of cell p of board b.
+template <class G>
+KC_D int padCell(int b, int p) {
+  const int y = p / G::X, x = p - y * G::X;
+  return b * G::PA + (y + 1) * G::PX + x + 1;
 }
 
-// Implicit-GEMM convolution over the wave's tiles: acc[t][ct] += A(t, K) * B(K, ct).
-// Weights are staged per tap through a double-buffered LDS slab shared by the
-// workgroup's 8 waves: the next tap's fragments are loaded from L2 into registers
-// while this tap's MFMAs run, then stored to the other buffer (one barrier per tap).
+// Byte address of this lane's activation-fragment row for tile t, shifted to the
+// (-1,-1) neighbour so every tap / channel block is a non-negative immediate
+// offset.  Padding rows read row 0's cells (their outputs are never stored).
+template <class G>
+KC_D void aBases(int (&ab)[G::MAXT], const uint16_t* rowPa, int tstart, int lane) {
+#pragma unroll
+  for(int t = 0; t < G::MAXT; t++) {
+    const int r = (tstart + t) * 16 + (lane & 15);
+    ab[t] = ((int)rowPa[r] - G::PX - 1) * G::ROWB + 16 * (lane >> 4);
+  }
+}
+
+// Implicit-GEMM convolution over the wave's tiles, computed transposed:
+// acc[t][ct] += W(ct, K) * act(K, t), so each lane's accumulator holds 4
+// consecutive output channels of one position (16-byte-friendly epilogues).
+//
+// Weights stream through a 3-slot LDS ring shared by the workgroup's 8 waves
+// (tap k in slot k%3): tap k+2 is loaded from L2 into registers while tap k's
+// MFMAs run and stored to its slot at the end of the tap, one barrier per tap.
+// Within a wave the A/B fragments of the next K-step (next 32-channel block, or
+// the next tap's first block) are read from LDS while the current step's MFMAs
+// issue, so LDS latency overlaps the matrix cores instead of following a barrier.
+// Fully unrolled: every slot and fragment buffer index is a compile-time constant
+// and every LDS address a per-lane base plus an immediate.  The caller separates
+// consecutive convolutions with a barrier (the act rewrite).
 template <class G, int NTAPS, int NCB>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
-                    f32x4 (&acc)[G::MAXT][G::NCT], int tstart, int ntiles, int cg, int lane, int tid) {
+                    f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid) {
   constexpr int UNITS = NCB * G::NCT_ALL * 64;  // 16-B fragments per tap
   constexpr int PER = (UNITS + NN_NT - 1) / NN_NT;
-  {
+  constexpr int STEPS = NTAPS * NCB;
+#pragma unroll
+  for(int tap = 0; tap < (NTAPS < 2 ? NTAPS : 2); tap++) {
     h16x8 r[PER];
 #pragma unroll
     for(int u = 0; u < PER; u++)
       if(tid + u * NN_NT < UNITS)
-        r[u] = w[tid + u * NN_NT];
+        r[u] = w[(size_t)tap * UNITS + tid + u * NN_NT];
 #pragma unroll
     for(int u = 0; u < PER; u++)
       if(tid + u * NN_NT < UNITS)
-        wl[tid + u * NN_NT] = r[u];
+        wl[tap * G::WBUF + tid + u * NN_NT] = r[u];
   }
   __syncthreads();
-  const int kq = 8 * (lane >> 4);
-  const int r0 = tstart * 16 + (lane & 15);
-#pragma unroll 1
+  const char* actB = reinterpret_cast<const char*>(act);
+  const h16x8* wlane = wl + (cg * G::NCT) * 64 + lane;
+  h16x8 af[2][G::MAXT], bf[2][G::NCT];
+  auto loadStep = [&](int st, int buf) {
+    const int tap = st / NCB, cb = st - tap * NCB;
+    const int tb = NTAPS == 9 ? tap : 4;  // 1x1: the centre tap
+    const int aoff = ((tb / 3) * G::PX + tb % 3) * G::ROWB + cb * 64;
+    const h16x8* wb = wlane + (tap % 3) * G::WBUF + cb * G::NCT_ALL * 64;
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++)
+      bf[buf][ct] = wb[ct * 64];
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++)
+      af[buf][t] = *reinterpret_cast<const h16x8*>(actB + ab[t] + aoff);
+  };
+  loadStep(0, 0);
+#pragma unroll
   for(int tap = 0; tap < NTAPS; tap++) {
-    const bool more = tap + 1 < NTAPS;
+    const bool more = tap + 2 < NTAPS;
     h16x8 nx[PER];
     if(more) {
+      int tq = tid;
+      asm volatile("" : "+v"(tq));
 #pragma unroll
       for(int u = 0; u < PER; u++)
         if(tid + u * NN_NT < UNITS)
-          nx[u] = w[(size_t)(tap + 1) * UNITS + tid + u * NN_NT];
+          nx[u] = w[(size_t)(tap + 2) * UNITS + tq + u * NN_NT];
     }
-    const h16x8* wb = wl + (tap & 1) * G::WBUF;
-    const int dy = NTAPS == 9 ? tap / 3 - 1 : 0;
-    const int dx = NTAPS == 9 ? tap % 3 - 1 : 0;
-    // neighbour row (or the zero row) per tile, as an LDS element offset
-    int roff[G::MAXT];
-#pragma unroll
-    for(int t = 0; t < G::MAXT; t++) {
-      int r = r0 + t * 16;
-      int b = r / G::A;
-      int p = r - b * G::A;
-      int yy = p / G::X + dy;
-      int xx = p - (p / G::X) * G::X + dx;
-      bool ok = r < G::ROWS && yy >= 0 && yy < G::Y && xx >= 0 && xx < G::X;
-      roff[t] = (ok ? (r + dy * G::X + dx) : G::ZROW) * G::ASTR + kq;
-    }
-    // Issue every LDS read of the tap first (all K-chunks' A and B fragments), then
-    // the MFMAs: one exposed LDS latency per tap instead of one per K-chunk.
-    h16x8 bfr[NCB][G::NCT], afr[NCB][G::MAXT];
 #pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
-#pragma unroll
-      for(int ct = 0; ct < G::NCT; ct++)
-        bfr[cb][ct] = wb[(cb * G::NCT_ALL + cg * G::NCT + ct) * 64 + lane];
-#pragma unroll
-      for(int t = 0; t < G::MAXT; t++)
-        afr[cb][t] = *reinterpret_cast<const h16x8*>(act + roff[t] + cb * 32);
-    }
-#pragma unroll
-    for(int cb = 0; cb < NCB; cb++)
+      const int st = tap * NCB + cb;
+      if(st + 1 < STEPS)
+        loadStep(st + 1, (st + 1) & 1);
+      // keep the next step's LDS reads ahead of this step's MFMAs (the scheduler
+      // otherwise sinks them behind the MFMAs to shorten live ranges)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for(int t = 0; t < G::MAXT; t++)
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++)
-          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afr[cb][t], bfr[cb][ct], acc[t][ct], 0, 0, 0);
-    (void)ntiles;
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[st & 1][ct], af[st & 1][t], acc[t][ct], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if(more) {
-      h16x8* nb = wl + ((tap + 1) & 1) * G::WBUF;
+      h16x8* nb = wl + ((tap + 2) % 3) * G::WBUF;
 #pragma unroll
       for(int u = 0; u < PER; u++)
         if(tid + u * NN_NT < UNITS)
           nb[tid + u * NN_NT] = nx[u];
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -219,37 +255,173 @@ KC_D void zeroAcc(f32x4 (&a)[G::MAXT][G::NCT]) {
       a[t][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
-// act[row][col] = bf16(relu(v * s[col] + b[col])) for cols in [c0, c1).
+// First of the 4 consecutive channels lane `lane` holds in column tile ct.
+template <class G>
+KC_D int chOf(int cg, int ct, int lane) {
+  return cg * (G::C / 2) + ct * 16 + 4 * (lane >> 4);
+}
+
+KC_D uint2 packH4(float a, float b, float c, float d) {
+  return uint2{(uint32_t)f16bits(a) | ((uint32_t)f16bits(b) << 16), (uint32_t)f16bits(c) | ((uint32_t)f16bits(d) << 16)};
+}
+
+// act[pad(row)][ch..ch+3] = f16(relu(v * s[ch] + b[ch])) for on-board rows, all channels.
 template <class G, class V>
-KC_D void storeBnRelu(uint16_t* act, const V (&v)[G::MAXT][G::NCT], const float* __restrict__ s,
-                      const float* __restrict__ bb, int tstart, int ntiles, int cg, int lane, int c0, int c1) {
-  const int rl = laneRow(tstart, lane);
+KC_D void storeBnRelu(uint16_t* act, const uint16_t* rowPa, const V (&v)[G::MAXT][G::NCT], const float* __restrict__ s,
+                      const float* __restrict__ bb, int tstart, int cg, int lane) {
+  float4 sc[G::NCT], bi[G::NCT];
 #pragma unroll
   for(int ct = 0; ct < G::NCT; ct++) {
-    const int col = cg * (G::C / 2) + ct * 16 + (lane & 15);
-    if(cg * (G::C / 2) + ct * 16 < c0 || cg * (G::C / 2) + ct * 16 >= c1)
+    const int ch = chOf<G>(cg, ct, lane);
+    sc[ct] = *reinterpret_cast<const float4*>(s + ch);
+    bi[ct] = *reinterpret_cast<const float4*>(bb + ch);
+  }
+#pragma unroll
+  for(int t = 0; t < G::MAXT; t++) {
+    const int row = (tstart + t) * 16 + (lane & 15);
+    if(row >= G::ROWS)
       continue;
-    const float sc = s[col], bi = bb[col];
+    uint16_t* dst = act + (int)rowPa[row] * G::ASTR;
 #pragma unroll
-    for(int t = 0; t < G::MAXT; t++) {
-      if(t >= ntiles)
-        continue;
-#pragma unroll
-      for(int j = 0; j < 4; j++) {
-        int row = rl + t * 16 + j;
-        float x = (float)v[t][ct][j] * sc + bi;
-        x = x > 0.0f ? x : 0.0f;
-        act[row * G::ASTR + col] = f16bits(x);
+    for(int ct = 0; ct < G::NCT; ct++) {
+      const float y0 = fmaxf((float)v[t][ct][0] * sc[ct].x + bi[ct].x, 0.0f);
+      const float y1 = fmaxf((float)v[t][ct][1] * sc[ct].y + bi[ct].y, 0.0f);
+      const float y2 = fmaxf((float)v[t][ct][2] * sc[ct].z + bi[ct].z, 0.0f);
+      const float y3 = fmaxf((float)v[t][ct][3] * sc[ct].w + bi[ct].w, 0.0f);
+      *reinterpret_cast<uint2*>(dst + chOf<G>(cg, ct, lane)) = packH4(y0, y1, y2, y3);
+    }
+  }
+}
+
+// Zero the border cells of every board (all channels) after act was used as f32
+// scratch; 16-byte stores.
+template <class G>
+KC_D void zeroBorders(uint16_t* act, int tid) {
+  constexpr int CH = G::ASTR / 8;  // 16-B chunks per row
+  constexpr int NBORD = G::PA - G::A;
+  for(int idx = tid; idx < G::NB * NBORD * CH; idx += NN_NT) {
+    const int q = idx / CH, c = idx - q * CH;
+    const int b = q / NBORD, k = q - b * NBORD;
+    // k-th border cell: top row, bottom row, then left/right columns
+    int cell;
+    if(k < G::PX)
+      cell = k;
+    else if(k < 2 * G::PX)
+      cell = (G::PY - 1) * G::PX + (k - G::PX);
+    else {
+      const int m = k - 2 * G::PX;
+      cell = (1 + (m >> 1)) * G::PX + ((m & 1) ? G::PX - 1 : 0);
+    }
+    reinterpret_cast<uint4*>(act + (b * G::PA + cell) * G::ASTR)[c] = uint4{0u, 0u, 0u, 0u};
+  }
+}
+
+// KataGPool over 32 f32 channels of scr ([b*A+p][SCR]) per board: mean,
+// mean * (sqrt(A)-14)/10, max (model_pytorch.py:326-352); with vsrc also the value
+// head's mean, mean * (sqrt(A)-14)/10, mean * ((sqrt(A)-14)^2/100 - 0.1).
+// A lane pair per (board, channel), each summing half of the board's cells.
+template <class G>
+KC_D void poolBoards(const float* scr, const float* vsrc, float* poolP, float* poolV, float sqOff, int tid) {
+  for(int idx = tid; idx < G::NB * 64; idx += NN_NT) {
+    const int pr = idx >> 1, half = idx & 1;
+    const int b = pr >> 5, c = pr & 31;
+    const int p0 = half ? (G::A + 1) / 2 : 0, p1 = half ? G::A : (G::A + 1) / 2;
+    float s = 0.0f, m = 0.0f, sv = 0.0f;
+#pragma unroll 4
+    for(int p = p0; p < p1; p++) {
+      const int o = (b * G::A + p) * G::SCR + c;
+      const float v = scr[o];
+      s += v;
+      m = v > m ? v : m;
+      if(vsrc)
+        sv += vsrc[o];
+    }
+    s = s + __shfl_xor(s, 1, 64);
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    if(vsrc)
+      sv = sv + __shfl_xor(sv, 1, 64);
+    if(half == 0) {
+      const float mean = s / (float)G::A;
+      poolP[b * 96 + c] = mean;
+      poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
+      poolP[b * 96 + 64 + c] = m;
+      if(vsrc) {
+        const float meanv = sv / (float)G::A;
+        poolV[b * 96 + c] = meanv;
+        poolV[b * 96 + 32 + c] = meanv * (sqOff / 10.0f);
+        poolV[b * 96 + 64 + c] = meanv * ((sqOff * sqOff) / 100.0f - 0.1f);
       }
     }
   }
 }
 
+// out[b*ostr + o] = f(bias[o] + sum_i wT[i*O + o] * in[b*96 + i]) for every board,
+// O % 4 == 0, wT staged transposed in LDS.  A lane owns 4 consecutive outputs and
+// a quarter of the 96 inputs; the quarters are reduced across adjacent lanes.
+template <class G>
+KC_D void linear96(const float* wT, int O, const float* in, float* out, int ostr, const float* bias, bool relu,
+                   int tid) {
+  const int quads = O >> 2;
+  for(int idx = tid; idx < G::NB * quads * 4; idx += NN_NT) {
+    const int ks = idx & 3, q = (idx >> 2) % quads, b = (idx >> 2) / quads;
+    float4 s = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    const float* xi = in + b * 96 + ks * 24;
+    const float* wi = wT + (ks * 24) * O + 4 * q;
+#pragma unroll 4
+    for(int i = 0; i < 24; i++) {
+      const float4 w4 = *reinterpret_cast<const float4*>(wi + i * O);
+      const float xv = xi[i];
+      s.x += w4.x * xv;
+      s.y += w4.y * xv;
+      s.z += w4.z * xv;
+      s.w += w4.w * xv;
+    }
+#pragma unroll
+    for(int m = 1; m < 4; m <<= 1) {
+      s.x += __shfl_xor(s.x, m, 64);
+      s.y += __shfl_xor(s.y, m, 64);
+      s.z += __shfl_xor(s.z, m, 64);
+      s.w += __shfl_xor(s.w, m, 64);
+    }
+    if(ks == 0) {
+      float r[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+      for(int j = 0; j < 4; j++) {
+        float v = bias ? bias[4 * q + j] + r[j] : r[j];
+        out[b * ostr + 4 * q + j] = relu ? fmaxf(v, 0.0f) : v;
+      }
+    }
+  }
+}
+
+// Element `tid` of parameter slab k: block k's BN1/BN2 scale+bias and gpool BN
+// ([0,96) bn1s [96,192) bn1b [192,288) bn2s [288,384) bn2b [384,416) bngs
+// [416,448) bngb), or for k == nblocks the tip BN and head biases ([0,96) tips
+// [96,192) tipb [192,224) pBiasG [224,256) vBias1 [256,288) pBias2).
+KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ WF, int k, int tid) {
+  int src = -1;
+  const int f = tid < 384 ? tid / 96 : (tid < 416 ? 4 : 5), i = tid < 384 ? tid - 96 * f : (tid - 384) & 31;
+  if(k < L->nblocks) {
+    if(f == 0) src = L->bn1s[k] + i;
+    else if(f == 1) src = L->bn1b[k] + i;
+    else if(f == 2) src = L->bn2s[k] + i;
+    else if(f == 3) src = L->bn2b[k] + i;
+    else if(tid < 448 && L->kinds[k] == 1) src = (f == 4 ? L->bngs[k] : L->bngb[k]) + i;
+  } else if(tid < 288) {
+    if(tid < 96) src = L->tips + tid;
+    else if(tid < 192) src = L->tipb + tid - 96;
+    else if(tid < 224) src = L->pBiasG + tid - 192;
+    else if(tid < 256) src = L->vBias1 + tid - 224;
+    else src = L->pBias2 + tid - 256;
+  }
+  return src >= 0 ? WF[src] : 0.0f;
+}
+
 template <int X, int Y, int C>
 __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
-    kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF, int n,
-               const int* __restrict__ countDev, int inWords, float winLen, const uint64_t* __restrict__ in,
-               float* __restrict__ out) {
+    kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
+               const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev, int inWords,
+               float winLen, const uint64_t* __restrict__ in, float* __restrict__ out) {
   using G = NNGeo<X, Y, C>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
@@ -261,7 +433,6 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rg = wave >> 1, cg = wave & 1;
   const int tstart = rg * G::MAXT;
-  const int ntiles = G::MAXT;
   uint16_t* act = reinterpret_cast<uint16_t*>(smem);
   float* actF = reinterpret_cast<float*>(smem);
   float* scr = reinterpret_cast<float*>(smem + G::OFF_SCR);
@@ -269,197 +440,172 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   float* poolV = poolP + G::NB * 96;
   float* biasS = reinterpret_cast<float*>(smem + G::OFF_BIAS);
   float* vh = reinterpret_cast<float*>(smem + G::OFF_VH);
+  uint16_t* rowPa = reinterpret_cast<uint16_t*>(smem + G::OFF_TAB);  // [MROWS] padded cell of row
+  uint16_t* rowBP = rowPa + G::MROWS;                                 // [MROWS] b*A+p (0xFFFF: padding)
+  float* prm = reinterpret_cast<float*>(smem + G::OFF_PRM);  // [2][NPRM] parameter slabs
   h16x8* wl = reinterpret_cast<h16x8*>(smem + G::OFF_W);
   const float sqOff = sqrtf((float)G::A) - 14.0f;
 
-  // ---- unpack the packed V1 planes: act[row][0..31] (15 planes + zero pad), zero row ----
-  for(int idx = tid; idx < (G::ZROW + 1) * 32; idx += NN_NT) {
-    int row = idx >> 5, c = idx & 31;
-    uint16_t v = 0;
-    if(row < nb * G::A && c < NUM_SPATIAL) {
-      int b = row / G::A, p = row - b * G::A;
-      int i = c * G::A + p;
-      uint64_t word = in[(size_t)(base + b) * inWords + (i >> 6)];
-      v = ((word >> (i & 63)) & 1ULL) ? (uint16_t)0x3c00 : (uint16_t)0;
-    }
-    act[row * G::ASTR + c] = v;
+  // ---- row tables; unpack the packed V1 planes into the zero-bordered act ----
+  float pre = loadParam(L, WF, 0, tid);  // block 0's slab, stored after the stem conv
+  for(int i = tid; i < G::NTAB; i += NN_NT)
+    rowPa[i] = tabs[i];
+  for(int idx = tid; idx < G::ACT_BYTES / 16; idx += NN_NT)
+    reinterpret_cast<uint4*>(smem)[idx] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  for(int idx = tid; idx < nb * G::A * NUM_SPATIAL; idx += NN_NT) {
+    const int b = idx / (G::A * NUM_SPATIAL), i = idx - b * (G::A * NUM_SPATIAL);
+    const int c = i / G::A, p = i - c * G::A;
+    const uint64_t word = in[(size_t)(base + b) * inWords + (i >> 6)];
+    if((word >> (i & 63)) & 1ULL)
+      act[padCell<G>(b, p) * G::ASTR + c] = (uint16_t)0x3c00;
   }
-  for(int c = 32 + tid; c < G::C; c += NN_NT)
-    act[G::ZROW * G::ASTR + c] = 0;
   __syncthreads();
 
   NN_PHASE(1);
+  int ab[G::MAXT];
+  aBases<G>(ab, rowPa, tstart, lane);
   f16x4 x[G::MAXT][G::NCT];
   f32x4 acc[G::MAXT][G::NCT];
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1>(act, WB + L->wInit, wl, acc, tstart, ntiles, cg, lane, tid);
+  convTiles<G, 9, 1>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++) {
-      const int col = cg * (G::C / 2) + ct * 16 + (lane & 15);
-      const float gb = WF[L->globInit + col] * winLen;
+      const float4 g4 = *reinterpret_cast<const float4*>(WF + L->globInit + chOf<G>(cg, ct, lane));
 #pragma unroll
-      for(int t = 0; t < G::MAXT; t++)
-#pragma unroll
-        for(int j = 0; j < 4; j++)
-          acc[t][ct][j] += gb;
+      for(int t = 0; t < G::MAXT; t++) {
+        acc[t][ct][0] += g4.x * winLen;
+        acc[t][ct][1] += g4.y * winLen;
+        acc[t][ct][2] += g4.z * winLen;
+        acc[t][ct][3] += g4.w * winLen;
+      }
     }
   }
   packX<G>(x, acc);
+  if(tid < G::NPRM)
+    prm[tid] = pre;
   const int Cr = G::C - L->Cg;
   NN_PHASE(2);
   for(int blk = 0; blk < L->nblocks; blk++) {
     __syncthreads();  // previous conv finished reading act
     NN_PHASE(3 + 4 * blk);
-    storeBnRelu<G>(act, x, WF + L->bn1s[blk], WF + L->bn1b[blk], tstart, ntiles, cg, lane, 0, G::C);
+    const float* P = prm + (blk & 1) * G::NPRM;
+    storeBnRelu<G>(act, rowPa, x, P, P + 96, tstart, cg, lane);
     __syncthreads();
     zeroAcc<G>(acc);
+    pre = loadParam(L, WF, blk + 1, tid);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
-    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], wl, acc, tstart, ntiles, cg, lane, tid);
+    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid);
+    if(tid < G::NPRM)
+      prm[((blk + 1) & 1) * G::NPRM + tid] = pre;
     __syncthreads();
     NN_PHASE(5 + 4 * blk);
     if(L->kinds[blk] == 0) {
-      storeBnRelu<G>(act, acc, WF + L->bn2s[blk], WF + L->bn2b[blk], tstart, ntiles, cg, lane, 0, G::C);
+      storeBnRelu<G>(act, rowPa, acc, P + 192, P + 288, tstart, cg, lane);
       __syncthreads();
       unpackX<G>(acc, x);
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], wl, acc, tstart, ntiles, cg, lane, tid);
+      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid);
       packX<G>(x, acc);
     } else {
-      // g branch: BN-ReLU into scr (f32), then KataGPool per board (model_pytorch.py:326-352)
-      const float* gs = WF + L->bngs[blk];
-      const float* gbias = WF + L->bngb[blk];
-      const int rl = laneRow(tstart, lane);
+      // g branch: BN-ReLU into scr (f32, aliases the dead conv input), then
+      // KataGPool per board (model_pytorch.py:326-352)
+      const float* gs = P + 384;
+      const float* gbias = P + 416;
 #pragma unroll
       for(int ct = 0; ct < G::NCT; ct++) {
-        const int c0 = cg * (G::C / 2) + ct * 16;
-        if(c0 < Cr)
+        const int ch = chOf<G>(cg, ct, lane);
+        if(cg * (G::C / 2) + ct * 16 < Cr)
           continue;
-        const int gc = c0 - Cr + (lane & 15);
-        const float sc = gs[gc], bi = gbias[gc];
+        const int gc = ch - Cr;
+        const float4 sc = *reinterpret_cast<const float4*>(gs + gc);
+        const float4 bi = *reinterpret_cast<const float4*>(gbias + gc);
 #pragma unroll
         for(int t = 0; t < G::MAXT; t++) {
-          if(t >= ntiles)
+          const int row = (tstart + t) * 16 + (lane & 15);
+          if(row >= G::ROWS)
             continue;
-#pragma unroll
-          for(int j = 0; j < 4; j++) {
-            int row = rl + t * 16 + j;
-            float v = acc[t][ct][j] * sc + bi;
-            scr[row * G::SCR + gc] = v > 0.0f ? v : 0.0f;
-          }
+          *reinterpret_cast<float4*>(scr + (int)rowBP[row] * G::SCR + gc) =
+              float4{fmaxf(acc[t][ct][0] * sc.x + bi.x, 0.0f), fmaxf(acc[t][ct][1] * sc.y + bi.y, 0.0f),
+                     fmaxf(acc[t][ct][2] * sc.z + bi.z, 0.0f), fmaxf(acc[t][ct][3] * sc.w + bi.w, 0.0f)};
         }
       }
       __syncthreads();
       NN_PHASE(50);
-      float* lgT = reinterpret_cast<float*>(wl);  // weight slab is idle between convs
+      float* lgT = actF;  // transposed linear weights in the idle front of act
       stageT96(lgT, WF + L->linG[blk], Cr, tid);
-      // pooling: a lane pair per (board, channel), each summing half of the positions
-      for(int idx = tid; idx < G::NB * 64; idx += NN_NT) {
-        const int pr = idx >> 1, half = idx & 1;
-        const int b = pr >> 5, c = pr & 31;
-        const int p0 = half ? (G::A + 1) / 2 : 0, p1 = half ? G::A : (G::A + 1) / 2;
-        float s = 0.0f, m = 0.0f;
-#pragma unroll 4
-        for(int p = p0; p < p1; p++) {
-          float v = scr[(b * G::A + p) * G::SCR + c];
-          s += v;
-          m = v > m ? v : m;
-        }
-        s = s + __shfl_xor(s, 1, 64);
-        m = fmaxf(m, __shfl_xor(m, 1, 64));
-        if(half == 0) {
-          float mean = s / (float)G::A;
-          poolP[b * 96 + c] = mean;
-          poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
-          poolP[b * 96 + 64 + c] = m;
-        }
-      }
+      poolBoards<G>(scr, nullptr, poolP, poolV, sqOff, tid);
       __syncthreads();
       NN_PHASE(51);
-      {
-        for(int idx = tid; idx < G::NB * Cr; idx += NN_NT) {
-          const int b = idx / Cr, o = idx - b * Cr;
-          float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;  // four independent chains
-#pragma unroll 4
-          for(int i = 0; i < 96; i += 4) {
-            s0 += lgT[i * Cr + o] * poolP[b * 96 + i];
-            s1 += lgT[(i + 1) * Cr + o] * poolP[b * 96 + i + 1];
-            s2 += lgT[(i + 2) * Cr + o] * poolP[b * 96 + i + 2];
-            s3 += lgT[(i + 3) * Cr + o] * poolP[b * 96 + i + 3];
-          }
-          biasS[b * Cr + o] = (s0 + s1) + (s2 + s3);
-        }
-      }
+      linear96<G>(lgT, Cr, poolP, biasS, Cr, nullptr, false, tid);
       __syncthreads();
+      zeroBorders<G>(act, tid);  // the f32 scratch overwrote border cells (disjoint from r-epi cells)
       NN_PHASE(52);
       {
-        // r branch + gpool bias -> BN2-ReLU -> bf16 act (cols < Cr)
-        const float* s2 = WF + L->bn2s[blk];
-        const float* b2 = WF + L->bn2b[blk];
-        const int rl = laneRow(tstart, lane);
+        // r branch + gpool bias -> BN2-ReLU -> f16 act (channels < Cr)
+        const float* s2 = P + 192;
+        const float* b2 = P + 288;
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++) {
-          const int c0 = cg * (G::C / 2) + ct * 16;
-          if(c0 >= Cr)
+          if(cg * (G::C / 2) + ct * 16 >= Cr)
             continue;
-          const int col = c0 + (lane & 15);
-          const float sc = s2[col], bi = b2[col];
+          const int ch = chOf<G>(cg, ct, lane);
+          const float4 sc = *reinterpret_cast<const float4*>(s2 + ch);
+          const float4 bi = *reinterpret_cast<const float4*>(b2 + ch);
 #pragma unroll
           for(int t = 0; t < G::MAXT; t++) {
-            if(t >= ntiles)
+            const int row = (tstart + t) * 16 + (lane & 15);
+            if(row >= G::ROWS)
               continue;
-#pragma unroll
-            for(int j = 0; j < 4; j++) {
-              int row = rl + t * 16 + j;
-              int brd = row / G::A;
-              brd = brd < G::NB ? brd : G::NB - 1;
-              float v = (acc[t][ct][j] + biasS[brd * Cr + col]) * sc + bi;
-              act[row * G::ASTR + col] = f16bits(v > 0.0f ? v : 0.0f);
-            }
+            const float4 gb = *reinterpret_cast<const float4*>(biasS + ((int)rowBP[row] / G::A) * Cr + ch);
+            *reinterpret_cast<uint2*>(act + (int)rowPa[row] * G::ASTR + ch) =
+                packH4(fmaxf((acc[t][ct][0] + gb.x) * sc.x + bi.x, 0.0f),
+                       fmaxf((acc[t][ct][1] + gb.y) * sc.y + bi.y, 0.0f),
+                       fmaxf((acc[t][ct][2] + gb.z) * sc.z + bi.z, 0.0f),
+                       fmaxf((acc[t][ct][3] + gb.w) * sc.w + bi.w, 0.0f));
           }
         }
       }
       __syncthreads();
       unpackX<G>(acc, x);
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], wl, acc, tstart, ntiles, cg, lane, tid);
+      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid);
       packX<G>(x, acc);
     }
   }
   // ---- trunk tip ----
   __syncthreads();
   NN_PHASE(40);
-  storeBnRelu<G>(act, x, WF + L->tips, WF + L->tipb, tstart, ntiles, cg, lane, 0, G::C);
+  const float* PT = prm + (L->nblocks & 1) * G::NPRM;  // tip slab
+  storeBnRelu<G>(act, rowPa, x, PT, PT + 96, tstart, cg, lane);
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, wl, acc, tstart, ntiles, cg, lane, tid);
-  __syncthreads();  // act dead from here; reuse it as f32 [ROWS][32] for the value branch
+  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid);
+  __syncthreads();  // act dead from here: f32 [MROWS][SCR] value branch at actF, g branch at scr
   NN_PHASE(41);
   {
-    const float* pbg = WF + L->pBiasG;
-    const float* vb1 = WF + L->vBias1;
-    const int rl = laneRow(tstart, lane);
+    const float* pbg = PT + 192;
+    const float* vb1 = PT + 224;
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++) {
       const int c0 = cg * (G::C / 2) + ct * 16;
       if(c0 < 32)
         continue;
       const bool isG = c0 < 64;
-      const int hc = (c0 - (isG ? 32 : 64)) + (lane & 15);
-      const float bi = isG ? pbg[hc] : vb1[hc];
+      const int hc = chOf<G>(cg, ct, lane) - (isG ? 32 : 64);
+      const float4 bi = *reinterpret_cast<const float4*>((isG ? pbg : vb1) + hc);
       float* dst = isG ? scr : actF;
 #pragma unroll
       for(int t = 0; t < G::MAXT; t++) {
-        if(t >= ntiles)
+        const int row = (tstart + t) * 16 + (lane & 15);
+        if(row >= G::ROWS)
           continue;
-#pragma unroll
-        for(int j = 0; j < 4; j++) {
-          int row = rl + t * 16 + j;
-          float v = acc[t][ct][j] + bi;
-          dst[row * G::SCR + hc] = v > 0.0f ? v : 0.0f;
-        }
+        *reinterpret_cast<float4*>(dst + (int)rowBP[row] * G::SCR + hc) =
+            float4{fmaxf(acc[t][ct][0] + bi.x, 0.0f), fmaxf(acc[t][ct][1] + bi.y, 0.0f),
+                   fmaxf(acc[t][ct][2] + bi.z, 0.0f), fmaxf(acc[t][ct][3] + bi.w, 0.0f)};
       }
     }
   }
@@ -469,62 +615,11 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   float* l2T = plgT + 32 * 96;
   stageT96(plgT, WF + L->pLinG, 32, tid);
   stageT96(l2T, WF + L->vLin2, L->v2, tid);
-  for(int idx = tid; idx < G::NB * 64; idx += NN_NT) {
-    const int pr = idx >> 1, half = idx & 1;
-    const int b = pr >> 5, c = pr & 31;
-    const int p0 = half ? (G::A + 1) / 2 : 0, p1 = half ? G::A : (G::A + 1) / 2;
-    float s = 0.0f, m = 0.0f, sv = 0.0f;
-#pragma unroll 4
-    for(int p = p0; p < p1; p++) {
-      float v = scr[(b * G::A + p) * G::SCR + c];
-      s += v;
-      m = v > m ? v : m;
-      sv += actF[(b * G::A + p) * G::SCR + c];
-    }
-    s = s + __shfl_xor(s, 1, 64);
-    m = fmaxf(m, __shfl_xor(m, 1, 64));
-    sv = sv + __shfl_xor(sv, 1, 64);
-    if(half == 0) {
-      float mean = s / (float)G::A, meanv = sv / (float)G::A;
-      poolP[b * 96 + c] = mean;
-      poolP[b * 96 + 32 + c] = mean * (sqOff / 10.0f);
-      poolP[b * 96 + 64 + c] = m;
-      poolV[b * 96 + c] = meanv;
-      poolV[b * 96 + 32 + c] = meanv * (sqOff / 10.0f);
-      poolV[b * 96 + 64 + c] = meanv * ((sqOff * sqOff) / 100.0f - 0.1f);
-    }
-  }
+  poolBoards<G>(scr, actF, poolP, poolV, sqOff, tid);
   __syncthreads();
   NN_PHASE(54);
-  {
-    for(int idx = tid; idx < G::NB * 32; idx += NN_NT) {
-      const int b = idx >> 5, o = idx & 31;
-      float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-#pragma unroll 4
-      for(int i = 0; i < 96; i += 4) {
-        s0 += plgT[i * 32 + o] * poolP[b * 96 + i];
-        s1 += plgT[(i + 1) * 32 + o] * poolP[b * 96 + i + 1];
-        s2 += plgT[(i + 2) * 32 + o] * poolP[b * 96 + i + 2];
-        s3 += plgT[(i + 3) * 32 + o] * poolP[b * 96 + i + 3];
-      }
-      biasS[b * 32 + o] = (s0 + s1) + (s2 + s3);
-    }
-    const int v2 = L->v2;
-    const float* b2 = WF + L->vB2;
-    for(int idx = tid; idx < G::NB * v2; idx += NN_NT) {
-      const int b = idx / v2, oo = idx - b * v2;
-      float t0 = 0.0f, t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
-#pragma unroll 4
-      for(int i = 0; i < 96; i += 4) {
-        t0 += l2T[i * v2 + oo] * poolV[b * 96 + i];
-        t1 += l2T[(i + 1) * v2 + oo] * poolV[b * 96 + i + 1];
-        t2 += l2T[(i + 2) * v2 + oo] * poolV[b * 96 + i + 2];
-        t3 += l2T[(i + 3) * v2 + oo] * poolV[b * 96 + i + 3];
-      }
-      const float t = b2[oo] + ((t0 + t1) + (t2 + t3));
-      vh[b * 64 + oo] = t > 0.0f ? t : 0.0f;
-    }
-  }
+  linear96<G>(plgT, 32, poolP, biasS, 32, nullptr, false, tid);
+  linear96<G>(l2T, L->v2, poolV, vh, 64, WF + L->vB2, true, tid);
   __syncthreads();
   if(tid < G::NB * 4) {
     const int b = tid >> 2, o = tid & 3;
@@ -540,40 +635,40 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   }
   NN_PHASE(42);
   if(cg == 0) {
-    // policy: relu(p + gpool bias + bias2) -> 1x1 conv p1 -> 4 direction logits
-    const float* pb2 = WF + L->pBias2;
+    // policy: relu(p + gpool bias + bias2) -> 1x1 conv p1 -> 4 direction logits.
+    // Channels 0..31 live in column tiles 0 and 1: 8 per lane, reduced over the
+    // four lane groups (lane >> 4).
+    const float* pb2 = PT + 256;
     const float* w2 = WF + L->pConv2;
-    const int c0 = lane & 15, c1 = 16 + (lane & 15);
-    const int rl = laneRow(tstart, lane);
+    const int c0 = chOf<G>(0, 0, lane), c1 = chOf<G>(0, 1, lane);
 #pragma unroll
     for(int t = 0; t < G::MAXT; t++) {
-      if(t >= ntiles)
-        continue;
+      const int row = (tstart + t) * 16 + (lane & 15);
+      const int bp = row < G::ROWS ? (int)rowBP[row] : 0;
+      const int brd = bp / G::A;
+      float pv[8];
 #pragma unroll
       for(int j = 0; j < 4; j++) {
-        int row = rl + t * 16 + j;
-        int brd = row / G::A;
-        int bclamp = brd < G::NB ? brd : G::NB - 1;
-        float p0 = acc[t][0][j] + biasS[bclamp * 32 + c0] + pb2[c0];
-        float p1 = acc[t][1][j] + biasS[bclamp * 32 + c1] + pb2[c1];
-        p0 = p0 > 0.0f ? p0 : 0.0f;
-        p1 = p1 > 0.0f ? p1 : 0.0f;
-        float part[4];
+        pv[j] = fmaxf(acc[t][0][j] + biasS[brd * 32 + c0 + j] + pb2[c0 + j], 0.0f);
+        pv[4 + j] = fmaxf(acc[t][1][j] + biasS[brd * 32 + c1 + j] + pb2[c1 + j], 0.0f);
+      }
+      float part[4];
 #pragma unroll
-        for(int d = 0; d < 4; d++) {
-          float s = p0 * w2[d * 32 + c0] + p1 * w2[d * 32 + c1];
+      for(int d = 0; d < 4; d++) {
+        float s = 0.0f;
 #pragma unroll
-          for(int off = 1; off < 16; off <<= 1)
-            s += __shfl_xor(s, off, 64);
-          part[d] = s;
-        }
-        if((lane & 15) == 0 && row < nb * G::A) {
-          int pp = row - brd * G::A;
-          float* o = out + (size_t)(base + brd) * (G::P + 4);
+        for(int j = 0; j < 4; j++)
+          s += pv[j] * w2[d * 32 + c0 + j] + pv[4 + j] * w2[d * 32 + c1 + j];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        part[d] = s;
+      }
+      if((lane >> 4) == 0 && row < G::ROWS && brd < nb) {
+        const int pp = bp - brd * G::A;
+        float* o = out + (size_t)(base + brd) * (G::P + 4);
 #pragma unroll
-          for(int d = 0; d < 4; d++)
-            o[d * G::A + pp] = part[d];
-        }
+        for(int d = 0; d < 4; d++)
+          o[d * G::A + pp] = part[d];
       }
     }
   }
@@ -615,8 +710,42 @@ static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout
           }
 }
 
+// Output-row order of a workgroup's NB boards: row r takes a cell whose padded
+// LDS row is congruent to r mod 8 where possible.  With 224-byte activation rows
+// the 16 lanes of each ds_read_b128 lane group then hit 16 distinct 16-byte bank
+// slots (rows {0-3,12-15} and {4-11} of a tile each cover all residues).
+template <class G>
+static std::vector<uint16_t> rowTables() {
+  std::vector<uint16_t> tab(G::NTAB, 0);
+  uint16_t* rowPa = tab.data();
+  uint16_t* rowBP = rowPa + G::MROWS;
+  uint16_t* bpRow = rowBP + G::MROWS;
+  std::vector<std::vector<int>> bucket(8);
+  for(int b = 0; b < G::NB; b++)
+    for(int p = 0; p < G::A; p++) {
+      const int pa = b * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1;
+      bucket[pa % 8].push_back(b * G::A + p);
+    }
+  std::vector<size_t> next(8, 0);
+  for(int r = 0; r < G::ROWS; r++) {
+    int m = r % 8;
+    for(int k = 0; k < 8 && next[m] >= bucket[m].size(); k++)
+      m = (m + 1) % 8;
+    const int bp = bucket[m][next[m]++];
+    const int b = bp / G::A, p = bp % G::A;
+    rowPa[r] = (uint16_t)(b * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1);
+    rowBP[r] = (uint16_t)bp;
+    bpRow[bp] = (uint16_t)r;
+  }
+  for(int r = G::ROWS; r < G::MROWS; r++) {
+    rowPa[r] = rowPa[0];
+    rowBP[r] = 0xFFFF;
+  }
+  return tab;
+}
+
 bool NNEngine::supported(const ModelCfg& c, int X, int Y) {
-  return X == 5 && Y == 5 && c.C == 96 && c.Cg == 32 && c.p1 == 32 && c.g1 == 32 && c.v1 == 32 && c.v2 <= 64 &&
+  return X == 5 && Y == 5 && c.C == 96 && c.Cg == 32 && c.p1 == 32 && c.g1 == 32 && c.v1 == 32 && c.v2 <= 64 && c.v2 % 4 == 0 &&
          c.cin == NUM_SPATIAL && c.gin == 1 && (int)c.kinds.size() <= NN_MAX_BLOCKS;
 }
 
@@ -697,6 +826,9 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W) : cfg_(m.cfg), X_(X)
   KC_HIP(hipMalloc(&layoutDev_, sizeof(NNLayout)));
   KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
   using G = NNGeo<5, 5, 96>;
+  const std::vector<uint16_t> tab = rowTables<G>();
+  KC_HIP(hipMalloc(&tabDev_, tab.size() * 2));
+  KC_HIP(hipMemcpy(tabDev_, tab.data(), tab.size() * 2, hipMemcpyHostToDevice));
   static std::once_flag once;
   std::call_once(once, [] {
     KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -707,6 +839,7 @@ NNEngine::~NNEngine() {
   (void)hipFree(wHalf_);
   (void)hipFree(wF32_);
   (void)hipFree(layoutDev_);
+  (void)hipFree(tabDev_);
 }
 
 void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev) {
@@ -716,7 +849,7 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
   int grid = (n + G::NB - 1) / G::NB;
   hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_,
-                     (const h16x8*)wHalf_, wF32_, n, countDev, inWords, (float)W_, in, out);
+                     (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, inWords, (float)W_, in, out);
   KC_HIP(hipGetLastError());
 }
 

@@ -12,6 +12,7 @@ __global__ void __launch_bounds__(512, 2) k(float* out, unsigned long long* cyc,
   for(int t = 0; t < 4; t++) for(int c = 0; c < 3; c++) acc[t][c] = (f4){0, 0, 0, 0};
   __syncthreads();
   unsigned long long t0 = clock64();
+  unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
   for(int it = 0; it < iters; it++) {
 #pragma unroll
     for(int t = 0; t < 4; t++)
@@ -20,10 +21,14 @@ __global__ void __launch_bounds__(512, 2) k(float* out, unsigned long long* cyc,
         acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], b[c], acc[t][c], 0, 0, 0);
   }
   unsigned long long t1 = clock64();
+  unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
   float s = 0;
   for(int t = 0; t < 4; t++) for(int c = 0; c < 3; c++) s += acc[t][c][0];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-  if(threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  if(threadIdx.x == 0) {
+    cyc[2 * blockIdx.x] = t1 - t0;
+    cyc[2 * blockIdx.x + 1] = r1 - r0;  // 100 MHz constant clock
+  }
 }
 int main() {
   float* out; unsigned long long* cyc;
@@ -36,7 +41,9 @@ int main() {
   hipEventRecord(e1, 0);
   hipDeviceSynchronize();
   float ms; hipEventElapsedTime(&ms, e0, e1);
-  unsigned long long c; hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+  unsigned long long cc[2]; hipMemcpy(cc, cyc, 16, hipMemcpyDeviceToHost);
+  unsigned long long c = cc[0];
+  printf("wave0: %llu ticks in %.1f us (memrealtime) -> tick %.3f GHz\n", c, cc[1] / 100.0, c / (cc[1] * 10.0));
   double mf = iters * 12.0 * 2;  // per SIMD: 2 waves
   printf("256 WGs x 512 thr: wall %.3f ms -> %.1f ns/MFMA/SIMD; wave0 %.1f cycles per own MFMA, TFLOP/s %.0f\n", ms,
          ms * 1e6 / mf, (double)c / (iters * 12.0), 256 * 8 * iters * 12.0 * 16384 / (ms * 1e-3) / 1e12);

@@ -61,6 +61,8 @@ int main() {
       prev = ph[wg][i];
     }
     printf("  total %lld cycles\n", (long long)(prev - ph[wg][0]));
+    printf("  wall %.1f us (s_memrealtime) -> tick %.3f GHz\n", (ph[wg][63] - ph[wg][62]) / 100.0,
+           (double)(ph[wg][42] - ph[wg][0]) / ((ph[wg][63] - ph[wg][62]) * 10.0));
   }
   return 0;
 }
