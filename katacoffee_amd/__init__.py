@@ -110,7 +110,8 @@ def lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        L = ctypes.CDLL(LIB_PATH)
+        # KATACOFFEE_LIB: an alternative build of the same library (profiling builds)
+        L = ctypes.CDLL(os.environ.get("KATACOFFEE_LIB", LIB_PATH))
         L.coffee_last_error.restype = ctypes.c_char_p
         L.coffee_model_write_random.argtypes = [ctypes.c_char_p, c_u64, ctypes.c_char_p]
         L.coffee_model_flops.argtypes = [ctypes.c_char_p, c_i, c_p]

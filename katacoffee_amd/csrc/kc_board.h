@@ -200,21 +200,58 @@ KC_D bool v1Bit(const DTables& T, const DBoard& b, int plane, int c, int sym) {
 
 // Packs the 15 V1 planes (symmetric frame) into T.inWords words: bit i of the
 // flat [plane][cell] index lands in word i>>6, bit i&63 (oracle packPlanes).
+// Lane s evaluates all 15 features of symmetric cell s (one table lookup, the
+// four axes once), one ballot per plane collects them, and lane w assembles
+// word w from the uniform plane masks.
 KC_D void encodePackedWave(const DTables& T, const DBoard& b, int sym, uint64_t* out) {
   if(T.X != T.Y)
     sym &= 3;
-  const int A = T.A;
-  for(int w = 0; w < T.inWords; w++) {
-    int i = w * 64 + laneId();
-    bool bit = false;
-    if(i < NUM_SPATIAL * A) {
-      int plane = i / A, s = i % A;
-      bit = v1Bit(T, b, plane, T.invSymCell[sym][s], sym);
+  const int A = T.A, lane = laneId();
+  const int h0 = hCell(b, 0);
+  const int sd0 = h0 >= 0 ? T.symDir[sym][hDir(b, 0)] : -1;
+  uint64_t word = 0;
+  for(int base = 0; base < A; base += 64) {
+    const int s = base + lane;
+    uint32_t f = 0;
+    if(s < A) {
+      const int c = T.invSymCell[sym][s];
+      const int col = colorAt(b, c);
+      f = 1u;
+      if(col != 0)
+        f |= col == b.pla ? 2u : 4u;
+      if(h0 == c && sd0 >= 0 && sd0 < 4)
+        f |= 1u << (3 + sd0);
+#pragma unroll
+      for(int k = 1; k < 5; k++)
+        if(hCell(b, k) == c)
+          f |= 1u << (6 + k);
+      bool legal = false, run[3] = {false, false, false};
+      for(int d = 0; d < 4; d++) {
+        legal = legal || isLegal(T, b, c, d);
+        const int n = runAlong(T, b, c, d);
+#pragma unroll
+        for(int j = 0; j < 3; j++)
+          run[j] = run[j] || (n >= 1 && n == T.W - 1 - j);
+      }
+      f |= (legal ? 1u : 0u) << 11;
+#pragma unroll
+      for(int j = 0; j < 3; j++)
+        f |= (run[j] ? 1u : 0u) << (12 + j);
     }
-    uint64_t word = ballot(bit);
-    if(laneId() == 0)
-      out[w] = word;
+    // plane p's chunk covers flat bits [p*A + base, p*A + base + 64): OR the part
+    // falling into this lane's word [64*lane, 64*lane + 64)
+#pragma unroll
+    for(int p = 0; p < NUM_SPATIAL; p++) {
+      const uint64_t m = ballot((f >> p) & 1u);
+      const int o = p * A + base - 64 * lane;
+      if(o >= 0 && o < 64)
+        word |= m << o;
+      else if(o < 0 && o > -64)
+        word |= m >> (-o);
+    }
   }
+  if(lane < T.inWords)
+    out[lane] = word;
 }
 
 }  // namespace kc

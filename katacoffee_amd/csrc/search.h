@@ -118,7 +118,6 @@ struct SearchDev {
   // network batch
   uint64_t* nnIn;        // [G][inWords]
   float* nnOut;          // [G][P+4]
-  int32_t* nnCount;      // rows in this round's batch
   // commit queue
   int32_t* commitList;   // [G]
   int32_t* commitCount;

@@ -30,7 +30,59 @@ static constexpr int BIG = 0x7fffffff;
 KC_D int64_t svbQ(float x) { return llrintf(x * 4294967296.0f); }
 KC_D float svbF(int64_t v) { return (float)v * (1.0f / 4294967296.0f); }
 
-KC_D void waveSync() { __syncthreads(); }  // blocks are one wave: barrier + memory fence
+// Search blocks are a single wave and only that wave touches its game's arrays
+// during a launch.  A wave's LDS and vector-memory instructions are performed in
+// program order, so lane-to-lane visibility (one lane writes, all lanes read)
+// needs only a compiler barrier; a __syncthreads() fence would additionally make
+// every such step wait for all outstanding global stores to reach L2.
+KC_D void waveSync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+#ifdef KC_SEARCH_PROFILE
+// Cycle accounting of the search kernels (tools/search_phase.py; profiling build
+// only): per-block phase cycles, accumulated in LDS during the kernel and added to
+// the block's own slot at exit (no contended atomics inside the timed paths).
+//  0 select blocks   1 select total   2 loadGame   3 descend   4 path levels
+//  5 selectBest      6 expansion      7 encode
+// 10 backup blocks  11 backup total  12 postprocess+order  13 path backup  14 leaf value
+constexpr int SPROF_MAXG = 16384;
+__device__ unsigned long long g_searchProf[SPROF_MAXG * 16];
+KC_D unsigned long long* sprofLds() {
+  __shared__ unsigned long long c[16];
+  return c;
+}
+#define SPROF_NOW() clock64()
+#define SPROF_INIT()                   \
+  do {                                 \
+    if(laneId() < 16)                  \
+      sprofLds()[laneId()] = 0;        \
+    __syncthreads();                   \
+  } while(0)
+#define SPROF_ADD(i, v)                                 \
+  do {                                                  \
+    if(laneId() == 0)                                   \
+      sprofLds()[(i)] += (unsigned long long)(v);       \
+  } while(0)
+#define SPROF_FLUSH()                                                           \
+  do {                                                                          \
+    __syncthreads();                                                            \
+    if(laneId() < 16 && blockIdx.x < SPROF_MAXG)                                \
+      g_searchProf[blockIdx.x * 16 + laneId()] += sprofLds()[laneId()];         \
+  } while(0)
+#else
+#define SPROF_NOW() 0ull
+#define SPROF_INIT() \
+  do {               \
+  } while(0)
+#define SPROF_ADD(i, v) \
+  do {                  \
+  } while(0)
+#define SPROF_FLUSH() \
+  do {                \
+  } while(0)
+#endif
 
 // Per-game view of the SoA arrays.
 struct GV {
@@ -547,13 +599,18 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
     const bool isRoot = ni == s.rootIdx;
     const float* pol = isRoot ? v.rootNoised() : v.pol(ni);
     int newPos = -1;
+    const unsigned long long tSel = SPROF_NOW();
     int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits);
+    SPROF_ADD(5, SPROF_NOW() - tSel);
+    (void)tSel;
     if(slot < 0) {
       s.leafKind = LEAF_NOCHILD;
       s.leafNode = ni;
       break;
     }
     if(slot == n.numChildren) {
+      const unsigned long long tExp = SPROF_NOW();
+      (void)tExp;
       const int cell = newPos % T.A, dir = newPos / T.A;
       // SVB key of the expansion (needs the board before the move); computed
       // up front so no second board copy stays live across playMoveWave.
@@ -590,6 +647,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
       }
       s.pathLen++;
       waveSync();
+      SPROF_ADD(6, SPROF_NOW() - tExp);
       const Node& c = v.nodes()[child];
       if(c.visits > 0) {
         s.leafKind = LEAF_CATCHUP;
@@ -635,6 +693,8 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
   GV v(d, g);
   __shared__ GameDev s;
+  SPROF_INIT();
+  const unsigned long long t0 = SPROF_NOW();
   loadGame(v, s);
   if(s.phase == PH_COMMIT) {
     s.leafKind = LEAF_NONE;
@@ -642,6 +702,9 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
       d.games[g].leafKind = LEAF_NONE;
     return;
   }
+  const unsigned long long t1 = SPROF_NOW();
+  (void)t0;
+  (void)t1;
   DRng rng = DRng{s.rngSeed, s.rngCtr};
   if(s.phase == PH_ROOTEVAL) {
     if(s.rootK == 0) {
@@ -663,18 +726,28 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     if(s.leafKind == LEAF_NN)
       s.leafSym = (int)rng.below(8);
   }
+  const unsigned long long t2 = SPROF_NOW();
+  (void)t2;
   s.rngCtr = rng.ctr;
   if(s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL) {
-    int slot = 0;
-    if(v.lane == 0)
-      slot = atomicAdd(d.nnCount, 1);
-    slot = bcastI(slot, 0);
+    // the game's own batch row: no shared counter (a same-address atomic from
+    // every block serialises at L2); the network evaluates all G rows
+    const int slot = g;
     s.nnSlot = slot;
     s.nnEvals++;
     encodePackedWave(v.T, s.leaf, s.leafSym, d.nnIn + (size_t)slot * d.inWords);
   }
+  const unsigned long long t3 = SPROF_NOW();
+  (void)t3;
   waveSync();
   storeGame(v, s);
+  SPROF_ADD(0, 1);
+  SPROF_ADD(1, SPROF_NOW() - t0);
+  SPROF_ADD(2, t1 - t0);
+  SPROF_ADD(3, t2 - t1);
+  SPROF_ADD(4, s.pathLen);
+  SPROF_ADD(7, t3 - t2);
+  SPROF_FLUSH();
 }
 
 // oracle postprocess (nneval.cpp:702-815 + copyOutputsWithSymmetry nninputs.cpp:349-357)
@@ -858,9 +931,16 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
   __shared__ float scratch[2 * MAX_P];
   GV v(d, g);
   __shared__ GameDev s;
+  SPROF_INIT();
+  const unsigned long long t0 = SPROF_NOW();
+  (void)t0;
   loadGame(v, s);
   if(s.leafKind == LEAF_NONE)
     return;
+  unsigned long long tPost = 0, tLeaf = 0, tPath = 0;
+  (void)tPost;
+  (void)tLeaf;
+  (void)tPath;
   const SP& sp = d.sp;
   const int P = d.P;
   const float* o = d.nnOut + (size_t)s.nnSlot * (P + 4);
@@ -920,6 +1000,8 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
     if(s.leafKind == LEAF_NN) {
       float w, l;
       float* pol = v.pol(s.leafNode);
+      const unsigned long long ta = SPROF_NOW();
+      (void)ta;
       postprocess<NI>(v, s.leaf, s.leafSym, o, pol, w, l);
       waveSync();
       buildOrder(v, s.leafNode, pol, scratch);
@@ -930,7 +1012,11 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
         n->flags |= 1;
       }
       waveSync();
+      const unsigned long long tb = SPROF_NOW();
+      (void)tb;
       addLeafValue(v, s, s.leafNode, w - l, false, true);
+      tPost = tb - ta;
+      tLeaf = SPROF_NOW() - tb;
     } else if(s.leafKind == LEAF_TERMINAL) {
       float val = s.leaf.winner == 2 ? 1.0f : (s.leaf.winner == 1 ? -1.0f : 0.0f);
       addLeafValue(v, s, s.leafNode, val, true, false);
@@ -940,6 +1026,8 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
     }
     const int32_t* pn = v.pathNode();
     const int32_t* ps = v.pathSlot();
+    const unsigned long long tp0 = SPROF_NOW();
+    (void)tp0;
     for(int j = s.pathLen - 1; j >= 0; j--) {
       const int node = pn[j], slot = ps[j];
       waveSync();
@@ -948,6 +1036,7 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
       waveSync();
       recompute<NI>(v, s, node, 1, node == s.rootIdx);
     }
+    tPath = SPROF_NOW() - tp0;
     s.playouts++;
     needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)sp.maxVisits;
   }
@@ -959,7 +1048,33 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
   s.leafKind = LEAF_NONE;
   waveSync();
   storeGame(v, s);
+  SPROF_ADD(10, 1);
+  SPROF_ADD(11, SPROF_NOW() - t0);
+  SPROF_ADD(12, tPost);
+  SPROF_ADD(13, tPath);
+  SPROF_ADD(14, tLeaf);
+  SPROF_FLUSH();
 }
+
+#ifdef KC_SEARCH_PROFILE
+}  // namespace kc
+#include <algorithm>
+#include <vector>
+namespace kc {
+extern "C" void coffee_debug_search_profile(unsigned long long* out, int reset) {
+  std::vector<unsigned long long> all((size_t)SPROF_MAXG * 16);
+  KC_HIP(hipDeviceSynchronize());
+  KC_HIP(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(g_searchProf), all.size() * 8));
+  for(int i = 0; i < 16; i++)
+    out[i] = 0;
+  for(size_t k = 0; k < all.size(); k++)
+    out[k % 16] += all[k];
+  if(reset) {
+    std::fill(all.begin(), all.end(), 0ull);
+    KC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_searchProf), all.data(), all.size() * 8));
+  }
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Commit: move choice, targets, tree reuse, rows.

@@ -122,7 +122,6 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.turnPol = devAlloc<int16_t>(owned_, (size_t)G * d.maxTurns * P);
   d.nnIn = devAlloc<uint64_t>(owned_, (size_t)G * ht.inWords);
   d.nnOut = devAlloc<float>(owned_, (size_t)G * (P + 4));
-  d.nnCount = devAlloc<int32_t>(owned_, 1);
   d.commitList = devAlloc<int32_t>(owned_, G);
   d.commitCount = devAlloc<int32_t>(owned_, 1);
   const int pb = (A + 7) / 8;
@@ -203,13 +202,12 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
     st = stream_;
   const SearchDev& d = hd_;
   for(int r = 0; r < rounds; r++) {
-    KC_HIP(hipMemsetAsync(d.nnCount, 0, sizeof(int32_t), st));
     timed(0, st, [&] { launchSelect(d, dd_, st); });
     timed(1, st, [&] {
       if(nn_)
-        nn_->forward(d.G, d.nnIn, d.nnOut, st, d.nnCount);
+        nn_->forward(d.G, d.nnIn, d.nnOut, st, nullptr);
       else
-        launchFakeNet(T_, d.G, d.nnIn, d.nnOut, st, d.nnCount);
+        launchFakeNet(T_, d.G, d.nnIn, d.nnOut, st, nullptr);
     });
     timed(2, st, [&] { launchBackup(d, dd_, st); });
     rounds_++;

@@ -1,0 +1,47 @@
+"""Cycle accounting of the search kernels on the bench workload (C2).
+Needs the profiling build:  make -C katacoffee_amd/csrc prof
+usage: python tools/search_phase.py [--games 4096] [--rounds 300] [--warmup 600]"""
+import argparse
+import ctypes
+import os
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+os.environ.setdefault("KATACOFFEE_LIB", os.path.join(REPO, "tools", "_build", "libkatacoffee_prof.so"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--games", type=int, default=4096)
+    ap.add_argument("--visits", type=int, default=600)
+    ap.add_argument("--rounds", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=600)
+    a = ap.parse_args()
+    import katacoffee_amd as kc
+    L = kc.lib()
+    prof = (ctypes.c_ulonglong * 16)()
+    path = os.path.join(tempfile.mkdtemp(), "m.cfnn")
+    kc.write_random_model("b6c96", 0xC0FFEE, path)
+    sp = kc.Selfplay(5, 5, 4, num_games=a.games, max_visits=a.visits, seed=1, model_path=path, commit_interval=8)
+    sp.step(a.warmup)
+    sp.sync()
+    L.coffee_debug_search_profile(prof, 1)
+    sp.step(a.rounds)
+    sp.sync()
+    L.coffee_debug_search_profile(prof, 1)
+    p = list(prof)
+    nb, nk = max(p[0], 1), max(p[10], 1)
+    print("select: %d blocks over %d rounds" % (p[0], a.rounds))
+    for name, i in [("total", 1), ("loadGame", 2), ("descend", 3), ("  selectBest", 5), ("  expansion", 6),
+                    ("encode+slot", 7)]:
+        print("  %-14s %8.0f cycles/block" % (name, p[i] / nb))
+    print("  path levels    %8.2f per block" % (p[4] / nb))
+    print("backup: %d blocks" % p[10])
+    for name, i in [("total", 11), ("post+order", 12), ("leaf value", 14), ("path backup", 13)]:
+        print("  %-14s %8.0f cycles/block" % (name, p[i] / nk))
+
+
+if __name__ == "__main__":
+    main()
