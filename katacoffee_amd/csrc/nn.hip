@@ -124,38 +124,74 @@ KC_D void aBases(int (&ab)[G::MAXT], const uint16_t* rowPa, int tstart, int lane
   }
 }
 
+// LDS byte address of a pointer into dynamic shared memory.
+KC_D uint32_t ldsAddr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// One 1-KiB LDS-DMA piece: each lane's 16 bytes at src land at lds + 16 * lane
+// (global_load_lds_dwordx4, no VGPR destination).  Issued from inline asm so the
+// compiler neither waits on it nor reorders LDS accesses around it; completion is
+// counted by hand (s_waitcnt vmcnt) before the barrier that publishes the slot.
+KC_D void glds16(const void* src, uint32_t lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+
+// A tap's weights (CH pieces of 64 fragments) into its ring slot; piece c by wave c % 8.
+KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, int wave, int lane) {
+  for(int c = wave; c < ch; c += NN_WAVES)
+    glds16(src + c * 64 + lane, slotAddr + c * 1024);
+}
+
+template <int N>
+KC_D void waitVm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// Workgroup barrier that leaves LDS-DMA loads in flight (a __syncthreads()
+// would drain them with vmcnt(0)); LDS reads and writes issued before it complete.
+KC_D void barrierKeepDma() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Implicit-GEMM convolution over the wave's tiles, computed transposed:
 // acc[t][ct] += W(ct, K) * act(K, t), so each lane's accumulator holds 4
 // consecutive output channels of one position (16-byte-friendly epilogues).
 //
-// Weights stream through a 3-slot LDS ring shared by the workgroup's 8 waves
-// (tap k in slot k%3): tap k+2 is loaded from L2 into registers while tap k's
-// MFMAs run and stored to its slot at the end of the tap, one barrier per tap.
-// Within a wave the A/B fragments of the next K-step (next 32-channel block, or
-// the next tap's first block) are read from LDS while the current step's MFMAs
-// issue, so LDS latency overlaps the matrix cores instead of following a barrier.
-// Fully unrolled: every slot and fragment buffer index is a compile-time constant
-// and every LDS address a per-lane base plus an immediate.  The caller separates
-// consecutive convolutions with a barrier (the act rewrite).
-template <class G, int NTAPS, int NCB>
+// Weights stream through a 3-slot LDS ring shared by the workgroup's 8 waves by
+// LDS-DMA: tap k lives in slot k%3, and tap k+2 is requested at the start of tap
+// k, two taps ahead of its use.  The stream runs across convolutions: taps 7 and
+// 8 request the NEXT convolution's taps 0 and 1 (wNext, chNext pieces per tap,
+// nextTaps), so only the first convolution pays an L2 round trip up front.  One
+// barrier per tap, before its last K-step: it publishes tap k+1 (each wave first
+// retires its own pieces of it) and frees slot k%3 for the request of tap k+3.
+// Within a wave the A/B fragments of the next K-step are read from LDS while the
+// current step's MFMAs issue.  Fully unrolled: slot and fragment-buffer indices
+// are compile-time constants and every LDS read a per-lane base plus an immediate.
+// The caller keeps ring slots 0/1 untouched between convolutions and separates
+// them with __syncthreads() (which also retires the requests for taps 0/1).
+// DBG (tools/conv_bench.hip ablations only): bit 0 skips the weight requests, bit 1
+// the per-tap barriers, bit 3 the vmcnt waits, bit 8 the entry wait + barrier.
+template <class G, int NTAPS, int NCB, bool FIRST, int DBG = 0>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
-                    f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid) {
-  constexpr int UNITS = NCB * G::NCT_ALL * 64;  // 16-B fragments per tap
-  constexpr int PER = (UNITS + NN_NT - 1) / NN_NT;
+                    f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid,
+                    const h16x8* __restrict__ wNext, int chNext, int nextTaps) {
+  constexpr int CH = NCB * G::NCT_ALL;  // 1-KiB pieces per tap
+  constexpr int UNITS = CH * 64;        // 16-B fragments per tap
   constexpr int STEPS = NTAPS * NCB;
+  const int wave = tid >> 6;
+  const uint32_t ring = ldsAddr(wl);
+  if(FIRST) {
 #pragma unroll
-  for(int tap = 0; tap < (NTAPS < 2 ? NTAPS : 2); tap++) {
-    h16x8 r[PER];
-#pragma unroll
-    for(int u = 0; u < PER; u++)
-      if(tid + u * NN_NT < UNITS)
-        r[u] = w[(size_t)tap * UNITS + tid + u * NN_NT];
-#pragma unroll
-    for(int u = 0; u < PER; u++)
-      if(tid + u * NN_NT < UNITS)
-        wl[tap * G::WBUF + tid + u * NN_NT] = r[u];
+    for(int tap = 0; tap < (NTAPS < 2 ? NTAPS : 2); tap++)
+      stageTapDma(w + (size_t)tap * UNITS, ring + tap * G::WBUF * 16, CH, wave, lane);
   }
-  __syncthreads();
+  if(!(DBG & 256)) {
+    waitVm<0>();
+    __syncthreads();
+  }
   const char* actB = reinterpret_cast<const char*>(act);
   const h16x8* wlane = wl + (cg * G::NCT) * 64 + lane;
   h16x8 af[2][G::MAXT], bf[2][G::NCT];
@@ -174,19 +210,28 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   loadStep(0, 0);
 #pragma unroll
   for(int tap = 0; tap < NTAPS; tap++) {
-    const bool more = tap + 2 < NTAPS;
-    h16x8 nx[PER];
-    if(more) {
-      int tq = tid;
-      asm volatile("" : "+v"(tq));
-#pragma unroll
-      for(int u = 0; u < PER; u++)
-        if(tid + u * NN_NT < UNITS)
-          nx[u] = w[(size_t)(tap + 2) * UNITS + tq + u * NN_NT];
-    }
+    // request stream tap tap+2 (this conv's, or the next conv's tap 0 / 1)
+    if(DBG & 1) {
+    } else if(tap + 2 < NTAPS)
+      stageTapDma(w + (size_t)(tap + 2) * UNITS, ring + ((tap + 2) % 3) * G::WBUF * 16, CH, wave, lane);
+    else if(NTAPS == 9 && tap == 7)
+      stageTapDma(wNext, ring, chNext, wave, lane);
+    else if(NTAPS == 9 && tap == 8 && nextTaps > 1)
+      stageTapDma(wNext + chNext * 64, ring + G::WBUF * 16, chNext, wave, lane);
 #pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
       const int st = tap * NCB + cb;
+      if(cb == NCB - 1 && tap + 1 < NTAPS) {
+        // retire this wave's pieces of tap+1 (only the tap+2 request, >= N pieces
+        // per wave, may stay in flight), then publish them / free slot tap%3
+        if(DBG & 8) {
+        } else if(tap + 2 < NTAPS)
+          waitVm<CH / NN_WAVES>();
+        else
+          waitVm<(2 * G::NCT_ALL) / NN_WAVES>();  // next conv's tap 0: at least 12 pieces
+        if(!(DBG & 2))
+          barrierKeepDma();
+      }
       if(st + 1 < STEPS)
         loadStep(st + 1, (st + 1) & 1);
       // keep the next step's LDS reads ahead of this step's MFMAs (the scheduler
@@ -198,14 +243,6 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
         for(int ct = 0; ct < G::NCT; ct++)
           acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[st & 1][ct], af[st & 1][t], acc[t][ct], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-    }
-    if(more) {
-      h16x8* nb = wl + ((tap + 2) % 3) * G::WBUF;
-#pragma unroll
-      for(int u = 0; u < PER; u++)
-        if(tid + u * NN_NT < UNITS)
-          nb[tid + u * NN_NT] = nx[u];
-      __syncthreads();
     }
   }
 }
@@ -468,7 +505,8 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   f16x4 x[G::MAXT][G::NCT];
   f32x4 acc[G::MAXT][G::NCT];
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid);
+  convTiles<G, 9, 1, true>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
+                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL, L->nblocks > 0 ? 9 : 1);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
 #pragma unroll
@@ -497,17 +535,22 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     zeroAcc<G>(acc);
     pre = loadParam(L, WF, blk + 1, tid);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
-    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid);
+    convTiles<G, 9, G::C / 32, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
+                                      (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL, 9);
     if(tid < G::NPRM)
       prm[((blk + 1) & 1) * G::NPRM + tid] = pre;
     __syncthreads();
     NN_PHASE(5 + 4 * blk);
+    const bool lastBlk = blk + 1 == L->nblocks;
+    const h16x8* nextW = lastBlk ? WB + L->wHead : WB + L->wConv1[lastBlk ? 0 : blk + 1];
+    const int nextTaps = lastBlk ? 1 : 9;
     if(L->kinds[blk] == 0) {
       storeBnRelu<G>(act, rowPa, acc, P + 192, P + 288, tstart, cg, lane);
       __syncthreads();
       unpackX<G>(acc, x);
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid);
+      convTiles<G, 9, G::C / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                        3 * G::NCT_ALL, nextTaps);
       packX<G>(x, acc);
     } else {
       // g branch: BN-ReLU into scr (f32, aliases the dead conv input), then
@@ -571,7 +614,8 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       __syncthreads();
       unpackX<G>(acc, x);
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid);
+      convTiles<G, 9, (G::C - 32) / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                               3 * G::NCT_ALL, nextTaps);
       packX<G>(x, acc);
     }
   }
@@ -583,7 +627,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid);
+  convTiles<G, 1, G::C / 32, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0);
   __syncthreads();  // act dead from here: f32 [MROWS][SCR] value branch at actF, g branch at scr
   NN_PHASE(41);
   {

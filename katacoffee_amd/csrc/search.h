@@ -5,7 +5,8 @@
 //   Node      nodes[G][cap]                    64-B statistics record per search node
 //   Edge      edges[G][cap][P]                 (child, edgeVisits, prior, move) per child slot,
 //                                              slots in expansion order (SearchChildPointer, searchnode.h)
-//   uint16_t  order[G][cap][P]                 legal moves by descending prior (next expansion = order[k])
+//   OrderEnt  order[G][cap][P]                 legal moves by descending prior (next expansion = order[k])
+//   uint64_t  nodeKey[G][cap][2]               transposition key per node (TT rebuild after tree reuse)
 //   float     policy[G][cap][P]                NN policy of the node (NNOutput::policyProbs)
 //   uint32_t  freeList[G][cap], allocBits[G][cap/32]   node allocator
 //   TT        ttKey[G][ttCap][2], ttNode[G][ttCap]     transposition table (searchnodetable.h)
@@ -56,9 +57,21 @@ struct Node {
   uint16_t numChildren;
   uint8_t nextPla;
   uint8_t flags;                  // 1 expanded (NN output stored), 2 terminal
-  uint64_t key0, key1;            // transposition key
+  // next expansion of a non-root node (order[numChildren]), cached here so the
+  // selection reads it with the node record: prior and policy position
+  // (0xFFFF: every legal move expanded)
+  float nextPrior;
+  uint16_t nextPos;
+  uint16_t pad0;
+  uint32_t pad1[2];
 };
 static_assert(sizeof(Node) == 64, "Node layout");
+
+// One entry of a node's expansion order: the move and its prior (pos 0xFFFF ends the list).
+struct OrderEnt {
+  float prior;
+  uint32_t pos;
+};
 
 struct Edge {
   uint32_t child, visits;
@@ -99,7 +112,8 @@ struct SearchDev {
   GameDev* games;
   Node* nodes;
   Edge* edges;
-  uint16_t* order;
+  OrderEnt* order;
+  uint64_t* nodeKey;     // [G][cap][2] transposition key of each node (TT rebuild after reuse)
   float* policy;
   uint32_t* freeList;
   uint32_t* allocBits;

@@ -92,7 +92,8 @@ struct GV {
   KC_D GV(const SearchDev& d_, int g_) : d(d_), T(*d_.T), g(g_), lane(laneId()) {}
   KC_D Node* nodes() const { return d.nodes + (size_t)g * d.cap; }
   KC_D Edge* edges(int n) const { return d.edges + ((size_t)g * d.cap + n) * d.P; }
-  KC_D uint16_t* order(int n) const { return d.order + ((size_t)g * d.cap + n) * d.P; }
+  KC_D OrderEnt* order(int n) const { return d.order + ((size_t)g * d.cap + n) * d.P; }
+  KC_D uint64_t* nodeKey(int n) const { return d.nodeKey + ((size_t)g * d.cap + n) * 2; }
   KC_D float* pol(int n) const { return d.policy + ((size_t)g * d.cap + n) * d.P; }
   KC_D uint32_t* freeList() const { return d.freeList + (size_t)g * d.cap; }
   KC_D uint32_t* allocBits() const { return d.allocBits + (size_t)g * (d.cap / 32); }
@@ -142,6 +143,9 @@ KC_D float tsum(const float (&x)[NI], int n, int lane) {
 }
 
 KC_D int bcastI(int v, int srcLane) { return __shfl(v, srcLane, 64); }
+
+// Child slots read speculatively with their node record (2 x 128-B lines of Edge).
+constexpr int SPEC_EDGES = 16;
 KC_D int firstLane(uint64_t m) { return __builtin_ctzll(m); }
 
 KC_D float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeight) {
@@ -247,9 +251,13 @@ KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k
     n.numChildren = 0;
     n.nextPla = (uint8_t)nextPla;
     n.flags = terminal ? 2 : 0;
-    n.key0 = k0;
-    n.key1 = k1;
+    n.nextPrior = -1.0f;
+    n.nextPos = 0xFFFF;
+    n.pad0 = 0;
+    n.pad1[0] = n.pad1[1] = 0;
     v.nodes()[idx] = n;
+    v.nodeKey(idx)[0] = k0;
+    v.nodeKey(idx)[1] = k1;
     atomicOr(&v.allocBits()[idx >> 5], 1u << (idx & 31));
   }
   s.liveCount++;
@@ -480,7 +488,7 @@ KC_D float exploreScaling(const SP& sp, float totalChildWeight) {
 // oracle selectBest (selectBestChildToDescend searchexplorehelpers.cpp:304-451)
 template <int NI>
 KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool isRoot, int& newPos,
-                    uint32_t* hasBits) {
+                    uint32_t* hasBits, const Edge& e0) {
   const SP& sp = v.d.sp;
   const int P = v.d.P;
   const int k = n.numChildren;
@@ -500,7 +508,7 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
     probs[j] = cw[j] = pv[j] = cu[j] = 0.0f;
     cvis[j] = 0;
     if(i < k) {
-      Edge e = E[i];
+      const Edge e = j == 0 && i < SPEC_EDGES ? e0 : E[i];
       const Node& c = NS[e.child];
       float p = isRoot ? pol[e.move] : e.prior;
       cvis[j] = c.visits;
@@ -559,14 +567,12 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
       }
     }
     waveArgmax(bp, bpos);
-  } else if(k < P) {
+  } else if(n.nextPos != 0xFFFF) {
     // non-root: children are always created in prior order, so the best
-    // unexpanded move is the k-th entry of the node's expansion order
-    const int pos = v.order(ni)[k];
-    if(pos != 0xFFFF) {
-      bp = pol[pos];
-      bpos = pos;
-    }
+    // unexpanded move is the k-th entry of the node's expansion order, which
+    // the node record caches
+    bp = n.nextPrior;
+    bpos = n.nextPos;
   }
   newPos = -1;
   if(bpos != BIG) {
@@ -589,6 +595,10 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
   DBoard b = s.root;
   int ni = s.rootIdx;
   while(true) {
+    // the first SPEC_EDGES child slots (two cache lines) are read speculatively,
+    // together with the node record (slots past numChildren are ignored), saving
+    // a dependent round trip; wider speculation would touch cold lines
+    const Edge e0 = v.lane < SPEC_EDGES && v.lane < v.d.P ? v.edges(ni)[v.lane] : Edge{0u, 0u, 0.0f, 0u};
     const Node& n = v.nodes()[ni];
     if(n.flags & 2) {
       s.leafKind = LEAF_TERMINAL;
@@ -600,7 +610,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
     const float* pol = isRoot ? v.rootNoised() : v.pol(ni);
     int newPos = -1;
     const unsigned long long tSel = SPROF_NOW();
-    int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits);
+    int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits, e0);
     SPROF_ADD(5, SPROF_NOW() - tSel);
     (void)tSel;
     if(slot < 0) {
@@ -611,6 +621,11 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
     if(slot == n.numChildren) {
       const unsigned long long tExp = SPROF_NOW();
       (void)tExp;
+      // the node's following expansion candidate (non-root), loaded up front
+      OrderEnt nxt{-1.0f, 0xFFFFu};
+      if(!isRoot && slot + 1 < v.d.P)
+        nxt = v.order(ni)[slot + 1];
+      const float prior = isRoot ? v.pol(ni)[newPos] : n.nextPrior;
       const int cell = newPos % T.A, dir = newPos / T.A;
       // SVB key of the expansion (needs the board before the move); computed
       // up front so no second board copy stays live across playMoveWave.
@@ -640,8 +655,12 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
       }
       waveSync();
       if(v.lane == 0) {
-        v.edges(ni)[slot] = Edge{(uint32_t)child, 0u, v.pol(ni)[newPos], (uint32_t)newPos};
+        v.edges(ni)[slot] = Edge{(uint32_t)child, 0u, prior, (uint32_t)newPos};
         v.nodes()[ni].numChildren = (uint16_t)(slot + 1);
+        if(!isRoot) {
+          v.nodes()[ni].nextPos = (uint16_t)nxt.pos;
+          v.nodes()[ni].nextPrior = nxt.prior;
+        }
         v.pathNode()[s.pathLen] = ni;
         v.pathSlot()[s.pathLen] = slot;
       }
@@ -901,7 +920,7 @@ KC_D void buildOrder(const GV& v, int ni, const float* pol, float* lds) {
   for(int p = v.lane; p < P; p += 64)
     lds[p] = pol[p];
   waveSync();
-  uint16_t* ord = v.order(ni);
+  OrderEnt* ord = v.order(ni);
   int nLegal = 0;
   for(int p = v.lane; p < P; p += 64) {
     const float x = lds[p];
@@ -912,12 +931,18 @@ KC_D void buildOrder(const GV& v, int ni, const float* pol, float* lds) {
       const float y = lds[q];
       rank += (y > x || (y == x && q < p)) ? 1 : 0;
     }
-    ord[rank] = (uint16_t)p;
+    ord[rank] = OrderEnt{x, (uint32_t)p};
   }
   for(int base = 0; base < P; base += 64)
     nLegal += __builtin_popcountll(ballot(base + v.lane < P && lds[base + v.lane] >= 0.0f));
   for(int r = nLegal + v.lane; r < P; r += 64)
-    ord[r] = 0xFFFF;
+    ord[r] = OrderEnt{-1.0f, 0xFFFFu};
+  waveSync();
+  if(v.lane == 0) {
+    const OrderEnt first = ord[0];
+    v.nodes()[ni].nextPos = (uint16_t)first.pos;
+    v.nodes()[ni].nextPrior = first.prior;
+  }
   waveSync();
 }
 
@@ -1501,11 +1526,12 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
       continue;
     Node* n = &v.nodes()[i];
     if(i != child && v.d.sp.useGraph) {
-      int sl = (int)(n->key0 & (uint64_t)tmask);
+      const uint64_t k0 = v.nodeKey(i)[0], k1 = v.nodeKey(i)[1];
+      int sl = (int)(k0 & (uint64_t)tmask);
       while(atomicCAS(&tn[sl], -1, i) != -1)
         sl = (sl + 1) & tmask;
-      tk[2 * sl] = n->key0;
-      tk[2 * sl + 1] = n->key1;
+      tk[2 * sl] = k0;
+      tk[2 * sl + 1] = k1;
     }
     if(n->svbEntry >= 0) {
       const size_t oe = sb + n->svbEntry;
@@ -1872,10 +1898,11 @@ __global__ void kGameTree(const SearchDev* __restrict__ dp, int g, int maxNodes,
     o[8] = f2u(x.lastSvbDelta);
     o[9] = f2u(x.lastSvbWeight);
     o[10] = (uint32_t)x.numChildren | ((uint32_t)x.nextPla << 16) | ((uint32_t)x.flags << 24);
-    o[11] = (uint32_t)x.key0;
-    o[12] = (uint32_t)(x.key0 >> 32);
-    o[13] = (uint32_t)x.key1;
-    o[14] = (uint32_t)(x.key1 >> 32);
+    const uint64_t* nk = d.nodeKey + ((size_t)g * d.cap + idx) * 2;
+    o[11] = (uint32_t)nk[0];
+    o[12] = (uint32_t)(nk[0] >> 32);
+    o[13] = (uint32_t)nk[1];
+    o[14] = (uint32_t)(nk[1] >> 32);
     uint64_t sk = 0;
     int64_t sd = 0, sw = 0;
     if(x.svbEntry >= 0) {

@@ -104,8 +104,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.games = devAlloc<GameDev>(owned_, G);
   d.nodes = devAlloc<Node>(owned_, (size_t)G * cap, false);
   d.edges = devAlloc<Edge>(owned_, (size_t)G * cap * P, false);
-  d.order = devAlloc<uint16_t>(owned_, (size_t)G * cap * P, false);
+  d.order = devAlloc<OrderEnt>(owned_, (size_t)G * cap * P, false);
   d.policy = devAlloc<float>(owned_, (size_t)G * cap * P, false);
+  d.nodeKey = devAlloc<uint64_t>(owned_, (size_t)G * cap * 2, false);
   d.freeList = devAlloc<uint32_t>(owned_, (size_t)G * cap, false);
   d.allocBits = devAlloc<uint32_t>(owned_, (size_t)G * (cap / 32));
   d.ttKey = devAlloc<uint64_t>(owned_, (size_t)G * ttCap * 2, false);

@@ -1,0 +1,145 @@
+// Steady-state cycles of the network's 96->96 3x3 convolution (convTiles) and of
+// stripped variants, one 512-thread workgroup per CU, 256 workgroups.
+//   real      : convTiles as shipped (LDS weight ring + barriers + fragment loads)
+//   nobar     : same loads, weights read from a fixed LDS slot, no ring stores/barriers
+//   noload    : MFMAs on register-resident fragments only (no LDS reads)
+//   nodma / dma-nowait-nobar / dma-neverwait: convTiles with parts of the weight
+//               stream removed (convTiles' DBG ablation flags)
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I katacoffee_amd/csrc tools/conv_bench.hip
+//        katacoffee_amd/csrc/model.cpp -o tools/_build/conv_bench
+#include "../katacoffee_amd/csrc/nn.hip"
+
+#include <cstdio>
+#include <vector>
+
+using namespace kc;
+using G = NNGeo<5, 5, 96>;
+constexpr int REPS = 16;
+
+// convTiles DBG flags per mode (modes 1 and 2 are hand-written loops)
+constexpr int kDbg[6] = {0, 0, 0, 1, 10, 256 + 10};
+
+template <int MODE>
+__global__ void __launch_bounds__(NN_NT, 2) kConv(const h16x8* __restrict__ w, const uint16_t* __restrict__ tabs,
+                                                  float* out, unsigned long long* cyc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rg = wave >> 1, cg = wave & 1;
+  const int tstart = rg * G::MAXT;
+  uint16_t* act = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* rowPa = reinterpret_cast<uint16_t*>(smem + G::OFF_TAB);
+  h16x8* wl = reinterpret_cast<h16x8*>(smem + G::OFF_W);
+  for(int i = tid; i < G::NTAB; i += NN_NT)
+    rowPa[i] = tabs[i];
+  for(int i = tid; i < G::ACT_BYTES / 2; i += NN_NT)
+    act[i] = (uint16_t)(0x3000 + (i * 7 & 0x3ff));
+  for(int i = tid; i < 3 * G::WBUF; i += NN_NT)
+    wl[i] = w[i % (9 * G::WBUF)];
+  __syncthreads();
+  int ab[G::MAXT];
+  aBases<G>(ab, rowPa, tstart, lane);
+  f32x4 acc[G::MAXT][G::NCT];
+  zeroAcc<G>(acc);
+  unsigned long long t0 = clock64();
+  for(int r = 0; r < REPS; r++) {
+    if(MODE == 0 || MODE >= 3) {
+      // the stream's taps 7/8 re-request this conv's taps 0/1 for the next rep
+      constexpr int DBG = kDbg[MODE];
+      convTiles<G, 9, 3, false, DBG>(act, w, wl, acc, ab, cg, lane, tid, w, 3 * G::NCT_ALL, 9);
+      if(!(DBG & 256))
+        __syncthreads();
+    } else if(MODE == 1) {
+      const char* actB = reinterpret_cast<const char*>(act);
+      const h16x8* wlane = wl + (cg * G::NCT) * 64 + lane;
+      h16x8 af[2][G::MAXT], bf[2][G::NCT];
+      auto loadStep = [&](int st, int buf) {
+        const int tap = st / 3, cb = st - tap * 3;
+        const int aoff = ((tap / 3) * G::PX + tap % 3) * G::ROWB + cb * 64;
+        const h16x8* wb = wlane + (tap % 3) * G::WBUF + cb * G::NCT_ALL * 64;
+#pragma unroll
+        for(int ct = 0; ct < G::NCT; ct++)
+          bf[buf][ct] = wb[ct * 64];
+#pragma unroll
+        for(int t = 0; t < G::MAXT; t++)
+          af[buf][t] = *reinterpret_cast<const h16x8*>(actB + ab[t] + aoff);
+      };
+      loadStep(0, 0);
+#pragma unroll
+      for(int st = 0; st < 27; st++) {
+        if(st + 1 < 27)
+          loadStep(st + 1, (st + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+          for(int ct = 0; ct < G::NCT; ct++)
+            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[st & 1][ct], af[st & 1][t], acc[t][ct], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      h16x8 af[G::MAXT], bf[G::NCT];
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++)
+        af[t] = *reinterpret_cast<const h16x8*>(reinterpret_cast<const char*>(act) + ab[t]);
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++)
+        bf[ct] = wl[(cg * G::NCT + ct) * 64 + lane];
+#pragma unroll
+      for(int st = 0; st < 27; st++) {
+#pragma unroll
+        for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+          for(int ct = 0; ct < G::NCT; ct++)
+            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ct], af[t], acc[t][ct], 0, 0, 0);
+      }
+    }
+  }
+  unsigned long long t1 = clock64();
+  float s = 0;
+  for(int t = 0; t < G::MAXT; t++)
+    for(int ct = 0; ct < G::NCT; ct++)
+      s += acc[t][ct][0] + acc[t][ct][3];
+  out[blockIdx.x * NN_NT + tid] = s;
+  if(tid == 0)
+    cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int MODE>
+void run(const char* name, const h16x8* w, const uint16_t* tabs, float* out, unsigned long long* cyc) {
+  KC_HIP(hipFuncSetAttribute((const void*)kConv<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+  for(int it = 0; it < 3; it++)
+    hipLaunchKernelGGL(kConv<MODE>, dim3(256), dim3(NN_NT), G::LDS, 0, w, tabs, out, cyc);
+  KC_HIP(hipDeviceSynchronize());
+  std::vector<unsigned long long> c(256);
+  KC_HIP(hipMemcpy(c.data(), cyc, 256 * 8, hipMemcpyDeviceToHost));
+  double avg = 0;
+  for(auto v : c)
+    avg += v;
+  avg /= 256.0;
+  printf("%-8s %8.0f cycles per conv (%.1f per K-step; ideal 2-wave MFMA %.0f)\n", name, avg / REPS,
+         avg / REPS / 27, 27 * 24 * 8.7);
+}
+
+int main() {
+  std::vector<uint16_t> hw((size_t)9 * G::WBUF * 8);
+  for(size_t i = 0; i < hw.size(); i++)
+    hw[i] = (uint16_t)(0x2000 + (i * 13 & 0x7ff));
+  h16x8* w;
+  KC_HIP(hipMalloc(&w, hw.size() * 2));
+  KC_HIP(hipMemcpy(w, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+  std::vector<uint16_t> tab = rowTables<G>();
+  uint16_t* tabs;
+  KC_HIP(hipMalloc(&tabs, tab.size() * 2));
+  KC_HIP(hipMemcpy(tabs, tab.data(), tab.size() * 2, hipMemcpyHostToDevice));
+  float* out;
+  unsigned long long* cyc;
+  KC_HIP(hipMalloc(&out, 256 * NN_NT * 4));
+  KC_HIP(hipMalloc(&cyc, 256 * 8));
+  run<0>("real", w, tabs, out, cyc);
+  run<1>("nobar", w, tabs, out, cyc);
+  run<2>("noload", w, tabs, out, cyc);
+  run<3>("nodma", w, tabs, out, cyc);
+  run<4>("dma-nowait-nobar", w, tabs, out, cyc);
+  run<5>("dma-neverwait", w, tabs, out, cyc);
+  return 0;
+}
