@@ -90,6 +90,8 @@ struct GV {
   const DTables& T;
   int g, lane;
   KC_D GV(const SearchDev& d_, int g_) : d(d_), T(*d_.T), g(g_), lane(laneId()) {}
+  // tables through a readonly noalias kernel argument: uniform reads become scalar loads
+  KC_D GV(const SearchDev& d_, const DTables& t_, int g_) : d(d_), T(t_), g(g_), lane(laneId()) {}
   KC_D Node* nodes() const { return d.nodes + (size_t)g * d.cap; }
   KC_D Edge* edges(int n) const { return d.edges + ((size_t)g * d.cap + n) * d.P; }
   KC_D OrderEnt* order(int n) const { return d.order + ((size_t)g * d.cap + n) * d.P; }
@@ -704,13 +706,13 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
 // ---------------------------------------------------------------------------
 // kSelect: root evaluation or one descent; NN leaves are encoded into the batch.
 template <int NI>
-__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* __restrict__ dp) {
+__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
   if(g >= d.G)
     return;
   __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
-  GV v(d, g);
+  GV v(d, *Tp, g);
   __shared__ GameDev s;
   SPROF_INIT();
   const unsigned long long t0 = SPROF_NOW();
@@ -771,29 +773,57 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
 
 // oracle postprocess (nneval.cpp:702-815 + copyOutputsWithSymmetry nninputs.cpp:349-357)
 template <int NI>
+// The network row is staged in LDS (one coalesced read) and gathered from there in
+// the symmetric frame; pv returns each lane's policy values for buildOrder.
+// `stage` (>= P+4 floats) may alias polDst.
 KC_D void postprocess(const GV& v, const DBoard& b, int sym, const float* out, float* polDst, float& whiteWin,
-                      float& whiteLoss) {
+                      float& whiteLoss, float* stage, float (&pv)[NI]) {
   const DTables& T = v.T;
   const int P = T.P, A = T.A;
   if(T.X != T.Y)
     sym &= 3;
-  float logit[NI];
+  float raw[NI + 1];
+#pragma unroll
+  for(int j = 0; j <= NI; j++) {
+    const int i = v.lane + 64 * j;
+    raw[j] = i < P + 4 ? out[i] : 0.0f;
+  }
+  int src[NI];
   bool legal[NI];
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    const int pos = v.lane + 64 * j;
+    legal[j] = false;
+    src[j] = 0;
+    if(pos < P) {
+      const int dd = pos / A, cell = pos % A;
+      legal[j] = isLegal(T, b, cell, dd);
+      src[j] = T.symDir[sym][dd] * A + T.symCell[sym][cell];
+    }
+  }
+  waveSync();
+#pragma unroll
+  for(int j = 0; j <= NI; j++) {
+    const int i = v.lane + 64 * j;
+    if(i < P + 4)
+      stage[i] = raw[j];
+  }
+  waveSync();
+  float logit[NI];
   float mx = -1e25f;
   int legalCount = 0;
 #pragma unroll
   for(int j = 0; j < NI; j++) {
-    int pos = v.lane + 64 * j;
-    legal[j] = false;
+    const int pos = v.lane + 64 * j;
     logit[j] = -1e30f;
     if(pos < P) {
-      int dd = pos / A, cell = pos % A;
-      legal[j] = isLegal(T, b, cell, dd);
-      logit[j] = legal[j] ? out[T.symDir[sym][dd] * A + T.symCell[sym][cell]] : -1e30f;
+      logit[j] = legal[j] ? stage[src[j]] : -1e30f;
       mx = logit[j] > mx ? logit[j] : mx;
     }
     legalCount += __popcll(ballot(legal[j]));
   }
+  const float wlg = stage[P], llg = stage[P + 1];
+  waveSync();
   mx = waveMax(mx);
   float e[NI];
 #pragma unroll
@@ -803,10 +833,10 @@ KC_D void postprocess(const GV& v, const DBoard& b, int sym, const float* out, f
 #pragma unroll
   for(int j = 0; j < NI; j++) {
     int pos = v.lane + 64 * j;
+    pv[j] = legal[j] ? (sum <= 0.0f ? 1.0f / (float)legalCount : e[j] / sum) : -1.0f;
     if(pos < P)
-      polDst[pos] = legal[j] ? (sum <= 0.0f ? 1.0f / (float)legalCount : e[j] / sum) : -1.0f;
+      polDst[pos] = pv[j];
   }
-  float wlg = out[P], llg = out[P + 1];
   float m = wlg > llg ? wlg : llg;
   float wp = dexp(wlg - m), lp = dexp(llg - m);
   float ps = wp + lp;
@@ -915,23 +945,40 @@ KC_D void noiseAndTemp(const GV& v, GameDev& s, DRng& rng, const float* raw, flo
 // Expansion order of a freshly evaluated node: legal moves by descending prior,
 // ties by ascending position (the order selectBest's new-child scan yields),
 // 0xFFFF after the last legal move. Rank by counting; priors staged in LDS.
-KC_D void buildOrder(const GV& v, int ni, const float* pol, float* lds) {
+template <int NI>
+KC_D void buildOrder(const GV& v, int ni, const float (&pv)[NI], float* lds) {
   const int P = v.d.P;
-  for(int p = v.lane; p < P; p += 64)
-    lds[p] = pol[p];
+  waveSync();
+#pragma unroll
+  for(int j = 0; j < NI; j++)
+    if(v.lane + 64 * j < P)
+      lds[v.lane + 64 * j] = pv[j];
   waveSync();
   OrderEnt* ord = v.order(ni);
   int nLegal = 0;
-  for(int p = v.lane; p < P; p += 64) {
-    const float x = lds[p];
-    if(x < 0.0f)
-      continue;
-    int rank = 0;
-    for(int q = 0; q < P; q++) {
-      const float y = lds[q];
-      rank += (y > x || (y == x && q < p)) ? 1 : 0;
+  // rank of each of the lane's entries = entries ordered before it; 4 per LDS read
+  // (P = 4A is a multiple of 4)
+  int rank[NI];
+#pragma unroll
+  for(int j = 0; j < NI; j++)
+    rank[j] = 0;
+  for(int q = 0; q < P; q += 4) {
+    const float4 y = *reinterpret_cast<const float4*>(lds + q);
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      const float x = pv[j];
+      const int p = v.lane + 64 * j;
+      rank[j] += (y.x > x || (y.x == x && q < p)) ? 1 : 0;
+      rank[j] += (y.y > x || (y.y == x && q + 1 < p)) ? 1 : 0;
+      rank[j] += (y.z > x || (y.z == x && q + 2 < p)) ? 1 : 0;
+      rank[j] += (y.w > x || (y.w == x && q + 3 < p)) ? 1 : 0;
     }
-    ord[rank] = OrderEnt{x, (uint32_t)p};
+  }
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    const int p = v.lane + 64 * j;
+    if(p < P && pv[j] >= 0.0f)
+      ord[rank[j]] = OrderEnt{pv[j], (uint32_t)p};
   }
   for(int base = 0; base < P; base += 64)
     nLegal += __builtin_popcountll(ballot(base + v.lane < P && lds[base + v.lane] >= 0.0f));
@@ -948,13 +995,13 @@ KC_D void buildOrder(const GV& v, int ni, const float* pol, float* lds) {
 
 // kBackup: NN post-processing + leaf value + path backup.
 template <int NI>
-__global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) {
+__global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
   if(g >= d.G)
     return;
-  __shared__ float scratch[2 * MAX_P];
-  GV v(d, g);
+  __shared__ __attribute__((aligned(16))) float scratch[2 * MAX_P];
+  GV v(d, *Tp, g);
   __shared__ GameDev s;
   SPROF_INIT();
   const unsigned long long t0 = SPROF_NOW();
@@ -973,7 +1020,8 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
   if(s.leafKind == LEAF_ROOTEVAL) {
     float* pol = scratch;
     float w, l;
-    postprocess<NI>(v, s.root, s.leafSym, o, pol, w, l);
+    float pv[NI];
+    postprocess<NI>(v, s.root, s.leafSym, o, pol, w, l, scratch, pv);
     waveSync();
     float* acc = v.accPolicy();
     if(s.rootK == 0) {
@@ -1027,9 +1075,9 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp) 
       float* pol = v.pol(s.leafNode);
       const unsigned long long ta = SPROF_NOW();
       (void)ta;
-      postprocess<NI>(v, s.leaf, s.leafSym, o, pol, w, l);
-      waveSync();
-      buildOrder(v, s.leafNode, pol, scratch);
+      float pv[NI];
+      postprocess<NI>(v, s.leaf, s.leafSym, o, pol, w, l, scratch, pv);
+      buildOrder<NI>(v, s.leafNode, pv, scratch);
       if(v.lane == 0) {
         Node* n = &v.nodes()[s.leafNode];
         n->nnWin = w;
@@ -1726,7 +1774,7 @@ KC_D void finishGame(const GV& v, GameDev& s, DRng& rng, DBoard* boards, float* 
 // oracle commitMove (getChosenMoveLoc searchresults.cpp:435-453, extract*Targets
 // play.cpp:635-704, getPolicySurpriseAndEntropy searchresults.cpp:486-550, makeMove)
 template <int NI>
-__global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp) {
+__global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   if((int)blockIdx.x >= *d.commitCount)
     return;
@@ -1741,7 +1789,7 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp) 
   DBoard* boards = reinterpret_cast<DBoard*>(qtail + 4);      // [MAX_AREA+1]
   uint32_t* liveBits = reinterpret_cast<uint32_t*>(boards + (MAX_AREA + 1));  // [cap/32]
   uint16_t* queue = reinterpret_cast<uint16_t*>(liveBits + d.cap / 32);     // [cap]
-  GV v(d, g);
+  GV v(d, *Tp, g);
   __shared__ GameDev s;
   loadGame(v, s);
   const SP& sp = d.sp;
@@ -1848,12 +1896,12 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp) 
   storeGame(v, s);
 }
 
-__global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp) {
+__global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
   if(g >= d.G)
     return;
-  GV v(d, g);
+  GV v(d, *Tp, g);
   __shared__ GameDev s;
   for(int i = v.lane; i < (int)(sizeof(GameDev) / 4); i += 64)
     reinterpret_cast<uint32_t*>(&s)[i] = 0;
@@ -1949,24 +1997,24 @@ __global__ void kGameTree(const SearchDev* __restrict__ dp, int g, int maxNodes,
 static int laneItems(int P) { return P <= 128 ? 2 : (P <= 256 ? 4 : 7); }
 
 void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
-  hipLaunchKernelGGL(kInit, dim3(d.G), dim3(64), 0, st, dd);
+  hipLaunchKernelGGL(kInit, dim3(d.G), dim3(64), 0, st, dd, d.T);
   KC_HIP(hipGetLastError());
 }
 
 void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   switch(laneItems(d.P)) {
-    case 2: hipLaunchKernelGGL(kSelect<2>, dim3(d.G), dim3(64), 0, st, dd); break;
-    case 4: hipLaunchKernelGGL(kSelect<4>, dim3(d.G), dim3(64), 0, st, dd); break;
-    default: hipLaunchKernelGGL(kSelect<7>, dim3(d.G), dim3(64), 0, st, dd); break;
+    case 2: hipLaunchKernelGGL(kSelect<2>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
+    case 4: hipLaunchKernelGGL(kSelect<4>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
+    default: hipLaunchKernelGGL(kSelect<7>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
   }
   KC_HIP(hipGetLastError());
 }
 
 void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   switch(laneItems(d.P)) {
-    case 2: hipLaunchKernelGGL(kBackup<2>, dim3(d.G), dim3(64), 0, st, dd); break;
-    case 4: hipLaunchKernelGGL(kBackup<4>, dim3(d.G), dim3(64), 0, st, dd); break;
-    default: hipLaunchKernelGGL(kBackup<7>, dim3(d.G), dim3(64), 0, st, dd); break;
+    case 2: hipLaunchKernelGGL(kBackup<2>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
+    case 4: hipLaunchKernelGGL(kBackup<4>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
+    default: hipLaunchKernelGGL(kBackup<7>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
   }
   KC_HIP(hipGetLastError());
 }
@@ -1981,9 +2029,9 @@ size_t commitLdsBytes(int cap) {
 void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   const size_t lds = commitLdsBytes(d.cap);
   switch(laneItems(d.P)) {
-    case 2: hipLaunchKernelGGL(kCommit<2>, dim3(d.G), dim3(64), lds, st, dd); break;
-    case 4: hipLaunchKernelGGL(kCommit<4>, dim3(d.G), dim3(64), lds, st, dd); break;
-    default: hipLaunchKernelGGL(kCommit<7>, dim3(d.G), dim3(64), lds, st, dd); break;
+    case 2: hipLaunchKernelGGL(kCommit<2>, dim3(d.G), dim3(64), lds, st, dd, d.T); break;
+    case 4: hipLaunchKernelGGL(kCommit<4>, dim3(d.G), dim3(64), lds, st, dd, d.T); break;
+    default: hipLaunchKernelGGL(kCommit<7>, dim3(d.G), dim3(64), lds, st, dd, d.T); break;
   }
   KC_HIP(hipGetLastError());
 }
