@@ -155,6 +155,7 @@ typedef struct coffee_selfplay_stats {
   uint64_t rows_written;    /* rows produced so far (drained + pending) */
   uint64_t rows_pending;    /* rows on the device not yet drained */
   uint64_t rows_dropped;    /* rows lost to a full row buffer (drain more often) */
+  uint64_t games_dropped;   /* game records lost to a full record buffer (2 x num_games) */
 } coffee_selfplay_stats;
 
 int coffee_selfplay_create(const coffee_selfplay_config* cfg, coffee_selfplay** out);
@@ -175,6 +176,16 @@ int coffee_selfplay_stats_get(coffee_selfplay* h, coffee_selfplay_stats* out);
  * Any output pointer may be NULL.  *n_out = rows copied. */
 int coffee_selfplay_drain_rows(coffee_selfplay* h, int max_rows, uint8_t* bin, float* glob, int16_t* pol,
                                float* gtgt, int8_t* value, int32_t* meta, int* n_out);
+/* Copies up to max_games finished-game records to HOST buffers and removes them
+ * (the moves the reference's SGF writer prints, sgf.cpp:1526-1700 / selfplaymanager.cpp:350):
+ *   header [g][4] i32  (slot, game number, number of moves, winner 0 draw / 1 black / 2 white)
+ *   moves  [g][A][2] u8 (cell = y*x_len + x, direction 0..3 = N, W, NW, NE; 0xFF past the end)
+ * Either output pointer may be NULL.  *n_out = records copied. */
+int coffee_selfplay_drain_games(coffee_selfplay* h, int max_games, int32_t* header, uint8_t* moves, int* n_out);
+/* Replaces the network for every subsequent round of every game (the reference's
+ * model hot reload with switchNetsMidGame, selfplay.cpp:135-260, play.cpp:1210-1226).
+ * On error (unreadable / mismatched model) the current network stays in use. */
+int coffee_selfplay_set_model(coffee_selfplay* h, const char* model_path);
 int coffee_selfplay_destroy(coffee_selfplay* h);
 
 /* Writes n rows (HOST arrays, drain_rows layout) as a training .npz in the reference's

@@ -75,7 +75,7 @@ class SelfplayConfig(ctypes.Structure):
 class SelfplayStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ["rounds", "playouts", "nn_evals", "moves", "games_finished", "rows_written", "rows_pending",
-                 "rows_dropped"]]
+                 "rows_dropped", "games_dropped"]]
 
 
 # Every symbol include/katacoffee.h declares (checked by tests/test_abi.py).
@@ -85,7 +85,8 @@ EXPORTS = [
     "coffee_encode_batch", "coffee_model_write_random", "coffee_model_flops", "coffee_nn_create",
     "coffee_nn_forward", "coffee_nn_destroy", "coffee_fake_net", "coffee_search_params_default",
     "coffee_selfplay_create", "coffee_selfplay_step", "coffee_selfplay_sync", "coffee_selfplay_stats_get",
-    "coffee_selfplay_drain_rows", "coffee_selfplay_destroy", "coffee_selfplay_game_info",
+    "coffee_selfplay_drain_rows", "coffee_selfplay_drain_games", "coffee_selfplay_set_model",
+    "coffee_selfplay_destroy", "coffee_selfplay_game_info",
     "coffee_selfplay_game_tree", "coffee_selfplay_root_policy", "coffee_debug_cdf_table", "coffee_debug_zobrist",
     "coffee_selfplay_enable_timing", "coffee_selfplay_kernel_time", "coffee_write_npz",
 ]
@@ -129,6 +130,8 @@ def lib():
         L.coffee_selfplay_sync.argtypes = [c_p]
         L.coffee_selfplay_stats_get.argtypes = [c_p, c_p]
         L.coffee_selfplay_drain_rows.argtypes = [c_p, c_i] + [c_p] * 7
+        L.coffee_selfplay_drain_games.argtypes = [c_p, c_i, c_p, c_p, c_p]
+        L.coffee_selfplay_set_model.argtypes = [c_p, ctypes.c_char_p]
         L.coffee_selfplay_destroy.argtypes = [c_p]
         L.coffee_selfplay_game_info.argtypes = [c_p, c_i, c_p]
         L.coffee_selfplay_game_tree.argtypes = [c_p, c_i, c_i, c_p, c_p, c_p]
@@ -371,6 +374,21 @@ class Selfplay:
         check(lib().coffee_selfplay_drain_rows(self.h, n, *[_ptr(rows[k]) for k in order], ctypes.byref(got)))
         assert got.value == n
         return rows
+
+    def drain_games(self, max_games=1 << 20):
+        """Finished-game records: header [g][4] i32 (slot, game number, moves, winner)
+        and moves [g][A][2] u8 (cell, direction; 0xFF past the last move)."""
+        cap = min(max_games, 2 * self.num_games)
+        header = np.zeros((cap, 4), np.int32)
+        moves = np.zeros((cap, self.A, 2), np.uint8)
+        got = ctypes.c_int()
+        check(lib().coffee_selfplay_drain_games(self.h, cap, _ptr(header), _ptr(moves), ctypes.byref(got)))
+        return header[:got.value], moves[:got.value]
+
+    def set_model(self, model_path):
+        """Hot reload: every later round of every game uses this network."""
+        self._model = model_path.encode()
+        check(lib().coffee_selfplay_set_model(self.h, self._model))
 
     def game_info(self, slot):
         info = np.zeros(16, np.int64)

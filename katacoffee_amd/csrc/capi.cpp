@@ -300,6 +300,21 @@ int coffee_selfplay_drain_rows(coffee_selfplay* h, int max_rows, uint8_t* bin, f
   });
 }
 
+int coffee_selfplay_drain_games(coffee_selfplay* h, int max_games, int32_t* header, uint8_t* moves, int* n_out) {
+  return guarded([&] {
+    need(h && h->eng && n_out, "NULL argument");
+    need(max_games >= 0, "max_games must be >= 0");
+    *n_out = h->eng->drainGames(max_games, header, moves);
+  });
+}
+
+int coffee_selfplay_set_model(coffee_selfplay* h, const char* model_path) {
+  return guarded([&] {
+    need(h && h->eng && model_path, "NULL argument");
+    h->eng->setModel(model_path);
+  });
+}
+
 int coffee_selfplay_destroy(coffee_selfplay* h) {
   return guarded([&] {
     if(h) {

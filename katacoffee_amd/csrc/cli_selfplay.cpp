@@ -6,11 +6,17 @@
 //
 // Reads KataGo-style `key = value` config files (selfplay1.cfg keys that apply to this
 // path, plus `winLen`, `numGpus`, `boardXLen`/`boardYLen`; `bSizes` first entry sets a
-// square board).  Uses the newest model file in -models-dir (CFNN v1); writes
+// square board).  Uses the newest model file in -models-dir (CFNN v1) and polls the
+// directory every `modelPollSeconds` (default 10): a newer file is loaded into every
+// engine and used by all games from their next round on (hot reload with
+// switchNetsMidGame semantics, selfplay.cpp:135-260 / :366-384).  Writes
 // <output-dir>/<modelName>/tdata/<hex>.npz (maxRowsPerTrainFile rows each, reference
-// layout) and <output-dir>/log<time>.log.  One engine per GPU, each GPU on its own
-// thread with games [gpu*numGameThreads, (gpu+1)*numGameThreads); each writes its own
-// files (SURVEY §8e fallback, no collective).  SIGINT/SIGTERM: flush rows and exit.
+// layout), <output-dir>/<modelName>/sgfs/<hex>.sgfs (one SGF per finished game per
+// line, sgf.cpp:1526-1700 with Coffee's 3-letter moves, selfplaymanager.cpp:350-354)
+// and <output-dir>/log<time>.log.  Rows and games drained after a switch go to the new
+// model's directories.  One engine per GPU, each GPU on its own thread with games
+// [gpu*numGameThreads, (gpu+1)*numGameThreads); each writes its own files (SURVEY §8e
+// fallback, no collective).  SIGINT/SIGTERM: flush rows and exit.
 #include <dirent.h>
 #include <sys/stat.h>
 
@@ -89,10 +95,11 @@ static void check(int rc, const char* what) {
     die(std::string(what) + ": " + coffee_last_error());
 }
 
-static std::string newestModel(const std::string& dir) {
+// Newest regular file in dir ("" if none); its mtime in *mt.
+static std::string newestModelOrEmpty(const std::string& dir, time_t* mt) {
   DIR* d = opendir(dir.c_str());
   if(!d)
-    die("cannot open models dir " + dir);
+    return "";
   std::string best;
   time_t bestT = 0;
   while(dirent* e = readdir(d)) {
@@ -106,10 +113,52 @@ static std::string newestModel(const std::string& dir) {
     }
   }
   closedir(d);
-  if(best.empty())
-    die("no model file in " + dir);
+  if(mt)
+    *mt = bestT;
   return best;
 }
+
+static std::string newestModel(const std::string& dir) {
+  const std::string m = newestModelOrEmpty(dir, nullptr);
+  if(m.empty())
+    die("no model file in " + dir);
+  return m;
+}
+
+static std::string modelNameOf(const std::string& path) {
+  std::string n = path.substr(path.find_last_of('/') + 1);
+  return n.find('.') != std::string::npos ? n.substr(0, n.find('.')) : n;
+}
+
+// The models directory as seen by all GPU threads: version bumps when a newer file
+// (path or mtime) appears; each thread switches when its version lags.
+struct ModelWatch {
+  std::mutex mu;
+  std::string dir, path;
+  time_t mtime = 0;
+  int version = 0;
+  double pollSeconds = 10.0;
+  std::chrono::steady_clock::time_point lastPoll = std::chrono::steady_clock::now();
+
+  void current(std::string& p, int& v) {
+    std::lock_guard<std::mutex> lk(mu);
+    const auto now = std::chrono::steady_clock::now();
+    if(std::chrono::duration<double>(now - lastPoll).count() >= pollSeconds) {
+      lastPoll = now;
+      time_t mt = 0;
+      const std::string np = newestModelOrEmpty(dir, &mt);
+      if(!np.empty() && (np != path || mt > mtime)) {
+        path = np;
+        mtime = mt;
+        version++;
+        logf("models dir: new model %s", path.c_str());
+      }
+    }
+    p = path;
+    v = version;
+  }
+};
+static ModelWatch gModels;
 
 static void mkdirs(const std::string& path) {
   std::string cur;
@@ -127,6 +176,7 @@ static void mkdirs(const std::string& path) {
 
 struct Settings {
   int x = 5, y = 5, winLen = 4, games = 4096, gpus = 1, maxRowsPerFile = 10000;
+  float modelPollSeconds = 10.0f;
   int64_t maxGamesTotal = -1;
   uint64_t seed = 0;
   coffee_search_params sp;
@@ -159,6 +209,7 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   geti("numGamesPerGpu", s.games);
   geti("numGpus", s.gpus);
   geti("maxRowsPerTrainFile", s.maxRowsPerFile);
+  getf("modelPollSeconds", s.modelPollSeconds);
   coffee_search_params& p = s.sp;
   geti("maxVisits", p.max_visits);
   getf("cpuctExploration", p.cpuct_exploration);
@@ -234,10 +285,66 @@ struct RowSink {
   }
 };
 
+// Finished games as SGF, one game per line of <dir>/<hex>.sgfs (sgf.cpp:1526-1700:
+// FF[4] GM[Coffee] SZ WLL PB PW RE, moves B[xyd] / W[xyd] with d = a..d for N, W,
+// NW, NE; Coffee draws — SPEC B16 — are RE[0]).
+struct SgfSink {
+  std::string dir, modelName;
+  int x, y, winLen;
+  uint64_t fileId;
+  FILE* f = nullptr;
+  int64_t games = 0;
+
+  void write(int n, const int32_t* hdr, const uint8_t* mv) {
+    if(n <= 0)
+      return;
+    if(!f) {
+      char name[64];
+      snprintf(name, sizeof(name), "%016llX.sgfs", (unsigned long long)fileId);
+      f = fopen((dir + "/" + name).c_str(), "a");
+      if(!f)
+        die("cannot write sgfs in " + dir);
+    }
+    const int A = x * y;
+    const char* coord = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ";
+    for(int i = 0; i < n; i++) {
+      const int32_t* h = hdr + 4 * i;
+      const char* res = h[3] == 1 ? "B+" : (h[3] == 2 ? "W+" : "0");
+      std::string g = "(;FF[4]GM[Coffee]";
+      g += x == y ? "SZ[" + std::to_string(x) + "]" : "SZ[" + std::to_string(x) + ":" + std::to_string(y) + "]";
+      g += "WLL[" + std::to_string(winLen) + "]PB[" + modelName + "]PW[" + modelName + "]RE[" + res + "]";
+      g += "C[startTurnIdx=0,initTurnNum=0,gameId=" + std::to_string(h[0]) + ":" + std::to_string(h[1]) +
+           ",gtype=normal]";
+      for(int t = 0; t < h[2] && t < A; t++) {
+        const int cell = mv[((size_t)i * A + t) * 2], d = mv[((size_t)i * A + t) * 2 + 1];
+        g += t % 2 == 0 ? ";B[" : ";W[";
+        g += coord[cell % x];
+        g += coord[cell / x];
+        g += (char)('a' + d);
+        g += "]";
+        if(t + 1 == h[2])
+          g += std::string("C[result=") + res + "]";
+      }
+      g += ")\n";
+      fputs(g.c_str(), f);
+      games++;
+    }
+    fflush(f);
+  }
+  void close() {
+    if(f)
+      fclose(f);
+    f = nullptr;
+  }
+};
+
 static std::atomic<int64_t> gGamesDone(0);
 
-static void runGpu(int gpu, const Settings& s, const std::string& model, const std::string& tdata) {
+static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
   check(coffee_set_device(gpu), "set device");
+  std::string model;
+  int version = 0;
+  gModels.current(model, version);
   coffee_selfplay_config c;
   memset(&c, 0, sizeof(c));
   c.x = s.x;
@@ -252,7 +359,17 @@ static void runGpu(int gpu, const Settings& s, const std::string& model, const s
   c.search = s.sp;
   coffee_selfplay* h = nullptr;
   check(coffee_selfplay_create(&c, &h), "create engine");
-  RowSink sink{tdata, s.x, s.y, s.maxRowsPerFile, std::mt19937_64(s.seed ^ (0x9E3779B97F4A7C15ULL * (gpu + 1)))};
+  std::mt19937_64 fileRng(s.seed ^ (0x9E3779B97F4A7C15ULL * (gpu + 1)));
+  auto dirsFor = [&](const std::string& m, std::string& tdata, std::string& sgfs) {
+    tdata = outDir + "/" + modelNameOf(m) + "/tdata";
+    sgfs = outDir + "/" + modelNameOf(m) + "/sgfs";
+    mkdirs(tdata);
+    mkdirs(sgfs);
+  };
+  std::string tdata, sgfs;
+  dirsFor(model, tdata, sgfs);
+  RowSink sink{tdata, s.x, s.y, s.maxRowsPerFile, std::mt19937_64(fileRng())};
+  SgfSink games{sgfs, modelNameOf(model), s.x, s.y, s.winLen, fileRng()};
   const int A = s.x * s.y, pb = (A + 7) / 8, P = 4 * A;
   const int chunk = 65536;
   std::vector<uint8_t> bin((size_t)chunk * 15 * pb);
@@ -260,10 +377,13 @@ static void runGpu(int gpu, const Settings& s, const std::string& model, const s
   std::vector<int16_t> pol((size_t)chunk * 2 * P);
   std::vector<int8_t> val((size_t)chunk * 5 * A);
   std::vector<int32_t> meta((size_t)chunk * 4);
+  const int gchunk = 2 * s.games;
+  std::vector<int32_t> ghdr((size_t)gchunk * 4);
+  std::vector<uint8_t> gmv((size_t)gchunk * A * 2);
   uint64_t lastGames = 0;
+  int64_t filesBefore = 0, rowsBefore = 0;
   auto t0 = std::chrono::steady_clock::now();
-  while(!gStop) {
-    check(coffee_selfplay_step(h, 200, nullptr), "step");
+  auto drainAll = [&]() {
     int got = 0;
     do {
       check(coffee_selfplay_drain_rows(h, chunk, bin.data(), glob.data(), pol.data(), gt.data(), val.data(),
@@ -272,7 +392,36 @@ static void runGpu(int gpu, const Settings& s, const std::string& model, const s
       if(got > 0)
         sink.append(got, bin.data(), glob.data(), pol.data(), gt.data(), val.data());
     } while(got == chunk);
+    check(coffee_selfplay_drain_games(h, gchunk, ghdr.data(), gmv.data(), &got), "drain games");
+    games.write(got, ghdr.data(), gmv.data());
+  };
+  while(!gStop) {
+    check(coffee_selfplay_step(h, 200, nullptr), "step");
+    drainAll();
     sink.flush(false);
+    std::string latest;
+    int v = 0;
+    gModels.current(latest, v);
+    if(v != version) {
+      // hot reload: finish the old model's files, then switch every game to the new net
+      sink.flush(true);
+      games.close();
+      if(coffee_selfplay_set_model(h, latest.c_str()) == COFFEE_OK) {
+        logf("gpu %d: switched to model %s", gpu, latest.c_str());
+        model = latest;
+        filesBefore += sink.filesWritten;
+        rowsBefore += sink.rowsWritten;
+        dirsFor(model, tdata, sgfs);
+        sink.dir = tdata;
+        sink.filesWritten = sink.rowsWritten = 0;
+        games.dir = sgfs;
+        games.modelName = modelNameOf(model);
+        games.fileId = fileRng();
+      } else {
+        logf("gpu %d: cannot load %s (%s); keeping %s", gpu, latest.c_str(), coffee_last_error(), model.c_str());
+      }
+      version = v;
+    }
     coffee_selfplay_stats st;
     check(coffee_selfplay_stats_get(h, &st), "stats");
     gGamesDone += (int64_t)(st.games_finished - lastGames);
@@ -284,9 +433,12 @@ static void runGpu(int gpu, const Settings& s, const std::string& model, const s
     if(s.maxGamesTotal >= 0 && gGamesDone >= s.maxGamesTotal)
       gStop = true;
   }
+  drainAll();
   sink.flush(true);
+  games.close();
   coffee_selfplay_destroy(h);
-  logf("gpu %d done: %lld files, %lld rows", gpu, (long long)sink.filesWritten, (long long)sink.rowsWritten);
+  logf("gpu %d done: %lld files, %lld rows, %lld games", gpu, (long long)(filesBefore + sink.filesWritten),
+       (long long)(rowsBefore + sink.rowsWritten), (long long)games.games);
 }
 
 int main(int argc, char** argv) {
@@ -339,12 +491,11 @@ int main(int argc, char** argv) {
   gLog = fopen((outDir + "/" + lname).c_str(), "w");
   std::signal(SIGINT, onSignal);
   std::signal(SIGTERM, onSignal);
-  const std::string model = newestModel(modelsDir);
-  std::string modelName = model.substr(model.find_last_of('/') + 1);
-  if(modelName.find('.') != std::string::npos)
-    modelName = modelName.substr(0, modelName.find('.'));
-  const std::string tdata = outDir + "/" + modelName + "/tdata";
-  mkdirs(tdata);
+  gModels.dir = modelsDir;
+  gModels.path = newestModel(modelsDir);
+  newestModelOrEmpty(modelsDir, &gModels.mtime);
+  gModels.pollSeconds = s.modelPollSeconds;
+  const std::string model = gModels.path;
   int ndev = 0;
   check(coffee_device_count(&ndev), "device count");
   if(s.gpus < 1 || s.gpus > ndev)
@@ -353,7 +504,7 @@ int main(int argc, char** argv) {
        s.games, s.gpus, s.sp.max_visits);
   std::vector<std::thread> th;
   for(int g = 0; g < s.gpus; g++)
-    th.emplace_back(runGpu, g, std::cref(s), std::cref(model), std::cref(tdata));
+    th.emplace_back(runGpu, g, std::cref(s), std::cref(outDir));
   for(auto& t : th)
     t.join();
   if(gLog)

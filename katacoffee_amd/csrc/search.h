@@ -79,6 +79,12 @@ struct Edge {
   uint32_t move;  // policy position dir*A + cell
 };
 
+// A finished game's move record (SGF output): header then the moves in order.
+struct GameRec {
+  int32_t slot, gameNum, numMoves, winner;  // winner 0 draw, 1 black, 2 white
+  uint8_t cell[MAX_AREA], dir[MAX_AREA];
+};
+
 struct TurnRec {
   float whiteWin, whiteLoss, rawWhiteWL, rawPolicyEntropy;
   float policySurprise, policyEntropy, searchEntropy;
@@ -144,6 +150,11 @@ struct SearchDev {
   int32_t* rMeta;        // [rowCap][4]
   unsigned long long* rCount;
   unsigned long long* rDropped;
+  // finished-game records (drained by the host for SGF files)
+  int gCap;
+  GameRec* gRec;               // [gCap]
+  unsigned long long* gCount;
+  unsigned long long* gDropped;
 };
 
 // Kernel launchers (search.hip).

@@ -1643,6 +1643,31 @@ KC_D void finishGame(const GV& v, GameDev& s, DRng& rng, DBoard* boards, float* 
     }
   }
   waveSync();
+  {
+    // the game's move record (SGF)
+    unsigned long long gi = 0;
+    if(v.lane == 0) {
+      gi = atomicAdd(d.gCount, 1ull);
+      if(gi >= (unsigned long long)d.gCap) {
+        atomicAdd(d.gCount, (unsigned long long)-1ll);
+        atomicAdd(d.gDropped, 1ull);
+      }
+    }
+    gi = (unsigned long long)(uint32_t)__shfl((int)(uint32_t)gi, 0, 64);
+    if(gi < (unsigned long long)d.gCap) {
+      GameRec* gr = d.gRec + gi;
+      if(v.lane == 0) {
+        gr->slot = d.slotBase + v.g;
+        gr->gameNum = (int32_t)s.gameNum;
+        gr->numMoves = numMoves;
+        gr->winner = s.root.winner;
+      }
+      for(int t = v.lane; t < numMoves; t += 64) {
+        gr->cell[t] = (uint8_t)tr[t].cell;
+        gr->dir[t] = (uint8_t)tr[t].dir;
+      }
+    }
+  }
   const DBoard& fin = boards[numMoves];
   unsigned long long base = 0;
   bool fits = true;

@@ -86,6 +86,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     ModelHost m = loadModel(c.model_path);
     nn_.reset(new NNEngine(m, c.x, c.y, c.win_len));
   }
+  xLen_ = c.x;
+  yLen_ = c.y;
+  winLen_ = c.win_len;
   SearchDev& d = hd_;
   memset(&d, 0, sizeof(d));
   d.T = T_;
@@ -134,6 +137,10 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.rMeta = devAlloc<int32_t>(owned_, (size_t)rowCap * 4, false);
   d.rCount = devAlloc<unsigned long long>(owned_, 1);
   d.rDropped = devAlloc<unsigned long long>(owned_, 1);
+  d.gCap = 2 * G;
+  d.gRec = devAlloc<GameRec>(owned_, (size_t)d.gCap, false);
+  d.gCount = devAlloc<unsigned long long>(owned_, 1);
+  d.gDropped = devAlloc<unsigned long long>(owned_, 1);
   dd_ = devAlloc<SearchDev>(owned_, 1);
   KC_HIP(hipMemcpy(dd_, &d, sizeof(SearchDev), hipMemcpyHostToDevice));
   KC_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -242,6 +249,9 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
   out.rows_pending = cnt;
   out.rows_written = rowsDrained_ + cnt;
   out.rows_dropped = dropped;
+  unsigned long long gdrop = 0;
+  KC_HIP(hipMemcpy(&gdrop, hd_.gDropped, 8, hipMemcpyDeviceToHost));
+  out.games_dropped = gdrop;
 }
 
 int SelfplayEngine::drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, float* gt, int8_t* val,
@@ -262,10 +272,15 @@ int SelfplayEngine::drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, 
   cp(val, hd_.rVal, (size_t)5 * A);
   cp(meta, hd_.rMeta, 16);
   if(n > 0 && (unsigned long long)n < cnt) {
-    // keep the undrained tail at the front of the buffer
+    // keep the undrained tail at the front of the buffer, in chunks of n rows so
+    // no copy's source overlaps its destination
     const size_t rest = cnt - n;
     auto mv = [&](void* base, size_t rowBytes) {
-      KC_HIP(hipMemcpy(base, (char*)base + rowBytes * n, rowBytes * rest, hipMemcpyDeviceToDevice));
+      for(size_t off = 0; off < rest; off += (size_t)n) {
+        const size_t k = std::min(rest - off, (size_t)n);
+        KC_HIP(hipMemcpy((char*)base + rowBytes * off, (char*)base + rowBytes * (n + off), rowBytes * k,
+                         hipMemcpyDeviceToDevice));
+      }
     };
     mv(hd_.rBin, (size_t)NUM_SPATIAL * pb);
     mv(hd_.rGlob, 4);
@@ -278,6 +293,49 @@ int SelfplayEngine::drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, 
   KC_HIP(hipMemcpy(hd_.rCount, &left, 8, hipMemcpyHostToDevice));
   rowsDrained_ += n;
   return n;
+}
+
+int SelfplayEngine::drainGames(int maxGames, int32_t* header, uint8_t* moves) {
+  sync();
+  unsigned long long cnt = 0;
+  KC_HIP(hipMemcpy(&cnt, hd_.gCount, 8, hipMemcpyDeviceToHost));
+  const int n = (int)std::min<unsigned long long>(cnt, (unsigned long long)std::max(maxGames, 0));
+  if(n > 0) {
+    std::vector<GameRec> recs(n);
+    KC_HIP(hipMemcpy(recs.data(), hd_.gRec, sizeof(GameRec) * n, hipMemcpyDeviceToHost));
+    const int A = hd_.A;
+    for(int i = 0; i < n; i++) {
+      const GameRec& r = recs[i];
+      if(header) {
+        header[4 * i + 0] = r.slot;
+        header[4 * i + 1] = r.gameNum;
+        header[4 * i + 2] = r.numMoves;
+        header[4 * i + 3] = r.winner;
+      }
+      if(moves)
+        for(int t = 0; t < A; t++) {
+          moves[((size_t)i * A + t) * 2 + 0] = t < r.numMoves ? r.cell[t] : 0xFF;
+          moves[((size_t)i * A + t) * 2 + 1] = t < r.numMoves ? r.dir[t] : 0xFF;
+        }
+    }
+    const size_t rest = cnt - n;
+    for(size_t off = 0; off < rest; off += (size_t)n) {
+      const size_t k = std::min(rest - off, (size_t)n);
+      KC_HIP(hipMemcpy(hd_.gRec + off, hd_.gRec + n + off, sizeof(GameRec) * k, hipMemcpyDeviceToDevice));
+    }
+  }
+  unsigned long long left = cnt - (unsigned long long)n;
+  KC_HIP(hipMemcpy(hd_.gCount, &left, 8, hipMemcpyHostToDevice));
+  return n;
+}
+
+void SelfplayEngine::setModel(const char* path) {
+  if(!nn_)
+    throw std::invalid_argument("engine runs the stand-in network (use_fake_net)");
+  ModelHost m = loadModel(path);  // throws on a bad file; the current network stays
+  std::unique_ptr<NNEngine> next(new NNEngine(m, xLen_, yLen_, winLen_));
+  sync();
+  nn_ = std::move(next);
 }
 
 void SelfplayEngine::gameInfo(int slot, int64_t* info) {

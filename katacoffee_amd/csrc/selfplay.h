@@ -20,6 +20,9 @@ class SelfplayEngine {
   void sync();
   void stats(coffee_selfplay_stats& out);
   int drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, float* gt, int8_t* val, int32_t* meta);
+  int drainGames(int maxGames, int32_t* header, uint8_t* moves);
+  // Replaces the network for all subsequent rounds (all games: switchNetsMidGame).
+  void setModel(const char* path);
   void gameInfo(int slot, int64_t* info);
   int gameTree(int slot, int maxNodes, uint32_t* nodes, uint32_t* edges);
   void rootPolicy(int slot, float* out);
@@ -44,6 +47,7 @@ class SelfplayEngine {
   std::vector<void*> owned_;
   hipStream_t stream_ = nullptr;
   int commitInterval_ = 8;
+  int xLen_ = 0, yLen_ = 0, winLen_ = 0;
   uint64_t rounds_ = 0;
   uint64_t rowsDrained_ = 0;
   bool timing_ = false;

@@ -193,3 +193,50 @@ def test_selfplay_network_smoke(model_path):
     assert r["policyTargetsNCMove"][:, 0].sum(axis=1).min() > 0
     np.testing.assert_array_equal(r["globalTargetsNC"][:, 63], 1.0)
     sp.close()
+
+
+def test_game_records_match_rows_and_rules(model_path):
+    """Finished-game records (SGF source) agree with the rows of the same games and
+    replay legally under the reference-pinned rules to the recorded result."""
+    sp = kc.Selfplay(5, 5, 4, num_games=32, max_visits=16, seed=9, model_path=model_path, commit_interval=1)
+    parts, hs, ms = [], [], []
+    for _ in range(10):  # drain every 250 rounds (record buffer: 2 x num_games)
+        sp.step(250)
+        parts.append(sp.drain_rows())
+        h, m = sp.drain_games()
+        hs.append(h)
+        ms.append(m)
+    rows = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    header, moves = np.concatenate(hs), np.concatenate(ms)
+    assert len(header) > 0 and sp.stats()["games_dropped"] == 0
+    nmoves = {(int(m[0]), int(m[1])): int(m[3]) for m in rows["meta"]}
+    fin = {}
+    for m, v in zip(rows["meta"], rows["valueTargetsNCHW"]):
+        if int(m[2]) == 0:
+            fin[(int(m[0]), int(m[1]))] = v[0]  # final board from Black's (turn 0 mover) view
+    for h, mv in zip(header, moves):
+        key = (int(h[0]), int(h[1]))
+        assert nmoves.get(key) == int(h[2])
+        colors = np.zeros((1, 25), np.uint8)
+        lc, ld, pla = np.array([-1], np.int8), np.array([4], np.int8), np.array([1], np.uint8)
+        for t in range(int(h[2])):
+            cell, d = int(mv[t, 0]), int(mv[t, 1])
+            legal, _ = oracle.rules_batch(5, 5, 4, colors, lc, ld, pla)
+            assert legal[0, d * 25 + cell]
+            res = oracle.play_batch(5, 5, 4, colors, lc, ld, pla, np.array([d * 25 + cell], np.int32))
+            colors, lc, ld, pla = res["colors"], np.array([cell], np.int8), np.array([d], np.int8), 3 - pla
+        assert int(res["finished"][0]) == 1 and int(res["winner"][0]) == int(h[3])
+        assert np.all(mv[int(h[2]):] == 0xFF)
+        board = np.where(colors[0] == 1, 1, np.where(colors[0] == 2, -1, 0)).reshape(5, 5)
+        np.testing.assert_array_equal(board, fin[key])
+    # hot reload: a different network takes over for every game; the engine keeps running
+    other = model_path.replace(".cfnn", "-other.cfnn")
+    kc.write_random_model("b6c96", 77, other)
+    sp.set_model(other)
+    sp.step(300)
+    sp.sync()
+    assert sp.stats()["rounds"] == 2800
+    with pytest.raises(kc.CoffeeError):
+        sp.set_model(model_path + ".missing")
+    sp.step(10)
+    sp.sync()
