@@ -2,7 +2,7 @@
 GPU, 600 visits, random-init b6c96; the network runs fp16 MFMA with f32 accumulation
 -- same rate as bf16 on gfx950, more mantissa) on N GPUs of one node.
 
-A "step" is `--rounds-per-step` rounds of the hot path over the whole batch of
+A "step" is `--rounds-per-step` (1000) rounds of the hot path over the whole batch of
 games (one round = select/expand for every game -> one batched network
 evaluation -> backup, plus the periodic move-commit launch).  Games shard across
 ranks (slot_base = rank * games); finished rows are drained each step and, for
@@ -12,6 +12,20 @@ value = training rows/s over the timed steps for the whole job.  In benchmark mo
 (one row per move at full visits) a row is fixed the moment its move is
 committed; rows are emitted to the buffer when the game ends.  We count committed
 moves (= rows) in the window; rows actually drained in the window are reported too.
+
+All games start together and stay roughly in phase (a 5x5 game at 600 visits lasts
+about 9000 rounds), so rates swing over a game cycle: ~20k rows/s mid-game, ~40k at
+game ends, and a cache hit rate near 95% in the shared opening.  The defaults (10
+warm-up steps = 10k rounds, then 20 timed steps = 20k rounds) time more than two full
+game cycles after the first games have finished (tools/steady_state.py shows the
+trajectory); short --steps/--warmup values time a mid-game window, which
+underestimates the cycle average.
+
+The NN evaluation cache is on at the reference's own selfplay1.cfg size
+(nnCacheSizePowerOfTwo = 21, nneval.cpp:611-623): a search leaf whose state was
+evaluated earlier, by any game, takes that evaluation instead of the network, as in
+the reference; nn_evals_per_sec counts only real network evaluations.  The CPU
+baseline runs the same cache.
 """
 import argparse
 import json
@@ -31,12 +45,14 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--games", type=int, default=4096)
     ap.add_argument("--visits", type=int, default=600)
     ap.add_argument("--arch", default="b6c96")
-    ap.add_argument("--rounds-per-step", type=int, default=100)
+    ap.add_argument("--rounds-per-step", type=int, default=1000)
     ap.add_argument("--commit-interval", type=int, default=8)
+    ap.add_argument("--nn-cache-log2", type=int, default=21,
+                    help="NN evaluation cache entries = 2^k (selfplay1.cfg nnCacheSizePowerOfTwo = 21); 0 = off")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -46,7 +62,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(model_path, visits, seconds):
+def cpu_baseline(model_path, visits, seconds, cache_log2):
     """The oracle (C++ CPU restatement: same rules/search/rows, fp32 Eigen-semantics
     network) on this host's cores: a bounded sample of the same workload."""
     import numpy as np  # noqa: F401
@@ -57,7 +73,7 @@ def cpu_baseline(model_path, visits, seconds):
     games = 2 * cores
     model = oracle.Model(model_path)
     sp = oracle.Selfplay(5, 5, 4, games=games, max_visits=visits, node_cap=max(2048, 3 * visits), seed=1,
-                         nn_mode=1, model=model, nn_threads=cores)
+                         nn_mode=1, model=model, nn_threads=cores, nn_cache_log2=cache_log2)
     sp.rounds(8)  # warm-up: root evaluations
     i0 = [sp.info(g) for g in range(games)]
     t0 = time.perf_counter()
@@ -101,7 +117,8 @@ def main():
     flops_per_eval = kc.model_flops(model_path, 25)
 
     sp = kc.Selfplay(5, 5, 4, num_games=args.games, max_visits=args.visits, seed=args.seed,
-                     slot_base=rank * args.games, model_path=model_path, commit_interval=args.commit_interval)
+                     slot_base=rank * args.games, model_path=model_path, commit_interval=args.commit_interval,
+                     nn_cache_log2=args.nn_cache_log2)
     for _ in range(args.warmup):
         sp.step(args.rounds_per_step)
     sp.sync()
@@ -173,7 +190,7 @@ def main():
                     "avg_launch_us": net["avg_us"]}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(model_path, args.visits, args.cpu_seconds)
+            cpu = cpu_baseline(model_path, args.visits, args.cpu_seconds, args.nn_cache_log2)
         out = {
             "metric": "self-play training rows/sec + MCTS playouts/sec, 5x5 Coffee b6c96 @600 visits",
             "value": rows_per_sec,
@@ -189,7 +206,8 @@ def main():
             "data": "synthetic: self-play from empty 5x5 boards, random-init b6c96 (seed 0xC0FFEE)",
             "config": {"workload": "C2: 5x5 connect-4, %d games/GPU, %d visits, b6c96 (fp16 MFMA)" % (args.games, args.visits),
                        "games_per_gpu": args.games, "visits": args.visits, "rounds_per_step": args.rounds_per_step,
-                       "commit_interval": args.commit_interval, "parallelism": "game-sharded x%d" % world},
+                       "commit_interval": args.commit_interval, "nn_cache_log2": args.nn_cache_log2,
+                       "parallelism": "game-sharded x%d" % world},
             "playouts_per_sec": playouts / elapsed,
             "nn_evals_per_sec": evals / elapsed,
             "rows_drained": rows_gathered,

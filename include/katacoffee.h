@@ -142,6 +142,8 @@ typedef struct coffee_selfplay_config {
                               the round the root reaches max_visits, like the oracle */
   const char* model_path;/* CFNN model (host string), ignored with use_fake_net */
   coffee_search_params search;
+  int32_t nn_cache_log2; /* NN evaluation cache entries = 2^nn_cache_log2 (selfplay1.cfg
+                            nnCacheSizePowerOfTwo = 21); 0 disables (SPEC a7) */
 } coffee_selfplay_config;
 
 typedef struct coffee_selfplay coffee_selfplay;

@@ -69,6 +69,7 @@ class SelfplayConfig(ctypes.Structure):
         ("commit_interval", ctypes.c_int32),
         ("model_path", ctypes.c_char_p),
         ("search", SearchParams),
+        ("nn_cache_log2", ctypes.c_int32),
     ]
 
 
@@ -324,7 +325,7 @@ class Selfplay:
     """One device's self-play engine (games [slot_base, slot_base + num_games))."""
 
     def __init__(self, X=5, Y=5, W=4, num_games=4096, max_visits=600, seed=1, slot_base=0, model_path=None,
-                 node_cap=0, row_capacity=0, commit_interval=0, **search_over):
+                 node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, **search_over):
         _torch_cuda()
         self.X, self.Y, self.W = X, Y, W
         self.A, self.P = X * Y, 4 * X * Y
@@ -338,6 +339,7 @@ class Selfplay:
         cfg.slot_base = slot_base
         cfg.use_fake_net = 1 if model_path is None else 0
         cfg.commit_interval = commit_interval
+        cfg.nn_cache_log2 = nn_cache_log2
         self._model = model_path.encode() if model_path else None
         cfg.model_path = self._model
         cfg.search = default_search_params(max_visits=max_visits, **search_over)

@@ -20,6 +20,7 @@
 #include <dirent.h>
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdarg>
 #include <chrono>
@@ -177,6 +178,7 @@ static void mkdirs(const std::string& path) {
 struct Settings {
   int x = 5, y = 5, winLen = 4, games = 4096, gpus = 1, maxRowsPerFile = 10000;
   float modelPollSeconds = 10.0f;
+  int nnCacheLog2 = 21;  // selfplay1.cfg:121 nnCacheSizePowerOfTwo
   int64_t maxGamesTotal = -1;
   uint64_t seed = 0;
   coffee_search_params sp;
@@ -210,6 +212,8 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   geti("numGpus", s.gpus);
   geti("maxRowsPerTrainFile", s.maxRowsPerFile);
   getf("modelPollSeconds", s.modelPollSeconds);
+  geti("nnCacheSizePowerOfTwo", s.nnCacheLog2);  // setup.cpp:268; <= 0 disables the cache
+  s.nnCacheLog2 = std::max(0, s.nnCacheLog2);
   coffee_search_params& p = s.sp;
   geti("maxVisits", p.max_visits);
   getf("cpuctExploration", p.cpuct_exploration);
@@ -357,6 +361,7 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
   c.commit_interval = 8;
   c.model_path = model.c_str();
   c.search = s.sp;
+  c.nn_cache_log2 = s.nnCacheLog2;
   coffee_selfplay* h = nullptr;
   check(coffee_selfplay_create(&c, &h), "create engine");
   std::mt19937_64 fileRng(s.seed ^ (0x9E3779B97F4A7C15ULL * (gpu + 1)));

@@ -44,7 +44,10 @@ class NNEngine {
   ~NNEngine();
   // in: packed V1 words [n][inWords] (device); out: [n][P+4] f32 (device):
   // policy logits [4][A] in the symmetric frame, value logits (win, loss), misc[2].
-  void forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev = nullptr);
+  // rows [0, min(n, *countDev)) of the batch; with rowIdx, batch row r is game row rowIdx[r]
+  // (input in[rowIdx[r]], output out[rowIdx[r]]), otherwise r.
+  void forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev = nullptr,
+               const int* rowIdx = nullptr);
   const ModelCfg& cfg() const { return cfg_; }
   double flopsPerEval() const { return flops_; }
   static bool supported(const ModelCfg& c, int X, int Y);
@@ -62,6 +65,6 @@ class NNEngine {
 
 // Deterministic stand-in network (see oracle fakeNet); same I/O as NNEngine.
 void launchFakeNet(const DTables* T, int n, const uint64_t* in, float* out, hipStream_t st,
-                   const int* countDev = nullptr);
+                   const int* countDev = nullptr, const int* rowIdx = nullptr);
 
 }  // namespace kc

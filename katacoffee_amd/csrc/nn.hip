@@ -457,8 +457,9 @@ KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ W
 template <int X, int Y, int C>
 __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
-               const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev, int inWords,
-               float winLen, const uint64_t* __restrict__ in, float* __restrict__ out) {
+               const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
+               const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
+               float* __restrict__ out) {
   using G = NNGeo<X, Y, C>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
@@ -493,7 +494,8 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   for(int idx = tid; idx < nb * G::A * NUM_SPATIAL; idx += NN_NT) {
     const int b = idx / (G::A * NUM_SPATIAL), i = idx - b * (G::A * NUM_SPATIAL);
     const int c = i / G::A, p = i - c * G::A;
-    const uint64_t word = in[(size_t)(base + b) * inWords + (i >> 6)];
+    const int src = rowIdx ? rowIdx[base + b] : base + b;
+    const uint64_t word = in[(size_t)src * inWords + (i >> 6)];
     if((word >> (i & 63)) & 1ULL)
       act[padCell<G>(b, p) * G::ASTR + c] = (uint16_t)0x3c00;
   }
@@ -674,7 +676,8 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
 #pragma unroll 4
       for(int i = 0; i < v2; i++)
         s += w[i] * vh[b * 64 + i];
-      out[(size_t)(base + b) * (G::P + 4) + G::P + o] = s;
+      const int dst = rowIdx ? rowIdx[base + b] : base + b;
+      out[(size_t)dst * (G::P + 4) + G::P + o] = s;
     }
   }
   NN_PHASE(42);
@@ -709,7 +712,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       }
       if((lane >> 4) == 0 && row < G::ROWS && brd < nb) {
         const int pp = bp - brd * G::A;
-        float* o = out + (size_t)(base + brd) * (G::P + 4);
+        float* o = out + (size_t)(rowIdx ? rowIdx[base + brd] : base + brd) * (G::P + 4);
 #pragma unroll
         for(int d = 0; d < 4; d++)
           o[d * G::A + pp] = part[d];
@@ -886,26 +889,28 @@ NNEngine::~NNEngine() {
   (void)hipFree(tabDev_);
 }
 
-void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev) {
+void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev,
+                       const int* rowIdx) {
   if(n <= 0)
     return;
   using G = NNGeo<5, 5, 96>;
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
   int grid = (n + G::NB - 1) / G::NB;
   hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_,
-                     (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, inWords, (float)W_, in, out);
+                     (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out);
   KC_HIP(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------
 // Deterministic stand-in network (oracle fakeNet).
 __global__ void __launch_bounds__(64) kFakeNet(const DTables* __restrict__ Tp, int n, const int* countDev,
-                                               const uint64_t* __restrict__ in, float* __restrict__ out) {
+                                               const int* __restrict__ rowIdx, const uint64_t* __restrict__ in,
+                                               float* __restrict__ out) {
   const DTables& T = *Tp;
   const int count = countDev ? min(*countDev, n) : n;
-  int i = blockIdx.x;
-  if(i >= count)
+  if((int)blockIdx.x >= count)
     return;
+  const int i = rowIdx ? rowIdx[blockIdx.x] : (int)blockIdx.x;
   uint64_t h = 0x243f6a8885a308d3ULL;
   for(int w = 0; w < T.inWords; w++)
     h = mix64(h ^ in[(size_t)i * T.inWords + w]);
@@ -918,10 +923,11 @@ __global__ void __launch_bounds__(64) kFakeNet(const DTables* __restrict__ Tp, i
   }
 }
 
-void launchFakeNet(const DTables* T, int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev) {
+void launchFakeNet(const DTables* T, int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev,
+                   const int* rowIdx) {
   if(n <= 0)
     return;
-  hipLaunchKernelGGL(kFakeNet, dim3(n), dim3(64), 0, st, T, n, countDev, in, out);
+  hipLaunchKernelGGL(kFakeNet, dim3(n), dim3(64), 0, st, T, n, countDev, rowIdx, in, out);
   KC_HIP(hipGetLastError());
 }
 

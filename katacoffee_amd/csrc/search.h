@@ -24,7 +24,21 @@ namespace kc {
 constexpr int MAX_DEPTH = MAX_AREA + 2;
 constexpr int MAX_LANE_ITEMS = (MAX_P + 63) / 64;  // 7
 
-enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5 };
+enum LeafKind {
+  LEAF_NONE = 0,
+  LEAF_NN = 1,
+  LEAF_TERMINAL = 2,
+  LEAF_CATCHUP = 3,
+  LEAF_NOCHILD = 4,
+  LEAF_ROOTEVAL = 5,
+  LEAF_CACHED = 6  // NN output taken from the evaluation cache (SPEC a7)
+};
+
+// NN evaluation cache slot of a state key (SPEC a7; oracle ora_search.cpp cacheSlot).
+KC_HD uint32_t cacheSlot(uint64_t k0, uint64_t k1, uint32_t mask) {
+  const uint64_t h = k0 ^ ((k1 << 29) | (k1 >> 35));
+  return (uint32_t)(h ^ (h >> 32)) & mask;
+}
 enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2 };
 
 // SearchParams (searchparams.h) restricted to Coffee self-play.
@@ -102,7 +116,9 @@ struct GameDev {
   uint64_t playouts, nnEvals, moves, gamesFinished;
   int32_t phase, rootK;
   uint32_t syms;                  // four root symmetries, 4 bits each
-  int32_t pad0, pad1, pad2;
+  int32_t cSlot;                  // NN-cache slot of the leaf (hit or bid)
+  int32_t cBid;                   // 1: this round's evaluation bids for cSlot
+  int32_t pad2;
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
@@ -138,6 +154,18 @@ struct SearchDev {
   // network batch
   uint64_t* nnIn;        // [G][inWords]
   float* nnOut;          // [G][P+4]
+  int32_t* nnNeed;       // [G] 1 when the game's row needs the network this round
+  int32_t* nnIdx;        // [G] compacted rows to evaluate (kCompact)
+  int32_t* nnCount;      // rows in nnIdx
+  // NN evaluation cache (SPEC a7): direct-mapped by state key, written between rounds
+  uint32_t cacheMask;    // entries - 1 (0 with cacheOn == 0)
+  int32_t cacheOn;
+  uint64_t* cKey;        // [entries][2]
+  float* cPol;           // [entries][P] post-processed policy (illegal = -1)
+  float* cVal;           // [entries][2] white win / loss
+  uint32_t* cTag;        // [entries] this round's highest bidding game + 1 (0 = none)
+  float* cStage;         // [G][P+2] a bidding game's payload
+  uint64_t* cStageKey;   // [G][2]
   // commit queue
   int32_t* commitList;   // [G]
   int32_t* commitCount;
@@ -160,6 +188,8 @@ struct SearchDev {
 // Kernel launchers (search.hip).
 void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchGameTree(const SearchDev* dd, int slot, int maxNodes, uint32_t* nodesOut, uint32_t* edgesOut,

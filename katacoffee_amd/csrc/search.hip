@@ -49,6 +49,25 @@ KC_D void waveSync() {
 // 10 backup blocks  11 backup total  12 postprocess+order  13 path backup  14 leaf value
 constexpr int SPROF_MAXG = 16384;
 __device__ unsigned long long g_searchProf[SPROF_MAXG * 16];
+// NN-cache probe: every evaluated leaf's state key goes into an open-addressing set;
+// a key already present counts as a potential cross-game cache hit (slot 9).
+__device__ unsigned long long* g_probeKeys = nullptr;
+__device__ unsigned long long g_probeMask = 0;
+KC_D void probeLeafKey(uint64_t k0, uint64_t k1) {
+  if(!g_probeKeys)
+    return;
+  uint64_t key = (k0 ^ (k1 * 0x9e3779b97f4a7c15ULL)) | 1ull;
+  uint64_t i = (key >> 7) & g_probeMask;
+  for(int probe = 0; probe < 64; probe++, i = (i + 1) & g_probeMask) {
+    const unsigned long long prev = atomicCAS(&g_probeKeys[i], 0ull, (unsigned long long)key);
+    if(prev == 0ull)
+      return;
+    if(prev == key) {
+      atomicAdd(&g_searchProf[9], 1ull);
+      return;
+    }
+  }
+}
 KC_D unsigned long long* sprofLds() {
   __shared__ unsigned long long c[16];
   return c;
@@ -719,8 +738,10 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   loadGame(v, s);
   if(s.phase == PH_COMMIT) {
     s.leafKind = LEAF_NONE;
-    if(v.lane == 0)
+    if(v.lane == 0) {
       d.games[g].leafKind = LEAF_NONE;
+      d.nnNeed[g] = 0;
+    }
     return;
   }
   const unsigned long long t1 = SPROF_NOW();
@@ -744,15 +765,28 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     s.leaf = s.root;
   } else {
     descend<NI>(v, s, hasBits);
+    if(s.leafKind == LEAF_NN && d.cacheOn) {
+      // NN evaluation cache (SPEC a7): a state evaluated in an earlier round by any
+      // game is taken from the cache instead of the network
+      const uint64_t k0 = v.nodeKey(s.leafNode)[0], k1 = v.nodeKey(s.leafNode)[1];
+      const uint32_t slot = cacheSlot(k0, k1, d.cacheMask);
+      if(d.cKey[2 * (size_t)slot] == k0 && d.cKey[2 * (size_t)slot + 1] == k1) {
+        s.leafKind = LEAF_CACHED;
+        s.cSlot = (int32_t)slot;
+      }
+    }
     if(s.leafKind == LEAF_NN)
       s.leafSym = (int)rng.below(8);
   }
   const unsigned long long t2 = SPROF_NOW();
   (void)t2;
   s.rngCtr = rng.ctr;
-  if(s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL) {
+  const bool needNN = s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL;
+  if(v.lane == 0)
+    d.nnNeed[g] = needNN ? 1 : 0;
+  if(needNN) {
     // the game's own batch row: no shared counter (a same-address atomic from
-    // every block serialises at L2); the network evaluates all G rows
+    // every block serialises at L2); kCompact lists the rows the network evaluates
     const int slot = g;
     s.nnSlot = slot;
     s.nnEvals++;
@@ -1070,13 +1104,50 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
       needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)sp.maxVisits;
     }
   } else {
-    if(s.leafKind == LEAF_NN) {
+    if(s.leafKind == LEAF_NN || s.leafKind == LEAF_CACHED) {
       float w, l;
       float* pol = v.pol(s.leafNode);
       const unsigned long long ta = SPROF_NOW();
       (void)ta;
       float pv[NI];
-      postprocess<NI>(v, s.leaf, s.leafSym, o, pol, w, l, scratch, pv);
+#ifdef KC_SEARCH_PROFILE
+      if(v.lane == 0)
+        probeLeafKey(v.nodeKey(s.leafNode)[0], v.nodeKey(s.leafNode)[1]);
+#endif
+      if(s.leafKind == LEAF_CACHED) {
+        const float* cp = d.cPol + (size_t)s.cSlot * P;
+#pragma unroll
+        for(int j = 0; j < NI; j++) {
+          const int pos = v.lane + 64 * j;
+          pv[j] = pos < P ? cp[pos] : -1.0f;
+          if(pos < P)
+            pol[pos] = pv[j];
+        }
+        w = d.cVal[2 * (size_t)s.cSlot];
+        l = d.cVal[2 * (size_t)s.cSlot + 1];
+      } else {
+        postprocess<NI>(v, s.leaf, s.leafSym, o, pol, w, l, scratch, pv);
+        if(d.cacheOn) {
+          // bid for the state's cache slot; kCacheWrite stores the highest bidder's
+          // payload after this kernel (deterministic whatever the block order)
+          const uint64_t k0 = v.nodeKey(s.leafNode)[0], k1 = v.nodeKey(s.leafNode)[1];
+          const uint32_t slot = cacheSlot(k0, k1, d.cacheMask);
+          float* st = d.cStage + (size_t)g * (P + 2);
+#pragma unroll
+          for(int j = 0; j < NI; j++)
+            if(v.lane + 64 * j < P)
+              st[v.lane + 64 * j] = pv[j];
+          if(v.lane == 0) {
+            st[P] = w;
+            st[P + 1] = l;
+            d.cStageKey[2 * (size_t)g] = k0;
+            d.cStageKey[2 * (size_t)g + 1] = k1;
+            atomicMax(&d.cTag[slot], (uint32_t)g + 1u);
+          }
+          s.cSlot = (int32_t)slot;
+          s.cBid = 1;
+        }
+      }
       buildOrder<NI>(v, s.leafNode, pv, scratch);
       if(v.lane == 0) {
         Node* n = &v.nodes()[s.leafNode];
@@ -1134,6 +1205,13 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
 #include <algorithm>
 #include <vector>
 namespace kc {
+extern "C" void coffee_debug_probe_table(void* keys, unsigned long long cap /* power of two */) {
+  unsigned long long* k = (unsigned long long*)keys;
+  unsigned long long m = cap ? cap - 1 : 0;
+  KC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_probeKeys), &k, sizeof(k)));
+  KC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_probeMask), &m, sizeof(m)));
+}
+
 extern "C" void coffee_debug_search_profile(unsigned long long* out, int reset) {
   std::vector<unsigned long long> all((size_t)SPROF_MAXG * 16);
   KC_HIP(hipDeviceSynchronize());
@@ -1921,6 +1999,61 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   storeGame(v, s);
 }
 
+// kCacheWrite: the winning bidder of every cache slot stores its evaluation (runs
+// after kBackup, before the next kSelect reads the cache).
+__global__ void __launch_bounds__(64) kCacheWrite(const SearchDev* __restrict__ dp) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  if(g >= d.G || !d.games[g].cBid)
+    return;
+  const int lane = laneId();
+  const uint32_t slot = (uint32_t)d.games[g].cSlot;
+  const bool won = d.cTag[slot] == (uint32_t)g + 1u;
+  if(won) {
+    const int P = d.P;
+    const float* st = d.cStage + (size_t)g * (P + 2);
+    for(int p = lane; p < P; p += 64)
+      d.cPol[(size_t)slot * P + p] = st[p];
+    if(lane == 0) {
+      d.cVal[2 * (size_t)slot] = st[P];
+      d.cVal[2 * (size_t)slot + 1] = st[P + 1];
+      d.cKey[2 * (size_t)slot] = d.cStageKey[2 * (size_t)g];
+      d.cKey[2 * (size_t)slot + 1] = d.cStageKey[2 * (size_t)g + 1];
+    }
+  }
+  __syncthreads();
+  if(lane == 0) {
+    if(won)
+      d.cTag[slot] = 0;
+    d.games[g].cBid = 0;
+  }
+}
+
+// kCompact: ascending list of the games whose row needs the network this round.
+__global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp) {
+  const SearchDev& d = *dp;
+  __shared__ int part[1024];
+  const int t = threadIdx.x, per = (d.G + 1023) / 1024;
+  const int lo = t * per, hi = min(d.G, lo + per);
+  int c = 0;
+  for(int i = lo; i < hi; i++)
+    c += d.nnNeed[i];
+  part[t] = c;
+  __syncthreads();
+  for(int off = 1; off < 1024; off <<= 1) {  // inclusive scan
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int o = part[t] - c;
+  for(int i = lo; i < hi; i++)
+    if(d.nnNeed[i])
+      d.nnIdx[o++] = i;
+  if(t == 1023)
+    *d.nnCount = part[1023];
+}
+
 __global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
@@ -2023,6 +2156,19 @@ static int laneItems(int P) { return P <= 128 ? 2 : (P <= 256 ? 4 : 7); }
 
 void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   hipLaunchKernelGGL(kInit, dim3(d.G), dim3(64), 0, st, dd, d.T);
+  KC_HIP(hipGetLastError());
+}
+
+void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+  (void)d;
+  hipLaunchKernelGGL(kCompact, dim3(1), dim3(1024), 0, st, dd);
+  KC_HIP(hipGetLastError());
+}
+
+void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+  if(!d.cacheOn)
+    return;
+  hipLaunchKernelGGL(kCacheWrite, dim3(d.G), dim3(64), 0, st, dd);
   KC_HIP(hipGetLastError());
 }
 

@@ -137,6 +137,22 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.rMeta = devAlloc<int32_t>(owned_, (size_t)rowCap * 4, false);
   d.rCount = devAlloc<unsigned long long>(owned_, 1);
   d.rDropped = devAlloc<unsigned long long>(owned_, 1);
+  d.nnNeed = devAlloc<int32_t>(owned_, G);
+  d.nnIdx = devAlloc<int32_t>(owned_, G);
+  d.nnCount = devAlloc<int32_t>(owned_, 1);
+  if(c.nn_cache_log2 < 0 || c.nn_cache_log2 > 26)
+    throw std::invalid_argument("nn_cache_log2 must be in 0..26");
+  d.cacheOn = c.nn_cache_log2 > 0 ? 1 : 0;
+  {
+    const size_t entries = d.cacheOn ? (size_t)1 << c.nn_cache_log2 : 1;
+    d.cacheMask = (uint32_t)(entries - 1);
+    d.cKey = devAlloc<uint64_t>(owned_, entries * 2);  // zero key: never a state
+    d.cPol = devAlloc<float>(owned_, entries * P, false);
+    d.cVal = devAlloc<float>(owned_, entries * 2, false);
+    d.cTag = devAlloc<uint32_t>(owned_, entries);
+    d.cStage = devAlloc<float>(owned_, (size_t)G * (P + 2), false);
+    d.cStageKey = devAlloc<uint64_t>(owned_, (size_t)G * 2, false);
+  }
   d.gCap = 2 * G;
   d.gRec = devAlloc<GameRec>(owned_, (size_t)d.gCap, false);
   d.gCount = devAlloc<unsigned long long>(owned_, 1);
@@ -210,14 +226,20 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
     st = stream_;
   const SearchDev& d = hd_;
   for(int r = 0; r < rounds; r++) {
-    timed(0, st, [&] { launchSelect(d, dd_, st); });
+    timed(0, st, [&] {
+      launchSelect(d, dd_, st);
+      launchCompact(d, dd_, st);
+    });
     timed(1, st, [&] {
       if(nn_)
-        nn_->forward(d.G, d.nnIn, d.nnOut, st, nullptr);
+        nn_->forward(d.G, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
       else
-        launchFakeNet(T_, d.G, d.nnIn, d.nnOut, st, nullptr);
+        launchFakeNet(T_, d.G, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
     });
-    timed(2, st, [&] { launchBackup(d, dd_, st); });
+    timed(2, st, [&] {
+      launchBackup(d, dd_, st);
+      launchCacheWrite(d, dd_, st);
+    });
     rounds_++;
     if(rounds_ % (uint64_t)commitInterval_ == 0 || r == rounds - 1) {
       timed(3, st, [&] { launchCommit(d, dd_, st); });
@@ -336,6 +358,10 @@ void SelfplayEngine::setModel(const char* path) {
   std::unique_ptr<NNEngine> next(new NNEngine(m, xLen_, yLen_, winLen_));
   sync();
   nn_ = std::move(next);
+  // cached evaluations belong to the previous network (the reference builds a new
+  // NNEvaluator, and with it a new cache, per model: cpp/command/selfplay.cpp:150-200)
+  if(hd_.cacheOn)
+    KC_HIP(hipMemset(hd_.cKey, 0, sizeof(uint64_t) * 2 * ((size_t)hd_.cacheMask + 1)));
 }
 
 void SelfplayEngine::gameInfo(int slot, int64_t* info) {

@@ -122,7 +122,7 @@ int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* 
 }
 
 void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
-                    int nnMode, void* model, int nnThreads) {
+                    int nnMode, void* model, int nnThreads, int cacheLog2) {
   if(!T.loaded)
     return nullptr;
   Selfplay* s = new Selfplay();
@@ -135,6 +135,9 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
   cfg.nnMode = nnMode;
   cfg.model = (const Model*)model;
   cfg.nnThreads = nnThreads;
+  if(cacheLog2 < 0 || cacheLog2 > 26)
+    return nullptr;
+  cfg.cacheLog2 = cacheLog2;
   selfplayInit(*s, cfg, games);
   return s;
 }

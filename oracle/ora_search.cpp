@@ -1130,9 +1130,21 @@ void Ctx::finishGame() {
 
 }  // namespace
 
+// Cache slot of a state key (SPEC a7): fold of the two key words, low bits.
+static uint32_t cacheSlotOf(uint64_t k0, uint64_t k1, uint32_t mask) {
+  const uint64_t h = k0 ^ ((k1 << 29) | (k1 >> 35));
+  return (uint32_t)(h ^ (h >> 32)) & mask;
+}
+
 void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames) {
   s.cfg = cfg;
   const Geom& g = s.cfg.g;
+  if(cfg.cacheLog2 > 0) {
+    const size_t entries = (size_t)1 << cfg.cacheLog2;
+    s.cacheKey.assign(2 * entries, 0);  // zero key: never a state
+    s.cachePol.assign(entries * g.P, 0.0f);
+    s.cacheVal.assign(2 * entries, 0.0f);
+  }
   Rng zr;
   zr.seed = SVB_SEED;
   s.svbZ.resize(2 * (MAX_P + 1) + 3 + 4 * 25);
@@ -1168,6 +1180,8 @@ void selfplayRound(Selfplay& s) {
   const int A = g.A;
   std::vector<float> bin((size_t)G * NUM_SPATIAL * A), glob((size_t)G);
   std::vector<int> need(G, 0);
+  const bool cacheOn = s.cfg.cacheLog2 > 0;
+  const uint32_t cacheMask = cacheOn ? (uint32_t)((1u << s.cfg.cacheLog2) - 1) : 0u;
   // ---- select ----
   for(int i = 0; i < G; i++) {
     Game& gm = s.games[i];
@@ -1186,6 +1200,15 @@ void selfplayRound(Selfplay& s) {
       gm.leafBoard = gm.root;
     } else {
       cx.descend();
+      if(gm.leafKind == LEAF_NN && cacheOn) {
+        // lookups see the cache as it stood at the end of the previous round
+        const Node& ln = cx.N(gm.leafNode);
+        const uint32_t slot = cacheSlotOf(ln.key0, ln.key1, cacheMask);
+        if(s.cacheKey[2 * slot] == ln.key0 && s.cacheKey[2 * slot + 1] == ln.key1) {
+          gm.leafKind = LEAF_CACHED;
+          gm.cacheSlot = (int)slot;
+        }
+      }
       if(gm.leafKind == LEAF_NN)
         gm.leafSym = (int)gm.rng.below(8);
     }
@@ -1224,6 +1247,13 @@ void selfplayRound(Selfplay& s) {
     }
   }
   // ---- backup ----
+  struct CacheWrite {
+    uint32_t slot;
+    uint64_t k0, k1;
+    std::vector<float> pol;
+    float w, l;
+  };
+  std::vector<CacheWrite> cacheWrites;  // fresh evaluations, in game order
   for(int i = 0; i < G; i++) {
     Game& gm = s.games[i];
     Ctx cx(s, gm);
@@ -1269,10 +1299,21 @@ void selfplayRound(Selfplay& s) {
       continue;
     }
     // PH_SEARCH leaf
-    if(gm.leafKind == LEAF_NN) {
+    if(gm.leafKind == LEAF_NN || gm.leafKind == LEAF_CACHED) {
       Node& n = cx.N(gm.leafNode);
       float w, l;
-      cx.postprocess(gm.leafBoard, gm.leafSym, o, cx.POL(gm.leafNode), w, l);
+      float* pol = cx.POL(gm.leafNode);
+      if(gm.leafKind == LEAF_CACHED) {
+        memcpy(pol, &s.cachePol[(size_t)gm.cacheSlot * g.P], sizeof(float) * g.P);
+        w = s.cacheVal[2 * gm.cacheSlot];
+        l = s.cacheVal[2 * gm.cacheSlot + 1];
+      } else {
+        cx.postprocess(gm.leafBoard, gm.leafSym, o, pol, w, l);
+        if(cacheOn) {  // staged now: commitMove below may compact the node pool
+          const uint32_t slot = cacheSlotOf(n.key0, n.key1, cacheMask);
+          cacheWrites.push_back({slot, n.key0, n.key1, std::vector<float>(pol, pol + g.P), w, l});
+        }
+      }
       n.nnWin = w;
       n.nnLoss = l;
       n.flags |= 1;
@@ -1293,6 +1334,15 @@ void selfplayRound(Selfplay& s) {
     gm.playouts++;
     if(cx.N(gm.rootIdx).visits >= (uint32_t)s.cfg.sp.maxVisits)
       cx.commitMove();
+  }
+  // ---- cache write: after every read of this round; in game order, so a slot ends
+  // up holding its highest-numbered evaluator (the device's atomicMax bid) ----
+  for(const CacheWrite& c : cacheWrites) {
+    s.cacheKey[2 * c.slot] = c.k0;
+    s.cacheKey[2 * c.slot + 1] = c.k1;
+    memcpy(&s.cachePol[(size_t)c.slot * g.P], c.pol.data(), sizeof(float) * g.P);
+    s.cacheVal[2 * c.slot] = c.w;
+    s.cacheVal[2 * c.slot + 1] = c.l;
   }
   s.rounds++;
 }

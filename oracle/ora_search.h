@@ -43,7 +43,8 @@ struct Node {
   uint64_t key0, key1;             // transposition key (stateHash)
 };
 
-enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5 };
+enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5,
+               LEAF_CACHED = 6 };
 enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1 };
 
 struct TurnRec {
@@ -74,6 +75,7 @@ struct SelfplayCfg {
   int nnMode = 0;          // 0 fake deterministic net, 1 model fp32, 2 model bf16-emulation
   const Model* model = nullptr;
   int nnThreads = 1;
+  int cacheLog2 = 0;       // NN evaluation cache of 2^cacheLog2 entries, 0 = off (SPEC a7)
 };
 
 struct Game {
@@ -100,7 +102,7 @@ struct Game {
   std::vector<int64_t> svbDelta, svbWeight;  // fixed point, 2^-32 units (SPEC B27)
   std::vector<uint8_t> svbUsed;
   // playout scratch
-  int leafKind = LEAF_NONE, leafNode = -1, leafSym = 0;
+  int leafKind = LEAF_NONE, leafNode = -1, leafSym = 0, cacheSlot = 0;
   Board leafBoard;
   std::vector<int> pathNode, pathSlot;
   // game record
@@ -116,6 +118,10 @@ struct Selfplay {
   std::vector<uint64_t> svbZ;  // SVB pattern zobrist (SPEC a19)
   Rows rows;
   uint64_t rounds = 0;
+  // NN evaluation cache (nneval.h:18 NNCacheTable, restated as a direct-mapped table
+  // written once per round; SPEC a7): key pair, postprocessed policy row, white win/loss
+  std::vector<uint64_t> cacheKey;
+  std::vector<float> cachePol, cacheVal;
 };
 
 void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames);

@@ -149,11 +149,17 @@ def _sorted_rows(r):
     return {k: v[order] for k, v in r.items()}
 
 
-@pytest.mark.parametrize("games,visits,rounds,seed", [(6, 40, 900, 3), (4, 24, 700, 99)])
-def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed):
+# cache_log2: 0 = no NN cache; 5 = a 32-entry cache, so slots are contended and
+# overwritten every round (the round-synchronous write order decides the contents);
+# 14 = hits across games (SPEC a7)
+@pytest.mark.parametrize("games,visits,rounds,seed,cache_log2",
+                         [(6, 40, 900, 3, 0), (4, 24, 700, 99, 0), (8, 40, 800, 3, 5), (12, 32, 700, 7, 14)])
+def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2):
     cap = 128
-    gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1)
-    ora = oracle.Selfplay(5, 5, 4, games=games, max_visits=visits, node_cap=cap, seed=seed)
+    gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,
+                      nn_cache_log2=cache_log2)
+    ora = oracle.Selfplay(5, 5, 4, games=games, max_visits=visits, node_cap=cap, seed=seed,
+                          nn_cache_log2=cache_log2)
     done = 0
     for chunk in [1, 4, 20, rounds]:
         step = chunk - done

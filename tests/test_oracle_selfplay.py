@@ -57,3 +57,25 @@ def test_tree_export_is_canonical():
     assert root_children > 0
     child_idx = edges[0, :root_children, 0]
     assert np.all(child_idx < len(nodes))
+
+
+def test_nn_cache_cuts_evaluations():
+    """SPEC a7: with the evaluation cache on, repeated states across games and moves
+    skip the network; the search stays deterministic and rows keep their invariants."""
+    G = 64
+
+    def run(cache):
+        sp = oracle.Selfplay(5, 5, 4, games=G, max_visits=32, node_cap=128, seed=4, nn_cache_log2=cache)
+        sp.rounds(400)
+        info = [sp.info(g) for g in range(G)]
+        # search-leaf evaluations per playout (root evaluations: 4 symmetries per move)
+        leaf = sum(i["nnEvals"] - 4 * i["movesMade"] for i in info)
+        return leaf / sum(i["playouts"] for i in info), sp
+    r0, _ = run(0)
+    r1, a = run(14)
+    _, b = run(14)
+    assert r0 > 0.95 and r1 < 0.95 * r0
+    ra, rb = a.rows(), b.rows()
+    assert len(ra["meta"]) > 0
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k])

@@ -18,15 +18,22 @@ def main():
     ap.add_argument("--visits", type=int, default=600)
     ap.add_argument("--rounds", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=600)
+    ap.add_argument("--probe", action="store_true", help="count evaluated leaves whose state repeats (NN-cache bound)")
+    ap.add_argument("--nn-cache-log2", type=int, default=21)
     a = ap.parse_args()
     import katacoffee_amd as kc
     L = kc.lib()
     prof = (ctypes.c_ulonglong * 16)()
     path = os.path.join(tempfile.mkdtemp(), "m.cfnn")
     kc.write_random_model("b6c96", 0xC0FFEE, path)
-    sp = kc.Selfplay(5, 5, 4, num_games=a.games, max_visits=a.visits, seed=1, model_path=path, commit_interval=8)
+    sp = kc.Selfplay(5, 5, 4, num_games=a.games, max_visits=a.visits, seed=1, model_path=path, commit_interval=8,
+                     nn_cache_log2=a.nn_cache_log2)
     sp.step(a.warmup)
     sp.sync()
+    if a.probe:
+        import torch
+        keys = torch.zeros(1 << 24, dtype=torch.int64, device="cuda")
+        L.coffee_debug_probe_table(ctypes.c_void_p(keys.data_ptr()), ctypes.c_ulonglong(1 << 24))
     L.coffee_debug_search_profile(prof, 1)
     sp.step(a.rounds)
     sp.sync()
@@ -38,6 +45,9 @@ def main():
                     ("encode+slot", 7)]:
         print("  %-14s %8.0f cycles/block" % (name, p[i] / nb))
     print("  path levels    %8.2f per block" % (p[4] / nb))
+    if a.probe:
+        print("NN-cache bound: %d of %d evaluated leaves repeat an earlier state (%.1f%%)" %
+              (p[9], p[10], 100.0 * p[9] / max(1, p[10])))
     print("backup: %d blocks" % p[10])
     for name, i in [("total", 11), ("post+order", 12), ("leaf value", 14), ("path backup", 13)]:
         print("  %-14s %8.0f cycles/block" % (name, p[i] / nk))
