@@ -217,9 +217,14 @@ int coffee_debug_zobrist(int x, int y, int win_len, uint64_t* board, uint64_t* b
                          uint64_t* init, uint64_t* game_over);
 
 /* Kernel timing (HIP events on the engine stream) for roofline reporting:
- * which: 0 select, 1 network, 2 backup, 3 commit.  Summed ms and launch count. */
+ * which: 0 select, 1 network, 2 backup, 3 commit (+ rows).  Summed ms and launch
+ * count of the timed launches.  enable = 0 off, N > 0: every N-th launch of each
+ * group is bracketed by an event pair (each pair costs a few microseconds of stream
+ * gap, so N > 1 keeps a timed run representative of an untimed one). */
 int coffee_selfplay_enable_timing(coffee_selfplay* h, int enable);
 int coffee_selfplay_kernel_time(coffee_selfplay* h, int which, double* ms, uint64_t* launches);
+/* Network evaluations performed by the timed network launches (sum of their batch sizes). */
+int coffee_selfplay_timed_nn_evals(coffee_selfplay* h, uint64_t* evals);
 
 #ifdef __cplusplus
 }

@@ -89,7 +89,8 @@ EXPORTS = [
     "coffee_selfplay_drain_rows", "coffee_selfplay_drain_games", "coffee_selfplay_set_model",
     "coffee_selfplay_destroy", "coffee_selfplay_game_info",
     "coffee_selfplay_game_tree", "coffee_selfplay_root_policy", "coffee_debug_cdf_table", "coffee_debug_zobrist",
-    "coffee_selfplay_enable_timing", "coffee_selfplay_kernel_time", "coffee_write_npz",
+    "coffee_selfplay_enable_timing", "coffee_selfplay_kernel_time", "coffee_selfplay_timed_nn_evals",
+    "coffee_write_npz",
 ]
 
 
@@ -139,6 +140,7 @@ def lib():
         L.coffee_selfplay_root_policy.argtypes = [c_p, c_i, c_p]
         L.coffee_selfplay_enable_timing.argtypes = [c_p, c_i]
         L.coffee_selfplay_kernel_time.argtypes = [c_p, c_i, c_p, c_p]
+        L.coffee_selfplay_timed_nn_evals.argtypes = [c_p, c_p]
         L.coffee_debug_cdf_table.argtypes = [c_i, c_i, c_i, c_p]
         L.coffee_debug_zobrist.argtypes = [c_i, c_i, c_i] + [c_p] * 5
         L.coffee_write_npz.argtypes = [ctypes.c_char_p, c_i, c_i, c_i] + [c_p] * 5
@@ -411,8 +413,15 @@ class Selfplay:
         check(lib().coffee_selfplay_root_policy(self.h, slot, _ptr(out)))
         return out
 
-    def enable_timing(self, on=True):
-        check(lib().coffee_selfplay_enable_timing(self.h, 1 if on else 0))
+    def enable_timing(self, every=1):
+        """Time every `every`-th launch of each kernel group with HIP events (0 = off)."""
+        check(lib().coffee_selfplay_enable_timing(self.h, int(every)))
+
+    def timed_nn_evals(self):
+        """Network evaluations performed by the timed network launches."""
+        n = ctypes.c_uint64()
+        check(lib().coffee_selfplay_timed_nn_evals(self.h, ctypes.byref(n)))
+        return n.value
 
     def kernel_time(self, which):
         ms = ctypes.c_double()

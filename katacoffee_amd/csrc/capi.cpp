@@ -381,7 +381,15 @@ int coffee_debug_zobrist(int x, int y, int win_len, uint64_t* board, uint64_t* b
 int coffee_selfplay_enable_timing(coffee_selfplay* h, int enable) {
   return guarded([&] {
     need(h && h->eng, "NULL handle");
-    h->eng->setTiming(enable != 0);
+    need(enable >= 0, "enable must be >= 0");
+    h->eng->setTiming(enable);
+  });
+}
+
+int coffee_selfplay_timed_nn_evals(coffee_selfplay* h, uint64_t* evals) {
+  return guarded([&] {
+    need(h && h->eng && evals, "NULL argument");
+    *evals = h->eng->timedNNEvals();
   });
 }
 

@@ -166,36 +166,32 @@ KC_D void playMoveWave(const DTables& T, DBoard& b, int cell, int dir) {
   }
 }
 
-// Feature bit of V1 plane `plane` at ORIGINAL cell c, for symmetry sym (the bit
-// is stored at symCell[sym][c]).
-KC_D bool v1Bit(const DTables& T, const DBoard& b, int plane, int c, int sym) {
-  int pla = b.pla;
-  switch(plane) {
-    case 0: return true;
-    case 1: return colorAt(b, c) == pla;
-    case 2: return colorAt(b, c) == 3 - pla;
-    case 3: case 4: case 5: case 6:
-      return hCell(b, 0) == c && T.symDir[sym][hDir(b, 0)] == plane - 3;
-    case 7: return hCell(b, 1) == c;
-    case 8: return hCell(b, 2) == c;
-    case 9: return hCell(b, 3) == c;
-    case 10: return hCell(b, 4) == c;
-    case 11: {
-      for(int d = 0; d < 4; d++)
-        if(isLegal(T, b, c, d))
-          return true;
-      return false;
-    }
-    default: {
-      int len = T.W - 1 - (plane - 12);
-      if(len < 1)
-        return false;
-      for(int d = 0; d < 4; d++)
-        if(runAlong(T, b, c, d) == len)
-          return true;
-      return false;
-    }
+// The 15 V1 feature bits of ORIGINAL cell c (bit p = plane p); sd0 is the
+// symmetric direction of the last move (-1 when there is none).
+KC_D uint32_t v1CellFeatures(const DTables& T, const DBoard& b, int c, int sd0) {
+  const int col = colorAt(b, c);
+  uint32_t f = 1u;
+  if(col != 0)
+    f |= col == b.pla ? 2u : 4u;
+  if(hCell(b, 0) == c && sd0 >= 0 && sd0 < 4)
+    f |= 1u << (3 + sd0);
+#pragma unroll
+  for(int k = 1; k < 5; k++)
+    if(hCell(b, k) == c)
+      f |= 1u << (6 + k);
+  bool legal = false, run[3] = {false, false, false};
+  for(int d = 0; d < 4; d++) {
+    legal = legal || isLegal(T, b, c, d);
+    const int n = runAlong(T, b, c, d);
+#pragma unroll
+    for(int j = 0; j < 3; j++)
+      run[j] = run[j] || (n >= 1 && n == T.W - 1 - j);
   }
+  f |= (legal ? 1u : 0u) << 11;
+#pragma unroll
+  for(int j = 0; j < 3; j++)
+    f |= (run[j] ? 1u : 0u) << (12 + j);
+  return f;
 }
 
 // Packs the 15 V1 planes (symmetric frame) into T.inWords words: bit i of the
@@ -212,32 +208,7 @@ KC_D void encodePackedWave(const DTables& T, const DBoard& b, int sym, uint64_t*
   uint64_t word = 0;
   for(int base = 0; base < A; base += 64) {
     const int s = base + lane;
-    uint32_t f = 0;
-    if(s < A) {
-      const int c = T.invSymCell[sym][s];
-      const int col = colorAt(b, c);
-      f = 1u;
-      if(col != 0)
-        f |= col == b.pla ? 2u : 4u;
-      if(h0 == c && sd0 >= 0 && sd0 < 4)
-        f |= 1u << (3 + sd0);
-#pragma unroll
-      for(int k = 1; k < 5; k++)
-        if(hCell(b, k) == c)
-          f |= 1u << (6 + k);
-      bool legal = false, run[3] = {false, false, false};
-      for(int d = 0; d < 4; d++) {
-        legal = legal || isLegal(T, b, c, d);
-        const int n = runAlong(T, b, c, d);
-#pragma unroll
-        for(int j = 0; j < 3; j++)
-          run[j] = run[j] || (n >= 1 && n == T.W - 1 - j);
-      }
-      f |= (legal ? 1u : 0u) << 11;
-#pragma unroll
-      for(int j = 0; j < 3; j++)
-        f |= (run[j] ? 1u : 0u) << (12 + j);
-    }
+    const uint32_t f = s < A ? v1CellFeatures(T, b, T.invSymCell[sym][s], sd0) : 0u;
     // plane p's chunk covers flat bits [p*A + base, p*A + base + 64): OR the part
     // falling into this lane's word [64*lane, 64*lane + 64)
 #pragma unroll
@@ -252,6 +223,28 @@ KC_D void encodePackedWave(const DTables& T, const DBoard& b, int sym, uint64_t*
   }
   if(lane < T.inWords)
     out[lane] = word;
+}
+
+// Training-row bin planes (trainingwrite.cpp:218-232 packBits, identity symmetry):
+// plane p occupies ceil(A/8) bytes, cell 8j+i at bit 7-i of byte j.  Wave-
+// cooperative: lane s computes cell s's features, one ballot per plane and chunk,
+// lanes j < ceil(A/8) store the bytes.  out = the row's NUM_SPATIAL*ceil(A/8) bytes.
+KC_D void packRowBinWave(const DTables& T, const DBoard& b, uint8_t* out) {
+  const int A = T.A, pb = (A + 7) / 8, lane = laneId();
+  const int h0 = hCell(b, 0);
+  const int sd0 = h0 >= 0 ? T.symDir[0][hDir(b, 0)] : -1;
+  const uint32_t f0 = lane < A ? v1CellFeatures(T, b, lane, sd0) : 0u;
+  const uint32_t f1 = 64 + lane < A ? v1CellFeatures(T, b, 64 + lane, sd0) : 0u;
+  const int c0 = 8 * lane;
+#pragma unroll
+  for(int p = 0; p < NUM_SPATIAL; p++) {
+    const uint64_t m0 = ballot((f0 >> p) & 1u), m1 = ballot((f1 >> p) & 1u);
+    if(lane < pb) {
+      const uint64_t m = c0 < 64 ? m0 : m1;
+      const uint32_t bits = (uint32_t)(m >> (c0 & 63)) & 0xFFu;
+      out[p * pb + lane] = (uint8_t)(__builtin_bitreverse32(bits) >> 24);
+    }
+  }
 }
 
 }  // namespace kc

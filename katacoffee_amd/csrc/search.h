@@ -108,6 +108,14 @@ struct TurnRec {
 };
 static_assert(sizeof(TurnRec) == 40, "TurnRec layout");
 
+// A game finished by kCommit whose training rows kRows emits right after it.
+struct FinRec {
+  uint64_t rngSeed, rngCtr;  // history-mask stream state after the game's last move choice
+  uint64_t gameHash0, gameHash1;
+  unsigned long long rowBase;
+  int32_t numMoves, winner, gameNum, pending;  // pending 1: rows reserved at rowBase
+};
+
 struct GameDev {
   DBoard root;
   DBoard leaf;
@@ -157,6 +165,7 @@ struct SearchDev {
   int32_t* nnNeed;       // [G] 1 when the game's row needs the network this round
   int32_t* nnIdx;        // [G] compacted rows to evaluate (kCompact)
   int32_t* nnCount;      // rows in nnIdx
+  unsigned long long* nnTimedEvals;  // summed nnCount of the rounds whose network launch was timed
   // NN evaluation cache (SPEC a7): direct-mapped by state key, written between rounds
   uint32_t cacheMask;    // entries - 1 (0 with cacheOn == 0)
   int32_t cacheOn;
@@ -167,6 +176,7 @@ struct SearchDev {
   float* cStage;         // [G][P+2] a bidding game's payload
   uint64_t* cStageKey;   // [G][2]
   // commit queue
+  FinRec* fin;           // [G] games finished by the current commit (kRows)
   int32_t* commitList;   // [G]
   int32_t* commitCount;
   // rows
@@ -188,10 +198,11 @@ struct SearchDev {
 // Kernel launchers (search.hip).
 void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st);
-void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+// accumulate: add the batch size to *d.nnTimedEvals (rounds whose network launch is timed)
+void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate);
 void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st);
-void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);  // + kRows
 void launchGameTree(const SearchDev* dd, int slot, int maxNodes, uint32_t* nodesOut, uint32_t* edgesOut,
                     int32_t* count, hipStream_t st);
 // Dynamic LDS bytes the commit kernel needs for node_cap `cap`.

@@ -47,8 +47,11 @@ KC_D void waveSync() {
 //  0 select blocks   1 select total   2 loadGame   3 descend   4 path levels
 //  5 selectBest      6 expansion      7 encode
 // 10 backup blocks  11 backup total  12 postprocess+order  13 path backup  14 leaf value
+// 16 commit blocks  17 commit total  18 move choice+targets  19 tree reuse  20 finishGame
+// 21 startGame      22 live nodes kept  23 finished games
+constexpr int SPROF_N = 32;
 constexpr int SPROF_MAXG = 16384;
-__device__ unsigned long long g_searchProf[SPROF_MAXG * 16];
+__device__ unsigned long long g_searchProf[SPROF_MAXG * SPROF_N];
 // NN-cache probe: every evaluated leaf's state key goes into an open-addressing set;
 // a key already present counts as a potential cross-game cache hit (slot 9).
 __device__ unsigned long long* g_probeKeys = nullptr;
@@ -69,13 +72,13 @@ KC_D void probeLeafKey(uint64_t k0, uint64_t k1) {
   }
 }
 KC_D unsigned long long* sprofLds() {
-  __shared__ unsigned long long c[16];
+  __shared__ unsigned long long c[SPROF_N];
   return c;
 }
 #define SPROF_NOW() clock64()
 #define SPROF_INIT()                   \
   do {                                 \
-    if(laneId() < 16)                  \
+    if(laneId() < SPROF_N)             \
       sprofLds()[laneId()] = 0;        \
     __syncthreads();                   \
   } while(0)
@@ -87,8 +90,8 @@ KC_D unsigned long long* sprofLds() {
 #define SPROF_FLUSH()                                                           \
   do {                                                                          \
     __syncthreads();                                                            \
-    if(laneId() < 16 && blockIdx.x < SPROF_MAXG)                                \
-      g_searchProf[blockIdx.x * 16 + laneId()] += sprofLds()[laneId()];         \
+    if(laneId() < SPROF_N && blockIdx.x < SPROF_MAXG)                           \
+      g_searchProf[blockIdx.x * SPROF_N + laneId()] += sprofLds()[laneId()];    \
   } while(0)
 #else
 #define SPROF_NOW() 0ull
@@ -1213,13 +1216,13 @@ extern "C" void coffee_debug_probe_table(void* keys, unsigned long long cap /* p
 }
 
 extern "C" void coffee_debug_search_profile(unsigned long long* out, int reset) {
-  std::vector<unsigned long long> all((size_t)SPROF_MAXG * 16);
+  std::vector<unsigned long long> all((size_t)SPROF_MAXG * SPROF_N);
   KC_HIP(hipDeviceSynchronize());
   KC_HIP(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(g_searchProf), all.size() * 8));
-  for(int i = 0; i < 16; i++)
+  for(int i = 0; i < SPROF_N; i++)
     out[i] = 0;
   for(size_t k = 0; k < all.size(); k++)
-    out[k % 16] += all[k];
+    out[k % SPROF_N] += all[k];
   if(reset) {
     std::fill(all.begin(), all.end(), 0ull);
     KC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_searchProf), all.data(), all.size() * 8));
@@ -1574,12 +1577,22 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
       const int nd = queue[head + v.lane];
       const int kc = v.nodes()[nd].numChildren;
       const Edge* E = v.edges(nd);
-      for(int i = 0; i < kc; i++) {
-        const int c = (int)E[i].child;
-        const uint32_t bit = 1u << (c & 31);
-        uint32_t old = atomicOr(&liveBits[c >> 5], bit);
-        if(!(old & bit))
-          queue[atomicAdd(qtail, 1)] = (uint16_t)c;
+      // four child loads in flight before the LDS atomics that consume them
+      for(int i = 0; i < kc; i += 4) {
+        int ch[4];
+#pragma unroll
+        for(int u = 0; u < 4; u++)
+          ch[u] = i + u < kc ? (int)E[i + u].child : -1;
+#pragma unroll
+        for(int u = 0; u < 4; u++) {
+          const int c = ch[u];
+          if(c < 0)
+            continue;
+          const uint32_t bit = 1u << (c & 31);
+          uint32_t old = atomicOr(&liveBits[c >> 5], bit);
+          if(!(old & bit))
+            queue[atomicAdd(qtail, 1)] = (uint16_t)c;
+        }
       }
     }
     head += cnt;
@@ -1595,21 +1608,58 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
     clearTables(v, s);
     return;
   }
-  // removeSubtreeValueBias for dead table nodes and the promoted child (fixed point: any order)
+  // removeSubtreeValueBias for dead table nodes and the promoted child (fixed point: any order).
+  // The dead allocated nodes are compacted into the queue behind the live ones
+  // (queue[0..liveCount) = live nodes in BFS order; dead <= cap - liveCount), so the
+  // node reads below are independent and batched; lane 0 adds the child.
   const size_t sb = v.svbBase(s.svbSel);
   uint32_t* ab = v.allocBits();
-  for(int i = v.lane; i < cap; i += 64) {
-    bool alloc = (ab[i >> 5] >> (i & 31)) & 1u;
-    bool live = (liveBits[i >> 5] >> (i & 31)) & 1u;
-    if(!alloc || (live && i != child))
-      continue;
-    const Node& n = v.nodes()[i];
-    if(n.svbEntry < 0)
-      continue;
-    atomicAdd((unsigned long long*)&v.d.svbD[sb + n.svbEntry],
-              (unsigned long long)(-svbQ(n.lastSvbDelta * sp.svbFreeProp)));
-    atomicAdd((unsigned long long*)&v.d.svbW[sb + n.svbEntry],
-              (unsigned long long)(-svbQ(n.lastSvbWeight * sp.svbFreeProp)));
+  const int nw = cap / 32;
+  uint16_t* dead = queue + liveCount;
+  int nDead = 0;
+  for(int wb = 0; wb < nw; wb += 64) {
+    const int w = wb + v.lane;
+    uint32_t m = 0;
+    if(w < nw)
+      m = ab[w] & ~liveBits[w];
+    int cnt = __popc(m), incl = cnt;
+#pragma unroll
+    for(int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off, 64);
+      if(v.lane >= off)
+        incl += y;
+    }
+    int o = nDead + incl - cnt;
+    while(m) {
+      const int b = __builtin_ctz(m);
+      m &= m - 1;
+      dead[o++] = (uint16_t)(w * 32 + b);
+    }
+    nDead += __shfl(incl, 63, 64);
+  }
+  waveSync();
+  for(int base = 0; base < nDead + 1; base += 256) {
+    int32_t e[4];
+    float dl[4], wl[4];
+#pragma unroll
+    for(int u = 0; u < 4; u++) {
+      const int i = base + 64 * u + v.lane;  // i == nDead: the promoted child
+      e[u] = -1;
+      dl[u] = wl[u] = 0.0f;
+      if(i <= nDead) {
+        const Node& n = v.nodes()[i < nDead ? (int)dead[i] : child];
+        e[u] = n.svbEntry;
+        dl[u] = n.lastSvbDelta;
+        wl[u] = n.lastSvbWeight;
+      }
+    }
+#pragma unroll
+    for(int u = 0; u < 4; u++) {
+      if(e[u] < 0)
+        continue;
+      atomicAdd((unsigned long long*)&v.d.svbD[sb + e[u]], (unsigned long long)(-svbQ(dl[u] * sp.svbFreeProp)));
+      atomicAdd((unsigned long long*)&v.d.svbW[sb + e[u]], (unsigned long long)(-svbQ(wl[u] * sp.svbFreeProp)));
+    }
   }
   waveSync();
   if(v.lane == 0) {
@@ -1646,21 +1696,21 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
     v.d.svbKey[nb + i] = 0;
   waveSync();
   const int tmask = v.d.ttCap - 1, smask = v.d.svbCap - 1;
-  for(int i = v.lane; i < cap; i += 64) {
-    bool live = (liveBits[i >> 5] >> (i & 31)) & 1u;
-    if(!live)
-      continue;
-    Node* n = &v.nodes()[i];
-    if(i != child && v.d.sp.useGraph) {
-      const uint64_t k0 = v.nodeKey(i)[0], k1 = v.nodeKey(i)[1];
+  // live nodes, in the order of the BFS queue (queue[0..liveCount) holds them all)
+  for(int i = v.lane; i < liveCount; i += 64) {
+    const int ni = queue[i];
+    Node* n = &v.nodes()[ni];
+    const int32_t se = n->svbEntry;
+    if(ni != child && v.d.sp.useGraph) {
+      const uint64_t k0 = v.nodeKey(ni)[0], k1 = v.nodeKey(ni)[1];
       int sl = (int)(k0 & (uint64_t)tmask);
-      while(atomicCAS(&tn[sl], -1, i) != -1)
+      while(atomicCAS(&tn[sl], -1, ni) != -1)
         sl = (sl + 1) & tmask;
       tk[2 * sl] = k0;
       tk[2 * sl + 1] = k1;
     }
-    if(n->svbEntry >= 0) {
-      const size_t oe = sb + n->svbEntry;
+    if(se >= 0) {
+      const size_t oe = sb + se;
       const uint64_t key = v.d.svbKey[oe];
       int sl = (int)(key & (uint64_t)smask);
       while(true) {
@@ -1694,33 +1744,14 @@ KC_D void startGame(const GV& v, GameDev& s) {
   s.leafKind = LEAF_NONE;
 }
 
-// oracle finishGame (play.cpp:1431-1460 + trainingwrite.cpp:316-565, 774-890).
-// boards: LDS [numMoves+1] DBoard; f32 scratch [2*(MAX_AREA+1)].
-KC_D void finishGame(const GV& v, GameDev& s, DRng& rng, DBoard* boards, float* tw) {
-  const DTables& T = v.T;
+// oracle finishGame (play.cpp:1431-1460 + trainingwrite.cpp:316-565, 774-890), commit
+// part: the SGF move record, the row reservation and the FinRec kRows reads.  The
+// turn records and per-turn policies stay in place until the game's next commit,
+// so kRows (launched right after this kernel) reads them there.
+KC_D void finishGameRecord(const GV& v, const GameDev& s, const DRng& rng) {
   const SearchDev& d = v.d;
   const int numMoves = s.numTurns;
-  const int A = T.A, P = T.P, pb = (A + 7) / 8;
   const TurnRec* tr = v.turns();
-  const float finalWin = s.root.winner == 2 ? 1.0f : (s.root.winner == 1 ? 0.0f : 0.5f);
-  float* tWin = tw;
-  float* tLoss = tw + (MAX_AREA + 1);
-  for(int t = v.lane; t < numMoves; t += 64) {
-    tWin[t] = tr[t].whiteWin;
-    tLoss[t] = tr[t].whiteLoss;
-  }
-  if(v.lane == 0) {
-    tWin[numMoves] = finalWin;
-    tLoss[numMoves] = 1.0f - finalWin;
-    DBoard b;
-    boardInit(T, b);
-    boards[0] = b;
-    for(int t = 0; t < numMoves; t++) {
-      applyMove(T, b, tr[t].cell, tr[t].dir);
-      boards[t + 1] = b;
-    }
-  }
-  waveSync();
   {
     // the game's move record (SGF)
     unsigned long long gi = 0;
@@ -1746,60 +1777,107 @@ KC_D void finishGame(const GV& v, GameDev& s, DRng& rng, DBoard* boards, float* 
       }
     }
   }
-  const DBoard& fin = boards[numMoves];
-  unsigned long long base = 0;
-  bool fits = true;
   if(v.lane == 0) {
-    base = atomicAdd(d.rCount, (unsigned long long)numMoves);
+    unsigned long long base = atomicAdd(d.rCount, (unsigned long long)numMoves);
+    bool fits = true;
     if(base + (unsigned long long)numMoves > (unsigned long long)d.rowCap) {
       atomicAdd(d.rCount, (unsigned long long)(-(long long)numMoves));
       atomicAdd(d.rDropped, (unsigned long long)numMoves);
       fits = false;
     }
+    FinRec* f = d.fin + v.g;
+    f->rngSeed = rng.seed;
+    f->rngCtr = rng.ctr;
+    f->gameHash0 = s.gameHash0;
+    f->gameHash1 = s.gameHash1;
+    f->rowBase = base;
+    f->numMoves = numMoves;
+    f->winner = s.root.winner;
+    f->gameNum = s.gameNum;
+    f->pending = fits ? 1 : 0;
   }
-  fits = __shfl((int)fits, 0, 64) != 0;
-  base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(base >> 32), 0, 64) << 32) |
-         (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
+}
+
+// kRows: the training rows of the games the preceding kCommit finished
+// (trainingwrite.cpp:316-565 addRow via writeGame :774-890).  One 256-thread block
+// per committed game; the boards after every move and the final board's per-cell
+// max runs are built once in LDS, then wave w writes rows t = w, w + 4, ...
+constexpr int ROWS_WAVES = 4;
+__global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __restrict__ dp,
+                                                         const DTables* __restrict__ Tp) {
+  const SearchDev& d = *dp;
+  if((int)blockIdx.x >= *d.commitCount)
+    return;
+  const int g = d.commitList[blockIdx.x];
+  FinRec* fp = d.fin + g;
+  if(fp->pending != 1)
+    return;
+  const FinRec f = *fp;
+  const DTables& T = *Tp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  GV v(d, T, g);
+  __shared__ DBoard boards[MAX_AREA + 1];
+  __shared__ float tWin[MAX_AREA + 1], tLoss[MAX_AREA + 1];
+  __shared__ int8_t finRun[MAX_AREA];
+  __shared__ uint8_t hMask[MAX_AREA];
+  const int numMoves = f.numMoves;
+  const int A = T.A, P = T.P, pb = (A + 7) / 8;
+  const TurnRec* tr = v.turns();
+  const float finalWin = f.winner == 2 ? 1.0f : (f.winner == 1 ? 0.0f : 0.5f);
+  for(int t = threadIdx.x; t < numMoves; t += 64 * ROWS_WAVES) {
+    tWin[t] = tr[t].whiteWin;
+    tLoss[t] = tr[t].whiteLoss;
+  }
+  if(threadIdx.x == 0) {
+    tWin[numMoves] = finalWin;
+    tLoss[numMoves] = 1.0f - finalWin;
+    DBoard b;
+    boardInit(T, b);
+    boards[0] = b;
+    for(int t = 0; t < numMoves; t++) {
+      applyMove(T, b, tr[t].cell, tr[t].dir);
+      boards[t + 1] = b;
+    }
+    // history-mask draws, in row order from the game's stream (the chain stops
+    // drawing at its first failure, so the draws are consumed sequentially)
+    DRng rng{f.rngSeed, f.rngCtr};
+    for(int t = 0; t < numMoves; t++) {
+      bool h = true;
+      uint32_t hm = 0;
+      for(int i = 0; i < 5; i++) {
+        h = h && rng.uni() < 0.98f;
+        hm |= (h ? 1u : 0u) << i;
+      }
+      hMask[t] = (uint8_t)hm;
+    }
+  }
+  __syncthreads();
+  const DBoard& fin = boards[numMoves];
+  for(int c = threadIdx.x; c < A; c += 64 * ROWS_WAVES)
+    finRun[c] = colorAt(fin, c) == 0 ? 0 : (int8_t)maxRun(T, fin, c);
+  __syncthreads();
   const float nowF1 = 1.0f / (1.0f + (float)A * 0.176f), nowF2 = 1.0f / (1.0f + (float)A * 0.056f),
               nowF3 = 1.0f / (1.0f + (float)A * 0.016f);
-  for(int t = 0; t < numMoves; t++) {
-    // history-mask draws (uniform; consumed even when the row is dropped)
-    bool h = true;
-    uint32_t hm = 0;
-#pragma unroll
-    for(int i = 0; i < 5; i++) {
-      h = h && rng.uni() < 0.98f;
-      hm |= (h ? 1u : 0u) << i;
-    }
-    if(!fits)
-      continue;
-    const size_t r = (size_t)base + t;
+  for(int t = wave; t < numMoves; t += ROWS_WAVES) {
+    const uint32_t hm = hMask[t];
+    const size_t r = (size_t)f.rowBase + t;
     const DBoard& b = boards[t];
     const int pla = b.pla, opp = 3 - pla;
-    for(int idx = v.lane; idx < NUM_SPATIAL * pb; idx += 64) {
-      const int plane = idx / pb, byte = idx % pb;
-      uint32_t bits = 0;
-      for(int bit = 0; bit < 8; bit++) {
-        int cell = byte * 8 + bit;
-        if(cell < A && v1Bit(T, b, plane, cell, 0))
-          bits |= 1u << (7 - bit);
-      }
-      d.rBin[r * NUM_SPATIAL * pb + idx] = (uint8_t)bits;
-    }
-    if(v.lane == 0)
+    packRowBinWave(T, b, d.rBin + r * NUM_SPATIAL * pb);
+    if(lane == 0)
       d.rGlob[r] = (float)T.W;
     const int16_t* p0 = v.turnPol(t);
     const int16_t* p1 = t + 1 < numMoves ? v.turnPol(t + 1) : nullptr;
     int16_t* pol = d.rPol + r * 2 * P;
-    for(int p = v.lane; p < P; p += 64) {
+    for(int p = lane; p < P; p += 64) {
       pol[p] = p0[p];
       pol[P + p] = p1 ? p1[p] : (int16_t)1;
     }
     float gval = 0.0f;
-    const int li = v.lane;
+    const int li = lane;
     if(li < 10) {
-      const int f = li >> 1;
-      const float nf = f == 0 ? 0.0f : (f == 1 ? nowF1 : (f == 2 ? nowF2 : (f == 3 ? nowF3 : 1.0f)));
+      const int fi = li >> 1;
+      const float nf = fi == 0 ? 0.0f : (fi == 1 ? nowF1 : (fi == 2 ? nowF2 : (fi == 3 ? nowF3 : 1.0f)));
       float win = 0.0f, loss = 0.0f, left = 1.0f;
       for(int i = t; i <= numMoves; i++) {
         float now;
@@ -1835,17 +1913,17 @@ KC_D void finishGame(const GV& v, GameDev& s, DRng& rng, DBoard* boards, float* 
     } else if(li >= 36 && li <= 40) {
       gval = ((hm >> (li - 36)) & 1u) ? 1.0f : 0.0f;
     } else if(li == 41) {
-      gval = (float)(s.gameHash0 & 0x3FFFFF);
+      gval = (float)(f.gameHash0 & 0x3FFFFF);
     } else if(li == 42) {
-      gval = (float)((s.gameHash0 >> 22) & 0x3FFFFF);
+      gval = (float)((f.gameHash0 >> 22) & 0x3FFFFF);
     } else if(li == 43) {
-      gval = (float)((s.gameHash0 >> 44) & 0xFFFFF);
+      gval = (float)((f.gameHash0 >> 44) & 0xFFFFF);
     } else if(li == 44) {
-      gval = (float)(s.gameHash1 & 0x3FFFFF);
+      gval = (float)(f.gameHash1 & 0x3FFFFF);
     } else if(li == 45) {
-      gval = (float)((s.gameHash1 >> 22) & 0x3FFFFF);
+      gval = (float)((f.gameHash1 >> 22) & 0x3FFFFF);
     } else if(li == 46) {
-      gval = (float)((s.gameHash1 >> 44) & 0xFFFFF);
+      gval = (float)((f.gameHash1 >> 44) & 0xFFFFF);
     } else if(li == 51) {
       gval = (float)t;
     } else if(li == 57) {
@@ -1859,19 +1937,22 @@ KC_D void finishGame(const GV& v, GameDev& s, DRng& rng, DBoard* boards, float* 
     int8_t* vt = d.rVal + r * 5 * A;
     const DBoard& b2 = boards[min(t + 2, numMoves)];
     const DBoard& b3 = boards[min(t + 6, numMoves)];
-    for(int c = v.lane; c < A; c += 64) {
+    for(int c = lane; c < A; c += 64) {
       int fc = colorAt(fin, c), c2 = colorAt(b2, c), c3 = colorAt(b3, c);
       vt[c] = fc == pla ? 1 : (fc == opp ? -1 : 0);
       vt[A + c] = 0;
       vt[2 * A + c] = c2 == pla ? 1 : (c2 == opp ? -1 : 0);
       vt[3 * A + c] = c3 == pla ? 1 : (c3 == opp ? -1 : 0);
-      vt[4 * A + c] = fc == 0 ? 0 : (int8_t)maxRun(T, fin, c);
+      vt[4 * A + c] = finRun[c];
     }
-    if(v.lane < 4) {
-      int m = v.lane == 0 ? d.slotBase + v.g : (v.lane == 1 ? s.gameNum : (v.lane == 2 ? t : numMoves));
-      d.rMeta[r * 4 + v.lane] = m;
+    if(lane < 4) {
+      int m = lane == 0 ? d.slotBase + g : (lane == 1 ? f.gameNum : (lane == 2 ? t : numMoves));
+      d.rMeta[r * 4 + lane] = m;
     }
   }
+  __syncthreads();
+  if(threadIdx.x == 0)
+    fp->pending = 0;
 }
 
 // oracle commitMove (getChosenMoveLoc searchresults.cpp:435-453, extract*Targets
@@ -1887,13 +1968,13 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   float* vals = reinterpret_cast<float*>(posv + MAX_P);       // [MAX_P]
   float* tmp = vals + MAX_P;                                  // [MAX_P]
   float* tmp2 = tmp + MAX_P;                                  // [MAX_P]
-  float* tw = tmp2 + MAX_P;                                   // [2*(MAX_AREA+1)]
-  int* qtail = reinterpret_cast<int*>(tw + 2 * (MAX_AREA + 1));
-  DBoard* boards = reinterpret_cast<DBoard*>(qtail + 4);      // [MAX_AREA+1]
-  uint32_t* liveBits = reinterpret_cast<uint32_t*>(boards + (MAX_AREA + 1));  // [cap/32]
+  int* qtail = reinterpret_cast<int*>(tmp2 + MAX_P);
+  uint32_t* liveBits = reinterpret_cast<uint32_t*>(qtail + 4);  // [cap/32]
   uint16_t* queue = reinterpret_cast<uint16_t*>(liveBits + d.cap / 32);     // [cap]
   GV v(d, *Tp, g);
   __shared__ GameDev s;
+  SPROF_INIT();
+  [[maybe_unused]] const unsigned long long t0 = SPROF_NOW();
   loadGame(v, s);
   const SP& sp = d.sp;
   const int P = d.P, A = d.A;
@@ -1981,15 +2062,25 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   if(v.lane == 0)
     v.turns()[t] = rec;
   s.numTurns++;
+  [[maybe_unused]] const unsigned long long t1 = SPROF_NOW();
   reuseTree(v, s, chosen, liveBits, queue, qtail);
+  [[maybe_unused]] const unsigned long long t2 = SPROF_NOW();
+  SPROF_ADD(18, t1 - t0);
+  SPROF_ADD(19, t2 - t1);
+  SPROF_ADD(22, s.liveCount);
   playMoveWave(v.T, s.root, chosen % A, chosen / A);
   s.moves++;
   waveSync();
   if(s.root.finished) {
-    finishGame(v, s, rng, boards, tw);
+    [[maybe_unused]] const unsigned long long t3 = SPROF_NOW();
+    finishGameRecord(v, s, rng);
+    [[maybe_unused]] const unsigned long long t4 = SPROF_NOW();
     s.gamesFinished++;
     s.gameNum++;
     startGame(v, s);
+    SPROF_ADD(20, t4 - t3);
+    SPROF_ADD(21, SPROF_NOW() - t4);
+    SPROF_ADD(23, 1);
   } else {
     s.rngCtr = rng.ctr;
     s.phase = PH_ROOTEVAL;
@@ -1997,6 +2088,9 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   }
   waveSync();
   storeGame(v, s);
+  SPROF_ADD(16, 1);
+  SPROF_ADD(17, SPROF_NOW() - t0);
+  SPROF_FLUSH();
 }
 
 // kCacheWrite: the winning bidder of every cache slot stores its evaluation (runs
@@ -2030,7 +2124,8 @@ __global__ void __launch_bounds__(64) kCacheWrite(const SearchDev* __restrict__ 
 }
 
 // kCompact: ascending list of the games whose row needs the network this round.
-__global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp) {
+// accumulate != 0: the count is also added to *d.nnTimedEvals (sampled kernel timing).
+__global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
   __shared__ int part[1024];
   const int t = threadIdx.x, per = (d.G + 1023) / 1024;
@@ -2050,8 +2145,11 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
   for(int i = lo; i < hi; i++)
     if(d.nnNeed[i])
       d.nnIdx[o++] = i;
-  if(t == 1023)
+  if(t == 1023) {
     *d.nnCount = part[1023];
+    if(accumulate)
+      *d.nnTimedEvals += (unsigned long long)part[1023];
+  }
 }
 
 __global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
@@ -2159,9 +2257,9 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
   KC_HIP(hipGetLastError());
 }
 
-void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate) {
   (void)d;
-  hipLaunchKernelGGL(kCompact, dim3(1), dim3(1024), 0, st, dd);
+  hipLaunchKernelGGL(kCompact, dim3(1), dim3(1024), 0, st, dd, accumulate ? 1 : 0);
   KC_HIP(hipGetLastError());
 }
 
@@ -2191,8 +2289,7 @@ void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
 }
 
 size_t commitLdsBytes(int cap) {
-  size_t b = (size_t)MAX_P * 4 * 4 + 2 * (MAX_AREA + 1) * 4 + 16;
-  b += sizeof(DBoard) * (MAX_AREA + 1);
+  size_t b = (size_t)MAX_P * 4 * 4 + 16;
   b += (size_t)(cap / 32) * 4 + (size_t)cap * 2;
   return (b + 15) / 16 * 16;
 }
@@ -2204,6 +2301,8 @@ void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
     case 4: hipLaunchKernelGGL(kCommit<4>, dim3(d.G), dim3(64), lds, st, dd, d.T); break;
     default: hipLaunchKernelGGL(kCommit<7>, dim3(d.G), dim3(64), lds, st, dd, d.T); break;
   }
+  KC_HIP(hipGetLastError());
+  hipLaunchKernelGGL(kRows, dim3(d.G), dim3(64 * ROWS_WAVES), 0, st, dd, d.T);
   KC_HIP(hipGetLastError());
 }
 

@@ -126,7 +126,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.turnPol = devAlloc<int16_t>(owned_, (size_t)G * d.maxTurns * P);
   d.nnIn = devAlloc<uint64_t>(owned_, (size_t)G * ht.inWords);
   d.nnOut = devAlloc<float>(owned_, (size_t)G * (P + 4));
+  d.fin = devAlloc<FinRec>(owned_, G);
   d.commitList = devAlloc<int32_t>(owned_, G);
+  d.nnTimedEvals = devAlloc<unsigned long long>(owned_, 1);
   d.commitCount = devAlloc<int32_t>(owned_, 1);
   const int pb = (A + 7) / 8;
   d.rBin = devAlloc<uint8_t>(owned_, (size_t)rowCap * NUM_SPATIAL * pb, false);
@@ -196,8 +198,8 @@ hipEvent_t SelfplayEngine::takeEvent() {
   return e;
 }
 
-void SelfplayEngine::timed(int which, hipStream_t st, const std::function<void()>& f) {
-  if(!timing_) {
+void SelfplayEngine::timed(int which, hipStream_t st, const std::function<void()>& f, bool on) {
+  if(!on) {
     f();
     return;
   }
@@ -226,23 +228,25 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
     st = stream_;
   const SearchDev& d = hd_;
   for(int r = 0; r < rounds; r++) {
+    const bool t0 = sampleNow(0), t1 = sampleNow(1), t2 = sampleNow(2);
     timed(0, st, [&] {
       launchSelect(d, dd_, st);
-      launchCompact(d, dd_, st);
-    });
+      launchCompact(d, dd_, st, t1);
+    }, t0);
     timed(1, st, [&] {
       if(nn_)
         nn_->forward(d.G, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
       else
         launchFakeNet(T_, d.G, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
-    });
+    }, t1);
     timed(2, st, [&] {
       launchBackup(d, dd_, st);
       launchCacheWrite(d, dd_, st);
-    });
+    }, t2);
     rounds_++;
     if(rounds_ % (uint64_t)commitInterval_ == 0 || r == rounds - 1) {
-      timed(3, st, [&] { launchCommit(d, dd_, st); });
+      const bool t3 = sampleNow(3);
+      timed(3, st, [&] { launchCommit(d, dd_, st); }, t3);
       KC_HIP(hipMemsetAsync(d.commitCount, 0, sizeof(int32_t), st));
     }
   }
@@ -402,6 +406,13 @@ void SelfplayEngine::rootPolicy(int slot, float* out) {
     throw std::invalid_argument("slot out of range");
   sync();
   KC_HIP(hipMemcpy(out, hd_.rootNoised + (size_t)slot * hd_.P, sizeof(float) * hd_.P, hipMemcpyDeviceToHost));
+}
+
+uint64_t SelfplayEngine::timedNNEvals() {
+  sync();
+  unsigned long long v = 0;
+  KC_HIP(hipMemcpy(&v, hd_.nnTimedEvals, 8, hipMemcpyDeviceToHost));
+  return v;
 }
 
 void SelfplayEngine::kernelTime(int which, double& ms, uint64_t& launches) {

@@ -26,8 +26,12 @@ class SelfplayEngine {
   void gameInfo(int slot, int64_t* info);
   int gameTree(int slot, int maxNodes, uint32_t* nodes, uint32_t* edges);
   void rootPolicy(int slot, float* out);
-  void setTiming(bool on) { timing_ = on; }
+  // every = 0: off; N: time every N-th launch of each kernel group (HIP events;
+  // each event pair costs a few microseconds of stream gap, so sampling keeps
+  // the timed run representative)
+  void setTiming(int every) { timingEvery_ = every > 0 ? every : 0; }
   void kernelTime(int which, double& ms, uint64_t& launches);
+  uint64_t timedNNEvals();
   const SearchDev& dev() const { return hd_; }
 
  private:
@@ -35,7 +39,8 @@ class SelfplayEngine {
     int which;
     hipEvent_t a, b;
   };
-  void timed(int which, hipStream_t st, const std::function<void()>& f);
+  void timed(int which, hipStream_t st, const std::function<void()>& f, bool on);
+  bool sampleNow(int which) { return timingEvery_ > 0 && groupLaunches_[which]++ % (uint64_t)timingEvery_ == 0; }
   hipEvent_t takeEvent();
   void resolveTiming();
   std::vector<PendingTiming> pending_;
@@ -50,7 +55,8 @@ class SelfplayEngine {
   int xLen_ = 0, yLen_ = 0, winLen_ = 0;
   uint64_t rounds_ = 0;
   uint64_t rowsDrained_ = 0;
-  bool timing_ = false;
+  int timingEvery_ = 0;
+  uint64_t groupLaunches_[4] = {0, 0, 0, 0};
   double kernelMs_[4] = {0, 0, 0, 0};
   uint64_t kernelLaunches_[4] = {0, 0, 0, 0};
 };

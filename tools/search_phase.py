@@ -23,7 +23,7 @@ def main():
     a = ap.parse_args()
     import katacoffee_amd as kc
     L = kc.lib()
-    prof = (ctypes.c_ulonglong * 16)()
+    prof = (ctypes.c_ulonglong * 32)()
     path = os.path.join(tempfile.mkdtemp(), "m.cfnn")
     kc.write_random_model("b6c96", 0xC0FFEE, path)
     sp = kc.Selfplay(5, 5, 4, num_games=a.games, max_visits=a.visits, seed=1, model_path=path, commit_interval=8,
@@ -51,6 +51,13 @@ def main():
     print("backup: %d blocks" % p[10])
     for name, i in [("total", 11), ("post+order", 12), ("leaf value", 14), ("path backup", 13)]:
         print("  %-14s %8.0f cycles/block" % (name, p[i] / nk))
+    nc = max(p[16], 1)
+    print("commit: %d blocks, %d finished games, %.0f live nodes kept per move" % (p[16], p[23], p[22] / nc))
+    for name, i in [("total", 17), ("choice+targets", 18), ("tree reuse", 19)]:
+        print("  %-14s %8.0f cycles/block" % (name, p[i] / nc))
+    nf = max(p[23], 1)
+    for name, i in [("finishGame", 20), ("startGame", 21)]:
+        print("  %-14s %8.0f cycles/finished game" % (name, p[i] / nf))
 
 
 if __name__ == "__main__":
