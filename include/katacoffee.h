@@ -126,6 +126,19 @@ typedef struct coffee_search_params {
   float lcb_stdevs, min_visit_prop_for_lcb;
   float subtree_value_bias_factor, subtree_value_bias_weight_exponent, subtree_value_bias_free_prop;
   int32_t use_graph_search;
+  /* PlaySettings (playsettings.cpp): per-move search limits (getSearchLimitsThisMove
+   * play.cpp:871-1004) and row weighting (play.cpp:1470-1697).  Defaults are the
+   * benchmark mode of SURVEY 8d (all off); selfplay1.cfg values in comments. */
+  float cheap_search_prob;           /* 0.75 */
+  int32_t cheap_search_visits;       /* 100 */
+  float cheap_search_target_weight;  /* 0.0 */
+  int32_t reduce_visits;             /* 1 */
+  float reduce_visits_threshold;     /* 0.9 */
+  int32_t reduce_visits_threshold_lookback; /* 3 */
+  int32_t reduced_visits_min;        /* 100 */
+  float reduced_visits_weight;       /* 0.1 */
+  float policy_surprise_data_weight; /* 0.5 */
+  float value_surprise_data_weight;  /* 0.1 */
 } coffee_search_params;
 
 void coffee_search_params_default(coffee_search_params* p);

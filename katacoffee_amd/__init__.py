@@ -58,6 +58,11 @@ class SearchParams(ctypes.Structure):
         ("subtree_value_bias_factor", ctypes.c_float), ("subtree_value_bias_weight_exponent", ctypes.c_float),
         ("subtree_value_bias_free_prop", ctypes.c_float),
         ("use_graph_search", ctypes.c_int32),
+        ("cheap_search_prob", ctypes.c_float), ("cheap_search_visits", ctypes.c_int32),
+        ("cheap_search_target_weight", ctypes.c_float), ("reduce_visits", ctypes.c_int32),
+        ("reduce_visits_threshold", ctypes.c_float), ("reduce_visits_threshold_lookback", ctypes.c_int32),
+        ("reduced_visits_min", ctypes.c_int32), ("reduced_visits_weight", ctypes.c_float),
+        ("policy_surprise_data_weight", ctypes.c_float), ("value_surprise_data_weight", ctypes.c_float),
     ]
 
 

@@ -83,7 +83,7 @@ static void checkGeom(int x, int y, int w) {
 extern "C" {
 
 const char* coffee_last_error(void) { return gLastError.c_str(); }
-int coffee_abi_version(void) { return 101; }
+int coffee_abi_version(void) { return 102; }
 
 int coffee_device_count(int* count) {
   return guarded([&] {
@@ -249,6 +249,17 @@ void coffee_search_params_default(coffee_search_params* p) {
   p->subtree_value_bias_weight_exponent = 0.8f;
   p->subtree_value_bias_free_prop = 0.8f;
   p->use_graph_search = 1;
+  // play settings: benchmark mode (one row per move at full visits)
+  p->cheap_search_prob = 0.0f;
+  p->cheap_search_visits = 100;
+  p->cheap_search_target_weight = 0.0f;
+  p->reduce_visits = 0;
+  p->reduce_visits_threshold = 0.9f;
+  p->reduce_visits_threshold_lookback = 3;
+  p->reduced_visits_min = 100;
+  p->reduced_visits_weight = 0.1f;
+  p->policy_surprise_data_weight = 0.0f;
+  p->value_surprise_data_weight = 0.0f;
 }
 
 struct coffee_selfplay {

@@ -245,6 +245,17 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   getf("subtreeValueBiasWeightExponent", p.subtree_value_bias_weight_exponent);
   getf("subtreeValueBiasFreeProp", p.subtree_value_bias_free_prop);
   getb("useGraphSearch", p.use_graph_search);
+  // PlaySettings (playsettings.cpp:80-99)
+  getf("cheapSearchProb", p.cheap_search_prob);
+  geti("cheapSearchVisits", p.cheap_search_visits);
+  getf("cheapSearchTargetWeight", p.cheap_search_target_weight);
+  getb("reduceVisits", p.reduce_visits);
+  getf("reduceVisitsThreshold", p.reduce_visits_threshold);
+  geti("reduceVisitsThresholdLookback", p.reduce_visits_threshold_lookback);
+  geti("reducedVisitsMin", p.reduced_visits_min);
+  getf("reducedVisitsWeight", p.reduced_visits_weight);
+  getf("policySurpriseDataWeight", p.policy_surprise_data_weight);
+  getf("valueSurpriseDataWeight", p.value_surprise_data_weight);
 }
 
 struct RowSink {

@@ -60,7 +60,30 @@ struct SP {
   float lcbStdevs, minVisitPropLcb;
   float svbFactor, svbExp, svbFreeProp;
   int useGraph;
+  // PlaySettings per-move limits and row weighting (play.cpp:871-1004, :1470-1697)
+  float cheapProb;
+  int cheapVisits;
+  float cheapWeight;
+  int reduceVisits;
+  float reduceThreshold;
+  int reduceLookback, reducedMin;
+  float reducedWeight;
+  float policySurpriseWeight, valueSurpriseWeight;
 };
+
+// The parameters of a cheap search whose rows are not recorded (runBotWithLimits
+// removeRootNoise, play.cpp:1024-1037).
+inline SP cheapSearchSP(const SP& p) {
+  SP c = p;
+  c.rootNoise = 0;
+  c.rootTemp = 1.0f;
+  c.rootTempEarly = 1.0f;
+  c.rootFpuLossProp = p.fpuLossProp;
+  c.rootFpuRedMax = p.fpuRedMax;
+  c.rootDesiredCoeff = 0.0f;
+  c.rootSyms = 1;
+  return c;
+}
 
 struct Node {
   uint32_t visits;
@@ -103,10 +126,14 @@ struct TurnRec {
   float whiteWin, whiteLoss, rawWhiteWL, rawPolicyEntropy;
   float policySurprise, policyEntropy, searchEntropy;
   uint32_t visits;
+  float rootWL;                // getRootValues winLossValue (reduceVisits history)
+  float rootNNWin, rootNNLoss; // getRootRawNNValues (value surprise)
+  float targetWeight;          // limits.targetWeight, surprise-weighted at the game's end
   int8_t cell, dir;
-  int8_t pad[6];
+  uint8_t rows;                // resolved integer weight: copies of this turn's row
+  int8_t pad[5];
 };
-static_assert(sizeof(TurnRec) == 40, "TurnRec layout");
+static_assert(sizeof(TurnRec) == 56, "TurnRec layout");
 
 // A game finished by kCommit whose training rows kRows emits right after it.
 struct FinRec {
@@ -114,6 +141,7 @@ struct FinRec {
   uint64_t gameHash0, gameHash1;
   unsigned long long rowBase;
   int32_t numMoves, winner, gameNum, pending;  // pending 1: rows reserved at rowBase
+  int32_t numRows, pad;
 };
 
 struct GameDev {
@@ -126,7 +154,9 @@ struct GameDev {
   uint32_t syms;                  // four root symmetries, 4 bits each
   int32_t cSlot;                  // NN-cache slot of the leaf (hit or bid)
   int32_t cBid;                   // 1: this round's evaluation bids for cSlot
-  int32_t pad2;
+  int32_t noNoise;                // this move is a cheap search without recorded rows
+  int32_t visitLimit;             // this move's maxVisits (getSearchLimitsThisMove)
+  float moveWeight;               // this move's target weight
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
@@ -136,6 +166,7 @@ struct GameDev {
 struct SearchDev {
   const DTables* T;
   SP sp;
+  SP spCheap;            // cheapSearchSP(sp): parameters of games with noNoise set
   int G, cap, ttCap, svbCap, P, A, inWords, maxTurns;
   int rowCap, slotBase;
   uint64_t seed;

@@ -111,9 +111,10 @@ struct GV {
   const SearchDev& d;
   const DTables& T;
   int g, lane;
-  KC_D GV(const SearchDev& d_, int g_) : d(d_), T(*d_.T), g(g_), lane(laneId()) {}
+  const SP* sp;  // this move's search parameters (moveParams after loadGame)
+  KC_D GV(const SearchDev& d_, int g_) : d(d_), T(*d_.T), g(g_), lane(laneId()), sp(&d_.sp) {}
   // tables through a readonly noalias kernel argument: uniform reads become scalar loads
-  KC_D GV(const SearchDev& d_, const DTables& t_, int g_) : d(d_), T(t_), g(g_), lane(laneId()) {}
+  KC_D GV(const SearchDev& d_, const DTables& t_, int g_) : d(d_), T(t_), g(g_), lane(laneId()), sp(&d_.sp) {}
   KC_D Node* nodes() const { return d.nodes + (size_t)g * d.cap; }
   KC_D Edge* edges(int n) const { return d.edges + ((size_t)g * d.cap + n) * d.P; }
   KC_D OrderEnt* order(int n) const { return d.order + ((size_t)g * d.cap + n) * d.P; }
@@ -146,12 +147,15 @@ KC_D void storeGame(const GV& v, const GameDev& s) {
     dst[i] = src[i];
 }
 
-KC_D void loadGame(const GV& v, GameDev& s) {
+KC_D void loadGame(GV& v, GameDev& s) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&v.d.games[v.g]);
   uint32_t* dst = reinterpret_cast<uint32_t*>(&s);
   for(int i = v.lane; i < (int)(sizeof(GameDev) / 4); i += 64)
     dst[i] = src[i];
   waveSync();
+  // a cheap search without recorded rows runs without root noise and root-specific
+  // settings (runBotWithLimits play.cpp:1024-1037); the flag is uniform
+  v.sp = __builtin_amdgcn_readfirstlane(s.noNoise) ? &v.d.spCheap : &v.d.sp;
 }
 
 template <int NI>
@@ -291,7 +295,7 @@ KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k
 // ---------------------------------------------------------------------------
 // oracle addLeafValue (searchupdatehelpers.cpp:12-82)
 KC_D void addLeafValue(const GV& v, const GameDev& s, int ni, float wl, bool isTerminal, bool assumeNoExisting) {
-  const SP& sp = v.d.sp;
+  const SP& sp = *v.sp;
   Node* np = &v.nodes()[ni];
   const int svbEntry = np->svbEntry;
   uint32_t visits = np->visits;
@@ -349,7 +353,7 @@ KC_D float cdfT(const DTables& T, float z) {
 // downweightBadChildrenAndNormalizeWeight :330-419)
 template <int NI>
 KC_D void recompute(const GV& v, const GameDev& s, int ni, int numVisitsToAdd, bool isRoot) {
-  const SP& sp = v.d.sp;
+  const SP& sp = *v.sp;
   Node* np = &v.nodes()[ni];
   const int k = np->numChildren;
   const int nextPla = np->nextPla;
@@ -513,7 +517,7 @@ KC_D float exploreScaling(const SP& sp, float totalChildWeight) {
 template <int NI>
 KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool isRoot, int& newPos,
                     uint32_t* hasBits, const Edge& e0) {
-  const SP& sp = v.d.sp;
+  const SP& sp = *v.sp;
   const int P = v.d.P;
   const int k = n.numChildren;
   const int pla = n.nextPla;
@@ -613,7 +617,7 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
 // maybeCatchUpEdgeVisits :1169-1207)
 template <int NI>
 KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
-  const SP& sp = v.d.sp;
+  const SP& sp = *v.sp;
   const DTables& T = v.T;
   s.pathLen = 0;
   DBoard b = s.root;
@@ -906,7 +910,7 @@ KC_D float seqSum(float* lds, int n, int lane) {
 
 // oracle noiseAndTemp (maybeAddPolicyNoiseAndTemp searchhelpers.cpp:122-222)
 KC_D void noiseAndTemp(const GV& v, GameDev& s, DRng& rng, const float* raw, float* out, float* scratch) {
-  const SP& sp = v.d.sp;
+  const SP& sp = *v.sp;
   const int P = v.d.P;
   for(int pos = v.lane; pos < P; pos += 64)
     out[pos] = raw[pos];
@@ -1050,7 +1054,7 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
   (void)tPost;
   (void)tLeaf;
   (void)tPath;
-  const SP& sp = d.sp;
+  const SP& sp = *v.sp;
   const int P = d.P;
   const float* o = d.nnOut + (size_t)s.nnSlot * (P + 4);
   bool needCommit = false;
@@ -1104,7 +1108,7 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
       noiseAndTemp(v, s, rng, rp, v.rootNoised(), scratch);
       s.rngCtr = rng.ctr;
       s.phase = PH_SEARCH;
-      needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)sp.maxVisits;
+      needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)s.visitLimit;
     }
   } else {
     if(s.leafKind == LEAF_NN || s.leafKind == LEAF_CACHED) {
@@ -1185,7 +1189,7 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
     }
     tPath = SPROF_NOW() - tp0;
     s.playouts++;
-    needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)sp.maxVisits;
+    needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)s.visitLimit;
   }
   if(needCommit) {
     s.phase = PH_COMMIT;
@@ -1260,9 +1264,8 @@ KC_D void lcbAndRadius(const SP& sp, int pla, uint32_t cVisits, float cWs, float
 // oracle playSelectionValues (getPlaySelectionValues searchresults.cpp:63-309).
 // posOut/vals are LDS arrays [P]; returns the count (uniform).
 template <int NI>
-KC_D int playSelectionValues(const GV& v, const GameDev& s, float scaleMaxToAtLeast, bool allowDirect, int* posOut,
-                             float* vals) {
-  const SP& sp = v.d.sp;
+KC_D int playSelectionValues(const GV& v, const SP& sp, const GameDev& s, float scaleMaxToAtLeast, bool allowDirect,
+                             int* posOut, float* vals, bool useLcb) {
   const int ri = s.rootIdx;
   const Node& n = v.nodes()[ri];
   const int k = n.numChildren;
@@ -1375,7 +1378,7 @@ KC_D int playSelectionValues(const GV& v, const GameDev& s, float scaleMaxToAtLe
       val[j] = ceilf(reduced);
     }
   }
-  if(sp.useLcb && k > 0) {
+  if(useLcb && k > 0) {
     float lcb[NI], rad[NI];
     float bestLcb = -1e10f;
     int bestLcbIdx = BIG;
@@ -1535,7 +1538,7 @@ KC_D void clearTables(const GV& v, GameDev& s) {
 // SubtreeValueBiasTable::clearUnusedSynchronous :47-59) as mark / free / rebuild.
 // lds: live bitmap [cap/32] u32 + BFS queue [cap] u16.
 KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, uint16_t* queue, int* qtail) {
-  const SP& sp = v.d.sp;
+  const SP& sp = *v.sp;
   const int cap = v.d.cap;
   const int ri = s.rootIdx;
   int child = -1;
@@ -1729,6 +1732,47 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
   waveSync();
 }
 
+// oracle setMoveLimits (getSearchLimitsThisMove play.cpp:871-1004) for the move about
+// to be searched; every lane runs it on the same state.  lastWL: the root value of the
+// move just committed (the newest reduceVisits history entry).  Returns
+// clearBotBeforeSearchThisMove (self-play clears before every search, play.cpp:1941-1946,
+// except a cheap search whose rows are not recorded, :920-925).
+KC_D bool setMoveLimits(const GV& v, GameDev& s, DRng& rng, float lastWL) {
+  const SP& b = v.d.sp;
+  s.visitLimit = b.maxVisits;
+  s.moveWeight = 1.0f;
+  s.noNoise = 0;
+  bool clear = true;
+  if(b.cheapProb > 0.0f && rng.uni() < b.cheapProb) {
+    s.visitLimit = min(b.maxVisits, b.cheapVisits);
+    s.moveWeight = 1.0f * b.cheapWeight;
+    if(b.cheapWeight <= 0.0f) {
+      clear = false;
+      s.noNoise = 1;
+    }
+  } else if(b.reduceVisits && s.numTurns >= b.reduceLookback) {
+    const TurnRec* tr = v.turns();
+    float mn = 1e20f, mx = -1e20f;
+    for(int j = 0; j < b.reduceLookback; j++) {
+      const float w = j == 0 ? lastWL : tr[s.numTurns - 1 - j].rootWL;
+      mn = w < mn ? w : mn;
+      mx = w > mx ? w : mx;
+    }
+    float extreme = fmaxf(mn, -mx);
+    if(extreme > 1.0f)
+      extreme = 1.0f;
+    const float through = extreme - b.reduceThreshold;
+    if(through > 0.0f) {
+      const float prop = through / (1.0f - b.reduceThreshold);
+      const float red = prop * prop;
+      const int vl = (int)roundf((float)b.maxVisits + red * ((float)b.reducedMin - (float)b.maxVisits));
+      s.moveWeight = 1.0f + red * (b.reducedWeight - 1.0f);
+      s.visitLimit = max(vl, b.reducedMin);
+    }
+  }
+  return clear;
+}
+
 KC_D void startGame(const GV& v, GameDev& s) {
   s.rngSeed = mix64(v.d.seed ^ mix64(((uint64_t)(v.d.slotBase + v.g) << 32) | (uint32_t)s.gameNum));
   s.rngCtr = 0;
@@ -1738,6 +1782,7 @@ KC_D void startGame(const GV& v, GameDev& s) {
   DRng rng{s.rngSeed, s.rngCtr};
   s.gameHash0 = rng.next();
   s.gameHash1 = rng.next();
+  setMoveLimits(v, s, rng, 0.0f);
   s.rngCtr = rng.ctr;
   s.phase = PH_ROOTEVAL;
   s.rootK = 0;
@@ -1748,10 +1793,85 @@ KC_D void startGame(const GV& v, GameDev& s) {
 // part: the SGF move record, the row reservation and the FinRec kRows reads.  The
 // turn records and per-turn policies stay in place until the game's next commit,
 // so kRows (launched right after this kernel) reads them there.
-KC_D void finishGameRecord(const GV& v, const GameDev& s, const DRng& rng) {
+// oracle resolveTurnWeights: value surprise (play.cpp:1470-1497), surprise-weighted
+// target weights (:1498-1574), probabilistic resolution (:1683-1697).  Every lane runs
+// the sequential loops on the same data; lane 0 stores each turn's row count.
+// Returns the game's number of rows.
+KC_D int resolveTurnWeights(const GV& v, const GameDev& s, DRng& rng, float* vs /* LDS [MAX_AREA] */) {
+  const SP& b = v.d.sp;
+  const int n = s.numTurns, A = v.T.A;
+  TurnRec* tr = v.turns();
+  const float finalWin = s.root.winner == 2 ? 1.0f : (s.root.winner == 1 ? 0.0f : 0.5f);
+  float psdw = b.policySurpriseWeight, vsdw = b.valueSurpriseWeight;
+  bool reweight = false;
+  float sumW = 0.0f, sumPPV = 0.0f, sumVPV = 0.0f, thr = 0.0f;
+  if(psdw > 0.0f || vsdw > 0.0f) {
+    if(v.lane == 0) {
+      const float nowFactor = 1.0f / (1.0f + (float)A * 0.016f);
+      float winV = finalWin, lossV = 1.0f - finalWin;
+      for(int i = n - 1; i >= 0; i--) {
+        winV = winV + nowFactor * (tr[i].whiteWin - winV);
+        lossV = lossV + nowFactor * (tr[i].whiteLoss - lossV);
+        float x = 0.0f;
+        if(winV > 1e-30f)
+          x = x + winV * (dlog(winV) - dlog(fmaxf(tr[i].rootNNWin, 1e-30f)));
+        if(lossV > 1e-30f)
+          x = x + lossV * (dlog(lossV) - dlog(fmaxf(tr[i].rootNNLoss, 1e-30f)));
+        if(x < 0.0f)
+          x = 0.0f;
+        vs[i] = fminf(x, 1.0f);
+      }
+    }
+    waveSync();
+    float sumPS = 0.0f, sumVS = 0.0f;
+    for(int i = 0; i < n; i++) {
+      const float tw = tr[i].targetWeight;
+      sumW = sumW + tw;
+      sumPS = sumPS + tr[i].policySurprise * tw;
+      sumVS = sumVS + vs[i] * tw;
+    }
+    if(sumW >= 1.0f) {
+      reweight = true;
+      const float avgPS = sumPS / sumW, avgVS = sumVS / sumW;
+      if(avgVS < 0.010f)
+        vsdw = vsdw * (avgVS / 0.010f);
+      thr = avgPS * 1.5f;
+      for(int i = 0; i < n; i++) {
+        const float tw = tr[i].targetWeight, ps = tr[i].policySurprise;
+        sumPPV = sumPPV + (tw * ps + (1.0f - tw) * fmaxf(0.0f, ps - thr));
+        sumVPV = sumVPV + tw * vs[i];
+      }
+      sumPPV = fmaxf(sumPPV, 1e-10f);
+      sumVPV = fmaxf(sumVPV, 1e-10f);
+    }
+  }
+  int total = 0;
+  for(int i = 0; i < n; i++) {
+    float w = tr[i].targetWeight;
+    if(reweight) {
+      const float ps = tr[i].policySurprise;
+      const float ppv = w * ps + (1.0f - w) * fmaxf(0.0f, ps - thr);
+      const float vpv = w * vs[i];
+      w = (1.0f - psdw - vsdw) * w + psdw * ppv * sumW / sumPPV + vsdw * vpv * sumW / sumVPV;
+    }
+    if(w <= 0.0f)
+      w = 0.0f;
+    const float fl = floorf(w), excess = w - fl;
+    const int rows = (int)(rng.uni() < excess ? fl + 1.0f : fl);
+    total += rows;
+    waveSync();
+    if(v.lane == 0)
+      tr[i].rows = (uint8_t)rows;
+  }
+  waveSync();
+  return total;
+}
+
+KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scratch) {
   const SearchDev& d = v.d;
   const int numMoves = s.numTurns;
   const TurnRec* tr = v.turns();
+  const int numRows = resolveTurnWeights(v, s, rng, scratch);
   {
     // the game's move record (SGF)
     unsigned long long gi = 0;
@@ -1778,11 +1898,11 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, const DRng& rng) {
     }
   }
   if(v.lane == 0) {
-    unsigned long long base = atomicAdd(d.rCount, (unsigned long long)numMoves);
+    unsigned long long base = atomicAdd(d.rCount, (unsigned long long)numRows);
     bool fits = true;
-    if(base + (unsigned long long)numMoves > (unsigned long long)d.rowCap) {
-      atomicAdd(d.rCount, (unsigned long long)(-(long long)numMoves));
-      atomicAdd(d.rDropped, (unsigned long long)numMoves);
+    if(base + (unsigned long long)numRows > (unsigned long long)d.rowCap) {
+      atomicAdd(d.rCount, (unsigned long long)(-(long long)numRows));
+      atomicAdd(d.rDropped, (unsigned long long)numRows);
       fits = false;
     }
     FinRec* f = d.fin + v.g;
@@ -1792,16 +1912,18 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, const DRng& rng) {
     f->gameHash1 = s.gameHash1;
     f->rowBase = base;
     f->numMoves = numMoves;
+    f->numRows = numRows;
     f->winner = s.root.winner;
     f->gameNum = s.gameNum;
-    f->pending = fits ? 1 : 0;
+    f->pending = fits && numRows > 0 ? 1 : 0;
   }
 }
 
 // kRows: the training rows of the games the preceding kCommit finished
-// (trainingwrite.cpp:316-565 addRow via writeGame :774-890).  One 256-thread block
-// per committed game; the boards after every move and the final board's per-cell
-// max runs are built once in LDS, then wave w writes rows t = w, w + 4, ...
+// (trainingwrite.cpp:316-565 addRow via writeGame :774-890; turn t is written
+// TurnRec::rows times).  One 256-thread block per committed game; the boards after
+// every move, the row -> turn map and the final board's per-cell max runs are built
+// once in LDS, then wave w writes rows w, w + 4, ...
 constexpr int ROWS_WAVES = 4;
 __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __restrict__ dp,
                                                          const DTables* __restrict__ Tp) {
@@ -1819,8 +1941,9 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
   __shared__ DBoard boards[MAX_AREA + 1];
   __shared__ float tWin[MAX_AREA + 1], tLoss[MAX_AREA + 1];
   __shared__ int8_t finRun[MAX_AREA];
-  __shared__ uint8_t hMask[MAX_AREA];
-  const int numMoves = f.numMoves;
+  __shared__ uint8_t hMask[2 * MAX_AREA];
+  __shared__ uint8_t rowTurn[2 * MAX_AREA];
+  const int numMoves = f.numMoves, numRows = min(f.numRows, 2 * MAX_AREA);  // <= 2 numMoves by construction
   const int A = T.A, P = T.P, pb = (A + 7) / 8;
   const TurnRec* tr = v.turns();
   const float finalWin = f.winner == 2 ? 1.0f : (f.winner == 1 ? 0.0f : 0.5f);
@@ -1838,17 +1961,21 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
       applyMove(T, b, tr[t].cell, tr[t].dir);
       boards[t + 1] = b;
     }
+    int j = 0;
+    for(int t = 0; t < numMoves; t++)
+      for(int c = 0; c < (int)tr[t].rows && j < 2 * MAX_AREA; c++)
+        rowTurn[j++] = (uint8_t)t;
     // history-mask draws, in row order from the game's stream (the chain stops
     // drawing at its first failure, so the draws are consumed sequentially)
     DRng rng{f.rngSeed, f.rngCtr};
-    for(int t = 0; t < numMoves; t++) {
+    for(int r = 0; r < numRows; r++) {
       bool h = true;
       uint32_t hm = 0;
       for(int i = 0; i < 5; i++) {
         h = h && rng.uni() < 0.98f;
         hm |= (h ? 1u : 0u) << i;
       }
-      hMask[t] = (uint8_t)hm;
+      hMask[r] = (uint8_t)hm;
     }
   }
   __syncthreads();
@@ -1858,9 +1985,10 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
   __syncthreads();
   const float nowF1 = 1.0f / (1.0f + (float)A * 0.176f), nowF2 = 1.0f / (1.0f + (float)A * 0.056f),
               nowF3 = 1.0f / (1.0f + (float)A * 0.016f);
-  for(int t = wave; t < numMoves; t += ROWS_WAVES) {
-    const uint32_t hm = hMask[t];
-    const size_t r = (size_t)f.rowBase + t;
+  for(int row = wave; row < numRows; row += ROWS_WAVES) {
+    const int t = rowTurn[row];
+    const uint32_t hm = hMask[row];
+    const size_t r = (size_t)f.rowBase + row;
     const DBoard& b = boards[t];
     const int pla = b.pla, opp = 3 - pla;
     packRowBinWave(T, b, d.rBin + r * NUM_SPATIAL * pb);
@@ -1979,7 +2107,8 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   const SP& sp = d.sp;
   const int P = d.P, A = d.A;
   DRng rng{s.rngSeed, s.rngCtr};
-  int n = playSelectionValues<NI>(v, s, 0.0f, true, posv, vals);
+  // move choice: self-play disables LCB here (runBotWithLimits play.cpp:1040-1046)
+  int n = playSelectionValues<NI>(v, *v.sp, s, 0.0f, true, posv, vals, false);
   if(n <= 0) {
     s.err = 2;
     n = 1;
@@ -1996,6 +2125,11 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     rec.whiteWin = fmaxf(0.0f, fminf(1.0f, 0.5f * (wl + 1.0f)));
     rec.whiteLoss = fmaxf(0.0f, fminf(1.0f, 0.5f * (-wl + 1.0f)));
     rec.visits = r.visits;
+    rec.rootWL = wl;
+    rec.rootNNWin = r.nnWin;
+    rec.rootNNLoss = r.nnLoss;
+    rec.targetWeight = s.moveWeight;
+    rec.rows = 0;
   }
   const int t = s.numTurns;
   int16_t* pt = v.turnPol(t);
@@ -2003,7 +2137,8 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   {
     for(int p = v.lane; p < P; p += 64)
       pt[p] = 0;
-    int m = playSelectionValues<NI>(v, s, 10.0f, false, posv, vals);
+    // the targets run after runBotWithLimits restored the base parameters (play.cpp:1066, :1307-1320)
+    int m = playSelectionValues<NI>(v, sp, s, 10.0f, false, posv, vals, sp.useLcb);
     float mx = 0.0f;
     for(int i = v.lane; i < m; i += 64)
       mx = vals[i] > mx ? vals[i] : mx;
@@ -2025,7 +2160,7 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   }
   {
     waveSync();
-    int m = playSelectionValues<NI>(v, s, 1.0f, true, posv, vals);
+    int m = playSelectionValues<NI>(v, sp, s, 1.0f, true, posv, vals, sp.useLcb);
     const float* pol = v.rootNoised();
     const float sumV = seqSum(vals, m, v.lane);
     // per-child terms (0 where the oracle skips), summed in order on lane 0
@@ -2056,24 +2191,20 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   }
   rec.cell = (int8_t)(chosen % A);
   rec.dir = (int8_t)(chosen / A);
-  for(int i = 0; i < 6; i++)
+  for(int i = 0; i < 5; i++)
     rec.pad[i] = 0;
   waveSync();
   if(v.lane == 0)
     v.turns()[t] = rec;
   s.numTurns++;
   [[maybe_unused]] const unsigned long long t1 = SPROF_NOW();
-  reuseTree(v, s, chosen, liveBits, queue, qtail);
-  [[maybe_unused]] const unsigned long long t2 = SPROF_NOW();
   SPROF_ADD(18, t1 - t0);
-  SPROF_ADD(19, t2 - t1);
-  SPROF_ADD(22, s.liveCount);
   playMoveWave(v.T, s.root, chosen % A, chosen / A);
   s.moves++;
   waveSync();
   if(s.root.finished) {
     [[maybe_unused]] const unsigned long long t3 = SPROF_NOW();
-    finishGameRecord(v, s, rng);
+    finishGameRecord(v, s, rng, tmp);
     [[maybe_unused]] const unsigned long long t4 = SPROF_NOW();
     s.gamesFinished++;
     s.gameNum++;
@@ -2082,6 +2213,14 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     SPROF_ADD(21, SPROF_NOW() - t4);
     SPROF_ADD(23, 1);
   } else {
+    // the next move's limits decide whether its search starts from a cleared tree
+    if(setMoveLimits(v, s, rng, rec.rootWL))
+      clearTables(v, s);
+    else
+      reuseTree(v, s, chosen, liveBits, queue, qtail);
+    [[maybe_unused]] const unsigned long long t2 = SPROF_NOW();
+    SPROF_ADD(19, t2 - t1);
+    SPROF_ADD(22, s.liveCount);
     s.rngCtr = rng.ctr;
     s.phase = PH_ROOTEVAL;
     s.rootK = 0;

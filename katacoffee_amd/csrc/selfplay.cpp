@@ -48,6 +48,16 @@ SP toSP(const coffee_search_params& p) {
   s.svbExp = p.subtree_value_bias_weight_exponent;
   s.svbFreeProp = p.subtree_value_bias_free_prop;
   s.useGraph = p.use_graph_search;
+  s.cheapProb = p.cheap_search_prob;
+  s.cheapVisits = p.cheap_search_visits;
+  s.cheapWeight = p.cheap_search_target_weight;
+  s.reduceVisits = p.reduce_visits;
+  s.reduceThreshold = p.reduce_visits_threshold;
+  s.reduceLookback = p.reduce_visits_threshold_lookback;
+  s.reducedMin = p.reduced_visits_min;
+  s.reducedWeight = p.reduced_visits_weight;
+  s.policySurpriseWeight = p.policy_surprise_data_weight;
+  s.valueSurpriseWeight = p.value_surprise_data_weight;
   return s;
 }
 
@@ -68,6 +78,20 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   const coffee_search_params& sp = c.search;
   if(sp.max_visits < 1 || sp.root_num_symmetries_to_sample < 1 || sp.root_num_symmetries_to_sample > 4)
     throw std::invalid_argument("search params: max_visits >= 1 and 1 <= root_num_symmetries_to_sample <= 4");
+  // the reference's own checks (play.cpp:906-910, :925-930)
+  if(sp.cheap_search_prob > 0.0f && (sp.cheap_search_visits <= 0 || sp.cheap_search_visits > sp.max_visits))
+    throw std::invalid_argument("cheap_search_visits must be in [1, max_visits]");
+  if(sp.reduce_visits && (sp.reduced_visits_min <= 0 || sp.reduced_visits_min > sp.max_visits))
+    throw std::invalid_argument("reduced_visits_min must be in [1, max_visits]");
+  if(sp.reduce_visits && (sp.reduce_visits_threshold < 0.0f || sp.reduce_visits_threshold >= 1.0f ||
+                          sp.reduce_visits_threshold_lookback < 1 || sp.reduce_visits_threshold_lookback > 100))
+    throw std::invalid_argument("reduce_visits_threshold must be in [0, 1) and lookback in [1, 100]");
+  // playsettings.cpp:80-99 ranges
+  auto unit = [](float x) { return x >= 0.0f && x <= 1.0f; };
+  if(!unit(sp.cheap_search_prob) || !unit(sp.cheap_search_target_weight) || !unit(sp.reduced_visits_weight) ||
+     !unit(sp.policy_surprise_data_weight) || !unit(sp.value_surprise_data_weight) ||
+     sp.policy_surprise_data_weight + sp.value_surprise_data_weight > 1.0f)
+    throw std::invalid_argument("play settings: probabilities and weights in [0, 1], surprise weights sum <= 1");
   const DTables& ht = hostTables(c.x, c.y, c.win_len);
   T_ = deviceTables(c.x, c.y, c.win_len);
   commitInterval_ = c.commit_interval > 0 ? c.commit_interval : 8;
@@ -93,6 +117,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   memset(&d, 0, sizeof(d));
   d.T = T_;
   d.sp = toSP(sp);
+  d.spCheap = cheapSearchSP(d.sp);
   d.G = G;
   d.cap = cap;
   d.ttCap = ttCap;

@@ -121,14 +121,30 @@ int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* 
   return 0;
 }
 
+// play: NULL or the 10 play settings in coffee_search_params order (cheap_search_prob,
+// cheap_search_visits, cheap_search_target_weight, reduce_visits, reduce_visits_threshold,
+// reduce_visits_threshold_lookback, reduced_visits_min, reduced_visits_weight,
+// policy_surprise_data_weight, value_surprise_data_weight).
 void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
-                    int nnMode, void* model, int nnThreads, int cacheLog2) {
+                    int nnMode, void* model, int nnThreads, int cacheLog2, const float* play) {
   if(!T.loaded)
     return nullptr;
   Selfplay* s = new Selfplay();
   SelfplayCfg cfg;
   cfg.g = Geom(X, Y, W);
   cfg.sp.maxVisits = maxVisits;
+  if(play) {
+    cfg.sp.cheapSearchProb = play[0];
+    cfg.sp.cheapSearchVisits = (int)play[1];
+    cfg.sp.cheapSearchTargetWeight = play[2];
+    cfg.sp.reduceVisits = (int)play[3];
+    cfg.sp.reduceVisitsThreshold = play[4];
+    cfg.sp.reduceVisitsThresholdLookback = (int)play[5];
+    cfg.sp.reducedVisitsMin = (int)play[6];
+    cfg.sp.reducedVisitsWeight = play[7];
+    cfg.sp.policySurpriseDataWeight = play[8];
+    cfg.sp.valueSurpriseDataWeight = play[9];
+  }
   cfg.nodeCap = nodeCap;
   cfg.seed = seed;
   cfg.slotBase = slotBase;

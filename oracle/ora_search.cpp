@@ -75,7 +75,10 @@ struct Ctx {
   Game& gm;
   const Geom& g;
   const SearchParams& sp;
-  Ctx(Selfplay& s_, Game& gm_) : s(s_), gm(gm_), g(s_.cfg.g), sp(s_.cfg.sp) {}
+  // sp: this move's parameters (a cheap search without recorded rows drops the root
+  // noise and root-specific settings, play.cpp:1024-1037)
+  Ctx(Selfplay& s_, Game& gm_) : s(s_), gm(gm_), g(s_.cfg.g), sp(gm_.noNoise ? s_.spCheap : s_.cfg.sp) {}
+  Ctx(Selfplay& s_, Game& gm_, const SearchParams& p) : s(s_), gm(gm_), g(s_.cfg.g), sp(p) {}
 
   Node& N(int i) { return gm.nodes[i]; }
   uint32_t& EC(int n, int i) { return gm.edgeChild[(size_t)n * g.P + i]; }
@@ -619,8 +622,10 @@ struct Ctx {
   }
 
   // getPlaySelectionValues searchresults.cpp:63-309 on the root.
-  // Fills pos[] and vals[]; returns count (0 = failure).
-  int playSelectionValues(float scaleMaxToAtLeast, bool allowDirectPolicyMoves, int* posOut, float* vals) {
+  // Fills pos[] and vals[]; returns count (0 = failure).  useLcb: searchParams.useLcbForSelection
+  // at the call (self-play turns it off for the move choice only, play.cpp:1040-1046, :1073-1076).
+  int playSelectionValues(float scaleMaxToAtLeast, bool allowDirectPolicyMoves, int* posOut, float* vals,
+                          bool useLcb) {
     int ri = gm.rootIdx;
     const Node& n = N(ri);
     const int k = n.numChildren;
@@ -689,7 +694,7 @@ struct Ctx {
         vals[i] = ceilf(reduced);
       }
     }
-    if(sp.useLcbForSelection && k > 0) {
+    if(useLcb && k > 0) {
       float lcb[MAX_P], rad[MAX_P];
       float bestLcb = -1e10f;
       int bestLcbIdx = -1;
@@ -900,6 +905,45 @@ struct Ctx {
     gm.svbUsed.swap(u2);
   }
 
+  // getSearchLimitsThisMove (play.cpp:871-1004) for the move about to be searched.
+  // Returns clearBotBeforeSearchThisMove: self-play clears the tree before every
+  // search (play.cpp:1941-1946, :1009-1010) except a cheap search whose rows are
+  // not recorded (:920-925), which keeps the subtree of the previous move.
+  bool setMoveLimits() {
+    const SearchParams& b = s.cfg.sp;
+    gm.visitLimit = b.maxVisits;
+    gm.moveWeight = 1.0f;
+    gm.noNoise = 0;
+    bool clear = true;
+    if(b.cheapSearchProb > 0.0f && gm.rng.uni() < b.cheapSearchProb) {
+      gm.visitLimit = std::min(b.maxVisits, b.cheapSearchVisits);
+      gm.moveWeight = 1.0f * b.cheapSearchTargetWeight;
+      if(b.cheapSearchTargetWeight <= 0.0f) {
+        clear = false;
+        gm.noNoise = 1;
+      }
+    } else if(b.reduceVisits && (int)gm.turns.size() >= b.reduceVisitsThresholdLookback) {
+      float mn = 1e20f, mx = -1e20f;
+      for(int j = 0; j < b.reduceVisitsThresholdLookback; j++) {
+        const float w = gm.turns[gm.turns.size() - 1 - j].rootWL;
+        mn = w < mn ? w : mn;
+        mx = w > mx ? w : mx;
+      }
+      float extreme = std::max(mn, -mx);
+      if(extreme > 1.0f)
+        extreme = 1.0f;
+      const float through = extreme - b.reduceVisitsThreshold;
+      if(through > 0.0f) {
+        const float prop = through / (1.0f - b.reduceVisitsThreshold);
+        const float red = prop * prop;
+        const int v = (int)roundf((float)b.maxVisits + red * ((float)b.reducedVisitsMin - (float)b.maxVisits));
+        gm.moveWeight = 1.0f + red * (b.reducedVisitsWeight - 1.0f);
+        gm.visitLimit = std::max(v, b.reducedVisitsMin);
+      }
+    }
+    return clear;
+  }
+
   void startGame() {
     gm.rng.seed = mix64(s.cfg.seed ^ mix64(((uint64_t)(s.cfg.slotBase + gm.slot) << 32) | gm.gameNum));
     gm.rng.ctr = 0;
@@ -908,6 +952,7 @@ struct Ctx {
     gm.turns.clear();
     gm.gameHash0 = gm.rng.next();
     gm.gameHash1 = gm.rng.next();
+    setMoveLimits();
     gm.phase = PH_ROOTEVAL;
     gm.rootK = 0;
   }
@@ -920,8 +965,9 @@ void Ctx::commitMove() {
   int posv[MAX_P];
   float vals[MAX_P];
   TurnRec tr;
-  // getChosenMoveLoc (searchresults.cpp:435-453)
-  int n = playSelectionValues(0.0f, true, posv, vals);
+  // getChosenMoveLoc (searchresults.cpp:435-453) inside runBotWithLimits, which disables
+  // LCB for the move choice in self-play (play.cpp:1040-1046)
+  int n = playSelectionValues(0.0f, true, posv, vals, false);
   if(n <= 0) {
     fprintf(stderr, "oracle: no move selectable\n");
     abort();
@@ -934,10 +980,17 @@ void Ctx::commitMove() {
   tr.whiteWin = std::max(0.0f, std::min(1.0f, 0.5f * (wl + 1.0f)));
   tr.whiteLoss = std::max(0.0f, std::min(1.0f, 0.5f * (-wl + 1.0f)));
   tr.visits = r.visits;
+  tr.rootWL = wl;
+  tr.rootNNWin = r.nnWin;
+  tr.rootNNLoss = r.nnLoss;
+  tr.targetWeight = gm.moveWeight;
+  // the targets below run after runBotWithLimits restored the base parameters
+  // (play.cpp:1066, :1307-1320)
+  Ctx base(s, gm, s.cfg.sp);
   // extractPolicyTarget play.cpp:635-672
   tr.policyTarget.assign(g.P, 0);
   {
-    int m = playSelectionValues(10.0f, false, posv, vals);
+    int m = base.playSelectionValues(10.0f, false, posv, vals, sp.useLcbForSelection);
     float mx = 0.0f;
     for(int i = 0; i < m; i++)
       if(vals[i] > mx)
@@ -959,7 +1012,7 @@ void Ctx::commitMove() {
   }
   // getPolicySurpriseAndEntropy searchresults.cpp:486-550
   {
-    int m = playSelectionValues(1.0f, true, posv, vals);
+    int m = base.playSelectionValues(1.0f, true, posv, vals, sp.useLcbForSelection);
     const float* pol = gm.rootNoised.data();
     float sumV = 0.0f;
     for(int i = 0; i < m; i++)
@@ -984,7 +1037,6 @@ void Ctx::commitMove() {
   tr.cell = (int8_t)(chosen % g.A);
   tr.dir = (int8_t)(chosen / g.A);
   gm.turns.push_back(tr);
-  reuseTree(chosen);
   playMove(g, gm.root, chosen % g.A, chosen / g.A);
   gm.movesMade++;
   if(gm.root.finished) {
@@ -994,6 +1046,10 @@ void Ctx::commitMove() {
     startGame();
     return;
   }
+  if(setMoveLimits())
+    clearTree();
+  else
+    reuseTree(chosen);
   // SPEC B26: Search::recursivelyRecomputeStats (search.cpp:671, :834-910) is not
   // run after tree reuse; the kept subtree keeps its statistics.
   gm.phase = PH_ROOTEVAL;
@@ -1009,8 +1065,69 @@ static void packBitsBE(const float* v, int len, uint8_t* out) {
       out[i >> 3] |= (uint8_t)(1u << (7 - (i & 7)));
 }
 
+// Play::runGame row weights: value surprise (play.cpp:1470-1497), surprise-weighted
+// target weights (:1498-1574) and their probabilistic resolution (:1683-1697), in f32
+// with the loops' own order.  Fills turns[].rows.
+static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec>& turns, const float* tWin,
+                               const float* tLoss, Rng& rng) {
+  const int n = (int)turns.size();
+  if(b.policySurpriseDataWeight > 0.0f || b.valueSurpriseDataWeight > 0.0f) {
+    std::vector<float> vs(n);
+    const float nowFactor = 1.0f / (1.0f + (float)A * 0.016f);
+    float winV = tWin[n], lossV = tLoss[n];
+    for(int i = n - 1; i >= 0; i--) {
+      winV = winV + nowFactor * (tWin[i] - winV);
+      lossV = lossV + nowFactor * (tLoss[i] - lossV);
+      float v = 0.0f;
+      if(winV > 1e-30f)
+        v = v + winV * (kLogf(winV) - kLogf(std::max(turns[i].rootNNWin, 1e-30f)));
+      if(lossV > 1e-30f)
+        v = v + lossV * (kLogf(lossV) - kLogf(std::max(turns[i].rootNNLoss, 1e-30f)));
+      if(v < 0.0f)
+        v = 0.0f;
+      vs[i] = std::min(v, 1.0f);
+    }
+    float sumW = 0.0f, sumPS = 0.0f, sumVS = 0.0f;
+    for(int i = 0; i < n; i++) {
+      const float tw = turns[i].targetWeight;
+      sumW = sumW + tw;
+      sumPS = sumPS + turns[i].policySurprise * tw;
+      sumVS = sumVS + vs[i] * tw;
+    }
+    if(sumW >= 1.0f) {
+      const float avgPS = sumPS / sumW, avgVS = sumVS / sumW;
+      float vsdw = b.valueSurpriseDataWeight;
+      if(avgVS < 0.010f)
+        vsdw = vsdw * (avgVS / 0.010f);
+      const float thr = avgPS * 1.5f;
+      float sumPPV = 0.0f, sumVPV = 0.0f;
+      for(int i = 0; i < n; i++) {
+        const float tw = turns[i].targetWeight, ps = turns[i].policySurprise;
+        sumPPV = sumPPV + (tw * ps + (1.0f - tw) * std::max(0.0f, ps - thr));
+        sumVPV = sumVPV + tw * vs[i];
+      }
+      sumPPV = std::max(sumPPV, 1e-10f);
+      sumVPV = std::max(sumVPV, 1e-10f);
+      for(int i = 0; i < n; i++) {
+        const float tw = turns[i].targetWeight, ps = turns[i].policySurprise;
+        const float ppv = tw * ps + (1.0f - tw) * std::max(0.0f, ps - thr);
+        const float vpv = tw * vs[i];
+        turns[i].targetWeight = (1.0f - b.policySurpriseDataWeight - vsdw) * tw +
+                                b.policySurpriseDataWeight * ppv * sumW / sumPPV + vsdw * vpv * sumW / sumVPV;
+      }
+    }
+  }
+  for(int i = 0; i < n; i++) {
+    float w = turns[i].targetWeight;
+    if(w <= 0.0f)
+      w = 0.0f;
+    const float fl = floorf(w), excess = w - fl;
+    turns[i].rows = (int)(rng.uni() < excess ? fl + 1.0f : fl);
+  }
+}
+
 // Play::runGame finalisation play.cpp:1431-1460 + TrainingDataWriter::writeGame
-// trainingwrite.cpp:774-890 + addRow :316-565 (benchmark mode: weight 1 per turn).
+// trainingwrite.cpp:774-890 + addRow :316-565: turn t is written turns[t].rows times.
 void Ctx::finishGame() {
   const int numMoves = (int)gm.turns.size();
   const int A = g.A, P = g.P, pb = (A + 7) / 8;
@@ -1033,8 +1150,13 @@ void Ctx::finishGame() {
   int8_t finalMaxLen[MAX_AREA];
   for(int c = 0; c < A; c++)
     finalMaxLen[c] = fin.c[c] == 0 ? 0 : (int8_t)maxRun(g, fin, c);
+  resolveTurnWeights(s.cfg.sp, A, gm.turns, tWin.data(), tLoss.data(), gm.rng);
+  std::vector<int> rowTurn;  // turn of each row, in row order
+  for(int t = 0; t < numMoves; t++)
+    for(int c = 0; c < gm.turns[t].rows; c++)
+      rowTurn.push_back(t);
   Rows& R = s.rows;
-  for(int t = 0; t < numMoves; t++) {
+  for(const int t : rowTurn) {
     const Board& b = boards[t];
     int pla = b.pla, opp = 3 - pla;
     float bin[NUM_SPATIAL * MAX_AREA], glob[1];
@@ -1138,6 +1260,7 @@ static uint32_t cacheSlotOf(uint64_t k0, uint64_t k1, uint32_t mask) {
 
 void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames) {
   s.cfg = cfg;
+  s.spCheap = cheapSearchParams(cfg.sp);
   const Geom& g = s.cfg.g;
   if(cfg.cacheLog2 > 0) {
     const size_t entries = (size_t)1 << cfg.cacheLog2;
@@ -1277,8 +1400,8 @@ void selfplayRound(Selfplay& s) {
         gm.accLoss = gm.accLoss + l;
       }
       gm.rootK++;
-      if(gm.rootK == s.cfg.sp.rootNumSymmetriesToSample) {
-        float fl = (float)s.cfg.sp.rootNumSymmetriesToSample;
+      if(gm.rootK == cx.sp.rootNumSymmetriesToSample) {
+        float fl = (float)cx.sp.rootNumSymmetriesToSample;
         bool fresh = gm.rootIdx < 0;
         if(fresh)
           gm.rootIdx = cx.allocNode(gm.root.pla, stateHash(g, gm.root), false);
@@ -1293,7 +1416,7 @@ void selfplayRound(Selfplay& s) {
           cx.addLeafValue(gm.rootIdx, r.nnWin - r.nnLoss, false, true);
         cx.noiseAndTemp(rp, gm.rootNoised.data());
         gm.phase = PH_SEARCH;
-        if(cx.N(gm.rootIdx).visits >= (uint32_t)s.cfg.sp.maxVisits)
+        if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit)
           cx.commitMove();
       }
       continue;
@@ -1332,7 +1455,7 @@ void selfplayRound(Selfplay& s) {
       cx.recompute(pn, 1, pn == gm.rootIdx);
     }
     gm.playouts++;
-    if(cx.N(gm.rootIdx).visits >= (uint32_t)s.cfg.sp.maxVisits)
+    if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit)
       cx.commitMove();
   }
   // ---- cache write: after every read of this round; in game order, so a slot ends

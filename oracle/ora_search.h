@@ -27,7 +27,33 @@ struct SearchParams {
   float lcbStdevs = 5.0f, minVisitPropForLCB = 0.15f;
   float subtreeValueBiasFactor = 0.30f, subtreeValueBiasWeightExponent = 0.8f, subtreeValueBiasFreeProp = 0.8f;
   int useGraphSearch = 1;
+  // PlaySettings (playsettings.cpp) per-move search limits and row weighting; the
+  // defaults are benchmark mode, selfplay1.cfg values in comments
+  float cheapSearchProb = 0.0f;          // 0.75
+  int cheapSearchVisits = 100;           // 100
+  float cheapSearchTargetWeight = 0.0f;  // 0.0
+  int reduceVisits = 0;                  // true
+  float reduceVisitsThreshold = 0.9f;    // 0.9
+  int reduceVisitsThresholdLookback = 3; // 3
+  int reducedVisitsMin = 100;            // 100
+  float reducedVisitsWeight = 0.1f;      // 0.1
+  float policySurpriseDataWeight = 0.0f; // 0.5
+  float valueSurpriseDataWeight = 0.0f;  // 0.1
 };
+
+// The search parameters of a cheap search whose rows are not recorded
+// (runBotWithLimits removeRootNoise, play.cpp:1024-1037).
+inline SearchParams cheapSearchParams(const SearchParams& p) {
+  SearchParams c = p;
+  c.rootNoiseEnabled = 0;
+  c.rootPolicyTemperature = 1.0f;
+  c.rootPolicyTemperatureEarly = 1.0f;
+  c.rootFpuLossProp = p.fpuLossProp;
+  c.rootFpuReductionMax = p.fpuReductionMax;
+  c.rootDesiredPerChildVisitsCoeff = 0.0f;
+  c.rootNumSymmetriesToSample = 1;
+  return c;
+}
 
 // Node record; identical fields and pool layout to the HIP engine so whole
 // pools can be compared bit-for-bit.
@@ -54,6 +80,10 @@ struct TurnRec {
   float rawWhiteWL, rawPolicyEntropy; // computeNNRawStats (play.cpp:684-704)
   float policySurprise, policyEntropy, searchEntropy;
   uint32_t visits;
+  float rootWL;                       // getRootValues winLossValue (reduceVisits history, play.cpp:1381-1384)
+  float rootNNWin, rootNNLoss;        // getRootRawNNValues (value surprise, play.cpp:1336)
+  float targetWeight;                 // limits.targetWeight, then surprise-weighted (play.cpp:1498-1574)
+  int rows = 0;                       // resolved integer weight (play.cpp:1683-1697)
 };
 
 struct Rows {
@@ -89,6 +119,9 @@ struct Game {
   float accWin = 0, accLoss = 0;
   std::vector<float> rawPolicy;  // first root eval (raw stats)
   float rawWin = 0, rawLoss = 0;
+  // this move's search limits (getSearchLimitsThisMove play.cpp:871-1004)
+  int visitLimit = 0, noNoise = 0;
+  float moveWeight = 1.0f;
   // tree
   int nodeCount = 0, rootIdx = -1;
   std::vector<Node> nodes;
@@ -114,6 +147,7 @@ struct Game {
 
 struct Selfplay {
   SelfplayCfg cfg;
+  SearchParams spCheap;        // cheapSearchParams(cfg.sp)
   std::vector<Game> games;
   std::vector<uint64_t> svbZ;  // SVB pattern zobrist (SPEC a19)
   Rows rows;

@@ -32,7 +32,7 @@ def lib():
         L.ora_model_load.restype = P
         L.ora_sp_create.restype = P
         L.ora_sp_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
-                                                       ctypes.c_int]
+                                                       ctypes.c_int, P]
         L.ora_nn_forward.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P, ctypes.c_int, ctypes.c_int]
         L.ora_sp_rounds.argtypes = [P, ctypes.c_int]
         L.ora_sp_game_info.argtypes = [P, ctypes.c_int, P]
@@ -135,16 +135,32 @@ class Model:
             lib().ora_model_free(self.h)
 
 
+# PlaySettings the oracle takes, in ora_sp_create order, with the benchmark-mode
+# defaults of coffee_search_params_default.
+PLAY_SETTINGS = {
+    "cheap_search_prob": 0.0, "cheap_search_visits": 100, "cheap_search_target_weight": 0.0,
+    "reduce_visits": 0, "reduce_visits_threshold": 0.9, "reduce_visits_threshold_lookback": 3,
+    "reduced_visits_min": 100, "reduced_visits_weight": 0.1,
+    "policy_surprise_data_weight": 0.0, "value_surprise_data_weight": 0.0,
+}
+
+
 class Selfplay:
     """Round-synchronous self-play engine (select -> batched NN -> backup per round)."""
 
     def __init__(self, X, Y, W, games, max_visits, node_cap=2048, seed=1, slot_base=0, nn_mode=0, model=None,
-                 nn_threads=1, nn_cache_log2=0):
+                 nn_threads=1, nn_cache_log2=0, **play):
+        """play: PLAY_SETTINGS keywords (the device's coffee_search_params names)."""
         self.X, self.Y, self.W, self.games = X, Y, W, games
         self.A, self.P = X * Y, 4 * X * Y
         self.model = model
+        unknown = set(play) - set(PLAY_SETTINGS)
+        if unknown:
+            raise TypeError("unknown play settings: %s" % sorted(unknown))
+        self._play = np.array([play.get(k, d) for k, d in PLAY_SETTINGS.items()], np.float32)
         self.h = lib().ora_sp_create(X, Y, W, games, max_visits, node_cap, seed, slot_base, nn_mode,
-                                     model.h if model is not None else None, nn_threads, nn_cache_log2)
+                                     model.h if model is not None else None, nn_threads, nn_cache_log2,
+                                     ptr(self._play))
         if not self.h:
             raise RuntimeError("oracle selfplay create failed")
 

@@ -36,7 +36,7 @@ def test_header_and_exports_agree(L):
 
 
 def test_abi_version_and_defaults(L):
-    assert L.coffee_abi_version() == 101
+    assert L.coffee_abi_version() == 102
     p = kc.default_search_params()
     # cpp/configs/training/selfplay1.cfg values
     assert p.max_visits == 600
@@ -46,6 +46,10 @@ def test_abi_version_and_defaults(L):
     assert abs(p.root_dirichlet_noise_total_concentration - 10.83) < 1e-5
     assert abs(p.subtree_value_bias_factor - 0.3) < 1e-6
     assert p.root_num_symmetries_to_sample == 4 and p.use_graph_search == 1
+    # play settings default to the benchmark mode (one row per move at full visits)
+    assert p.cheap_search_prob == 0.0 and p.reduce_visits == 0
+    assert p.policy_surprise_data_weight == 0.0 and p.value_surprise_data_weight == 0.0
+    assert p.cheap_search_visits == 100 and p.reduced_visits_min == 100
 
 
 def test_invalid_arguments_fail_loudly(L):

@@ -149,17 +149,28 @@ def _sorted_rows(r):
     return {k: v[order] for k, v in r.items()}
 
 
+# selfplay1.cfg's play settings (cheap searches, reduced visits, surprise-weighted
+# rows) with the visit counts scaled to the test's max_visits
+PRODUCTION = dict(cheap_search_prob=0.75, cheap_search_visits=10, cheap_search_target_weight=0.0, reduce_visits=1,
+                  reduce_visits_threshold=0.9, reduce_visits_threshold_lookback=3, reduced_visits_min=10,
+                  reduced_visits_weight=0.1, policy_surprise_data_weight=0.5, value_surprise_data_weight=0.1)
+# reduceVisits alone, with a low threshold so the reduction triggers in these short games
+REDUCED = dict(reduce_visits=1, reduce_visits_threshold=0.2, reduced_visits_min=8, reduced_visits_weight=0.3)
+
+
 # cache_log2: 0 = no NN cache; 5 = a 32-entry cache, so slots are contended and
 # overwritten every round (the round-synchronous write order decides the contents);
-# 14 = hits across games (SPEC a7)
-@pytest.mark.parametrize("games,visits,rounds,seed,cache_log2",
-                         [(6, 40, 900, 3, 0), (4, 24, 700, 99, 0), (8, 40, 800, 3, 5), (12, 32, 700, 7, 14)])
-def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2):
+# 14 = hits across games (SPEC a7).  play: benchmark mode ({}) or selfplay1.cfg-like.
+@pytest.mark.parametrize("games,visits,rounds,seed,cache_log2,play",
+                         [(6, 40, 1200, 3, 0, {}), (4, 24, 900, 99, 0, {}), (8, 40, 1400, 3, 5, {}),
+                          (12, 32, 1000, 7, 14, {}), (8, 40, 1200, 11, 0, PRODUCTION), (8, 32, 1200, 5, 12, REDUCED)],
+                         ids=["bench-a", "bench-b", "cache32", "cache16k", "production", "reduced"])
+def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2, play):
     cap = 128
     gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,
-                      nn_cache_log2=cache_log2)
+                      nn_cache_log2=cache_log2, **play)
     ora = oracle.Selfplay(5, 5, 4, games=games, max_visits=visits, node_cap=cap, seed=seed,
-                          nn_cache_log2=cache_log2)
+                          nn_cache_log2=cache_log2, **play)
     done = 0
     for chunk in [1, 4, 20, rounds]:
         step = chunk - done

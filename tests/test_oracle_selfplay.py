@@ -79,3 +79,45 @@ def test_nn_cache_cuts_evaluations():
     assert len(ra["meta"]) > 0
     for k in ra:
         np.testing.assert_array_equal(ra[k], rb[k])
+
+
+def test_benchmark_mode_searches_every_move_from_a_cleared_tree():
+    # self-play clears the search before every move (play.cpp:1941-1946, :1009-1010),
+    # so each row's root has exactly max_visits visits (tree reuse would overshoot)
+    r = _run(7, rounds=900).rows()
+    assert len(r["meta"]) > 0
+    np.testing.assert_array_equal(r["globalTargetsNC"][:, 60], 24.0)
+
+
+PRODUCTION = dict(cheap_search_prob=0.75, cheap_search_visits=8, cheap_search_target_weight=0.0, reduce_visits=1,
+                  reduce_visits_threshold=0.9, reduce_visits_threshold_lookback=3, reduced_visits_min=8,
+                  reduced_visits_weight=0.1, policy_surprise_data_weight=0.5, value_surprise_data_weight=0.1)
+
+
+def test_production_play_settings():
+    """selfplay1.cfg play settings (visit counts scaled to max_visits 24): cheap searches
+    (rows only when surprising), reduced visits, surprise-weighted and resolved weights."""
+    sp = oracle.Selfplay(5, 5, 4, games=6, max_visits=24, node_cap=128, seed=21, **PRODUCTION)
+    sp.rounds(1500)
+    moves = sum(sp.info(g)["movesMade"] for g in range(6))
+    r = sp.rows()
+    meta, gt = r["meta"], r["globalTargetsNC"]
+    assert len(meta) > 0
+    visits = gt[:, 60]
+    assert visits.min() >= 8 and visits.max() <= 24
+    # most moves are cheap searches without rows: fewer rows than finished-game moves
+    finished_moves = sum(int(m[3]) for m in {(int(a[0]), int(a[1]), int(a[3])): a for a in meta}.values())
+    assert len(meta) < finished_moves <= moves
+    # a turn may be written several times (weight > 1); all copies carry the same targets
+    keys = [tuple(m[:3]) for m in meta]
+    for k in set(keys):
+        idx = [i for i, kk in enumerate(keys) if kk == k]
+        for i in idx[1:]:
+            np.testing.assert_array_equal(r["policyTargetsNCMove"][i], r["policyTargetsNCMove"][idx[0]])
+    assert np.all(meta[:, 2] < meta[:, 3])
+    # determinism
+    sp2 = oracle.Selfplay(5, 5, 4, games=6, max_visits=24, node_cap=128, seed=21, **PRODUCTION)
+    sp2.rounds(1500)
+    r2 = sp2.rows()
+    for k in r:
+        np.testing.assert_array_equal(r[k], r2[k])
