@@ -13,13 +13,20 @@ value = training rows/s over the timed steps for the whole job.  In benchmark mo
 committed; rows are emitted to the buffer when the game ends.  We count committed
 moves (= rows) in the window; rows actually drained in the window are reported too.
 
+Self-play clears the search tree before every move, as the reference does for
+self-play (play.cpp:1941-1946), so every row costs a full 600-visit search.
+
 All games start together and stay roughly in phase (a 5x5 game at 600 visits lasts
-about 9000 rounds), so rates swing over a game cycle: ~20k rows/s mid-game, ~40k at
-game ends, and a cache hit rate near 95% in the shared opening.  The defaults (10
-warm-up steps = 10k rounds, then 20 timed steps = 20k rounds) time more than two full
-game cycles after the first games have finished (tools/steady_state.py shows the
-trajectory); short --steps/--warmup values time a mid-game window, which
-underestimates the cycle average.
+about 11000 rounds), so rates swing by up to 2x from one 1000-round chunk to the next
+(tools/steady_state.py prints the trajectory).  The defaults (20 warm-up steps =
+20k rounds, then 60 timed steps = 60k rounds, about 5 game cycles) average the swings
+out: over 100k+ rounds the long-run rate is within a few percent of this window's.
+Short --steps/--warmup values time a partial cycle and can be off by 30%.
+
+The network batch is capped at one full wave of network workgroups (compute units x
+8 boards = 2048 rows; coffee_selfplay_config.nn_batch_cap): a launch's cost steps with
+its number of workgroup waves, so rows past the cap wait one round (round-robin, so no
+row waits long) instead of paying for a mostly idle second wave.
 
 The NN evaluation cache is on at the reference's own selfplay1.cfg size
 (nnCacheSizePowerOfTwo = 21, nneval.cpp:611-623): a search leaf whose state was
@@ -44,8 +51,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--games", type=int, default=4096)
     ap.add_argument("--visits", type=int, default=600)
     ap.add_argument("--arch", default="b6c96")
@@ -53,6 +60,8 @@ def parse():
     ap.add_argument("--commit-interval", type=int, default=8)
     ap.add_argument("--nn-cache-log2", type=int, default=21,
                     help="NN evaluation cache entries = 2^k (selfplay1.cfg nnCacheSizePowerOfTwo = 21); 0 = off")
+    ap.add_argument("--nn-batch-cap", type=int, default=0,
+                    help="rows per network launch (0 = one full wave of network workgroups)")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -120,7 +129,7 @@ def main():
 
     sp = kc.Selfplay(5, 5, 4, num_games=args.games, max_visits=args.visits, seed=args.seed,
                      slot_base=rank * args.games, model_path=model_path, commit_interval=args.commit_interval,
-                     nn_cache_log2=args.nn_cache_log2)
+                     nn_cache_log2=args.nn_cache_log2, nn_batch_cap=args.nn_batch_cap)
     for _ in range(args.warmup):
         sp.step(args.rounds_per_step)
     sp.sync()
@@ -212,6 +221,7 @@ def main():
             "config": {"workload": "C2: 5x5 connect-4, %d games/GPU, %d visits, b6c96 (fp16 MFMA)" % (args.games, args.visits),
                        "games_per_gpu": args.games, "visits": args.visits, "rounds_per_step": args.rounds_per_step,
                        "commit_interval": args.commit_interval, "nn_cache_log2": args.nn_cache_log2,
+                       "nn_batch_cap": args.nn_batch_cap or "one workgroup wave",
                        "parallelism": "game-sharded x%d" % world},
             "playouts_per_sec": playouts / elapsed,
             "nn_evals_per_sec": evals / elapsed,

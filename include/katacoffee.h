@@ -157,6 +157,9 @@ typedef struct coffee_selfplay_config {
   coffee_search_params search;
   int32_t nn_cache_log2; /* NN evaluation cache entries = 2^nn_cache_log2 (selfplay1.cfg
                             nnCacheSizePowerOfTwo = 21); 0 disables (SPEC a7) */
+  int32_t nn_batch_cap;  /* rows per network launch; leaves past it wait for the next round,
+                            ahead of new ones.  0 = one full wave of network workgroups
+                            (compute units x 8 boards: 2048 on MI355X) */
 } coffee_selfplay_config;
 
 typedef struct coffee_selfplay coffee_selfplay;

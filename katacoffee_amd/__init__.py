@@ -75,6 +75,7 @@ class SelfplayConfig(ctypes.Structure):
         ("model_path", ctypes.c_char_p),
         ("search", SearchParams),
         ("nn_cache_log2", ctypes.c_int32),
+        ("nn_batch_cap", ctypes.c_int32),
     ]
 
 
@@ -332,7 +333,7 @@ class Selfplay:
     """One device's self-play engine (games [slot_base, slot_base + num_games))."""
 
     def __init__(self, X=5, Y=5, W=4, num_games=4096, max_visits=600, seed=1, slot_base=0, model_path=None,
-                 node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, **search_over):
+                 node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, nn_batch_cap=0, **search_over):
         _torch_cuda()
         self.X, self.Y, self.W = X, Y, W
         self.A, self.P = X * Y, 4 * X * Y
@@ -347,6 +348,7 @@ class Selfplay:
         cfg.use_fake_net = 1 if model_path is None else 0
         cfg.commit_interval = commit_interval
         cfg.nn_cache_log2 = nn_cache_log2
+        cfg.nn_batch_cap = nn_batch_cap
         self._model = model_path.encode() if model_path else None
         cfg.model_path = self._model
         cfg.search = default_search_params(max_visits=max_visits, **search_over)

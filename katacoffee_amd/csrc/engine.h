@@ -23,6 +23,8 @@ const DTables* deviceTables(int X, int Y, int W);
 const DTables& hostTables(int X, int Y, int W);
 
 // ---- nn.hip ----
+// Boards per network workgroup (one workgroup per compute unit at a time).
+constexpr int NN_BOARDS_PER_WG = 8;
 // Offsets (elements) into the packed weight buffers; see nn.hip.
 constexpr int NN_MAX_BLOCKS = 16;
 struct NNLayout {

@@ -42,7 +42,7 @@ constexpr int NN_NT = NN_WAVES * 64;
 template <int X_, int Y_, int C_>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
-  static constexpr int NB = 8;
+  static constexpr int NB = NN_BOARDS_PER_WG;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
   // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): output

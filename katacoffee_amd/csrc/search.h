@@ -196,6 +196,9 @@ struct SearchDev {
   int32_t* nnNeed;       // [G] 1 when the game's row needs the network this round
   int32_t* nnIdx;        // [G] compacted rows to evaluate (kCompact)
   int32_t* nnCount;      // rows in nnIdx
+  int32_t* nnDefer;      // [G] 1: the row did not fit this round's batch (kCompact); the game waits
+  int nnCap;             // rows per network launch (batch cap: one full wave of network workgroups)
+  int32_t* nnRR;         // round-robin start of the next batch (kCompact)
   unsigned long long* nnTimedEvals;  // summed nnCount of the rounds whose network launch was timed
   // NN evaluation cache (SPEC a7): direct-mapped by state key, written between rounds
   uint32_t cacheMask;    // entries - 1 (0 with cacheOn == 0)

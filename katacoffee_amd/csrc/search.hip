@@ -742,6 +742,13 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   __shared__ GameDev s;
   SPROF_INIT();
   const unsigned long long t0 = SPROF_NOW();
+  if(d.nnDefer[g]) {
+    // the leaf from an earlier round still waits for the network (kCompact); the
+    // game state stays as it is
+    if(v.lane == 0)
+      d.nnNeed[g] = 1;
+    return;
+  }
   loadGame(v, s);
   if(s.phase == PH_COMMIT) {
     s.leafKind = LEAF_NONE;
@@ -1039,7 +1046,7 @@ template <int NI>
 __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
-  if(g >= d.G)
+  if(g >= d.G || d.nnDefer[g])  // a deferred leaf is backed up in a later round
     return;
   __shared__ __attribute__((aligned(16))) float scratch[2 * MAX_P];
   GV v(d, *Tp, g);
@@ -2262,32 +2269,56 @@ __global__ void __launch_bounds__(64) kCacheWrite(const SearchDev* __restrict__ 
   }
 }
 
-// kCompact: ascending list of the games whose row needs the network this round.
+// kCompact: the list of games whose row the network evaluates this round, at most
+// d.nnCap rows (one full wave of network workgroups: a launch's cost steps with its
+// number of workgroup waves).  The needing games are taken in cyclic game order from
+// the round-robin pointer *d.nnRR, which moves past the last game taken whenever the
+// cap bites, so a deferred row waits at most ceil(G / cap) rounds.  Rows past the cap
+// are deferred (nnDefer): their games keep their leaf and skip the next select.  The
+// oracle applies the same rule (ora_search.cpp selfplayRound).
 // accumulate != 0: the count is also added to *d.nnTimedEvals (sampled kernel timing).
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
-  __shared__ int part[1024];
+  __shared__ int partHi[1024], partLo[1024];
   const int t = threadIdx.x, per = (d.G + 1023) / 1024;
   const int lo = t * per, hi = min(d.G, lo + per);
-  int c = 0;
-  for(int i = lo; i < hi; i++)
-    c += d.nnNeed[i];
-  part[t] = c;
+  const int p = *d.nnRR;
+  int ch = 0, cl = 0;
+  for(int i = lo; i < hi; i++) {
+    const int need = d.nnNeed[i];
+    ch += i >= p ? need : 0;
+    cl += i < p ? need : 0;
+  }
+  partHi[t] = ch;
+  partLo[t] = cl;
   __syncthreads();
-  for(int off = 1; off < 1024; off <<= 1) {  // inclusive scan
-    const int v = t >= off ? part[t - off] : 0;
+  for(int off = 1; off < 1024; off <<= 1) {  // inclusive scans
+    const int vh = t >= off ? partHi[t - off] : 0, vl = t >= off ? partLo[t - off] : 0;
     __syncthreads();
-    part[t] += v;
+    partHi[t] += vh;
+    partLo[t] += vl;
     __syncthreads();
   }
-  int o = part[t] - c;
-  for(int i = lo; i < hi; i++)
-    if(d.nnNeed[i])
-      d.nnIdx[o++] = i;
+  const int totalHi = partHi[1023], total = totalHi + partLo[1023], cap = d.nnCap;
+  int oh = partHi[t] - ch, ol = totalHi + partLo[t] - cl;
+  for(int i = lo; i < hi; i++) {
+    if(!d.nnNeed[i]) {
+      d.nnDefer[i] = 0;
+      continue;
+    }
+    const int pos = i >= p ? oh++ : ol++;
+    const bool in = pos < cap;
+    if(in)
+      d.nnIdx[pos] = i;
+    d.nnDefer[i] = in ? 0 : 1;
+    if(total > cap && pos == cap - 1)
+      *d.nnRR = i + 1 < d.G ? i + 1 : 0;
+  }
   if(t == 1023) {
-    *d.nnCount = part[1023];
+    const int count = min(total, cap);
+    *d.nnCount = count;
     if(accumulate)
-      *d.nnTimedEvals += (unsigned long long)part[1023];
+      *d.nnTimedEvals += (unsigned long long)count;
   }
 }
 

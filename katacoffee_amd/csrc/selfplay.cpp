@@ -165,6 +165,18 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.rCount = devAlloc<unsigned long long>(owned_, 1);
   d.rDropped = devAlloc<unsigned long long>(owned_, 1);
   d.nnNeed = devAlloc<int32_t>(owned_, G);
+  d.nnDefer = devAlloc<int32_t>(owned_, G);
+  d.nnRR = devAlloc<int32_t>(owned_, 1);
+  if(c.nn_batch_cap < 0)
+    throw std::invalid_argument("nn_batch_cap must be >= 0");
+  if(c.nn_batch_cap > 0) {
+    d.nnCap = c.nn_batch_cap;
+  } else {
+    int dev = 0, cus = 0;
+    KC_HIP(hipGetDevice(&dev));
+    KC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    d.nnCap = std::max(1, cus) * NN_BOARDS_PER_WG;
+  }
   d.nnIdx = devAlloc<int32_t>(owned_, G);
   d.nnCount = devAlloc<int32_t>(owned_, 1);
   if(c.nn_cache_log2 < 0 || c.nn_cache_log2 > 26)
@@ -259,10 +271,11 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
       launchCompact(d, dd_, st, t1);
     }, t0);
     timed(1, st, [&] {
+      const int rows = std::min(d.G, d.nnCap);  // grid bound; the batch is *d.nnCount rows
       if(nn_)
-        nn_->forward(d.G, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
+        nn_->forward(rows, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
       else
-        launchFakeNet(T_, d.G, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
+        launchFakeNet(T_, rows, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
     }, t1);
     timed(2, st, [&] {
       launchBackup(d, dd_, st);

@@ -126,7 +126,7 @@ int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* 
 // reduce_visits_threshold_lookback, reduced_visits_min, reduced_visits_weight,
 // policy_surprise_data_weight, value_surprise_data_weight).
 void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
-                    int nnMode, void* model, int nnThreads, int cacheLog2, const float* play) {
+                    int nnMode, void* model, int nnThreads, int cacheLog2, const float* play, int nnCap) {
   if(!T.loaded)
     return nullptr;
   Selfplay* s = new Selfplay();
@@ -154,6 +154,8 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
   if(cacheLog2 < 0 || cacheLog2 > 26)
     return nullptr;
   cfg.cacheLog2 = cacheLog2;
+  if(nnCap > 0)
+    cfg.nnCap = nnCap;
   selfplayInit(*s, cfg, games);
   return s;
 }

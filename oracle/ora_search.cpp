@@ -1301,7 +1301,11 @@ void selfplayRound(Selfplay& s) {
   const Geom& g = s.cfg.g;
   const int G = (int)s.games.size();
   const int A = g.A;
-  std::vector<float> bin((size_t)G * NUM_SPATIAL * A), glob((size_t)G);
+  // encoded leaves, per game (a deferred leaf keeps its row across rounds)
+  std::vector<float>& bin = s.nnBin;
+  std::vector<float>& glob = s.nnGlob;
+  bin.resize((size_t)G * NUM_SPATIAL * A);
+  glob.resize((size_t)G);
   std::vector<int> need(G, 0);
   const bool cacheOn = s.cfg.cacheLog2 > 0;
   const uint32_t cacheMask = cacheOn ? (uint32_t)((1u << s.cfg.cacheLog2) - 1) : 0u;
@@ -1309,6 +1313,10 @@ void selfplayRound(Selfplay& s) {
   for(int i = 0; i < G; i++) {
     Game& gm = s.games[i];
     Ctx cx(s, gm);
+    if(gm.nnDeferred) {  // the leaf (already encoded) waits for the network
+      need[i] = 1;
+      continue;
+    }
     if(gm.phase == PH_ROOTEVAL) {
       if(gm.rootK == 0) {
         int idx[8] = {0, 1, 2, 3, 4, 5, 6, 7};
@@ -1343,10 +1351,27 @@ void selfplayRound(Selfplay& s) {
   }
   // ---- NN ----
   std::vector<float> out((size_t)G * (g.P + 4));
+  // the batch: needing games in cyclic order from the round-robin pointer, at most
+  // nnCap rows; the rest are deferred, and the pointer moves past the last game taken
+  // when the cap bites (device kCompact)
   std::vector<int> idx;
-  for(int i = 0; i < G; i++)
-    if(need[i])
+  int total = 0, lastTaken = -1;
+  for(int k = 0; k < G; k++) {
+    const int i = (s.nnRR + k) % G;
+    if(!need[i]) {
+      s.games[i].nnDeferred = 0;
+      continue;
+    }
+    total++;
+    const bool in = (int)idx.size() < s.cfg.nnCap;
+    s.games[i].nnDeferred = in ? 0 : 1;
+    if(in) {
       idx.push_back(i);
+      lastTaken = i;
+    }
+  }
+  if(total > s.cfg.nnCap)
+    s.nnRR = (lastTaken + 1) % G;
   if(s.cfg.nnMode == 0) {
     for(int i : idx)
       fakeNet(g, &bin[(size_t)i * NUM_SPATIAL * A], &out[(size_t)i * (g.P + 4)], &out[(size_t)i * (g.P + 4) + g.P],
@@ -1379,6 +1404,8 @@ void selfplayRound(Selfplay& s) {
   std::vector<CacheWrite> cacheWrites;  // fresh evaluations, in game order
   for(int i = 0; i < G; i++) {
     Game& gm = s.games[i];
+    if(gm.nnDeferred)  // backed up in the round its row is evaluated
+      continue;
     Ctx cx(s, gm);
     const float* o = &out[(size_t)i * (g.P + 4)];
     if(gm.leafKind == LEAF_ROOTEVAL) {

@@ -106,6 +106,7 @@ struct SelfplayCfg {
   const Model* model = nullptr;
   int nnThreads = 1;
   int cacheLog2 = 0;       // NN evaluation cache of 2^cacheLog2 entries, 0 = off (SPEC a7)
+  int nnCap = 1 << 30;     // rows per network batch; the rest wait for the next round (device kCompact)
 };
 
 struct Game {
@@ -136,6 +137,7 @@ struct Game {
   std::vector<uint8_t> svbUsed;
   // playout scratch
   int leafKind = LEAF_NONE, leafNode = -1, leafSym = 0, cacheSlot = 0;
+  int nnDeferred = 0;      // the leaf missed the previous batch and waits for the network
   Board leafBoard;
   std::vector<int> pathNode, pathSlot;
   // game record
@@ -156,6 +158,8 @@ struct Selfplay {
   // written once per round; SPEC a7): key pair, postprocessed policy row, white win/loss
   std::vector<uint64_t> cacheKey;
   std::vector<float> cachePol, cacheVal;
+  std::vector<float> nnBin, nnGlob;  // [G][15][A], [G]: each game's encoded leaf
+  int nnRR = 0;                      // round-robin start of the next network batch
 };
 
 void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames);

@@ -32,7 +32,7 @@ def lib():
         L.ora_model_load.restype = P
         L.ora_sp_create.restype = P
         L.ora_sp_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
-                                                       ctypes.c_int, P]
+                                                       ctypes.c_int, P, ctypes.c_int]
         L.ora_nn_forward.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P, ctypes.c_int, ctypes.c_int]
         L.ora_sp_rounds.argtypes = [P, ctypes.c_int]
         L.ora_sp_game_info.argtypes = [P, ctypes.c_int, P]
@@ -149,7 +149,7 @@ class Selfplay:
     """Round-synchronous self-play engine (select -> batched NN -> backup per round)."""
 
     def __init__(self, X, Y, W, games, max_visits, node_cap=2048, seed=1, slot_base=0, nn_mode=0, model=None,
-                 nn_threads=1, nn_cache_log2=0, **play):
+                 nn_threads=1, nn_cache_log2=0, nn_batch_cap=0, **play):
         """play: PLAY_SETTINGS keywords (the device's coffee_search_params names)."""
         self.X, self.Y, self.W, self.games = X, Y, W, games
         self.A, self.P = X * Y, 4 * X * Y
@@ -160,7 +160,7 @@ class Selfplay:
         self._play = np.array([play.get(k, d) for k, d in PLAY_SETTINGS.items()], np.float32)
         self.h = lib().ora_sp_create(X, Y, W, games, max_visits, node_cap, seed, slot_base, nn_mode,
                                      model.h if model is not None else None, nn_threads, nn_cache_log2,
-                                     ptr(self._play))
+                                     ptr(self._play), nn_batch_cap)
         if not self.h:
             raise RuntimeError("oracle selfplay create failed")
 

@@ -121,3 +121,16 @@ def test_production_play_settings():
     r2 = sp2.rows()
     for k in r:
         np.testing.assert_array_equal(r[k], r2[k])
+
+
+def test_batch_cap_defers_leaves_without_losing_them():
+    """A network batch cap (the device's one-wave kCompact cap) defers leaves to the
+    next round; every game still completes its searches and the rows stay well formed."""
+    sp = oracle.Selfplay(5, 5, 4, games=6, max_visits=24, node_cap=128, seed=9, nn_batch_cap=2)
+    sp.rounds(2500)
+    info = [sp.info(g) for g in range(6)]
+    assert all(i["gamesFinished"] > 0 for i in info)
+    r = sp.rows()
+    np.testing.assert_array_equal(r["globalTargetsNC"][:, 60], 24.0)
+    # with the cap, each round evaluates at most 2 leaves
+    assert sum(i["nnEvals"] for i in info) <= 2 * 2500 + 6

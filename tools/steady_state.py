@@ -17,12 +17,13 @@ def main():
     ap.add_argument("--chunk", type=int, default=1000)
     ap.add_argument("--chunks", type=int, default=30)
     ap.add_argument("--nn-cache-log2", type=int, default=21)
+    ap.add_argument("--nn-batch-cap", type=int, default=0)
     a = ap.parse_args()
     import katacoffee_amd as kc
     path = os.path.join(tempfile.mkdtemp(), "m.cfnn")
     kc.write_random_model("b6c96", 0xC0FFEE, path)
     sp = kc.Selfplay(5, 5, 4, num_games=a.games, max_visits=a.visits, seed=20250217, model_path=path,
-                     commit_interval=8, nn_cache_log2=a.nn_cache_log2)
+                     commit_interval=8, nn_cache_log2=a.nn_cache_log2, nn_batch_cap=a.nn_batch_cap)
     prev = sp.stats()
     for c in range(a.chunks):
         t0 = time.perf_counter()
