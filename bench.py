@@ -132,7 +132,7 @@ def main():
                      nn_cache_log2=args.nn_cache_log2, nn_batch_cap=args.nn_batch_cap)
     for _ in range(args.warmup):
         sp.step(args.rounds_per_step)
-    sp.sync()
+        sp.sync()  # bounded launch queue (a profiler's per-dispatch state stays small)
     s0 = sp.stats()
     sp.drain_rows()
     if not args.no_timing:

@@ -21,26 +21,28 @@ PROF = os.path.join(REPO, "profiles")
 
 
 def short(name):
-    for k in ["kNNForward", "kSelect", "kBackup", "kCommit", "kFakeNet", "kInit", "fillBuffer", "copyBuffer"]:
+    for k in ["kNNForward", "kSelect", "kBackup", "kCommit", "kRows", "kCacheWrite", "kCompact", "kFakeNet", "kInit",
+              "fillBuffer", "copyBuffer"]:
         if k in name:
             return k
     return name[:40]
 
 
 def pmc(path, counter):
-    agg = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        if r.get("Counter_Name") == counter:
-            agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    """Per-kernel average of `counter` from a reduced PMC pass (tools/reduce_profile.py)."""
+    red = json.load(open(path))
+    return {k: v[counter]["avg"] for k, v in red.items() if counter in v}
 
 
 def main():
     rnd = sys.argv[1]
     os.makedirs(PROF, exist_ok=True)
     shutil.copy(os.path.join(OUT, "prof_trace", "trace_kernel_stats.csv"), os.path.join(PROF, rnd + "_kernel_stats.csv"))
-    fetch = pmc(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write = pmc(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE")
+    fetch = pmc(os.path.join(OUT, "prof_fetch", "fetch_pmc_avg.json"), "FETCH_SIZE")
+    write = pmc(os.path.join(OUT, "prof_write", "write_pmc_avg.json"), "WRITE_SIZE")
+    dur = os.path.join(OUT, "prof_trace", "trace_durations.json")
+    if os.path.exists(dur):
+        shutil.copy(dur, os.path.join(PROF, rnd + "_kernel_durations.json"))
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         f_kb, w_kb = fetch.get(k, 0.0), write.get(k, 0.0)
