@@ -659,25 +659,43 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   NN_PHASE(53);
   float* plgT = reinterpret_cast<float*>(wl);
   float* l2T = plgT + 32 * 96;
+  float* w3 = l2T + 96 * L->v2;  // value / misc output weights [4][v2], then their 4 biases
   stageT96(plgT, WF + L->pLinG, 32, tid);
   stageT96(l2T, WF + L->vLin2, L->v2, tid);
+  {
+    const int v2 = L->v2;
+    for(int i = tid; i < 4 * v2 + 4; i += NN_NT) {
+      float w;
+      if(i < 2 * v2)
+        w = WF[L->vLin3 + i];
+      else if(i < 4 * v2)
+        w = WF[L->vLinM + i - 2 * v2];
+      else
+        w = i - 4 * v2 < 2 ? WF[L->vB3 + i - 4 * v2] : WF[L->vBM + i - 4 * v2 - 2];
+      w3[i] = w;
+    }
+  }
   poolBoards<G>(scr, actF, poolP, poolV, sqOff, tid);
   __syncthreads();
   NN_PHASE(54);
   linear96<G>(plgT, 32, poolP, biasS, 32, nullptr, false, tid);
   linear96<G>(l2T, L->v2, poolV, vh, 64, WF + L->vB2, true, tid);
   __syncthreads();
-  if(tid < G::NB * 4) {
-    const int b = tid >> 2, o = tid & 3;
-    if(b < nb) {
-      const int v2 = L->v2;
-      const float* w = o < 2 ? WF + L->vLin3 + o * v2 : WF + L->vLinM + (o - 2) * v2;
-      float s = o < 2 ? WF[L->vB3 + o] : WF[L->vBM + o - 2];
-#pragma unroll 4
-      for(int i = 0; i < v2; i++)
-        s += w[i] * vh[b * 64 + i];
+  {
+    // value (2) and misc (2) outputs: a 16-lane group per (board, output), each lane
+    // summing every 16th term, reduced across the group
+    static_assert(G::NB * 4 * 16 == NN_NT, "one 16-lane group per (board, output)");
+    const int k = tid & 15, o = (tid >> 4) & 3, b = tid >> 6;
+    const int v2 = L->v2;
+    float s = 0.0f;
+    for(int i = k; i < v2; i += 16)
+      s += w3[o * v2 + i] * vh[b * 64 + i];
+#pragma unroll
+    for(int m = 8; m >= 1; m >>= 1)
+      s += __shfl_xor(s, m, 64);
+    if(k == 0 && b < nb) {
       const int dst = rowIdx ? rowIdx[base + b] : base + b;
-      out[(size_t)dst * (G::P + 4) + G::P + o] = s;
+      out[(size_t)dst * (G::P + 4) + G::P + o] = s + w3[4 * v2 + o];
     }
   }
   NN_PHASE(42);

@@ -1931,7 +1931,7 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scra
 // TurnRec::rows times).  One 256-thread block per committed game; the boards after
 // every move, the row -> turn map and the final board's per-cell max runs are built
 // once in LDS, then wave w writes rows w, w + 4, ...
-constexpr int ROWS_WAVES = 4;
+constexpr int ROWS_WAVES = 8;
 __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __restrict__ dp,
                                                          const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
@@ -1950,14 +1950,21 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
   __shared__ int8_t finRun[MAX_AREA];
   __shared__ uint8_t hMask[2 * MAX_AREA];
   __shared__ uint8_t rowTurn[2 * MAX_AREA];
+  __shared__ uint8_t tCell[MAX_AREA], tDir[MAX_AREA], tRows[MAX_AREA];
   const int numMoves = f.numMoves, numRows = min(f.numRows, 2 * MAX_AREA);  // <= 2 numMoves by construction
   const int A = T.A, P = T.P, pb = (A + 7) / 8;
   const TurnRec* tr = v.turns();
   const float finalWin = f.winner == 2 ? 1.0f : (f.winner == 1 ? 0.0f : 0.5f);
+  // the turn records into LDS in parallel; the serial steps below then read LDS only
   for(int t = threadIdx.x; t < numMoves; t += 64 * ROWS_WAVES) {
-    tWin[t] = tr[t].whiteWin;
-    tLoss[t] = tr[t].whiteLoss;
+    const TurnRec rec = tr[t];
+    tWin[t] = rec.whiteWin;
+    tLoss[t] = rec.whiteLoss;
+    tCell[t] = (uint8_t)rec.cell;
+    tDir[t] = (uint8_t)rec.dir;
+    tRows[t] = rec.rows;
   }
+  __syncthreads();
   if(threadIdx.x == 0) {
     tWin[numMoves] = finalWin;
     tLoss[numMoves] = 1.0f - finalWin;
@@ -1965,12 +1972,12 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
     boardInit(T, b);
     boards[0] = b;
     for(int t = 0; t < numMoves; t++) {
-      applyMove(T, b, tr[t].cell, tr[t].dir);
+      applyMove(T, b, tCell[t], tDir[t]);
       boards[t + 1] = b;
     }
     int j = 0;
     for(int t = 0; t < numMoves; t++)
-      for(int c = 0; c < (int)tr[t].rows && j < 2 * MAX_AREA; c++)
+      for(int c = 0; c < (int)tRows[t] && j < 2 * MAX_AREA; c++)
         rowTurn[j++] = (uint8_t)t;
     // history-mask draws, in row order from the game's stream (the chain stops
     // drawing at its first failure, so the draws are consumed sequentially)
