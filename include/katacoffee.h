@@ -139,6 +139,11 @@ typedef struct coffee_search_params {
   float reduced_visits_weight;       /* 0.1 */
   float policy_surprise_data_weight; /* 0.5 */
   float value_surprise_data_weight;  /* 0.1 */
+  /* opening moves sampled from the raw policy before the searched game
+   * (initializeGameUsingPolicy playutils.cpp:147-176) */
+  int32_t init_games_with_policy;    /* 1 */
+  float policy_init_area_prop;       /* 0.04: mean number of moves / board area */
+  float policy_init_area_temperature;/* 1.0 */
 } coffee_search_params;
 
 void coffee_search_params_default(coffee_search_params* p);

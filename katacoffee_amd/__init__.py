@@ -63,6 +63,8 @@ class SearchParams(ctypes.Structure):
         ("reduce_visits_threshold", ctypes.c_float), ("reduce_visits_threshold_lookback", ctypes.c_int32),
         ("reduced_visits_min", ctypes.c_int32), ("reduced_visits_weight", ctypes.c_float),
         ("policy_surprise_data_weight", ctypes.c_float), ("value_surprise_data_weight", ctypes.c_float),
+        ("init_games_with_policy", ctypes.c_int32), ("policy_init_area_prop", ctypes.c_float),
+        ("policy_init_area_temperature", ctypes.c_float),
     ]
 
 

@@ -260,6 +260,9 @@ void coffee_search_params_default(coffee_search_params* p) {
   p->reduced_visits_weight = 0.1f;
   p->policy_surprise_data_weight = 0.0f;
   p->value_surprise_data_weight = 0.0f;
+  p->init_games_with_policy = 0;
+  p->policy_init_area_prop = 0.04f;
+  p->policy_init_area_temperature = 1.0f;
 }
 
 struct coffee_selfplay {

@@ -256,6 +256,9 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   getf("reducedVisitsWeight", p.reduced_visits_weight);
   getf("policySurpriseDataWeight", p.policy_surprise_data_weight);
   getf("valueSurpriseDataWeight", p.value_surprise_data_weight);
+  getb("initGamesWithPolicy", p.init_games_with_policy);
+  getf("policyInitAreaProp", p.policy_init_area_prop);
+  getf("policyInitAreaTemperature", p.policy_init_area_temperature);
 }
 
 struct RowSink {

@@ -31,7 +31,8 @@ enum LeafKind {
   LEAF_CATCHUP = 3,
   LEAF_NOCHILD = 4,
   LEAF_ROOTEVAL = 5,
-  LEAF_CACHED = 6  // NN output taken from the evaluation cache (SPEC a7)
+  LEAF_CACHED = 6,  // NN output taken from the evaluation cache (SPEC a7)
+  LEAF_INIT = 7     // policy-initialisation move: the root evaluated for a sampled opening move
 };
 
 // NN evaluation cache slot of a state key (SPEC a7; oracle ora_search.cpp cacheSlot).
@@ -39,7 +40,7 @@ KC_HD uint32_t cacheSlot(uint64_t k0, uint64_t k1, uint32_t mask) {
   const uint64_t h = k0 ^ ((k1 << 29) | (k1 >> 35));
   return (uint32_t)(h ^ (h >> 32)) & mask;
 }
-enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2, PH_INIT = 3 };
 
 // SearchParams (searchparams.h) restricted to Coffee self-play.
 struct SP {
@@ -69,6 +70,8 @@ struct SP {
   int reduceLookback, reducedMin;
   float reducedWeight;
   float policySurpriseWeight, valueSurpriseWeight;
+  int initPolicy;            // initGamesWithPolicy
+  float initAreaProp, initTemp;  // policyInitAreaProp, policyInitAreaTemperature
 };
 
 // The parameters of a cheap search whose rows are not recorded (runBotWithLimits
@@ -141,7 +144,7 @@ struct FinRec {
   uint64_t gameHash0, gameHash1;
   unsigned long long rowBase;
   int32_t numMoves, winner, gameNum, pending;  // pending 1: rows reserved at rowBase
-  int32_t numRows, pad;
+  int32_t numRows, startTurn;                  // startTurn: policy-initialisation moves before the searched ones
 };
 
 struct GameDev {
@@ -157,6 +160,8 @@ struct GameDev {
   int32_t noNoise;                // this move is a cheap search without recorded rows
   int32_t visitLimit;             // this move's maxVisits (getSearchLimitsThisMove)
   float moveWeight;               // this move's target weight
+  int32_t initLeft;               // policy-initialisation moves still to play (PH_INIT)
+  int32_t startTurn;              // policy-initialisation moves played (turns [0, startTurn) have no rows)
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;

@@ -762,7 +762,12 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   (void)t0;
   (void)t1;
   DRng rng = DRng{s.rngSeed, s.rngCtr};
-  if(s.phase == PH_ROOTEVAL) {
+  if(s.phase == PH_INIT) {
+    // policy-initialisation move: one evaluation of the root, random symmetry
+    s.leafKind = LEAF_INIT;
+    s.leafSym = (int)rng.below(8);
+    s.leaf = s.root;
+  } else if(s.phase == PH_ROOTEVAL) {
     if(s.rootK == 0) {
       // partial Fisher-Yates over 0..7, kept as packed nibbles (no dynamic register indexing)
       uint32_t idx = 0x76543210u;
@@ -795,7 +800,7 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   const unsigned long long t2 = SPROF_NOW();
   (void)t2;
   s.rngCtr = rng.ctr;
-  const bool needNN = s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL;
+  const bool needNN = s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT;
   if(v.lane == 0)
     d.nnNeed[g] = needNN ? 1 : 0;
   if(needNN) {
@@ -1042,6 +1047,90 @@ KC_D void buildOrder(const GV& v, int ni, const float (&pv)[NI], float* lds) {
 }
 
 // kBackup: NN post-processing + leaf value + path backup.
+KC_D bool setMoveLimits(const GV& v, GameDev& s, DRng& rng, float lastWL);
+KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scratch);
+KC_D void startGame(const GV& v, GameDev& s);
+
+// oracle initMove (getGameInitializationMove playutils.cpp:97-145 + the move of
+// initializeGameUsingPolicy :163-175): a move sampled from the root's post-processed
+// policy raised to 1/temperature (2e-4 of the time uniformly among the candidates),
+// played without search and recorded as a turn without rows.  Returns true when the
+// move ended the game (kCommit then finishes it).
+template <int NI>
+KC_D bool initMove(const GV& v, GameDev& s, const float* o, float* scratch /* LDS [2*MAX_P] */) {
+  const SP& b = v.d.sp;
+  const int P = v.d.P, A = v.T.A;
+  float* pol = scratch;
+  float w, l;
+  float pv[NI];
+  postprocess<NI>(v, s.root, s.leafSym, o, pol, w, l, scratch, pv);
+  waveSync();
+  // candidates in ascending policy position: legal with probability > 0
+  int* cpos = reinterpret_cast<int*>(scratch + MAX_P);
+  float* cval = scratch;  // overwrites pol in place: candidate i <= its position
+  int n = 0;
+  const float invT = 1.0f / b.initTemp;
+  for(int base = 0; base < P; base += 64) {
+    const int p = base + v.lane;
+    const float q = p < P ? pol[p] : -1.0f;
+    const bool ok = q > 0.0f;
+    const uint64_t m = ballot(ok);
+    waveSync();
+    if(ok) {
+      const int i = n + __popcll(m & ((1ULL << v.lane) - 1ULL));
+      cpos[i] = p;
+      cval[i] = b.initTemp == 1.0f ? q : dpow(q, invT);
+    }
+    n += __popcll(m);
+    waveSync();
+  }
+  DRng rng{s.rngSeed, s.rngCtr};
+  int idx = 0;
+  if(rng.uni() < 0.0002f) {
+    idx = (int)rng.below((uint32_t)n);
+  } else {
+    const float sum = seqSum(cval, n, v.lane);
+    const float dd = rng.uni() * sum;
+    idx = n - 1;
+    if(v.lane == 0) {
+      float acc = 0.0f;
+      for(int i = 0; i < n; i++) {
+        acc = acc + cval[i];
+        if(acc > dd) {
+          idx = i;
+          break;
+        }
+      }
+    }
+    idx = bcastI(idx, 0);
+  }
+  s.rngCtr = rng.ctr;
+  const int chosen = cpos[idx];
+  waveSync();
+  if(v.lane == 0) {
+    TurnRec rec;
+    memset(&rec, 0, sizeof(rec));
+    rec.cell = (int8_t)(chosen % A);
+    rec.dir = (int8_t)(chosen / A);
+    v.turns()[s.numTurns] = rec;
+  }
+  s.numTurns++;
+  s.startTurn++;
+  s.initLeft--;
+  playMoveWave(v.T, s.root, chosen % A, chosen / A);
+  waveSync();
+  if(s.root.finished)
+    return true;
+  if(s.initLeft == 0) {
+    DRng r2{s.rngSeed, s.rngCtr};
+    setMoveLimits(v, s, r2, 0.0f);
+    s.rngCtr = r2.ctr;
+    s.phase = PH_ROOTEVAL;
+    s.rootK = 0;
+  }
+  return false;
+}
+
 template <int NI>
 __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
@@ -1065,7 +1154,9 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
   const int P = d.P;
   const float* o = d.nnOut + (size_t)s.nnSlot * (P + 4);
   bool needCommit = false;
-  if(s.leafKind == LEAF_ROOTEVAL) {
+  if(s.leafKind == LEAF_INIT) {
+    needCommit = initMove<NI>(v, s, o, scratch);
+  } else if(s.leafKind == LEAF_ROOTEVAL) {
     float* pol = scratch;
     float w, l;
     float pv[NI];
@@ -1757,7 +1848,7 @@ KC_D bool setMoveLimits(const GV& v, GameDev& s, DRng& rng, float lastWL) {
       clear = false;
       s.noNoise = 1;
     }
-  } else if(b.reduceVisits && s.numTurns >= b.reduceLookback) {
+  } else if(b.reduceVisits && s.numTurns - s.startTurn >= b.reduceLookback) {
     const TurnRec* tr = v.turns();
     float mn = 1e20f, mx = -1e20f;
     for(int j = 0; j < b.reduceLookback; j++) {
@@ -1789,9 +1880,24 @@ KC_D void startGame(const GV& v, GameDev& s) {
   DRng rng{s.rngSeed, s.rngCtr};
   s.gameHash0 = rng.next();
   s.gameHash1 = rng.next();
-  setMoveLimits(v, s, rng, 0.0f);
+  // initializeGameUsingPolicy (playutils.cpp:147-176): floor(Exp(1) * area * prop)
+  // opening moves sampled from the raw policy (nextExponential rand.h:299-305)
+  s.startTurn = 0;
+  s.initLeft = 0;
+  const SP& b = v.d.sp;
+  if(b.initPolicy && b.initAreaProp > 0.0f) {
+    float u = rng.uni();
+    while(u <= 0.0f)
+      u = rng.uni();
+    s.initLeft = (int)floorf(-dlog(u) * ((float)v.T.A * b.initAreaProp));
+  }
+  if(s.initLeft > 0) {
+    s.phase = PH_INIT;
+  } else {
+    setMoveLimits(v, s, rng, 0.0f);
+    s.phase = PH_ROOTEVAL;
+  }
   s.rngCtr = rng.ctr;
-  s.phase = PH_ROOTEVAL;
   s.rootK = 0;
   s.leafKind = LEAF_NONE;
 }
@@ -1806,7 +1912,7 @@ KC_D void startGame(const GV& v, GameDev& s) {
 // Returns the game's number of rows.
 KC_D int resolveTurnWeights(const GV& v, const GameDev& s, DRng& rng, float* vs /* LDS [MAX_AREA] */) {
   const SP& b = v.d.sp;
-  const int n = s.numTurns, A = v.T.A;
+  const int n = s.numTurns, t0 = s.startTurn, A = v.T.A;  // searched turns [t0, n)
   TurnRec* tr = v.turns();
   const float finalWin = s.root.winner == 2 ? 1.0f : (s.root.winner == 1 ? 0.0f : 0.5f);
   float psdw = b.policySurpriseWeight, vsdw = b.valueSurpriseWeight;
@@ -1816,7 +1922,7 @@ KC_D int resolveTurnWeights(const GV& v, const GameDev& s, DRng& rng, float* vs 
     if(v.lane == 0) {
       const float nowFactor = 1.0f / (1.0f + (float)A * 0.016f);
       float winV = finalWin, lossV = 1.0f - finalWin;
-      for(int i = n - 1; i >= 0; i--) {
+      for(int i = n - 1; i >= t0; i--) {
         winV = winV + nowFactor * (tr[i].whiteWin - winV);
         lossV = lossV + nowFactor * (tr[i].whiteLoss - lossV);
         float x = 0.0f;
@@ -1831,7 +1937,7 @@ KC_D int resolveTurnWeights(const GV& v, const GameDev& s, DRng& rng, float* vs 
     }
     waveSync();
     float sumPS = 0.0f, sumVS = 0.0f;
-    for(int i = 0; i < n; i++) {
+    for(int i = t0; i < n; i++) {
       const float tw = tr[i].targetWeight;
       sumW = sumW + tw;
       sumPS = sumPS + tr[i].policySurprise * tw;
@@ -1843,7 +1949,7 @@ KC_D int resolveTurnWeights(const GV& v, const GameDev& s, DRng& rng, float* vs 
       if(avgVS < 0.010f)
         vsdw = vsdw * (avgVS / 0.010f);
       thr = avgPS * 1.5f;
-      for(int i = 0; i < n; i++) {
+      for(int i = t0; i < n; i++) {
         const float tw = tr[i].targetWeight, ps = tr[i].policySurprise;
         sumPPV = sumPPV + (tw * ps + (1.0f - tw) * fmaxf(0.0f, ps - thr));
         sumVPV = sumVPV + tw * vs[i];
@@ -1853,7 +1959,7 @@ KC_D int resolveTurnWeights(const GV& v, const GameDev& s, DRng& rng, float* vs 
     }
   }
   int total = 0;
-  for(int i = 0; i < n; i++) {
+  for(int i = t0; i < n; i++) {
     float w = tr[i].targetWeight;
     if(reweight) {
       const float ps = tr[i].policySurprise;
@@ -1920,6 +2026,7 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scra
     f->rowBase = base;
     f->numMoves = numMoves;
     f->numRows = numRows;
+    f->startTurn = s.startTurn;
     f->winner = s.root.winner;
     f->gameNum = s.gameNum;
     f->pending = fits && numRows > 0 ? 1 : 0;
@@ -2068,6 +2175,8 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
       gval = (float)((f.gameHash1 >> 44) & 0xFFFFF);
     } else if(li == 51) {
       gval = (float)t;
+    } else if(li == 53) {
+      gval = (float)f.startTurn;
     } else if(li == 57) {
       gval = pla == 2 ? tr[t].rawWhiteWL : -tr[t].rawWhiteWL;
     } else if(li == 59) {
@@ -2121,6 +2230,17 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   const SP& sp = d.sp;
   const int P = d.P, A = d.A;
   DRng rng{s.rngSeed, s.rngCtr};
+  if(s.root.finished) {
+    // a policy-initialisation move ended the game: nothing was searched, no rows
+    // (the reference's main loop does not run, play.cpp:1262-1264)
+    finishGameRecord(v, s, rng, reinterpret_cast<float*>(lds) + 2 * MAX_P);
+    s.gamesFinished++;
+    s.gameNum++;
+    startGame(v, s);
+    waveSync();
+    storeGame(v, s);
+    return;
+  }
   // move choice: self-play disables LCB here (runBotWithLimits play.cpp:1040-1046)
   int n = playSelectionValues<NI>(v, *v.sp, s, 0.0f, true, posv, vals, false);
   if(n <= 0) {

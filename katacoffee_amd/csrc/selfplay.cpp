@@ -58,6 +58,9 @@ SP toSP(const coffee_search_params& p) {
   s.reducedWeight = p.reduced_visits_weight;
   s.policySurpriseWeight = p.policy_surprise_data_weight;
   s.valueSurpriseWeight = p.value_surprise_data_weight;
+  s.initPolicy = p.init_games_with_policy;
+  s.initAreaProp = p.policy_init_area_prop;
+  s.initTemp = p.policy_init_area_temperature;
   return s;
 }
 
@@ -92,6 +95,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
      !unit(sp.policy_surprise_data_weight) || !unit(sp.value_surprise_data_weight) ||
      sp.policy_surprise_data_weight + sp.value_surprise_data_weight > 1.0f)
     throw std::invalid_argument("play settings: probabilities and weights in [0, 1], surprise weights sum <= 1");
+  if(sp.init_games_with_policy && (!unit(sp.policy_init_area_prop) || sp.policy_init_area_temperature < 0.1f ||
+                                   sp.policy_init_area_temperature > 5.0f))
+    throw std::invalid_argument("policy_init_area_prop in [0, 1], policy_init_area_temperature in [0.1, 5]");
   const DTables& ht = hostTables(c.x, c.y, c.win_len);
   T_ = deviceTables(c.x, c.y, c.win_len);
   commitInterval_ = c.commit_interval > 0 ? c.commit_interval : 8;

@@ -121,10 +121,11 @@ int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* 
   return 0;
 }
 
-// play: NULL or the 10 play settings in coffee_search_params order (cheap_search_prob,
+// play: NULL or the 13 play settings in coffee_search_params order (cheap_search_prob,
 // cheap_search_visits, cheap_search_target_weight, reduce_visits, reduce_visits_threshold,
 // reduce_visits_threshold_lookback, reduced_visits_min, reduced_visits_weight,
-// policy_surprise_data_weight, value_surprise_data_weight).
+// policy_surprise_data_weight, value_surprise_data_weight, init_games_with_policy,
+// policy_init_area_prop, policy_init_area_temperature).
 void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
                     int nnMode, void* model, int nnThreads, int cacheLog2, const float* play, int nnCap) {
   if(!T.loaded)
@@ -144,6 +145,9 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
     cfg.sp.reducedVisitsWeight = play[7];
     cfg.sp.policySurpriseDataWeight = play[8];
     cfg.sp.valueSurpriseDataWeight = play[9];
+    cfg.sp.initGamesWithPolicy = (int)play[10];
+    cfg.sp.policyInitAreaProp = play[11];
+    cfg.sp.policyInitAreaTemperature = play[12];
   }
   cfg.nodeCap = nodeCap;
   cfg.seed = seed;

@@ -922,7 +922,7 @@ struct Ctx {
         clear = false;
         gm.noNoise = 1;
       }
-    } else if(b.reduceVisits && (int)gm.turns.size() >= b.reduceVisitsThresholdLookback) {
+    } else if(b.reduceVisits && (int)gm.turns.size() - gm.startTurn >= b.reduceVisitsThresholdLookback) {
       float mn = 1e20f, mx = -1e20f;
       for(int j = 0; j < b.reduceVisitsThresholdLookback; j++) {
         const float w = gm.turns[gm.turns.size() - 1 - j].rootWL;
@@ -952,9 +952,80 @@ struct Ctx {
     gm.turns.clear();
     gm.gameHash0 = gm.rng.next();
     gm.gameHash1 = gm.rng.next();
-    setMoveLimits();
-    gm.phase = PH_ROOTEVAL;
+    // initializeGameUsingPolicy (playutils.cpp:147-176): floor(Exp(1) * area * prop)
+    // opening moves (nextExponential rand.h:299-305)
+    gm.startTurn = 0;
+    gm.initLeft = 0;
+    const SearchParams& b = s.cfg.sp;
+    if(b.initGamesWithPolicy && b.policyInitAreaProp > 0.0f) {
+      float u = gm.rng.uni();
+      while(u <= 0.0f)
+        u = gm.rng.uni();
+      gm.initLeft = (int)floorf(-kLogf(u) * ((float)g.A * b.policyInitAreaProp));
+    }
+    if(gm.initLeft > 0) {
+      gm.phase = PH_INIT;
+    } else {
+      setMoveLimits();
+      gm.phase = PH_ROOTEVAL;
+    }
     gm.rootK = 0;
+  }
+
+  // getGameInitializationMove (playutils.cpp:97-145) + the move of
+  // initializeGameUsingPolicy (:163-175): a move sampled from the root's
+  // post-processed policy raised to 1/temperature (2e-4 of the time uniformly among
+  // the candidates), played without search, recorded as a turn without rows.
+  // Returns true when the move ended the game.
+  bool initMove(const float* out) {
+    const SearchParams& b = s.cfg.sp;
+    float pol[MAX_P], w, l;
+    postprocess(gm.root, gm.leafSym, out, pol, w, l);
+    int cpos[MAX_P];
+    float cval[MAX_P];
+    int n = 0;
+    const float invT = 1.0f / b.policyInitAreaTemperature;
+    for(int p = 0; p < g.P; p++)
+      if(pol[p] > 0.0f) {
+        cpos[n] = p;
+        cval[n] = b.policyInitAreaTemperature == 1.0f ? pol[p] : kPowf(pol[p], invT);
+        n++;
+      }
+    int idx;
+    if(gm.rng.uni() < 0.0002f) {
+      idx = (int)gm.rng.below((uint32_t)n);
+    } else {
+      float sum = 0.0f;
+      for(int i = 0; i < n; i++)
+        sum = sum + cval[i];
+      const float dd = gm.rng.uni() * sum;
+      idx = n - 1;
+      float acc = 0.0f;
+      for(int i = 0; i < n; i++) {
+        acc = acc + cval[i];
+        if(acc > dd) {
+          idx = i;
+          break;
+        }
+      }
+    }
+    const int chosen = cpos[idx];
+    TurnRec tr{};
+    tr.cell = (int8_t)(chosen % g.A);
+    tr.dir = (int8_t)(chosen / g.A);
+    tr.policyTarget.assign(g.P, 0);
+    gm.turns.push_back(tr);
+    gm.startTurn++;
+    gm.initLeft--;
+    playMove(g, gm.root, chosen % g.A, chosen / g.A);
+    if(gm.root.finished)
+      return true;
+    if(gm.initLeft == 0) {
+      setMoveLimits();
+      gm.phase = PH_ROOTEVAL;
+      gm.rootK = 0;
+    }
+    return false;
   }
 
   void finishGame();
@@ -1068,14 +1139,14 @@ static void packBitsBE(const float* v, int len, uint8_t* out) {
 // Play::runGame row weights: value surprise (play.cpp:1470-1497), surprise-weighted
 // target weights (:1498-1574) and their probabilistic resolution (:1683-1697), in f32
 // with the loops' own order.  Fills turns[].rows.
-static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec>& turns, const float* tWin,
+static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec>& turns, int t0, const float* tWin,
                                const float* tLoss, Rng& rng) {
-  const int n = (int)turns.size();
+  const int n = (int)turns.size();  // searched turns [t0, n)
   if(b.policySurpriseDataWeight > 0.0f || b.valueSurpriseDataWeight > 0.0f) {
     std::vector<float> vs(n);
     const float nowFactor = 1.0f / (1.0f + (float)A * 0.016f);
     float winV = tWin[n], lossV = tLoss[n];
-    for(int i = n - 1; i >= 0; i--) {
+    for(int i = n - 1; i >= t0; i--) {
       winV = winV + nowFactor * (tWin[i] - winV);
       lossV = lossV + nowFactor * (tLoss[i] - lossV);
       float v = 0.0f;
@@ -1088,7 +1159,7 @@ static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec
       vs[i] = std::min(v, 1.0f);
     }
     float sumW = 0.0f, sumPS = 0.0f, sumVS = 0.0f;
-    for(int i = 0; i < n; i++) {
+    for(int i = t0; i < n; i++) {
       const float tw = turns[i].targetWeight;
       sumW = sumW + tw;
       sumPS = sumPS + turns[i].policySurprise * tw;
@@ -1101,14 +1172,14 @@ static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec
         vsdw = vsdw * (avgVS / 0.010f);
       const float thr = avgPS * 1.5f;
       float sumPPV = 0.0f, sumVPV = 0.0f;
-      for(int i = 0; i < n; i++) {
+      for(int i = t0; i < n; i++) {
         const float tw = turns[i].targetWeight, ps = turns[i].policySurprise;
         sumPPV = sumPPV + (tw * ps + (1.0f - tw) * std::max(0.0f, ps - thr));
         sumVPV = sumVPV + tw * vs[i];
       }
       sumPPV = std::max(sumPPV, 1e-10f);
       sumVPV = std::max(sumVPV, 1e-10f);
-      for(int i = 0; i < n; i++) {
+      for(int i = t0; i < n; i++) {
         const float tw = turns[i].targetWeight, ps = turns[i].policySurprise;
         const float ppv = tw * ps + (1.0f - tw) * std::max(0.0f, ps - thr);
         const float vpv = tw * vs[i];
@@ -1117,7 +1188,7 @@ static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec
       }
     }
   }
-  for(int i = 0; i < n; i++) {
+  for(int i = t0; i < n; i++) {
     float w = turns[i].targetWeight;
     if(w <= 0.0f)
       w = 0.0f;
@@ -1150,7 +1221,7 @@ void Ctx::finishGame() {
   int8_t finalMaxLen[MAX_AREA];
   for(int c = 0; c < A; c++)
     finalMaxLen[c] = fin.c[c] == 0 ? 0 : (int8_t)maxRun(g, fin, c);
-  resolveTurnWeights(s.cfg.sp, A, gm.turns, tWin.data(), tLoss.data(), gm.rng);
+  resolveTurnWeights(s.cfg.sp, A, gm.turns, gm.startTurn, tWin.data(), tLoss.data(), gm.rng);
   std::vector<int> rowTurn;  // turn of each row, in row order
   for(int t = 0; t < numMoves; t++)
     for(int c = 0; c < gm.turns[t].rows; c++)
@@ -1233,6 +1304,7 @@ void Ctx::finishGame() {
     gt[45] = (float)((gm.gameHash1 >> 22) & 0x3FFFFF);
     gt[46] = (float)((gm.gameHash1 >> 44) & 0xFFFFF);
     gt[51] = (float)t;
+    gt[53] = (float)gm.startTurn;
     gt[57] = pla == 2 ? gm.turns[t].rawWhiteWL : -gm.turns[t].rawWhiteWL;
     gt[59] = gm.turns[t].rawPolicyEntropy;
     gt[60] = (float)gm.turns[t].visits;
@@ -1317,7 +1389,11 @@ void selfplayRound(Selfplay& s) {
       need[i] = 1;
       continue;
     }
-    if(gm.phase == PH_ROOTEVAL) {
+    if(gm.phase == PH_INIT) {
+      gm.leafKind = LEAF_INIT;
+      gm.leafSym = (int)gm.rng.below(8);
+      gm.leafBoard = gm.root;
+    } else if(gm.phase == PH_ROOTEVAL) {
       if(gm.rootK == 0) {
         int idx[8] = {0, 1, 2, 3, 4, 5, 6, 7};
         for(int k = 0; k < 4; k++) {
@@ -1343,7 +1419,7 @@ void selfplayRound(Selfplay& s) {
       if(gm.leafKind == LEAF_NN)
         gm.leafSym = (int)gm.rng.below(8);
     }
-    if(gm.leafKind == LEAF_NN || gm.leafKind == LEAF_ROOTEVAL) {
+    if(gm.leafKind == LEAF_NN || gm.leafKind == LEAF_ROOTEVAL || gm.leafKind == LEAF_INIT) {
       encodeV1(g, gm.leafBoard, gm.leafSym, &bin[(size_t)i * NUM_SPATIAL * A], &glob[i]);
       need[i] = 1;
       gm.nnEvals++;
@@ -1408,6 +1484,15 @@ void selfplayRound(Selfplay& s) {
       continue;
     Ctx cx(s, gm);
     const float* o = &out[(size_t)i * (g.P + 4)];
+    if(gm.leafKind == LEAF_INIT) {
+      if(cx.initMove(o)) {  // the opening ended the game: nothing searched, no rows
+        cx.finishGame();
+        gm.gamesFinished++;
+        gm.gameNum++;
+        cx.startGame();
+      }
+      continue;
+    }
     if(gm.leafKind == LEAF_ROOTEVAL) {
       float pol[MAX_P], w, l;
       cx.postprocess(gm.root, gm.leafSym, o, pol, w, l);

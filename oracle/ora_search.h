@@ -39,6 +39,9 @@ struct SearchParams {
   float reducedVisitsWeight = 0.1f;      // 0.1
   float policySurpriseDataWeight = 0.0f; // 0.5
   float valueSurpriseDataWeight = 0.0f;  // 0.1
+  int initGamesWithPolicy = 0;           // true
+  float policyInitAreaProp = 0.04f;      // 0.04
+  float policyInitAreaTemperature = 1.0f;
 };
 
 // The search parameters of a cheap search whose rows are not recorded
@@ -70,8 +73,8 @@ struct Node {
 };
 
 enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5,
-               LEAF_CACHED = 6 };
-enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1 };
+               LEAF_CACHED = 6, LEAF_INIT = 7 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_INIT = 3 };
 
 struct TurnRec {
   int8_t cell, dir;
@@ -123,6 +126,8 @@ struct Game {
   // this move's search limits (getSearchLimitsThisMove play.cpp:871-1004)
   int visitLimit = 0, noNoise = 0;
   float moveWeight = 1.0f;
+  // policy-initialisation moves (initializeGameUsingPolicy playutils.cpp:147-176)
+  int initLeft = 0, startTurn = 0;
   // tree
   int nodeCount = 0, rootIdx = -1;
   std::vector<Node> nodes;

@@ -142,6 +142,7 @@ PLAY_SETTINGS = {
     "reduce_visits": 0, "reduce_visits_threshold": 0.9, "reduce_visits_threshold_lookback": 3,
     "reduced_visits_min": 100, "reduced_visits_weight": 0.1,
     "policy_surprise_data_weight": 0.0, "value_surprise_data_weight": 0.0,
+    "init_games_with_policy": 0, "policy_init_area_prop": 0.04, "policy_init_area_temperature": 1.0,
 }
 
 

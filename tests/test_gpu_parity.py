@@ -165,9 +165,12 @@ REDUCED = dict(reduce_visits=1, reduce_visits_threshold=0.2, reduced_visits_min=
                          [(6, 40, 1200, 3, 0, {}), (4, 24, 900, 99, 0, {}), (8, 40, 1400, 3, 5, {}),
                           (12, 32, 1000, 7, 14, {}), (8, 40, 1200, 11, 0, PRODUCTION), (8, 32, 1200, 5, 12, REDUCED),
                           (10, 32, 1400, 13, 12, dict(nn_batch_cap=3)),
-                          (8, 32, 1400, 17, 5, dict(PRODUCTION, nn_batch_cap=2))],
+                          (8, 32, 1400, 17, 5, dict(PRODUCTION, nn_batch_cap=2)),
+                          (8, 32, 1200, 19, 12, dict(PRODUCTION, init_games_with_policy=1)),
+                          (8, 24, 1200, 23, 0, dict(init_games_with_policy=1, policy_init_area_prop=0.3,
+                                                    policy_init_area_temperature=2.0))],
                          ids=["bench-a", "bench-b", "cache32", "cache16k", "production", "reduced", "batch-cap",
-                              "production-cap"])
+                              "production-cap", "production-init", "policy-init"])
 def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2, play):
     cap = 128
     gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,

@@ -134,3 +134,24 @@ def test_batch_cap_defers_leaves_without_losing_them():
     np.testing.assert_array_equal(r["globalTargetsNC"][:, 60], 24.0)
     # with the cap, each round evaluates at most 2 leaves
     assert sum(i["nnEvals"] for i in info) <= 2 * 2500 + 6
+
+
+def test_policy_init_openings():
+    """initGamesWithPolicy: games open with floor(Exp(1) * A * prop) unsearched policy
+    moves; their turns carry no rows and the rows record the start turn (gt[53])."""
+    sp = oracle.Selfplay(5, 5, 4, games=6, max_visits=16, node_cap=128, seed=31, init_games_with_policy=1,
+                         policy_init_area_prop=0.3)
+    sp.rounds(1500)
+    r = sp.rows()
+    meta, gt = r["meta"], r["globalTargetsNC"]
+    assert len(meta) > 0
+    start = gt[:, 53]
+    assert start.max() > 0                       # some games opened with policy moves
+    np.testing.assert_array_equal(gt[:, 51], meta[:, 2])  # turn index is absolute
+    assert np.all(meta[:, 2] >= start)           # no row for an opening move
+    np.testing.assert_array_equal(gt[:, 60], 16.0)
+    # every game contributes one row per searched turn (benchmark weights)
+    for slot, gnum in {(int(m[0]), int(m[1])) for m in meta}:
+        sel = (meta[:, 0] == slot) & (meta[:, 1] == gnum)
+        t0 = int(start[sel][0])
+        np.testing.assert_array_equal(np.sort(meta[sel, 2]), np.arange(t0, meta[sel, 3][0]))
