@@ -350,9 +350,12 @@ KC_D float cdfT(const DTables& T, float z) {
 }
 
 // oracle recompute (recomputeNodeStats searchupdatehelpers.cpp:151-328 +
-// downweightBadChildrenAndNormalizeWeight :330-419)
+// downweightBadChildrenAndNormalizeWeight :330-419), after the path edge `slot` gained
+// a visit (the oracle's EV(pn, slot) += 1): the lane holding that edge adds it and
+// stores it back, so the increment rides on the edge load instead of costing a
+// dependent round trip of its own.  The node's SVB sums are loaded with the node.
 template <int NI>
-KC_D void recompute(const GV& v, const GameDev& s, int ni, int numVisitsToAdd, bool isRoot) {
+KC_D void recompute(const GV& v, const GameDev& s, int ni, int slot, int numVisitsToAdd, bool isRoot) {
   const SP& sp = *v.sp;
   Node* np = &v.nodes()[ni];
   const int k = np->numChildren;
@@ -361,8 +364,15 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int numVisitsToAdd, b
   const float nnWin = np->nnWin, nnLoss = np->nnLoss;
   const float lastSvbDelta = np->lastSvbDelta, lastSvbWeight = np->lastSvbWeight;
   const uint32_t visits0 = np->visits;
-  const Edge* E = v.edges(ni);
+  Edge* E = v.edges(ni);
   const Node* NS = v.nodes();
+  const bool svbOn = sp.svbFactor != 0.0f && svbEntry >= 0;
+  const size_t svbE = v.svbBase(s.svbSel) + (svbOn ? svbEntry : 0);
+  int64_t svbD0 = 0, svbW0 = 0;
+  if(svbOn) {
+    svbD0 = v.d.svbD[svbE];
+    svbW0 = v.d.svbW[svbE];
+  }
   bool good[NI];
   float wAdj[NI], selfU[NI], cU[NI], cUsq[NI], cWl[NI], cWs[NI], cWsq[NI], tmp[NI];
   int numGood = 0;
@@ -374,6 +384,10 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int numVisitsToAdd, b
     wAdj[j] = selfU[j] = cU[j] = cUsq[j] = cWl[j] = cWs[j] = cWsq[j] = 0.0f;
     if(i < k) {
       Edge e = E[i];
+      if(i == slot) {
+        e.visits += 1;
+        E[i].visits = e.visits;
+      }
       const Node& c = NS[e.child];
       uint32_t cv = c.visits;
       float ws = c.weightSum;
@@ -448,9 +462,9 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int numVisitsToAdd, b
   float wl = nnWin - nnLoss;
   float utility = wl;
   float newLastD = lastSvbDelta, newLastW = lastSvbWeight;
-  if(sp.svbFactor != 0.0f && svbEntry >= 0) {
-    size_t e = v.svbBase(s.svbSel) + svbEntry;
-    int64_t D = v.d.svbD[e], Wt = v.d.svbW[e];
+  if(svbOn) {
+    const size_t e = svbE;
+    int64_t D = svbD0, Wt = svbW0;
     if(currentTotal > 1e-10f) {
       float utilityChildren = utilitySum / currentTotal;
       float svbWv = dpow(origTotal, sp.svbExp);
@@ -1277,13 +1291,13 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
     const int32_t* ps = v.pathSlot();
     const unsigned long long tp0 = SPROF_NOW();
     (void)tp0;
+    // the path in registers (lane j holds level j; levels >= 64 re-read), one load
+    const int myNode = v.lane < s.pathLen ? pn[v.lane] : 0, mySlot = v.lane < s.pathLen ? ps[v.lane] : 0;
     for(int j = s.pathLen - 1; j >= 0; j--) {
-      const int node = pn[j], slot = ps[j];
+      const int node = j < 64 ? __shfl(myNode, j, 64) : pn[j];
+      const int slot = j < 64 ? __shfl(mySlot, j, 64) : ps[j];
       waveSync();
-      if(v.lane == 0)
-        v.edges(node)[slot].visits += 1;
-      waveSync();
-      recompute<NI>(v, s, node, 1, node == s.rootIdx);
+      recompute<NI>(v, s, node, slot, 1, node == s.rootIdx);
     }
     tPath = SPROF_NOW() - tp0;
     s.playouts++;
