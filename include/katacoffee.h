@@ -144,6 +144,15 @@ typedef struct coffee_search_params {
   int32_t init_games_with_policy;    /* 1 */
   float policy_init_area_prop;       /* 0.04: mean number of moves / board area */
   float policy_init_area_temperature;/* 1.0 */
+  /* forks (Play::maybeForkGame play.cpp:1741-1840): after a game, with these
+   * probabilities the slot's next game starts from a replayed position of it plus the
+   * best (by the value head) of a few random legal moves */
+  float early_fork_game_prob;            /* 0.04 */
+  float early_fork_game_expected_move_prop; /* 0.025 */
+  float fork_game_prob;                  /* 0.01 */
+  int32_t fork_game_min_choices;         /* 3 */
+  int32_t early_fork_game_max_choices;   /* 12 */
+  int32_t fork_game_max_choices;         /* 36 */
 } coffee_search_params;
 
 void coffee_search_params_default(coffee_search_params* p);

@@ -65,6 +65,9 @@ class SearchParams(ctypes.Structure):
         ("policy_surprise_data_weight", ctypes.c_float), ("value_surprise_data_weight", ctypes.c_float),
         ("init_games_with_policy", ctypes.c_int32), ("policy_init_area_prop", ctypes.c_float),
         ("policy_init_area_temperature", ctypes.c_float),
+        ("early_fork_game_prob", ctypes.c_float), ("early_fork_game_expected_move_prop", ctypes.c_float),
+        ("fork_game_prob", ctypes.c_float), ("fork_game_min_choices", ctypes.c_int32),
+        ("early_fork_game_max_choices", ctypes.c_int32), ("fork_game_max_choices", ctypes.c_int32),
     ]
 
 

@@ -263,6 +263,12 @@ void coffee_search_params_default(coffee_search_params* p) {
   p->init_games_with_policy = 0;
   p->policy_init_area_prop = 0.04f;
   p->policy_init_area_temperature = 1.0f;
+  p->early_fork_game_prob = 0.0f;
+  p->early_fork_game_expected_move_prop = 0.025f;
+  p->fork_game_prob = 0.0f;
+  p->fork_game_min_choices = 3;
+  p->early_fork_game_max_choices = 12;
+  p->fork_game_max_choices = 36;
 }
 
 struct coffee_selfplay {

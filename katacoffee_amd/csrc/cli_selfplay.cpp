@@ -259,6 +259,12 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   getb("initGamesWithPolicy", p.init_games_with_policy);
   getf("policyInitAreaProp", p.policy_init_area_prop);
   getf("policyInitAreaTemperature", p.policy_init_area_temperature);
+  getf("earlyForkGameProb", p.early_fork_game_prob);
+  getf("earlyForkGameExpectedMoveProp", p.early_fork_game_expected_move_prop);
+  getf("forkGameProb", p.fork_game_prob);
+  geti("forkGameMinChoices", p.fork_game_min_choices);
+  geti("earlyForkGameMaxChoices", p.early_fork_game_max_choices);
+  geti("forkGameMaxChoices", p.fork_game_max_choices);
 }
 
 struct RowSink {

@@ -32,7 +32,8 @@ enum LeafKind {
   LEAF_NOCHILD = 4,
   LEAF_ROOTEVAL = 5,
   LEAF_CACHED = 6,  // NN output taken from the evaluation cache (SPEC a7)
-  LEAF_INIT = 7     // policy-initialisation move: the root evaluated for a sampled opening move
+  LEAF_INIT = 7,    // policy-initialisation move: the root evaluated for a sampled opening move
+  LEAF_FORK = 8     // fork candidate: the position after one candidate move evaluated
 };
 
 // NN evaluation cache slot of a state key (SPEC a7; oracle ora_search.cpp cacheSlot).
@@ -40,7 +41,7 @@ KC_HD uint32_t cacheSlot(uint64_t k0, uint64_t k1, uint32_t mask) {
   const uint64_t h = k0 ^ ((k1 << 29) | (k1 >> 35));
   return (uint32_t)(h ^ (h >> 32)) & mask;
 }
-enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2, PH_INIT = 3 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2, PH_INIT = 3, PH_FORK = 4 };
 
 // SearchParams (searchparams.h) restricted to Coffee self-play.
 struct SP {
@@ -72,6 +73,8 @@ struct SP {
   float policySurpriseWeight, valueSurpriseWeight;
   int initPolicy;            // initGamesWithPolicy
   float initAreaProp, initTemp;  // policyInitAreaProp, policyInitAreaTemperature
+  float earlyForkProb, earlyForkMoveProp, forkProb;  // earlyForkGameProb, earlyForkGameExpectedMoveProp, forkGameProb
+  int forkMinChoices, earlyForkMaxChoices, forkMaxChoices;
 };
 
 // The parameters of a cheap search whose rows are not recorded (runBotWithLimits
@@ -138,13 +141,26 @@ struct TurnRec {
 };
 static_assert(sizeof(TurnRec) == 56, "TurnRec layout");
 
+// Fork in progress (Play::maybeForkGame play.cpp:1741-1840): the position the
+// finished game is replayed to and the candidate moves, evaluated one per round;
+// the best becomes the start of the slot's next game.
+constexpr int MAX_FORK_CHOICES = 100;
+struct ForkRec {
+  DBoard board;                    // the position before the fork move
+  int32_t numChoices, next, best, prefix;  // prefix: moves replayed (kept as the next game's first turns)
+  float bestWinrate;
+  int32_t pad;
+  uint16_t moves[MAX_FORK_CHOICES];  // candidate policy positions (dir * A + cell)
+};
+
 // A game finished by kCommit whose training rows kRows emits right after it.
 struct FinRec {
   uint64_t rngSeed, rngCtr;  // history-mask stream state after the game's last move choice
   uint64_t gameHash0, gameHash1;
   unsigned long long rowBase;
   int32_t numMoves, winner, gameNum, pending;  // pending 1: rows reserved at rowBase
-  int32_t numRows, startTurn;                  // startTurn: policy-initialisation moves before the searched ones
+  int32_t numRows, startTurn;                  // startTurn: unsearched moves before the searched ones
+  int32_t gameMode, pad;
 };
 
 struct GameDev {
@@ -161,7 +177,8 @@ struct GameDev {
   int32_t visitLimit;             // this move's maxVisits (getSearchLimitsThisMove)
   float moveWeight;               // this move's target weight
   int32_t initLeft;               // policy-initialisation moves still to play (PH_INIT)
-  int32_t startTurn;              // policy-initialisation moves played (turns [0, startTurn) have no rows)
+  int32_t startTurn;              // unsearched opening moves (policy init or fork prefix): turns [0, startTurn) have no rows
+  int32_t gameMode;               // FinishedGameData mode: 0 normal, 2 fork (trainingwrite.h:97-104)
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
@@ -216,6 +233,7 @@ struct SearchDev {
   uint64_t* cStageKey;   // [G][2]
   // commit queue
   FinRec* fin;           // [G] games finished by the current commit (kRows)
+  ForkRec* fork;         // [G] fork state (PH_FORK)
   int32_t* commitList;   // [G]
   int32_t* commitCount;
   // rows

@@ -781,6 +781,14 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     s.leafKind = LEAF_INIT;
     s.leafSym = (int)rng.below(8);
     s.leaf = s.root;
+  } else if(s.phase == PH_FORK) {
+    // fork candidate: the position after the next candidate move, random symmetry
+    const ForkRec* f = d.fork + g;
+    const int mv = f->moves[f->next];
+    s.leaf = f->board;
+    playMoveWave(v.T, s.leaf, mv % v.T.A, mv / v.T.A);
+    s.leafKind = LEAF_FORK;
+    s.leafSym = (int)rng.below(8);
   } else if(s.phase == PH_ROOTEVAL) {
     if(s.rootK == 0) {
       // partial Fisher-Yates over 0..7, kept as packed nibbles (no dynamic register indexing)
@@ -814,7 +822,8 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   const unsigned long long t2 = SPROF_NOW();
   (void)t2;
   s.rngCtr = rng.ctr;
-  const bool needNN = s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT;
+  const bool needNN =
+      s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT || s.leafKind == LEAF_FORK;
   if(v.lane == 0)
     d.nnNeed[g] = needNN ? 1 : 0;
   if(needNN) {
@@ -1064,6 +1073,8 @@ KC_D void buildOrder(const GV& v, int ni, const float (&pv)[NI], float* lds) {
 KC_D bool setMoveLimits(const GV& v, GameDev& s, DRng& rng, float lastWL);
 KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scratch);
 KC_D void startGame(const GV& v, GameDev& s);
+template <int NI>
+KC_D void forkEval(const GV& v, GameDev& s, const float* o, float* scratch);
 
 // oracle initMove (getGameInitializationMove playutils.cpp:97-145 + the move of
 // initializeGameUsingPolicy :163-175): a move sampled from the root's post-processed
@@ -1170,6 +1181,8 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
   bool needCommit = false;
   if(s.leafKind == LEAF_INIT) {
     needCommit = initMove<NI>(v, s, o, scratch);
+  } else if(s.leafKind == LEAF_FORK) {
+    forkEval<NI>(v, s, o, scratch);
   } else if(s.leafKind == LEAF_ROOTEVAL) {
     float* pol = scratch;
     float w, l;
@@ -1891,6 +1904,7 @@ KC_D void startGame(const GV& v, GameDev& s) {
   boardInit(v.T, s.root);
   clearTables(v, s);
   s.numTurns = 0;
+  s.gameMode = 0;
   DRng rng{s.rngSeed, s.rngCtr};
   s.gameHash0 = rng.next();
   s.gameHash1 = rng.next();
@@ -1914,6 +1928,145 @@ KC_D void startGame(const GV& v, GameDev& s) {
   s.rngCtr = rng.ctr;
   s.rootK = 0;
   s.leafKind = LEAF_NONE;
+}
+
+// oracle startForkGame: the slot's next game starts from the fork position `b`
+// (the finished game replayed to `prefix` moves plus the chosen move); those moves
+// stay in the turn records as unsearched turns, no policy initialisation (play.cpp:
+// 380-395), mode FORK in the rows (trainingwrite.cpp:468).
+KC_D void startForkGame(const GV& v, GameDev& s, const DBoard& b, int prefix, int move) {
+  s.rngSeed = mix64(v.d.seed ^ mix64(((uint64_t)(v.d.slotBase + v.g) << 32) | (uint32_t)s.gameNum));
+  s.rngCtr = 0;
+  s.root = b;
+  clearTables(v, s);
+  TurnRec* tr = v.turns();
+  for(int t = v.lane; t <= prefix; t += 64) {
+    const int8_t cell = t < prefix ? tr[t].cell : (int8_t)(move % v.T.A);
+    const int8_t dir = t < prefix ? tr[t].dir : (int8_t)(move / v.T.A);
+    TurnRec rec;
+    memset(&rec, 0, sizeof(rec));
+    rec.cell = cell;
+    rec.dir = dir;
+    tr[t] = rec;
+  }
+  s.numTurns = prefix + 1;
+  s.startTurn = prefix + 1;
+  s.initLeft = 0;
+  s.gameMode = 2;
+  DRng rng{s.rngSeed, s.rngCtr};
+  s.gameHash0 = rng.next();
+  s.gameHash1 = rng.next();
+  setMoveLimits(v, s, rng, 0.0f);
+  s.rngCtr = rng.ctr;
+  s.phase = PH_ROOTEVAL;
+  s.rootK = 0;
+  s.leafKind = LEAF_NONE;
+  waveSync();
+}
+
+// oracle maybeFork (Play::maybeForkGame play.cpp:1741-1840) at the end of a game, on
+// the finished game's stream: an early fork (position after floor(Exp(1) * A *
+// earlyForkGameExpectedMoveProp) moves) or a late one (uniform move index); the
+// candidates are numChoices uniform draws, with replacement, from the legal moves in
+// cell-major order (chooseRandomLegalMoves playutils.cpp:33-60).  Returns true when a
+// fork was set up (PH_FORK: one candidate evaluated per round).  No draws at all when
+// both probabilities are 0 (SPEC: benchmark mode's streams stay as they are).
+KC_D bool maybeFork(const GV& v, GameDev& s, DRng& rng, uint16_t* legal /* LDS [MAX_P] */) {
+  const SP& b = v.d.sp;
+  if(b.earlyForkProb <= 0.0f && b.forkProb <= 0.0f)
+    return false;
+  const DTables& T = v.T;
+  const bool early = rng.uni() < b.earlyForkProb;
+  const bool late = !early && b.forkProb > 0.0f && rng.uni() < b.forkProb;
+  if(!early && !late)
+    return false;
+  const int n = s.numTurns;
+  int moveIdx;
+  if(early) {
+    float u = rng.uni();
+    while(u <= 0.0f)
+      u = rng.uni();
+    moveIdx = (int)floorf(-dlog(u) * (b.earlyForkMoveProp * (float)T.A));
+  } else {
+    moveIdx = n <= 0 ? 0 : (int)rng.below((uint32_t)n);
+  }
+  moveIdx = min(moveIdx, max(n - 1, 0));
+  // replayGameUpToMove (play.cpp:1703-1739)
+  const TurnRec* tr = v.turns();
+  DBoard bd;
+  boardInit(T, bd);
+  for(int t = 0; t < moveIdx; t++) {
+    playMoveWave(T, bd, tr[t].cell, tr[t].dir);
+    if(bd.finished)
+      return false;
+  }
+  const int maxC = early ? b.earlyForkMaxChoices : b.forkMaxChoices;
+  const int numChoices = b.forkMinChoices + (int)rng.below((uint32_t)(maxC - b.forkMinChoices + 1));
+  int numLegal = 0;
+  for(int base = 0; base < T.P; base += 64) {
+    const int q = base + v.lane;  // cell-major: q = cell * 4 + dir
+    const bool ok = q < T.P && isLegal(T, bd, q >> 2, q & 3);
+    const uint64_t m = ballot(ok);
+    if(ok)
+      legal[numLegal + __popcll(m & ((1ULL << v.lane) - 1ULL))] = (uint16_t)((q & 3) * T.A + (q >> 2));
+    numLegal += __popcll(m);
+  }
+  waveSync();
+  if(numLegal <= 0)
+    return false;
+  ForkRec* f = v.d.fork + v.g;
+  for(int i = 0; i < numChoices; i++) {
+    const int k = (int)rng.below((uint32_t)numLegal);
+    if(v.lane == 0)
+      f->moves[i] = legal[k];
+  }
+  if(v.lane == 0) {
+    f->board = bd;
+    f->numChoices = numChoices;
+    f->next = 0;
+    f->best = -1;
+    f->bestWinrate = 0.0f;
+    f->prefix = moveIdx;
+  }
+  s.phase = PH_FORK;
+  s.leafKind = LEAF_NONE;
+  waveSync();
+  return true;
+}
+
+// oracle forkEval: the network's value for the position after candidate f.next; the
+// best for the player at the fork (first of equals) wins; after the last candidate the
+// slot's next game starts from the fork (or normally when the fork move ends the game).
+template <int NI>
+KC_D void forkEval(const GV& v, GameDev& s, const float* o, float* scratch) {
+  ForkRec* f = v.d.fork + v.g;
+  float w, l;
+  float pv[NI];
+  postprocess<NI>(v, s.leaf, s.leafSym, o, scratch, w, l, scratch, pv);
+  const float wr = 0.5f * (w - l + 1.0f);
+  const int pla = f->board.pla;
+  const int next = f->next;
+  int best = f->best;
+  float bestWr = f->bestWinrate;
+  if(best < 0 || (pla == 2 && wr > bestWr) || (pla == 1 && wr < bestWr)) {
+    best = next;
+    bestWr = wr;
+  }
+  waveSync();
+  if(v.lane == 0) {
+    f->best = best;
+    f->bestWinrate = bestWr;
+    f->next = next + 1;
+  }
+  if(next + 1 < f->numChoices)
+    return;
+  const int move = f->moves[best];
+  DBoard bd = f->board;
+  playMoveWave(v.T, bd, move % v.T.A, move / v.T.A);
+  if(bd.finished)
+    startGame(v, s);  // "if the game is over now, don't actually do anything"
+  else
+    startForkGame(v, s, bd, f->prefix, move);
 }
 
 // oracle finishGame (play.cpp:1431-1460 + trainingwrite.cpp:316-565, 774-890), commit
@@ -2041,6 +2194,7 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scra
     f->numMoves = numMoves;
     f->numRows = numRows;
     f->startTurn = s.startTurn;
+    f->gameMode = s.gameMode;
     f->winner = s.root.winner;
     f->gameNum = s.gameNum;
     f->pending = fits && numRows > 0 ? 1 : 0;
@@ -2191,6 +2345,8 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
       gval = (float)t;
     } else if(li == 53) {
       gval = (float)f.startTurn;
+    } else if(li == 55) {
+      gval = (float)f.gameMode;
     } else if(li == 57) {
       gval = pla == 2 ? tr[t].rawWhiteWL : -tr[t].rawWhiteWL;
     } else if(li == 59) {
@@ -2250,7 +2406,10 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     finishGameRecord(v, s, rng, reinterpret_cast<float*>(lds) + 2 * MAX_P);
     s.gamesFinished++;
     s.gameNum++;
-    startGame(v, s);
+    if(!maybeFork(v, s, rng, reinterpret_cast<uint16_t*>(lds)))
+      startGame(v, s);
+    else
+      s.rngCtr = rng.ctr;
     waveSync();
     storeGame(v, s);
     return;
@@ -2356,7 +2515,11 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     [[maybe_unused]] const unsigned long long t4 = SPROF_NOW();
     s.gamesFinished++;
     s.gameNum++;
-    startGame(v, s);
+    waveSync();
+    if(!maybeFork(v, s, rng, reinterpret_cast<uint16_t*>(posv)))
+      startGame(v, s);
+    else
+      s.rngCtr = rng.ctr;
     SPROF_ADD(20, t4 - t3);
     SPROF_ADD(21, SPROF_NOW() - t4);
     SPROF_ADD(23, 1);

@@ -61,6 +61,12 @@ SP toSP(const coffee_search_params& p) {
   s.initPolicy = p.init_games_with_policy;
   s.initAreaProp = p.policy_init_area_prop;
   s.initTemp = p.policy_init_area_temperature;
+  s.earlyForkProb = p.early_fork_game_prob;
+  s.earlyForkMoveProp = p.early_fork_game_expected_move_prop;
+  s.forkProb = p.fork_game_prob;
+  s.forkMinChoices = p.fork_game_min_choices;
+  s.earlyForkMaxChoices = p.early_fork_game_max_choices;
+  s.forkMaxChoices = p.fork_game_max_choices;
   return s;
 }
 
@@ -98,6 +104,12 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   if(sp.init_games_with_policy && (!unit(sp.policy_init_area_prop) || sp.policy_init_area_temperature < 0.1f ||
                                    sp.policy_init_area_temperature > 5.0f))
     throw std::invalid_argument("policy_init_area_prop in [0, 1], policy_init_area_temperature in [0.1, 5]");
+  // playsettings.cpp:74-79 ranges; play.cpp:1783-1788 checks
+  if(sp.early_fork_game_prob < 0.0f || sp.early_fork_game_prob > 0.5f || sp.fork_game_prob < 0.0f ||
+     sp.fork_game_prob > 0.5f || !unit(sp.early_fork_game_expected_move_prop) || sp.fork_game_min_choices < 1 ||
+     sp.early_fork_game_max_choices < sp.fork_game_min_choices || sp.fork_game_max_choices < sp.fork_game_min_choices ||
+     sp.early_fork_game_max_choices > MAX_FORK_CHOICES || sp.fork_game_max_choices > MAX_FORK_CHOICES)
+    throw std::invalid_argument("fork settings: probabilities in [0, 0.5], min <= max choices <= 100");
   const DTables& ht = hostTables(c.x, c.y, c.win_len);
   T_ = deviceTables(c.x, c.y, c.win_len);
   commitInterval_ = c.commit_interval > 0 ? c.commit_interval : 8;
@@ -158,6 +170,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.nnIn = devAlloc<uint64_t>(owned_, (size_t)G * ht.inWords);
   d.nnOut = devAlloc<float>(owned_, (size_t)G * (P + 4));
   d.fin = devAlloc<FinRec>(owned_, G);
+  d.fork = devAlloc<ForkRec>(owned_, G);
   d.commitList = devAlloc<int32_t>(owned_, G);
   d.nnTimedEvals = devAlloc<unsigned long long>(owned_, 1);
   d.commitCount = devAlloc<int32_t>(owned_, 1);

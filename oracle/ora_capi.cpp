@@ -125,7 +125,9 @@ int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* 
 // cheap_search_visits, cheap_search_target_weight, reduce_visits, reduce_visits_threshold,
 // reduce_visits_threshold_lookback, reduced_visits_min, reduced_visits_weight,
 // policy_surprise_data_weight, value_surprise_data_weight, init_games_with_policy,
-// policy_init_area_prop, policy_init_area_temperature).
+// policy_init_area_prop, policy_init_area_temperature, early_fork_game_prob,
+// early_fork_game_expected_move_prop, fork_game_prob, fork_game_min_choices,
+// early_fork_game_max_choices, fork_game_max_choices).
 void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
                     int nnMode, void* model, int nnThreads, int cacheLog2, const float* play, int nnCap) {
   if(!T.loaded)
@@ -148,6 +150,12 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
     cfg.sp.initGamesWithPolicy = (int)play[10];
     cfg.sp.policyInitAreaProp = play[11];
     cfg.sp.policyInitAreaTemperature = play[12];
+    cfg.sp.earlyForkGameProb = play[13];
+    cfg.sp.earlyForkGameExpectedMoveProp = play[14];
+    cfg.sp.forkGameProb = play[15];
+    cfg.sp.forkGameMinChoices = (int)play[16];
+    cfg.sp.earlyForkGameMaxChoices = (int)play[17];
+    cfg.sp.forkGameMaxChoices = (int)play[18];
   }
   cfg.nodeCap = nodeCap;
   cfg.seed = seed;

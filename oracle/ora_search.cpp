@@ -950,6 +950,7 @@ struct Ctx {
     boardInit(g, gm.root);
     clearTree();
     gm.turns.clear();
+    gm.gameMode = 0;
     gm.gameHash0 = gm.rng.next();
     gm.gameHash1 = gm.rng.next();
     // initializeGameUsingPolicy (playutils.cpp:147-176): floor(Exp(1) * area * prop)
@@ -1026,6 +1027,105 @@ struct Ctx {
       gm.rootK = 0;
     }
     return false;
+  }
+
+  // The slot's next game starts from the fork position b: the finished game's first
+  // `prefix` moves plus `move` stay as unsearched turns, no policy init, mode FORK.
+  void startForkGame(const Board& b, int prefix, int move) {
+    gm.rng.seed = mix64(s.cfg.seed ^ mix64(((uint64_t)(s.cfg.slotBase + gm.slot) << 32) | gm.gameNum));
+    gm.rng.ctr = 0;
+    gm.root = b;
+    clearTree();
+    std::vector<TurnRec> keep;
+    for(int t = 0; t <= prefix; t++) {
+      TurnRec tr{};
+      tr.cell = t < prefix ? gm.turns[t].cell : (int8_t)(move % g.A);
+      tr.dir = t < prefix ? gm.turns[t].dir : (int8_t)(move / g.A);
+      tr.policyTarget.assign(g.P, 0);
+      keep.push_back(tr);
+    }
+    gm.turns.swap(keep);
+    gm.startTurn = prefix + 1;
+    gm.initLeft = 0;
+    gm.gameMode = 2;
+    gm.gameHash0 = gm.rng.next();
+    gm.gameHash1 = gm.rng.next();
+    setMoveLimits();
+    gm.phase = PH_ROOTEVAL;
+    gm.rootK = 0;
+  }
+
+  // Play::maybeForkGame (play.cpp:1741-1840) on the finished game's stream; candidates
+  // are uniform draws with replacement from the legal moves in cell-major order
+  // (chooseRandomLegalMoves playutils.cpp:33-60).  No draws when forks are off.
+  bool maybeFork() {
+    const SearchParams& b = s.cfg.sp;
+    if(b.earlyForkGameProb <= 0.0f && b.forkGameProb <= 0.0f)
+      return false;
+    const bool early = gm.rng.uni() < b.earlyForkGameProb;
+    const bool late = !early && b.forkGameProb > 0.0f && gm.rng.uni() < b.forkGameProb;
+    if(!early && !late)
+      return false;
+    const int n = (int)gm.turns.size();
+    int moveIdx;
+    if(early) {
+      float u = gm.rng.uni();
+      while(u <= 0.0f)
+        u = gm.rng.uni();
+      moveIdx = (int)floorf(-kLogf(u) * (b.earlyForkGameExpectedMoveProp * (float)g.A));
+    } else {
+      moveIdx = n <= 0 ? 0 : (int)gm.rng.below((uint32_t)n);
+    }
+    moveIdx = std::min(moveIdx, std::max(n - 1, 0));
+    Board bd;
+    boardInit(g, bd);
+    for(int t = 0; t < moveIdx; t++) {
+      playMove(g, bd, gm.turns[t].cell, gm.turns[t].dir);
+      if(bd.finished)
+        return false;
+    }
+    const int maxC = early ? b.earlyForkGameMaxChoices : b.forkGameMaxChoices;
+    const int numChoices = b.forkGameMinChoices + (int)gm.rng.below((uint32_t)(maxC - b.forkGameMinChoices + 1));
+    std::vector<int> legal;
+    for(int cell = 0; cell < g.A; cell++)
+      for(int dir = 0; dir < 4; dir++)
+        if(isLegal(g, bd, cell, dir))
+          legal.push_back(dir * g.A + cell);
+    if(legal.empty())
+      return false;
+    gm.forkMoves.clear();
+    for(int i = 0; i < numChoices; i++)
+      gm.forkMoves.push_back(legal[gm.rng.below((uint32_t)legal.size())]);
+    gm.forkBoard = bd;
+    gm.forkNext = 0;
+    gm.forkBest = -1;
+    gm.forkBestWinrate = 0.0f;
+    gm.forkPrefix = moveIdx;
+    gm.phase = PH_FORK;
+    return true;
+  }
+
+  // The value of the position after candidate forkNext (first best for the player at
+  // the fork); after the last candidate the next game starts from the fork.
+  void forkEval(const float* out) {
+    float pol[MAX_P], w, l;
+    postprocess(gm.leafBoard, gm.leafSym, out, pol, w, l);
+    const float wr = 0.5f * (w - l + 1.0f);
+    const int pla = gm.forkBoard.pla;
+    if(gm.forkBest < 0 || (pla == 2 && wr > gm.forkBestWinrate) || (pla == 1 && wr < gm.forkBestWinrate)) {
+      gm.forkBest = gm.forkNext;
+      gm.forkBestWinrate = wr;
+    }
+    gm.forkNext++;
+    if(gm.forkNext < (int)gm.forkMoves.size())
+      return;
+    const int move = gm.forkMoves[gm.forkBest];
+    Board bd = gm.forkBoard;
+    playMove(g, bd, move % g.A, move / g.A);
+    if(bd.finished)
+      startGame();
+    else
+      startForkGame(bd, gm.forkPrefix, move);
   }
 
   void finishGame();
@@ -1114,7 +1214,8 @@ void Ctx::commitMove() {
     finishGame();
     gm.gamesFinished++;
     gm.gameNum++;
-    startGame();
+    if(!maybeFork())
+      startGame();
     return;
   }
   if(setMoveLimits())
@@ -1222,6 +1323,10 @@ void Ctx::finishGame() {
   for(int c = 0; c < A; c++)
     finalMaxLen[c] = fin.c[c] == 0 ? 0 : (int8_t)maxRun(g, fin, c);
   resolveTurnWeights(s.cfg.sp, A, gm.turns, gm.startTurn, tWin.data(), tLoss.data(), gm.rng);
+  // history-mask draws come from a copy of the game stream (the rows are written by a
+  // separate device kernel from a snapshot), so the stream a fork continues from is
+  // the one after the weight resolution
+  Rng hmRng = gm.rng;
   std::vector<int> rowTurn;  // turn of each row, in row order
   for(int t = 0; t < numMoves; t++)
     for(int c = 0; c < gm.turns[t].rows; c++)
@@ -1294,7 +1399,7 @@ void Ctx::finishGame() {
     gt[33] = 1.0f;
     bool h = true;
     for(int i = 0; i < 5; i++) {
-      h = h && gm.rng.uni() < 0.98f;
+      h = h && hmRng.uni() < 0.98f;
       gt[36 + i] = h ? 1.0f : 0.0f;
     }
     gt[41] = (float)(gm.gameHash0 & 0x3FFFFF);
@@ -1305,6 +1410,7 @@ void Ctx::finishGame() {
     gt[46] = (float)((gm.gameHash1 >> 44) & 0xFFFFF);
     gt[51] = (float)t;
     gt[53] = (float)gm.startTurn;
+    gt[55] = (float)gm.gameMode;
     gt[57] = pla == 2 ? gm.turns[t].rawWhiteWL : -gm.turns[t].rawWhiteWL;
     gt[59] = gm.turns[t].rawPolicyEntropy;
     gt[60] = (float)gm.turns[t].visits;
@@ -1393,6 +1499,12 @@ void selfplayRound(Selfplay& s) {
       gm.leafKind = LEAF_INIT;
       gm.leafSym = (int)gm.rng.below(8);
       gm.leafBoard = gm.root;
+    } else if(gm.phase == PH_FORK) {
+      const int mv = gm.forkMoves[gm.forkNext];
+      gm.leafBoard = gm.forkBoard;
+      playMove(g, gm.leafBoard, mv % g.A, mv / g.A);
+      gm.leafKind = LEAF_FORK;
+      gm.leafSym = (int)gm.rng.below(8);
     } else if(gm.phase == PH_ROOTEVAL) {
       if(gm.rootK == 0) {
         int idx[8] = {0, 1, 2, 3, 4, 5, 6, 7};
@@ -1419,7 +1531,8 @@ void selfplayRound(Selfplay& s) {
       if(gm.leafKind == LEAF_NN)
         gm.leafSym = (int)gm.rng.below(8);
     }
-    if(gm.leafKind == LEAF_NN || gm.leafKind == LEAF_ROOTEVAL || gm.leafKind == LEAF_INIT) {
+    if(gm.leafKind == LEAF_NN || gm.leafKind == LEAF_ROOTEVAL || gm.leafKind == LEAF_INIT ||
+       gm.leafKind == LEAF_FORK) {
       encodeV1(g, gm.leafBoard, gm.leafSym, &bin[(size_t)i * NUM_SPATIAL * A], &glob[i]);
       need[i] = 1;
       gm.nnEvals++;
@@ -1489,8 +1602,13 @@ void selfplayRound(Selfplay& s) {
         cx.finishGame();
         gm.gamesFinished++;
         gm.gameNum++;
-        cx.startGame();
+        if(!cx.maybeFork())
+          cx.startGame();
       }
+      continue;
+    }
+    if(gm.leafKind == LEAF_FORK) {
+      cx.forkEval(o);
       continue;
     }
     if(gm.leafKind == LEAF_ROOTEVAL) {

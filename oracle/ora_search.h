@@ -42,6 +42,10 @@ struct SearchParams {
   int initGamesWithPolicy = 0;           // true
   float policyInitAreaProp = 0.04f;      // 0.04
   float policyInitAreaTemperature = 1.0f;
+  float earlyForkGameProb = 0.0f;        // 0.04
+  float earlyForkGameExpectedMoveProp = 0.025f;
+  float forkGameProb = 0.0f;             // 0.01
+  int forkGameMinChoices = 3, earlyForkGameMaxChoices = 12, forkGameMaxChoices = 36;
 };
 
 // The search parameters of a cheap search whose rows are not recorded
@@ -73,8 +77,8 @@ struct Node {
 };
 
 enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5,
-               LEAF_CACHED = 6, LEAF_INIT = 7 };
-enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_INIT = 3 };
+               LEAF_CACHED = 6, LEAF_INIT = 7, LEAF_FORK = 8 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_INIT = 3, PH_FORK = 4 };
 
 struct TurnRec {
   int8_t cell, dir;
@@ -126,8 +130,15 @@ struct Game {
   // this move's search limits (getSearchLimitsThisMove play.cpp:871-1004)
   int visitLimit = 0, noNoise = 0;
   float moveWeight = 1.0f;
-  // policy-initialisation moves (initializeGameUsingPolicy playutils.cpp:147-176)
+  // policy-initialisation moves (initializeGameUsingPolicy playutils.cpp:147-176);
+  // startTurn: unsearched moves at the start (policy init or fork prefix)
   int initLeft = 0, startTurn = 0;
+  int gameMode = 0;                  // 0 normal, 2 fork (trainingwrite.h:97-104)
+  // fork in progress (Play::maybeForkGame play.cpp:1741-1840)
+  Board forkBoard;
+  std::vector<int> forkMoves;
+  int forkNext = 0, forkBest = -1, forkPrefix = 0;
+  float forkBestWinrate = 0.0f;
   // tree
   int nodeCount = 0, rootIdx = -1;
   std::vector<Node> nodes;

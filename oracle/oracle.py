@@ -143,6 +143,8 @@ PLAY_SETTINGS = {
     "reduced_visits_min": 100, "reduced_visits_weight": 0.1,
     "policy_surprise_data_weight": 0.0, "value_surprise_data_weight": 0.0,
     "init_games_with_policy": 0, "policy_init_area_prop": 0.04, "policy_init_area_temperature": 1.0,
+    "early_fork_game_prob": 0.0, "early_fork_game_expected_move_prop": 0.025, "fork_game_prob": 0.0,
+    "fork_game_min_choices": 3, "early_fork_game_max_choices": 12, "fork_game_max_choices": 36,
 }
 
 

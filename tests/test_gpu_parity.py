@@ -154,6 +154,9 @@ def _sorted_rows(r):
 PRODUCTION = dict(cheap_search_prob=0.75, cheap_search_visits=10, cheap_search_target_weight=0.0, reduce_visits=1,
                   reduce_visits_threshold=0.9, reduce_visits_threshold_lookback=3, reduced_visits_min=10,
                   reduced_visits_weight=0.1, policy_surprise_data_weight=0.5, value_surprise_data_weight=0.1)
+# forks at high rates (selfplay1.cfg: 0.04 / 0.01) so these short runs fork often
+FORKS = dict(early_fork_game_prob=0.5, early_fork_game_expected_move_prop=0.2, fork_game_prob=0.5,
+             fork_game_min_choices=2, early_fork_game_max_choices=5, fork_game_max_choices=7)
 # reduceVisits alone, with a low threshold so the reduction triggers in these short games
 REDUCED = dict(reduce_visits=1, reduce_visits_threshold=0.2, reduced_visits_min=8, reduced_visits_weight=0.3)
 
@@ -168,9 +171,12 @@ REDUCED = dict(reduce_visits=1, reduce_visits_threshold=0.2, reduced_visits_min=
                           (8, 32, 1400, 17, 5, dict(PRODUCTION, nn_batch_cap=2)),
                           (8, 32, 1200, 19, 12, dict(PRODUCTION, init_games_with_policy=1)),
                           (8, 24, 1200, 23, 0, dict(init_games_with_policy=1, policy_init_area_prop=0.3,
-                                                    policy_init_area_temperature=2.0))],
+                                                    policy_init_area_temperature=2.0)),
+                          (8, 24, 1600, 29, 12, FORKS),
+                          (8, 24, 1600, 37, 10, dict(PRODUCTION, init_games_with_policy=1, cheap_search_visits=8,
+                                                     reduced_visits_min=8, nn_batch_cap=5, **FORKS))],
                          ids=["bench-a", "bench-b", "cache32", "cache16k", "production", "reduced", "batch-cap",
-                              "production-cap", "production-init", "policy-init"])
+                              "production-cap", "production-init", "policy-init", "forks", "everything"])
 def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2, play):
     cap = 128
     gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,

@@ -155,3 +155,23 @@ def test_policy_init_openings():
         sel = (meta[:, 0] == slot) & (meta[:, 1] == gnum)
         t0 = int(start[sel][0])
         np.testing.assert_array_equal(np.sort(meta[sel, 2]), np.arange(t0, meta[sel, 3][0]))
+
+
+FORKS = dict(early_fork_game_prob=0.5, early_fork_game_expected_move_prop=0.2, fork_game_prob=0.5,
+             fork_game_min_choices=2, early_fork_game_max_choices=5, fork_game_max_choices=7)
+
+
+def test_fork_games():
+    """Forks (Play::maybeForkGame): some of a slot's games start from a position of its
+    previous game plus the best of a few random moves; their rows carry mode 2 (gt[55])
+    and start after the replayed prefix."""
+    sp = oracle.Selfplay(5, 5, 4, games=6, max_visits=16, node_cap=128, seed=41, **FORKS)
+    sp.rounds(2500)
+    r = sp.rows()
+    meta, gt = r["meta"], r["globalTargetsNC"]
+    fork = gt[:, 55] == 2.0
+    assert fork.any() and (~fork).any()
+    assert set(np.unique(gt[:, 55])) <= {0.0, 2.0}
+    assert np.all(gt[fork, 53] >= 1) and np.all(gt[~fork, 53] == 0)
+    assert np.all(meta[:, 2] >= gt[:, 53])
+    np.testing.assert_array_equal(gt[:, 60], 16.0)
