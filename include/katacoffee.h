@@ -153,6 +153,10 @@ typedef struct coffee_search_params {
   int32_t fork_game_min_choices;         /* 3 */
   int32_t early_fork_game_max_choices;   /* 12 */
   int32_t fork_game_max_choices;         /* 36 */
+  /* side positions (play.cpp:1328-1345, :1576-1662): after a searched move, with this
+   * probability a refutation position (the root policy's alternative to the played
+   * move) is queued and searched after the game; one row each */
+  float side_position_prob;              /* 0.02 */
 } coffee_search_params;
 
 void coffee_search_params_default(coffee_search_params* p);

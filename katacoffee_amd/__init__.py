@@ -68,6 +68,7 @@ class SearchParams(ctypes.Structure):
         ("early_fork_game_prob", ctypes.c_float), ("early_fork_game_expected_move_prop", ctypes.c_float),
         ("fork_game_prob", ctypes.c_float), ("fork_game_min_choices", ctypes.c_int32),
         ("early_fork_game_max_choices", ctypes.c_int32), ("fork_game_max_choices", ctypes.c_int32),
+        ("side_position_prob", ctypes.c_float),
     ]
 
 

@@ -269,6 +269,7 @@ void coffee_search_params_default(coffee_search_params* p) {
   p->fork_game_min_choices = 3;
   p->early_fork_game_max_choices = 12;
   p->fork_game_max_choices = 36;
+  p->side_position_prob = 0.0f;
 }
 
 struct coffee_selfplay {

@@ -265,6 +265,7 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   geti("forkGameMinChoices", p.fork_game_min_choices);
   geti("earlyForkGameMaxChoices", p.early_fork_game_max_choices);
   geti("forkGameMaxChoices", p.fork_game_max_choices);
+  getf("sidePositionProb", p.side_position_prob);
 }
 
 struct RowSink {

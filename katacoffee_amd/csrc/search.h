@@ -33,7 +33,8 @@ enum LeafKind {
   LEAF_ROOTEVAL = 5,
   LEAF_CACHED = 6,  // NN output taken from the evaluation cache (SPEC a7)
   LEAF_INIT = 7,    // policy-initialisation move: the root evaluated for a sampled opening move
-  LEAF_FORK = 8     // fork candidate: the position after one candidate move evaluated
+  LEAF_FORK = 8,    // fork candidate: the position after one candidate move evaluated
+  LEAF_SIDE = 9     // side-position continuation: the position after the search's response
 };
 
 // NN evaluation cache slot of a state key (SPEC a7; oracle ora_search.cpp cacheSlot).
@@ -41,7 +42,7 @@ KC_HD uint32_t cacheSlot(uint64_t k0, uint64_t k1, uint32_t mask) {
   const uint64_t h = k0 ^ ((k1 << 29) | (k1 >> 35));
   return (uint32_t)(h ^ (h >> 32)) & mask;
 }
-enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2, PH_INIT = 3, PH_FORK = 4 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2, PH_INIT = 3, PH_FORK = 4, PH_SIDEEVAL = 5 };
 
 // SearchParams (searchparams.h) restricted to Coffee self-play.
 struct SP {
@@ -75,6 +76,7 @@ struct SP {
   float initAreaProp, initTemp;  // policyInitAreaProp, policyInitAreaTemperature
   float earlyForkProb, earlyForkMoveProp, forkProb;  // earlyForkGameProb, earlyForkGameExpectedMoveProp, forkGameProb
   int forkMinChoices, earlyForkMaxChoices, forkMaxChoices;
+  float sideProb;            // sidePositionProb
 };
 
 // The parameters of a cheap search whose rows are not recorded (runBotWithLimits
@@ -141,6 +143,10 @@ struct TurnRec {
 };
 static_assert(sizeof(TurnRec) == 56, "TurnRec layout");
 
+// Side positions (play.cpp:1328-1345, :1576-1662): at most MAX_SIDE per game are
+// queued (a rare overflow drops the extra ones); each is searched after the game.
+constexpr int MAX_SIDE = 8;
+
 // Fork in progress (Play::maybeForkGame play.cpp:1741-1840): the position the
 // finished game is replayed to and the candidate moves, evaluated one per round;
 // the best becomes the start of the slot's next game.
@@ -179,6 +185,9 @@ struct GameDev {
   int32_t initLeft;               // policy-initialisation moves still to play (PH_INIT)
   int32_t startTurn;              // unsearched opening moves (policy init or fork prefix): turns [0, startTurn) have no rows
   int32_t gameMode;               // FinishedGameData mode: 0 normal, 2 fork (trainingwrite.h:97-104)
+  int32_t sideCount, sideNext;    // queued side positions of this game, the one being searched
+  int32_t sideMode;               // 1 while the finished game's side positions are searched
+  int32_t pad3;
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
@@ -234,6 +243,8 @@ struct SearchDev {
   // commit queue
   FinRec* fin;           // [G] games finished by the current commit (kRows)
   ForkRec* fork;         // [G] fork state (PH_FORK)
+  DBoard* side;          // [G][MAX_SIDE] queued side positions
+  int16_t* sidePol;      // [G][P] the policy target of the side position being written
   int32_t* commitList;   // [G]
   int32_t* commitCount;
   // rows

@@ -781,6 +781,11 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     s.leafKind = LEAF_INIT;
     s.leafSym = (int)rng.below(8);
     s.leaf = s.root;
+  } else if(s.phase == PH_SIDEEVAL) {
+    // side-position continuation: the position after the search's response (set by
+    // kCommit in s.leaf), random symmetry
+    s.leafKind = LEAF_SIDE;
+    s.leafSym = (int)rng.below(8);
   } else if(s.phase == PH_FORK) {
     // fork candidate: the position after the next candidate move, random symmetry
     const ForkRec* f = d.fork + g;
@@ -823,7 +828,8 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   (void)t2;
   s.rngCtr = rng.ctr;
   const bool needNN =
-      s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT || s.leafKind == LEAF_FORK;
+      s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT || s.leafKind == LEAF_FORK ||
+      s.leafKind == LEAF_SIDE;
   if(v.lane == 0)
     d.nnNeed[g] = needNN ? 1 : 0;
   if(needNN) {
@@ -1075,6 +1081,8 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scra
 KC_D void startGame(const GV& v, GameDev& s);
 template <int NI>
 KC_D void forkEval(const GV& v, GameDev& s, const float* o, float* scratch);
+template <int NI>
+KC_D void sideEval(const GV& v, GameDev& s, const float* o, float* scratch);
 
 // oracle initMove (getGameInitializationMove playutils.cpp:97-145 + the move of
 // initializeGameUsingPolicy :163-175): a move sampled from the root's post-processed
@@ -1162,7 +1170,7 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
   const int g = blockIdx.x;
   if(g >= d.G || d.nnDefer[g])  // a deferred leaf is backed up in a later round
     return;
-  __shared__ __attribute__((aligned(16))) float scratch[2 * MAX_P];
+  __shared__ __attribute__((aligned(16))) float scratch[3 * MAX_P];
   GV v(d, *Tp, g);
   __shared__ GameDev s;
   SPROF_INIT();
@@ -1183,6 +1191,8 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
     needCommit = initMove<NI>(v, s, o, scratch);
   } else if(s.leafKind == LEAF_FORK) {
     forkEval<NI>(v, s, o, scratch);
+  } else if(s.leafKind == LEAF_SIDE) {
+    sideEval<NI>(v, s, o, scratch);
   } else if(s.leafKind == LEAF_ROOTEVAL) {
     float* pol = scratch;
     float w, l;
@@ -1905,6 +1915,9 @@ KC_D void startGame(const GV& v, GameDev& s) {
   clearTables(v, s);
   s.numTurns = 0;
   s.gameMode = 0;
+  s.sideCount = 0;
+  s.sideNext = 0;
+  s.sideMode = 0;
   DRng rng{s.rngSeed, s.rngCtr};
   s.gameHash0 = rng.next();
   s.gameHash1 = rng.next();
@@ -1953,6 +1966,9 @@ KC_D void startForkGame(const GV& v, GameDev& s, const DBoard& b, int prefix, in
   s.startTurn = prefix + 1;
   s.initLeft = 0;
   s.gameMode = 2;
+  s.sideCount = 0;
+  s.sideNext = 0;
+  s.sideMode = 0;
   DRng rng{s.rngSeed, s.rngCtr};
   s.gameHash0 = rng.next();
   s.gameHash1 = rng.next();
@@ -2067,6 +2083,204 @@ KC_D void forkEval(const GV& v, GameDev& s, const float* o, float* scratch) {
     startGame(v, s);  // "if the game is over now, don't actually do anything"
   else
     startForkGame(v, s, bd, f->prefix, move);
+}
+
+// oracle forkingMove (chooseRandomForkingMove play.cpp:615-633): 70% a temperature-1
+// policy move, 25% temperature 2 (chooseRandomPolicyMove playutils.cpp:62-95: policy
+// positions in order, probability > 0, not `ban`, chooseIndexWithTemperature), 5% a
+// uniform legal move in cell-major order (chooseRandomLegalMove :10-31).  pol: the
+// post-processed policy (illegal < 0); cpos / cval / pr: LDS [MAX_P] scratch.
+// Returns the policy position, or -1 when there is none.
+KC_D int forkingMove(const GV& v, DRng& rng, const float* pol, const DBoard& b, int ban, int* cpos, float* cval,
+                     float* pr) {
+  const DTables& T = v.T;
+  const float r = rng.uni();
+  int n = 0;
+  if(r < 0.95f) {
+    const float temp = r < 0.70f ? 1.0f : 2.0f;
+    for(int base = 0; base < T.P; base += 64) {
+      const int p = base + v.lane;
+      const float q = p < T.P ? pol[p] : -1.0f;
+      const bool ok = q > 0.0f && p != ban;
+      const uint64_t m = ballot(ok);
+      if(ok) {
+        const int i = n + __popcll(m & ((1ULL << v.lane) - 1ULL));
+        cpos[i] = p;
+        cval[i] = q;
+      }
+      n += __popcll(m);
+    }
+    waveSync();
+    if(n <= 0)
+      return -1;
+    const int ci = chooseIndex(v, rng, cval, n, temp, pr);
+    waveSync();
+    return cpos[ci];
+  }
+  for(int base = 0; base < T.P; base += 64) {
+    const int q = base + v.lane;  // cell-major
+    const int p = (q & 3) * T.A + (q >> 2);
+    const bool ok = q < T.P && p != ban && isLegal(T, b, q >> 2, q & 3);
+    const uint64_t m = ballot(ok);
+    if(ok)
+      cpos[n + __popcll(m & ((1ULL << v.lane) - 1ULL))] = p;
+    n += __popcll(m);
+  }
+  waveSync();
+  if(n <= 0)
+    return -1;
+  const int k = (int)rng.below((uint32_t)n);
+  return cpos[k];
+}
+
+// A side position `b` joins the game's queue unless it is finished or the queue is full.
+KC_D void pushSide(const GV& v, GameDev& s, const DBoard& b) {
+  if(b.finished || s.sideCount >= MAX_SIDE)
+    return;
+  if(v.lane == 0)
+    v.d.side[(size_t)v.g * MAX_SIDE + s.sideCount] = b;
+  s.sideCount++;
+  waveSync();
+}
+
+// oracle startSideSearch: the next queued side position becomes the root of a full
+// search from a cleared tree (play.cpp:1586-1590: setPosition + runWholeSearchAndGetMove
+// with the bot's own parameters).
+KC_D void startSideSearch(const GV& v, GameDev& s) {
+  s.root = v.d.side[(size_t)v.g * MAX_SIDE + s.sideNext];
+  clearTables(v, s);
+  s.visitLimit = v.d.sp.maxVisits;
+  s.noNoise = 0;
+  s.moveWeight = 1.0f;
+  s.sideMode = 1;
+  s.phase = PH_ROOTEVAL;
+  s.rootK = 0;
+  s.leafKind = LEAF_NONE;
+  waveSync();
+}
+
+// After a game's rows: its side positions are searched, then the fork decision and
+// the slot's next game (play.cpp:1576-1662, selfplay gameLoop :2008).
+KC_D void afterGame(const GV& v, GameDev& s, DRng& rng, uint16_t* scratch) {
+  if(s.sideNext < s.sideCount) {
+    startSideSearch(v, s);
+    s.rngCtr = rng.ctr;
+    return;
+  }
+  s.sideMode = 0;
+  if(!maybeFork(v, s, rng, scratch))
+    startGame(v, s);
+  else
+    s.rngCtr = rng.ctr;
+}
+
+// oracle emitSideRow (writeGame side rows trainingwrite.cpp:894-937 + addRow with
+// isSidePosition, :316-565): the side position's search targets; one value target
+// (the search's root value), no next-move policy, no ownership / future boards /
+// final run lengths (the reference passes NULL for them; its finalMaxLength
+// dereference is B15, here zeros).  History masks from the game stream.
+KC_D void emitSideRow(const GV& v, const GameDev& s, const TurnRec& rec, DRng& rng) {
+  const SearchDev& d = v.d;
+  const DTables& T = v.T;
+  const int A = T.A, P = T.P, pb = (A + 7) / 8;
+  bool h = true;
+  uint32_t hm = 0;
+  for(int i = 0; i < 5; i++) {
+    h = h && rng.uni() < 0.98f;
+    hm |= (h ? 1u : 0u) << i;
+  }
+  unsigned long long r = 0;
+  if(v.lane == 0) {
+    r = atomicAdd(d.rCount, 1ull);
+    if(r >= (unsigned long long)d.rowCap) {
+      atomicAdd(d.rCount, (unsigned long long)-1ll);
+      atomicAdd(d.rDropped, 1ull);
+      r = ~0ull;
+    }
+  }
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)r, 0, 64), hi = (uint32_t)__shfl((int)(uint32_t)(r >> 32), 0, 64);
+  r = ((unsigned long long)hi << 32) | lo;
+  if(r == ~0ull)
+    return;
+  const DBoard& b = s.root;
+  const int pla = b.pla;
+  packRowBinWave(T, b, d.rBin + r * NUM_SPATIAL * pb);
+  if(v.lane == 0)
+    d.rGlob[r] = (float)T.W;
+  const int16_t* sp0 = d.sidePol + (size_t)v.g * P;
+  int16_t* pol = d.rPol + r * 2 * P;
+  for(int p = v.lane; p < P; p += 64) {
+    pol[p] = sp0[p];
+    pol[P + p] = (int16_t)1;
+  }
+  const int li = v.lane;
+  float gval = 0.0f;
+  if(li < 10)
+    gval = (li & 1) ? (pla == 2 ? rec.whiteLoss : rec.whiteWin) : (pla == 2 ? rec.whiteWin : rec.whiteLoss);
+  else if(li == 25 || li == 26 || li == 63)
+    gval = 1.0f;
+  else if(li == 30)
+    gval = rec.policySurprise;
+  else if(li == 31)
+    gval = rec.policyEntropy;
+  else if(li == 32)
+    gval = rec.searchEntropy;
+  else if(li >= 36 && li <= 40)
+    gval = ((hm >> (li - 36)) & 1u) ? 1.0f : 0.0f;
+  else if(li == 41)
+    gval = (float)(s.gameHash0 & 0x3FFFFF);
+  else if(li == 42)
+    gval = (float)((s.gameHash0 >> 22) & 0x3FFFFF);
+  else if(li == 43)
+    gval = (float)((s.gameHash0 >> 44) & 0xFFFFF);
+  else if(li == 44)
+    gval = (float)(s.gameHash1 & 0x3FFFFF);
+  else if(li == 45)
+    gval = (float)((s.gameHash1 >> 22) & 0x3FFFFF);
+  else if(li == 46)
+    gval = (float)((s.gameHash1 >> 44) & 0xFFFFF);
+  else if(li == 51)
+    gval = (float)b.turn;
+  else if(li == 53)
+    gval = (float)s.startTurn;
+  else if(li == 55)
+    gval = (float)s.gameMode;
+  else if(li == 57)
+    gval = pla == 2 ? rec.rawWhiteWL : -rec.rawWhiteWL;
+  else if(li == 59)
+    gval = rec.rawPolicyEntropy;
+  else if(li == 60)
+    gval = (float)rec.visits;
+  d.rGt[r * 64 + li] = gval;
+  int8_t* vt = d.rVal + r * 5 * A;
+  for(int i = v.lane; i < 5 * A; i += 64)
+    vt[i] = 0;
+  if(v.lane < 4) {
+    const int m = v.lane == 0 ? d.slotBase + v.g : (v.lane == 1 ? s.gameNum - 1 : (v.lane == 2 ? b.turn : s.numTurns));
+    d.rMeta[r * 4 + v.lane] = m;
+  }
+}
+
+// oracle sideEval: the network's policy at a side position's continuation picks a
+// forking move (no ban); the result joins the queue; then the next side position.
+template <int NI>
+KC_D void sideEval(const GV& v, GameDev& s, const float* o, float* scratch /* LDS [3*MAX_P] */) {
+  float w, l;
+  float pv[NI];
+  postprocess<NI>(v, s.leaf, s.leafSym, o, scratch, w, l, scratch, pv);
+  waveSync();
+  DRng rng{s.rngSeed, s.rngCtr};
+  // candidates compact in place over the policy (candidate i <= its position)
+  const int fm = forkingMove(v, rng, scratch, s.leaf, -1, reinterpret_cast<int*>(scratch + MAX_P), scratch,
+                             scratch + 2 * MAX_P);
+  if(fm >= 0) {
+    DBoard b3 = s.leaf;
+    playMoveWave(v.T, b3, fm % v.T.A, fm / v.T.A);
+    pushSide(v, s, b3);
+  }
+  s.sideNext++;
+  afterGame(v, s, rng, reinterpret_cast<uint16_t*>(scratch + MAX_P));
+  waveSync();
 }
 
 // oracle finishGame (play.cpp:1431-1460 + trainingwrite.cpp:316-565, 774-890), commit
@@ -2406,16 +2620,18 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     finishGameRecord(v, s, rng, reinterpret_cast<float*>(lds) + 2 * MAX_P);
     s.gamesFinished++;
     s.gameNum++;
-    if(!maybeFork(v, s, rng, reinterpret_cast<uint16_t*>(lds)))
-      startGame(v, s);
-    else
-      s.rngCtr = rng.ctr;
+    s.sideNext = 0;
+    afterGame(v, s, rng, reinterpret_cast<uint16_t*>(lds));
     waveSync();
     storeGame(v, s);
     return;
   }
-  // move choice: self-play disables LCB here (runBotWithLimits play.cpp:1040-1046)
-  int n = playSelectionValues<NI>(v, *v.sp, s, 0.0f, true, posv, vals, false);
+  // a side position's search (play.cpp:1576-1662) ends like a move search, but
+  // writes one row and plays nothing
+  const bool side = s.sideMode != 0;
+  // move choice: self-play disables LCB for the game's moves (runBotWithLimits
+  // play.cpp:1040-1046), not for a side position's response (:1590)
+  int n = playSelectionValues<NI>(v, *v.sp, s, 0.0f, true, posv, vals, side ? sp.useLcb != 0 : false);
   if(n <= 0) {
     s.err = 2;
     n = 1;
@@ -2439,7 +2655,7 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     rec.rows = 0;
   }
   const int t = s.numTurns;
-  int16_t* pt = v.turnPol(t);
+  int16_t* pt = side ? d.sidePol + (size_t)g * P : v.turnPol(t);
   waveSync();
   {
     for(int p = v.lane; p < P; p += 64)
@@ -2496,6 +2712,37 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     rec.searchEntropy = fmaxf(0.0f, searchEnt);
     rec.policyEntropy = fmaxf(0.0f, polEnt);
   }
+  if(side) {
+    emitSideRow(v, s, rec, rng);
+    // occasionally continue: the response, then a forking move from the network's
+    // policy there becomes another side position (play.cpp:1632-1656)
+    if(rng.uni() < 0.25f) {
+      DBoard b2 = s.root;
+      playMoveWave(v.T, b2, chosen % A, chosen / A);
+      if(!b2.finished) {
+        s.leaf = b2;
+        s.phase = PH_SIDEEVAL;
+        s.rngCtr = rng.ctr;
+        waveSync();
+        storeGame(v, s);
+        return;
+      }
+    }
+    s.sideNext++;
+    afterGame(v, s, rng, reinterpret_cast<uint16_t*>(posv));
+    waveSync();
+    storeGame(v, s);
+    return;
+  }
+  // a side position: the root policy's alternative to the move (play.cpp:1328-1345)
+  if(sp.sideProb > 0.0f && rng.uni() < sp.sideProb) {
+    const int fm = forkingMove(v, rng, v.pol(s.rootIdx), s.root, chosen, posv, vals, tmp);
+    if(fm >= 0) {
+      DBoard b2 = s.root;
+      playMoveWave(v.T, b2, fm % A, fm / A);
+      pushSide(v, s, b2);
+    }
+  }
   rec.cell = (int8_t)(chosen % A);
   rec.dir = (int8_t)(chosen / A);
   for(int i = 0; i < 5; i++)
@@ -2515,11 +2762,9 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     [[maybe_unused]] const unsigned long long t4 = SPROF_NOW();
     s.gamesFinished++;
     s.gameNum++;
+    s.sideNext = 0;
     waveSync();
-    if(!maybeFork(v, s, rng, reinterpret_cast<uint16_t*>(posv)))
-      startGame(v, s);
-    else
-      s.rngCtr = rng.ctr;
+    afterGame(v, s, rng, reinterpret_cast<uint16_t*>(posv));
     SPROF_ADD(20, t4 - t3);
     SPROF_ADD(21, SPROF_NOW() - t4);
     SPROF_ADD(23, 1);

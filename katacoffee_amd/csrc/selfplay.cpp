@@ -67,6 +67,7 @@ SP toSP(const coffee_search_params& p) {
   s.forkMinChoices = p.fork_game_min_choices;
   s.earlyForkMaxChoices = p.early_fork_game_max_choices;
   s.forkMaxChoices = p.fork_game_max_choices;
+  s.sideProb = p.side_position_prob;
   return s;
 }
 
@@ -110,6 +111,8 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
      sp.early_fork_game_max_choices < sp.fork_game_min_choices || sp.fork_game_max_choices < sp.fork_game_min_choices ||
      sp.early_fork_game_max_choices > MAX_FORK_CHOICES || sp.fork_game_max_choices > MAX_FORK_CHOICES)
     throw std::invalid_argument("fork settings: probabilities in [0, 0.5], min <= max choices <= 100");
+  if(!unit(sp.side_position_prob))
+    throw std::invalid_argument("side_position_prob must be in [0, 1]");
   const DTables& ht = hostTables(c.x, c.y, c.win_len);
   T_ = deviceTables(c.x, c.y, c.win_len);
   commitInterval_ = c.commit_interval > 0 ? c.commit_interval : 8;
@@ -171,6 +174,8 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.nnOut = devAlloc<float>(owned_, (size_t)G * (P + 4));
   d.fin = devAlloc<FinRec>(owned_, G);
   d.fork = devAlloc<ForkRec>(owned_, G);
+  d.side = devAlloc<DBoard>(owned_, (size_t)G * MAX_SIDE);
+  d.sidePol = devAlloc<int16_t>(owned_, (size_t)G * P);
   d.commitList = devAlloc<int32_t>(owned_, G);
   d.nnTimedEvals = devAlloc<unsigned long long>(owned_, 1);
   d.commitCount = devAlloc<int32_t>(owned_, 1);

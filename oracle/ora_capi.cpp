@@ -127,7 +127,7 @@ int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* 
 // policy_surprise_data_weight, value_surprise_data_weight, init_games_with_policy,
 // policy_init_area_prop, policy_init_area_temperature, early_fork_game_prob,
 // early_fork_game_expected_move_prop, fork_game_prob, fork_game_min_choices,
-// early_fork_game_max_choices, fork_game_max_choices).
+// early_fork_game_max_choices, fork_game_max_choices, side_position_prob).
 void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
                     int nnMode, void* model, int nnThreads, int cacheLog2, const float* play, int nnCap) {
   if(!T.loaded)
@@ -156,6 +156,7 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
     cfg.sp.forkGameMinChoices = (int)play[16];
     cfg.sp.earlyForkGameMaxChoices = (int)play[17];
     cfg.sp.forkGameMaxChoices = (int)play[18];
+    cfg.sp.sidePositionProb = play[19];
   }
   cfg.nodeCap = nodeCap;
   cfg.seed = seed;

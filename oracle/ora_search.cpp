@@ -70,6 +70,8 @@ inline int svbIdxMove1(int pos) { return (MAX_P + 1) + pos; }
 inline int svbIdxPla(int pla) { return 2 * (MAX_P + 1) + pla; }
 inline int svbIdxPat(int color, int wy, int wx) { return 2 * (MAX_P + 1) + 3 + color * 25 + wy * 5 + wx; }
 
+static void packBitsBE(const float* v, int len, uint8_t* out);
+
 struct Ctx {
   Selfplay& s;
   Game& gm;
@@ -951,6 +953,9 @@ struct Ctx {
     clearTree();
     gm.turns.clear();
     gm.gameMode = 0;
+    gm.side.clear();
+    gm.sideNext = 0;
+    gm.sideMode = 0;
     gm.gameHash0 = gm.rng.next();
     gm.gameHash1 = gm.rng.next();
     // initializeGameUsingPolicy (playutils.cpp:147-176): floor(Exp(1) * area * prop)
@@ -1048,6 +1053,9 @@ struct Ctx {
     gm.startTurn = prefix + 1;
     gm.initLeft = 0;
     gm.gameMode = 2;
+    gm.side.clear();
+    gm.sideNext = 0;
+    gm.sideMode = 0;
     gm.gameHash0 = gm.rng.next();
     gm.gameHash1 = gm.rng.next();
     setMoveLimits();
@@ -1128,6 +1136,146 @@ struct Ctx {
       startForkGame(bd, gm.forkPrefix, move);
   }
 
+  // chooseRandomForkingMove (play.cpp:615-633) over the post-processed policy `pol`
+  // (chooseRandomPolicyMove playutils.cpp:62-95, chooseRandomLegalMove :10-31).
+  // Returns the policy position, or -1.
+  int forkingMove(const float* pol, const Board& b, int ban) {
+    const float r = gm.rng.uni();
+    if(r < 0.95f) {
+      const float temp = r < 0.70f ? 1.0f : 2.0f;
+      int cpos[MAX_P];
+      float cval[MAX_P];
+      int n = 0;
+      for(int p = 0; p < g.P; p++)
+        if(pol[p] > 0.0f && p != ban) {
+          cpos[n] = p;
+          cval[n] = pol[p];
+          n++;
+        }
+      if(n <= 0)
+        return -1;
+      return cpos[chooseIndex(cval, n, temp)];
+    }
+    std::vector<int> legal;
+    for(int cell = 0; cell < g.A; cell++)
+      for(int dir = 0; dir < 4; dir++) {
+        const int p = dir * g.A + cell;
+        if(p != ban && isLegal(g, b, cell, dir))
+          legal.push_back(p);
+      }
+    if(legal.empty())
+      return -1;
+    return legal[gm.rng.below((uint32_t)legal.size())];
+  }
+
+  void pushSide(const Board& b) {
+    if(b.finished || (int)gm.side.size() >= MAX_SIDE)
+      return;
+    gm.side.push_back(b);
+  }
+
+  // The next side position: a full search from a cleared tree with the bot's own
+  // parameters (play.cpp:1586-1590).
+  void startSideSearch() {
+    gm.root = gm.side[gm.sideNext];
+    clearTree();
+    gm.visitLimit = s.cfg.sp.maxVisits;
+    gm.noNoise = 0;
+    gm.moveWeight = 1.0f;
+    gm.sideMode = 1;
+    gm.phase = PH_ROOTEVAL;
+    gm.rootK = 0;
+  }
+
+  // After a game's rows: its side positions, then the fork decision and the next game.
+  void afterGame() {
+    if(gm.sideNext < (int)gm.side.size()) {
+      startSideSearch();
+      return;
+    }
+    gm.sideMode = 0;
+    if(!maybeFork())
+      startGame();
+  }
+
+  // writeGame's side rows (trainingwrite.cpp:894-937, addRow with isSidePosition).
+  void emitSideRow(const TurnRec& tr) {
+    const int A = g.A, P = g.P, pb = (A + 7) / 8;
+    float hmv[5];
+    bool h = true;
+    for(int i = 0; i < 5; i++) {
+      h = h && gm.rng.uni() < 0.98f;
+      hmv[i] = h ? 1.0f : 0.0f;
+    }
+    Rows& R = s.rows;
+    const Board& b = gm.root;
+    const int pla = b.pla;
+    float bin[NUM_SPATIAL * MAX_AREA], glob[1];
+    encodeV1(g, b, 0, bin, glob);
+    const size_t r = (size_t)R.n;
+    R.n++;
+    R.bin.resize((size_t)R.n * NUM_SPATIAL * pb);
+    R.globIn.resize((size_t)R.n);
+    R.policy.resize((size_t)R.n * 2 * P);
+    R.globT.resize((size_t)R.n * 64);
+    R.value.resize((size_t)R.n * 5 * A);
+    R.meta.resize((size_t)R.n * 4);
+    R.meta[r * 4 + 0] = s.cfg.slotBase + gm.slot;
+    R.meta[r * 4 + 1] = (int32_t)gm.gameNum - 1;
+    R.meta[r * 4 + 2] = b.turn;
+    R.meta[r * 4 + 3] = (int32_t)gm.turns.size();
+    for(int ch = 0; ch < NUM_SPATIAL; ch++)
+      packBitsBE(bin + ch * A, A, &R.bin[(r * NUM_SPATIAL + ch) * pb]);
+    R.globIn[r] = glob[0];
+    for(int p = 0; p < P; p++) {
+      R.policy[r * 2 * P + p] = tr.policyTarget[p];
+      R.policy[r * 2 * P + P + p] = 1;
+    }
+    float* gt = &R.globT[r * 64];
+    for(int i = 0; i < 64; i++)
+      gt[i] = 0.0f;
+    for(int f = 0; f < 5; f++) {
+      gt[2 * f] = pla == 2 ? tr.whiteWin : tr.whiteLoss;
+      gt[2 * f + 1] = pla == 2 ? tr.whiteLoss : tr.whiteWin;
+    }
+    gt[25] = 1.0f;
+    gt[26] = 1.0f;
+    gt[30] = tr.policySurprise;
+    gt[31] = tr.policyEntropy;
+    gt[32] = tr.searchEntropy;
+    for(int i = 0; i < 5; i++)
+      gt[36 + i] = hmv[i];
+    gt[41] = (float)(gm.gameHash0 & 0x3FFFFF);
+    gt[42] = (float)((gm.gameHash0 >> 22) & 0x3FFFFF);
+    gt[43] = (float)((gm.gameHash0 >> 44) & 0xFFFFF);
+    gt[44] = (float)(gm.gameHash1 & 0x3FFFFF);
+    gt[45] = (float)((gm.gameHash1 >> 22) & 0x3FFFFF);
+    gt[46] = (float)((gm.gameHash1 >> 44) & 0xFFFFF);
+    gt[51] = (float)b.turn;
+    gt[53] = (float)gm.startTurn;
+    gt[55] = (float)gm.gameMode;
+    gt[57] = pla == 2 ? tr.rawWhiteWL : -tr.rawWhiteWL;
+    gt[59] = tr.rawPolicyEntropy;
+    gt[60] = (float)tr.visits;
+    gt[63] = 1.0f;
+    for(int i = 0; i < 5 * A; i++)
+      R.value[r * 5 * A + i] = 0;
+  }
+
+  // The network's policy at a side position's continuation picks a forking move.
+  void sideEval(const float* out) {
+    float pol[MAX_P], w, l;
+    postprocess(gm.leafBoard, gm.leafSym, out, pol, w, l);
+    const int fm = forkingMove(pol, gm.leafBoard, -1);
+    if(fm >= 0) {
+      Board b3 = gm.leafBoard;
+      playMove(g, b3, fm % g.A, fm / g.A);
+      pushSide(b3);
+    }
+    gm.sideNext++;
+    afterGame();
+  }
+
   void finishGame();
   void commitMove();
 };
@@ -1136,9 +1284,12 @@ void Ctx::commitMove() {
   int posv[MAX_P];
   float vals[MAX_P];
   TurnRec tr;
-  // getChosenMoveLoc (searchresults.cpp:435-453) inside runBotWithLimits, which disables
-  // LCB for the move choice in self-play (play.cpp:1040-1046)
-  int n = playSelectionValues(0.0f, true, posv, vals, false);
+  // a side position's search (play.cpp:1576-1662) ends like a move search, but writes
+  // one row and plays nothing
+  const bool side = gm.sideMode != 0;
+  // getChosenMoveLoc (searchresults.cpp:435-453); runBotWithLimits disables LCB for the
+  // game's moves in self-play (play.cpp:1040-1046), a side position's response keeps it
+  int n = playSelectionValues(0.0f, true, posv, vals, side ? sp.useLcbForSelection != 0 : false);
   if(n <= 0) {
     fprintf(stderr, "oracle: no move selectable\n");
     abort();
@@ -1205,6 +1356,31 @@ void Ctx::commitMove() {
     tr.searchEntropy = std::max(0.0f, searchEnt);
     tr.policyEntropy = std::max(0.0f, polEnt);
   }
+  if(side) {
+    emitSideRow(tr);
+    // occasionally continue: the response, then a forking move (play.cpp:1632-1656)
+    if(gm.rng.uni() < 0.25f) {
+      Board b2 = gm.root;
+      playMove(g, b2, chosen % g.A, chosen / g.A);
+      if(!b2.finished) {
+        gm.leafBoard = b2;
+        gm.phase = PH_SIDEEVAL;
+        return;
+      }
+    }
+    gm.sideNext++;
+    afterGame();
+    return;
+  }
+  // a side position: the root policy's alternative to the move (play.cpp:1328-1345)
+  if(s.cfg.sp.sidePositionProb > 0.0f && gm.rng.uni() < s.cfg.sp.sidePositionProb) {
+    const int fm = forkingMove(POL(gm.rootIdx), gm.root, chosen);
+    if(fm >= 0) {
+      Board b2 = gm.root;
+      playMove(g, b2, fm % g.A, fm / g.A);
+      pushSide(b2);
+    }
+  }
   tr.cell = (int8_t)(chosen % g.A);
   tr.dir = (int8_t)(chosen / g.A);
   gm.turns.push_back(tr);
@@ -1214,8 +1390,8 @@ void Ctx::commitMove() {
     finishGame();
     gm.gamesFinished++;
     gm.gameNum++;
-    if(!maybeFork())
-      startGame();
+    gm.sideNext = 0;
+    afterGame();
     return;
   }
   if(setMoveLimits())
@@ -1499,6 +1675,9 @@ void selfplayRound(Selfplay& s) {
       gm.leafKind = LEAF_INIT;
       gm.leafSym = (int)gm.rng.below(8);
       gm.leafBoard = gm.root;
+    } else if(gm.phase == PH_SIDEEVAL) {
+      gm.leafKind = LEAF_SIDE;  // leafBoard: the continuation position set by commitMove
+      gm.leafSym = (int)gm.rng.below(8);
     } else if(gm.phase == PH_FORK) {
       const int mv = gm.forkMoves[gm.forkNext];
       gm.leafBoard = gm.forkBoard;
@@ -1532,7 +1711,7 @@ void selfplayRound(Selfplay& s) {
         gm.leafSym = (int)gm.rng.below(8);
     }
     if(gm.leafKind == LEAF_NN || gm.leafKind == LEAF_ROOTEVAL || gm.leafKind == LEAF_INIT ||
-       gm.leafKind == LEAF_FORK) {
+       gm.leafKind == LEAF_FORK || gm.leafKind == LEAF_SIDE) {
       encodeV1(g, gm.leafBoard, gm.leafSym, &bin[(size_t)i * NUM_SPATIAL * A], &glob[i]);
       need[i] = 1;
       gm.nnEvals++;
@@ -1602,13 +1781,17 @@ void selfplayRound(Selfplay& s) {
         cx.finishGame();
         gm.gamesFinished++;
         gm.gameNum++;
-        if(!cx.maybeFork())
-          cx.startGame();
+        gm.sideNext = 0;
+        cx.afterGame();
       }
       continue;
     }
     if(gm.leafKind == LEAF_FORK) {
       cx.forkEval(o);
+      continue;
+    }
+    if(gm.leafKind == LEAF_SIDE) {
+      cx.sideEval(o);
       continue;
     }
     if(gm.leafKind == LEAF_ROOTEVAL) {

@@ -46,6 +46,7 @@ struct SearchParams {
   float earlyForkGameExpectedMoveProp = 0.025f;
   float forkGameProb = 0.0f;             // 0.01
   int forkGameMinChoices = 3, earlyForkGameMaxChoices = 12, forkGameMaxChoices = 36;
+  float sidePositionProb = 0.0f;         // 0.02
 };
 
 // The search parameters of a cheap search whose rows are not recorded
@@ -77,8 +78,9 @@ struct Node {
 };
 
 enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5,
-               LEAF_CACHED = 6, LEAF_INIT = 7, LEAF_FORK = 8 };
-enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_INIT = 3, PH_FORK = 4 };
+               LEAF_CACHED = 6, LEAF_INIT = 7, LEAF_FORK = 8, LEAF_SIDE = 9 };
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_INIT = 3, PH_FORK = 4, PH_SIDEEVAL = 5 };
+constexpr int MAX_SIDE = 8;  // side positions queued per game (device search.h)
 
 struct TurnRec {
   int8_t cell, dir;
@@ -139,6 +141,9 @@ struct Game {
   std::vector<int> forkMoves;
   int forkNext = 0, forkBest = -1, forkPrefix = 0;
   float forkBestWinrate = 0.0f;
+  // side positions (play.cpp:1328-1345, :1576-1662) queued during the game, searched after it
+  std::vector<Board> side;
+  int sideNext = 0, sideMode = 0;
   // tree
   int nodeCount = 0, rootIdx = -1;
   std::vector<Node> nodes;

@@ -145,6 +145,7 @@ PLAY_SETTINGS = {
     "init_games_with_policy": 0, "policy_init_area_prop": 0.04, "policy_init_area_temperature": 1.0,
     "early_fork_game_prob": 0.0, "early_fork_game_expected_move_prop": 0.025, "fork_game_prob": 0.0,
     "fork_game_min_choices": 3, "early_fork_game_max_choices": 12, "fork_game_max_choices": 36,
+    "side_position_prob": 0.0,
 }
 
 

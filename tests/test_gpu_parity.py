@@ -173,10 +173,13 @@ REDUCED = dict(reduce_visits=1, reduce_visits_threshold=0.2, reduced_visits_min=
                           (8, 24, 1200, 23, 0, dict(init_games_with_policy=1, policy_init_area_prop=0.3,
                                                     policy_init_area_temperature=2.0)),
                           (8, 24, 1600, 29, 12, FORKS),
-                          (8, 24, 1600, 37, 10, dict(PRODUCTION, init_games_with_policy=1, cheap_search_visits=8,
-                                                     reduced_visits_min=8, nn_batch_cap=5, **FORKS))],
+                          (8, 24, 1800, 43, 0, dict(side_position_prob=0.3)),
+                          (8, 24, 1800, 37, 10, dict(PRODUCTION, init_games_with_policy=1, cheap_search_visits=8,
+                                                     reduced_visits_min=8, nn_batch_cap=5, side_position_prob=0.2,
+                                                     **FORKS))],
                          ids=["bench-a", "bench-b", "cache32", "cache16k", "production", "reduced", "batch-cap",
-                              "production-cap", "production-init", "policy-init", "forks", "everything"])
+                              "production-cap", "production-init", "policy-init", "forks", "side-positions",
+                              "everything"])
 def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2, play):
     cap = 128
     gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,

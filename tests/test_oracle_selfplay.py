@@ -175,3 +175,22 @@ def test_fork_games():
     assert np.all(gt[fork, 53] >= 1) and np.all(gt[~fork, 53] == 0)
     assert np.all(meta[:, 2] >= gt[:, 53])
     np.testing.assert_array_equal(gt[:, 60], 16.0)
+
+
+def test_side_positions():
+    """Side positions (play.cpp:1328-1345, :1576-1662): searched after the game, one row
+    each with the search's value as every TD target, no next-move policy (gt[28] = 0),
+    no ownership / future boards (gt[27] = gt[33] = 0, value planes zero)."""
+    sp = oracle.Selfplay(5, 5, 4, games=6, max_visits=16, node_cap=128, seed=47, side_position_prob=0.3)
+    sp.rounds(2500)
+    r = sp.rows()
+    gt, val = r["globalTargetsNC"], r["valueTargetsNCHW"]
+    side = gt[:, 27] == 0.0
+    assert side.any() and (~side).any()
+    np.testing.assert_array_equal(gt[side, 28], 0.0)
+    np.testing.assert_array_equal(gt[side, 33], 0.0)
+    assert np.all(val[side] == 0)
+    for f in range(1, 5):  # a single value target: every TD horizon equals it
+        np.testing.assert_array_equal(gt[side, 2 * f], gt[side, 0])
+    np.testing.assert_array_equal(gt[:, 60], 16.0)
+    np.testing.assert_array_equal(r["policyTargetsNCMove"][side, 1], 1)
