@@ -62,6 +62,9 @@ def parse():
                     help="NN evaluation cache entries = 2^k (selfplay1.cfg nnCacheSizePowerOfTwo = 21); 0 = off")
     ap.add_argument("--nn-batch-cap", type=int, default=0,
                     help="rows per network launch (0 = one full wave of network workgroups)")
+    ap.add_argument("--play", choices=["benchmark", "production"], default="benchmark",
+                    help="benchmark: SURVEY 8d (one row per move at full visits, the metric's mode); "
+                         "production: selfplay1.cfg play settings (configs/selfplay1_coffee5.cfg)")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -71,6 +74,15 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the network kernel from a PMC pass (see profiles/)")
     return ap.parse_args()
+
+
+# selfplay1.cfg play settings (cpp/configs/training/selfplay1.cfg lines 24-76)
+PRODUCTION = dict(init_games_with_policy=1, policy_init_area_prop=0.04, side_position_prob=0.02,
+                  cheap_search_prob=0.75, cheap_search_visits=100, cheap_search_target_weight=0.0, reduce_visits=1,
+                  reduce_visits_threshold=0.9, reduce_visits_threshold_lookback=3, reduced_visits_min=100,
+                  reduced_visits_weight=0.1, policy_surprise_data_weight=0.5, value_surprise_data_weight=0.1,
+                  early_fork_game_prob=0.04, early_fork_game_expected_move_prop=0.025, fork_game_prob=0.01,
+                  fork_game_min_choices=3, early_fork_game_max_choices=12, fork_game_max_choices=36)
 
 
 def cpu_baseline(model_path, visits, seconds, cache_log2):
@@ -222,8 +234,10 @@ def main():
                        "games_per_gpu": args.games, "visits": args.visits, "rounds_per_step": args.rounds_per_step,
                        "commit_interval": args.commit_interval, "nn_cache_log2": args.nn_cache_log2,
                        "nn_batch_cap": args.nn_batch_cap or "one workgroup wave",
+                       "play_settings": args.play,
                        "parallelism": "game-sharded x%d" % world},
             "playouts_per_sec": playouts / elapsed,
+            "moves_per_sec": moves / elapsed,
             "nn_evals_per_sec": evals / elapsed,
             "rows_drained": rows_gathered,
             "kernels": kernels,

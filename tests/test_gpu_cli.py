@@ -104,3 +104,33 @@ def test_cli_writes_sgfs_and_hot_reloads(tmp_path):
         assert res == {1: "B+", 2: "W+", 0: "0"}[winner]
         if winner:
             assert n >= 7  # a connect-4 win needs at least 7 stones on the board
+
+
+def test_cli_production_play_settings(tmp_path):
+    """The selfplay1.cfg play settings through the CLI: rows are weighted (cheap
+    searches mostly write none), fork games and side-position rows appear, and every
+    SGF still replays legally from the empty board."""
+    models = tmp_path / "models"
+    models.mkdir()
+    kc.write_random_model("b6c96", 7, str(models / "net.cfnn"))
+    out = tmp_path / "out"
+    cmd = [os.path.join(REPO, "katacoffee_amd", "katago"), "selfplay", "-config",
+           os.path.join(REPO, "configs", "selfplay1_coffee5.cfg"), "-models-dir", str(models), "-output-dir", str(out),
+           "-max-games-total", "300", "-override-config",
+           "numGameThreads=64,maxVisits=24,cheapSearchVisits=8,reducedVisitsMin=8,maxRowsPerTrainFile=200,"
+           "sidePositionProb=0.2,earlyForkGameProb=0.3,forkGameProb=0.2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    gts = []
+    for f in glob.glob(str(out / "net" / "tdata" / "*.npz")):
+        with np.load(f) as z:
+            gts.append(z["globalTargetsNC"])
+    gt = np.concatenate(gts)
+    assert len(gt) > 0
+    assert (gt[:, 55] == 2.0).any()          # fork games
+    assert (gt[:, 27] == 0.0).any()          # side-position rows
+    assert gt[:, 60].min() >= 8 and gt[:, 60].max() <= 24
+    games = _sgf_games(glob.glob(str(out / "net" / "sgfs" / "*.sgfs")))
+    assert len(games) >= 300
+    for g in games[:80]:
+        _replay_sgf(g, 5, 5, 4)
