@@ -86,16 +86,33 @@ int coffee_encode_batch(int x, int y, int win_len, int n, const uint8_t* cells, 
 
 typedef struct coffee_nn coffee_nn;
 
-/* Writes a seeded random-init CFNN model file ("b6c96", "b10c128", "b2c32"). */
+/* Writes a seeded random-init CFNN model file ("b6c96", "b10c128", "b18c384nbt",
+ * "b2c32", "b2c32nbt"; modelconfigs.py:129/156/887). */
 int coffee_model_write_random(const char* arch, uint64_t seed, const char* path /* host */);
 /* FLOPs per evaluation (2 x MACs) of a CFNN model at area A. */
 int coffee_model_flops(const char* path, int area, double* flops);
 
-/* Loads a CFNN model and prepares device weights for boards X x Y with win length W. */
+/* Loads a CFNN model and prepares device weights for boards X x Y with win length W
+ * (NeuralNet::loadModelFile + createComputeHandle, nninterface.h:42-109).
+ * coffee_nn_create = coffee_nn_create2(..., COFFEE_NN_FAST, ...). */
 int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_nn** out);
+/* precision (the reference's useFP16 switch, nninterface.h:76-88):
+ *   COFFEE_NN_FAST          fp16 MFMA operands, f32 accumulation and residual trunk
+ *                           (the fused single-launch kernel where it covers the net,
+ *                           b6c96 @ 5x5; the layered kernels otherwise)
+ *   COFFEE_NN_ACCURATE      fp16 hi/lo operand pairs on three MFMAs (layered kernels):
+ *                           logits within 1e-3 of the fp32 (Eigen-semantics) forward
+ *   COFFEE_NN_FAST_LAYERED  fp16 operands on the layered kernels (any architecture) */
+#define COFFEE_NN_FAST 0
+#define COFFEE_NN_ACCURATE 1
+#define COFFEE_NN_FAST_LAYERED 2
+int coffee_nn_create2(const char* model_path, int x, int y, int win_len, int precision, coffee_nn** out);
+/* 1 when the handle runs the fused single-launch kernel, 0 for the layered kernels. */
+int coffee_nn_is_fused(coffee_nn* h, int* fused);
 /* in: packed V1 rows [n][ceil(15A/64)] (coffee_encode_batch layout);
  * out: [n][P+4] f32 = policy logits [4][A] (symmetric frame, dir-major), value logits
- * (win, loss) from the side to move, misc[2].  bf16 MFMA arithmetic, f32 accumulate. */
+ * (win, loss) from the side to move, misc[2].  fp16 MFMA operands (see precision),
+ * f32 accumulation. */
 int coffee_nn_forward(coffee_nn* h, int n, const uint64_t* in, float* out, void* stream);
 int coffee_nn_destroy(coffee_nn* h);
 
@@ -177,7 +194,9 @@ typedef struct coffee_selfplay_config {
                             nnCacheSizePowerOfTwo = 21); 0 disables (SPEC a7) */
   int32_t nn_batch_cap;  /* rows per network launch; leaves past it wait for the next round,
                             ahead of new ones.  0 = one full wave of network workgroups
-                            (compute units x 8 boards: 2048 on MI355X) */
+                            (compute units x 8 boards: 2048 on MI355X) for the fused
+                            kernel, unbounded for the layered kernels */
+  int32_t nn_precision;  /* COFFEE_NN_FAST / _ACCURATE / _FAST_LAYERED (0 = fast) */
 } coffee_selfplay_config;
 
 typedef struct coffee_selfplay coffee_selfplay;
@@ -192,6 +211,8 @@ typedef struct coffee_selfplay_stats {
   uint64_t rows_pending;    /* rows on the device not yet drained */
   uint64_t rows_dropped;    /* rows lost to a full row buffer (drain more often) */
   uint64_t games_dropped;   /* game records lost to a full record buffer (2 x num_games) */
+  uint64_t errors;          /* device invariant violations (node pool exhausted, no move
+                               candidate); nonzero makes step/stats return COFFEE_EINTERNAL */
 } coffee_selfplay_stats;
 
 int coffee_selfplay_create(const coffee_selfplay_config* cfg, coffee_selfplay** out);

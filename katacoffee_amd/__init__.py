@@ -22,6 +22,8 @@ CSRC = os.path.join(HERE, "csrc")
 
 NUM_SPATIAL = 15
 COFFEE_OK = 0
+# network precision / path (include/katacoffee.h COFFEE_NN_*)
+PRECISIONS = {"fast": 0, "accurate": 1, "fast-layered": 2}
 
 _lib = None
 
@@ -82,13 +84,14 @@ class SelfplayConfig(ctypes.Structure):
         ("search", SearchParams),
         ("nn_cache_log2", ctypes.c_int32),
         ("nn_batch_cap", ctypes.c_int32),
+        ("nn_precision", ctypes.c_int32),
     ]
 
 
 class SelfplayStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ["rounds", "playouts", "nn_evals", "moves", "games_finished", "rows_written", "rows_pending",
-                 "rows_dropped", "games_dropped"]]
+                 "rows_dropped", "games_dropped", "errors"]]
 
 
 # Every symbol include/katacoffee.h declares (checked by tests/test_abi.py).
@@ -96,7 +99,7 @@ EXPORTS = [
     "coffee_last_error", "coffee_abi_version", "coffee_device_count", "coffee_set_device", "coffee_malloc",
     "coffee_free", "coffee_memcpy", "coffee_synchronize", "coffee_rules_batch", "coffee_play_batch",
     "coffee_encode_batch", "coffee_model_write_random", "coffee_model_flops", "coffee_nn_create",
-    "coffee_nn_forward", "coffee_nn_destroy", "coffee_fake_net", "coffee_search_params_default",
+    "coffee_nn_forward", "coffee_nn_destroy", "coffee_nn_create2", "coffee_nn_is_fused", "coffee_fake_net", "coffee_search_params_default",
     "coffee_selfplay_create", "coffee_selfplay_step", "coffee_selfplay_sync", "coffee_selfplay_stats_get",
     "coffee_selfplay_drain_rows", "coffee_selfplay_drain_games", "coffee_selfplay_set_model",
     "coffee_selfplay_destroy", "coffee_selfplay_game_info",
@@ -131,6 +134,8 @@ def lib():
         L.coffee_model_write_random.argtypes = [ctypes.c_char_p, c_u64, ctypes.c_char_p]
         L.coffee_model_flops.argtypes = [ctypes.c_char_p, c_i, c_p]
         L.coffee_nn_create.argtypes = [ctypes.c_char_p, c_i, c_i, c_i, c_p]
+        L.coffee_nn_create2.argtypes = [ctypes.c_char_p, c_i, c_i, c_i, c_i, c_p]
+        L.coffee_nn_is_fused.argtypes = [c_p, c_p]
         L.coffee_nn_forward.argtypes = [c_p, c_i, c_p, c_p, c_p]
         L.coffee_nn_destroy.argtypes = [c_p]
         L.coffee_fake_net.argtypes = [c_i, c_i, c_i, c_i, c_p, c_p, c_p]
@@ -265,12 +270,22 @@ def model_flops(path, area):
 
 
 class Network:
-    """NeuralNet compute handle (nninterface.h createComputeHandle / getOutput)."""
+    """NeuralNet compute handle (nninterface.h createComputeHandle / getOutput).
 
-    def __init__(self, model_path, X, Y, W):
+    precision: "fast" (fp16 operands; the fused kernel where it covers the net),
+    "accurate" (fp16 hi/lo operand pairs: within 1e-3 of fp32 for any net) or
+    "fast-layered" (fp16 operands on the per-convolution kernels)."""
+
+    def __init__(self, model_path, X, Y, W, precision="fast"):
         self.X, self.Y, self.W = X, Y, W
         self.h = ctypes.c_void_p()
-        check(lib().coffee_nn_create(model_path.encode(), X, Y, W, ctypes.byref(self.h)))
+        check(lib().coffee_nn_create2(model_path.encode(), X, Y, W, PRECISIONS[precision], ctypes.byref(self.h)))
+
+    @property
+    def fused(self):
+        f = ctypes.c_int()
+        check(lib().coffee_nn_is_fused(self.h, ctypes.byref(f)))
+        return bool(f.value)
 
     def forward_device(self, n, packed_dev, out_dev, stream=None):
         check(lib().coffee_nn_forward(self.h, n, _dp(packed_dev), _dp(out_dev), stream))
@@ -339,7 +354,8 @@ class Selfplay:
     """One device's self-play engine (games [slot_base, slot_base + num_games))."""
 
     def __init__(self, X=5, Y=5, W=4, num_games=4096, max_visits=600, seed=1, slot_base=0, model_path=None,
-                 node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, nn_batch_cap=0, **search_over):
+                 node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, nn_batch_cap=0, nn_precision="fast",
+                 **search_over):
         _torch_cuda()
         self.X, self.Y, self.W = X, Y, W
         self.A, self.P = X * Y, 4 * X * Y
@@ -355,6 +371,7 @@ class Selfplay:
         cfg.commit_interval = commit_interval
         cfg.nn_cache_log2 = nn_cache_log2
         cfg.nn_batch_cap = nn_batch_cap
+        cfg.nn_precision = PRECISIONS[nn_precision]
         self._model = model_path.encode() if model_path else None
         cfg.model_path = self._model
         cfg.search = default_search_params(max_visits=max_visits, **search_over)

@@ -58,6 +58,9 @@ static int guarded(F&& f) {
   } catch(const std::invalid_argument& e) {
     gLastError = e.what();
     return COFFEE_EINVAL;
+  } catch(const InternalError& e) {
+    gLastError = e.what();
+    return COFFEE_EINTERNAL;
   } catch(const std::runtime_error& e) {
     gLastError = e.what();
     return COFFEE_EIO;
@@ -83,7 +86,7 @@ static void checkGeom(int x, int y, int w) {
 extern "C" {
 
 const char* coffee_last_error(void) { return gLastError.c_str(); }
-int coffee_abi_version(void) { return 102; }
+int coffee_abi_version(void) { return 103; }
 
 int coffee_device_count(int* count) {
   return guarded([&] {
@@ -172,14 +175,20 @@ struct coffee_nn {
 };
 
 int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_nn** out) {
+  return coffee_nn_create2(model_path, x, y, win_len, COFFEE_NN_FAST, out);
+}
+
+int coffee_nn_create2(const char* model_path, int x, int y, int win_len, int precision, coffee_nn** out) {
   return guarded([&] {
     need(model_path && out, "NULL argument");
+    need(precision == COFFEE_NN_FAST || precision == COFFEE_NN_ACCURATE || precision == COFFEE_NN_FAST_LAYERED,
+         "unknown precision");
     checkGeom(x, y, win_len);
     ModelHost m = loadModel(model_path);
     (void)deviceTables(x, y, win_len);
     coffee_nn* h = new coffee_nn{nullptr};
     try {
-      h->eng = new NNEngine(m, x, y, win_len);
+      h->eng = new NNEngine(m, x, y, win_len, precision);
     } catch(...) {
       delete h;
       throw;
@@ -194,6 +203,13 @@ int coffee_nn_forward(coffee_nn* h, int n, const uint64_t* in, float* out, void*
     need(n >= 0, "n must be >= 0");
     need(n == 0 || (in && out), "NULL buffer");
     h->eng->forward(n, in, out, (hipStream_t)stream);
+  });
+}
+
+int coffee_nn_is_fused(coffee_nn* h, int* fused) {
+  return guarded([&] {
+    need(h && h->eng && fused, "NULL argument");
+    *fused = h->eng->fused() ? 1 : 0;
   });
 }
 

@@ -39,10 +39,65 @@ struct NNLayout {
   int bngs[NN_MAX_BLOCKS], bngb[NN_MAX_BLOCKS], linG[NN_MAX_BLOCKS];
 };
 
+// Layered forward (nn_layered.hip): one implicit-GEMM MFMA launch per convolution
+// over the whole batch; any CFNN architecture (incl. nested bottlenecks) at 5x5,
+// 7x7 and 9x9.  split = "accurate" precision (fp16 hi/lo operand pairs).
+class NNLayered {
+ public:
+  NNLayered(const ModelHost& m, int X, int Y, int W, bool split);
+  ~NNLayered();
+  void forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev, const int* rowIdx);
+  static bool supportedGeometry(int X, int Y);
+
+ private:
+  struct Conv {
+    int kt = 3, cin = 0, cinReal = 0, cout = 0, tn = 3, coutTiles = 0;
+    long wOff = 0;  // 16-byte fragments into wHi_/wLo_
+  };
+  struct Block {
+    int kind = 0, width = 0;
+    int bn1s = -1, bn1b = -1, bn2s = -1, bn2b = -1, bngs = -1, bngb = -1, linGT = -1;
+    int bnPs = -1, bnPb = -1, bnQs = -1, bnQb = -1;
+    Conv conv1, conv2, convP, convQ;
+    std::vector<Block> inner;
+  };
+  struct HeadOff {
+    int pBiasG, pLinGT, pBias2, pConv2, vBias1, vLin2T, vB2, vLin3, vB3, vLinM, vBM;
+  };
+  void ensure(int n);
+  void conv(const Conv& c, int pro, const void* src, int srcLd, int srcOff, int psOff, int pbOff, const float* gb,
+            int gbLd, int epi, void* dst, int dstLd, int esOff, int ebOff, int n, const int* countDev,
+            const uint64_t* bits, const int* rowIdx, hipStream_t st);
+  void runBlock(const Block& b, float* x, int n, const int* countDev, hipStream_t st);
+  ModelCfg cfg_;
+  int X_, Y_, W_;
+  bool split_;
+  double flops_ = 0.0;
+  Conv stem_, head_;
+  std::vector<Block> blocks_;
+  int globInit_ = 0, tips_ = 0, tipb_ = 0;
+  HeadOff hw_{};
+  int maxW_ = 0, tW_ = 0, hW_ = 0;
+  void* wHi_ = nullptr;
+  void* wLo_ = nullptr;
+  float* wF_ = nullptr;
+  void* act_ = nullptr;
+  int cap_ = 0;
+  float *bufX_ = nullptr, *bufY_ = nullptr, *bufT_ = nullptr, *bufGB_ = nullptr;
+  uint16_t* bufH_ = nullptr;
+};
+
+// Network precision / path (coffee_nn_create2, coffee_selfplay_config.nn_precision)
+enum NNPath : int {
+  NN_FAST = 0,          // fp16 operands, f32 accumulation and trunk: fused kernel when it covers the net
+  NN_ACCURATE = 1,      // fp16 hi/lo operand pairs (layered path): logits within 1e-3 of fp32 for any net
+  NN_FAST_LAYERED = 2,  // fp16 operands on the layered path (comparison / any architecture)
+};
+
 class NNEngine {
  public:
   // Builds device weights for geometry X x Y (winLen W feeds the global input).
-  NNEngine(const ModelHost& m, int X, int Y, int W);
+  NNEngine(const ModelHost& m, int X, int Y, int W, int path = NN_FAST);
   ~NNEngine();
   // in: packed V1 words [n][inWords] (device); out: [n][P+4] f32 (device):
   // policy logits [4][A] in the symmetric frame, value logits (win, loss), misc[2].
@@ -52,7 +107,11 @@ class NNEngine {
                const int* rowIdx = nullptr);
   const ModelCfg& cfg() const { return cfg_; }
   double flopsPerEval() const { return flops_; }
-  static bool supported(const ModelCfg& c, int X, int Y);
+  bool fused() const { return !layered_; }
+  // rows per launch worth batching: the fused kernel costs one workgroup's latency
+  // per wave of workgroups, so its batch is capped at one wave (cus x 8 boards)
+  int batchCap(int cus) const { return layered_ ? (1 << 30) : cus * NN_BOARDS_PER_WG; }
+  static bool fusedSupported(const ModelCfg& c, int X, int Y);
 
  private:
   ModelCfg cfg_;
@@ -63,6 +122,9 @@ class NNEngine {
   float* wF32_ = nullptr;  // device
   NNLayout* layoutDev_ = nullptr;
   uint16_t* tabDev_ = nullptr;  // device row tables (nn.hip rowTables)
+  float* trunk_ = nullptr;      // f32 residual trunk scratch, [workgroup][fragment] (nn.hip)
+  int trunkCap_ = 0;            // workgroups it covers
+  std::unique_ptr<NNLayered> layered_;
 };
 
 // Deterministic stand-in network (see oracle fakeNet); same I/O as NNEngine.

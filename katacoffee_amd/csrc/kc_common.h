@@ -25,6 +25,12 @@ constexpr int MAX_IN_WORDS = (NUM_SPATIAL * MAX_AREA + 63) / 64;
 struct HipError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+// invariant violation detected on the device (COFFEE_EINTERNAL at the C ABI)
+struct InternalError : std::exception {
+  std::string msg;
+  explicit InternalError(std::string m) : msg(std::move(m)) {}
+  const char* what() const noexcept override { return msg.c_str(); }
+};
 
 #define KC_HIP(call)                                                                                      \
   do {                                                                                                    \

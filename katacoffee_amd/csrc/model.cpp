@@ -19,6 +19,15 @@ ModelCfg modelCfgByName(const std::string& name) {
     // modelconfigs.py:156-180
     c.C = 128; c.Cg = 32; c.p1 = 32; c.g1 = 32; c.v1 = 32; c.v2 = 80;
     c.kinds = {0, 0, 0, 0, 1, 0, 0, 1, 0, 0};
+  } else if(name == "b18c384nbt") {
+    // modelconfigs.py:887-924: 18 "bottlenest2" blocks (every third from rconv3 with a
+    // gpool inner block), trunk 384, bottleneck 192, gpool 64
+    c.C = 384; c.mid = 192; c.Cg = 64; c.p1 = 48; c.g1 = 48; c.v1 = 96; c.v2 = 128;
+    c.kinds = {2, 2, 3, 2, 2, 3, 2, 2, 3, 2, 2, 3, 2, 2, 3, 2, 2, 2};
+  } else if(name == "b2c32nbt") {
+    // small nested-bottleneck net for tests
+    c.C = 64; c.mid = 32; c.Cg = 16; c.p1 = 16; c.g1 = 16; c.v1 = 16; c.v2 = 32;
+    c.kinds = {3, 2};
   } else if(name == "b2c32") {
     c.C = 32; c.Cg = 16; c.p1 = 16; c.g1 = 16; c.v1 = 16; c.v2 = 32;
     c.kinds = {0, 1};
@@ -46,38 +55,54 @@ struct Init {
 };
 }  // namespace
 
+static ModelBlock randomBlock(Init& in, int k, int W, int Cg, int mid) {
+  auto he = [](int fanIn) { return std::sqrt(2.0f / (float)fanIn); };
+  ModelBlock b;
+  b.kind = k;
+  if(k >= 2) {
+    b.bnPs = in.around(W, 1.0f, 0.1f);
+    b.bnPb = in.normal(W, 0.1f);
+    b.convP = in.normal((size_t)mid * W, he(W));
+    b.inner.push_back(randomBlock(in, k == 3 ? 1 : 0, mid, Cg, 0));
+    b.inner.push_back(randomBlock(in, 0, mid, Cg, 0));
+    b.bnQs = in.around(mid, 1.0f, 0.1f);
+    b.bnQb = in.normal(mid, 0.1f);
+    b.convQ = in.normal((size_t)W * mid, 0.5f * he(mid));
+    return b;
+  }
+  const int Cr = W - Cg;
+  b.bn1s = in.around(W, 1.0f, 0.1f);
+  b.bn1b = in.normal(W, 0.1f);
+  if(k == 0) {
+    b.conv1 = in.normal((size_t)W * W * 9, he(W * 9));
+    b.bn2s = in.around(W, 1.0f, 0.1f);
+    b.bn2b = in.normal(W, 0.1f);
+    b.conv2 = in.normal((size_t)W * W * 9, 0.5f * he(W * 9));
+  } else {
+    b.conv1 = in.normal((size_t)Cr * W * 9, 0.8f * he(W * 9));
+    b.conv1g = in.normal((size_t)Cg * W * 9, he(W * 9));
+    b.bngs = in.around(Cg, 1.0f, 0.1f);
+    b.bngb = in.normal(Cg, 0.1f);
+    b.linG = in.normal((size_t)Cr * 3 * Cg, 0.6f * he(3 * Cg));
+    b.bn2s = in.around(Cr, 1.0f, 0.1f);
+    b.bn2b = in.normal(Cr, 0.1f);
+    b.conv2 = in.normal((size_t)W * Cr * 9, 0.5f * he(Cr * 9));
+  }
+  return b;
+}
+
 // He-normal convolutions, near-identity merged BN (SURVEY §8d synthetic init),
 // residual branches scaled by 0.5 so the trunk stays O(1) without fixup zeros.
 ModelHost randomModel(const ModelCfg& cfg, uint64_t seed) {
   ModelHost m;
   m.cfg = cfg;
   Init in{DRng{mix64(seed ^ 0xC0FFEEULL), 0}};
-  const int C = cfg.C, Cr = cfg.C - cfg.Cg;
+  const int C = cfg.C;
   auto he = [](int fanIn) { return std::sqrt(2.0f / (float)fanIn); };
   m.convInit = in.normal((size_t)C * cfg.cin * 9, he(cfg.cin * 9));
   m.globInit = in.normal((size_t)C * cfg.gin, 0.1f);
-  for(int k : cfg.kinds) {
-    ModelBlock b;
-    b.kind = k;
-    b.bn1s = in.around(C, 1.0f, 0.1f);
-    b.bn1b = in.normal(C, 0.1f);
-    if(k == 0) {
-      b.conv1 = in.normal((size_t)C * C * 9, he(C * 9));
-      b.bn2s = in.around(C, 1.0f, 0.1f);
-      b.bn2b = in.normal(C, 0.1f);
-      b.conv2 = in.normal((size_t)C * C * 9, 0.5f * he(C * 9));
-    } else {
-      b.conv1 = in.normal((size_t)Cr * C * 9, 0.8f * he(C * 9));
-      b.conv1g = in.normal((size_t)cfg.Cg * C * 9, he(C * 9));
-      b.bngs = in.around(cfg.Cg, 1.0f, 0.1f);
-      b.bngb = in.normal(cfg.Cg, 0.1f);
-      b.linG = in.normal((size_t)Cr * 3 * cfg.Cg, 0.6f * he(3 * cfg.Cg));
-      b.bn2s = in.around(Cr, 1.0f, 0.1f);
-      b.bn2b = in.normal(Cr, 0.1f);
-      b.conv2 = in.normal((size_t)C * Cr * 9, 0.5f * he(Cr * 9));
-    }
-    m.blocks.push_back(std::move(b));
-  }
+  for(int k : cfg.kinds)
+    m.blocks.push_back(randomBlock(in, k, C, cfg.Cg, cfg.mid));
   m.tips = in.around(C, 1.0f, 0.1f);
   m.tipb = in.normal(C, 0.1f);
   m.pConv1 = in.normal((size_t)cfg.p1 * C, 0.8f * he(C));
@@ -97,16 +122,42 @@ ModelHost randomModel(const ModelCfg& cfg, uint64_t seed) {
   return m;
 }
 
+static bool hasBottleneck(const ModelCfg& c) {
+  for(int k : c.kinds)
+    if(k >= 2)
+      return true;
+  return false;
+}
+
+static void writeBlock(FILE* f, const ModelBlock& b) {
+  auto w = [&](const std::vector<float>& v) { fwrite(v.data(), 4, v.size(), f); };
+  if(b.kind >= 2) {
+    w(b.bnPs); w(b.bnPb); w(b.convP);
+    writeBlock(f, b.inner[0]);
+    writeBlock(f, b.inner[1]);
+    w(b.bnQs); w(b.bnQb); w(b.convQ);
+    return;
+  }
+  w(b.bn1s);
+  w(b.bn1b);
+  if(b.kind == 0) {
+    w(b.conv1); w(b.bn2s); w(b.bn2b); w(b.conv2);
+  } else {
+    w(b.conv1); w(b.conv1g); w(b.bngs); w(b.bngb); w(b.linG); w(b.bn2s); w(b.bn2b); w(b.conv2);
+  }
+}
+
 void saveModel(const std::string& path, const ModelHost& m) {
   FILE* f = fopen(path.c_str(), "wb");
   if(!f)
     throw std::runtime_error("cannot write model " + path);
   fwrite("CFNN", 1, 4, f);
-  int32_t ver = 1;
-  fwrite(&ver, 4, 1, f);
   const ModelCfg& c = m.cfg;
-  int32_t hdr[9] = {c.cin, c.gin, c.C, c.Cg, c.p1, c.g1, c.v1, c.v2, (int32_t)c.kinds.size()};
-  fwrite(hdr, 4, 9, f);
+  const bool v2 = hasBottleneck(c);
+  int32_t ver = v2 ? 2 : 1;
+  fwrite(&ver, 4, 1, f);
+  int32_t hdr[10] = {c.cin, c.gin, c.C, c.Cg, c.p1, c.g1, c.v1, c.v2, (int32_t)c.kinds.size(), c.mid};
+  fwrite(hdr, 4, v2 ? 10 : 9, f);
   for(int k : c.kinds) {
     int32_t kk = k;
     fwrite(&kk, 4, 1, f);
@@ -114,79 +165,107 @@ void saveModel(const std::string& path, const ModelHost& m) {
   auto w = [&](const std::vector<float>& v) { fwrite(v.data(), 4, v.size(), f); };
   w(m.convInit);
   w(m.globInit);
-  for(const ModelBlock& b : m.blocks) {
-    w(b.bn1s);
-    w(b.bn1b);
-    if(b.kind == 0) {
-      w(b.conv1); w(b.bn2s); w(b.bn2b); w(b.conv2);
-    } else {
-      w(b.conv1); w(b.conv1g); w(b.bngs); w(b.bngb); w(b.linG); w(b.bn2s); w(b.bn2b); w(b.conv2);
-    }
-  }
+  for(const ModelBlock& b : m.blocks)
+    writeBlock(f, b);
   w(m.tips); w(m.tipb);
   w(m.pConv1); w(m.pConvG); w(m.pBiasG); w(m.pLinG); w(m.pBias2); w(m.pConv2);
   w(m.vConv1); w(m.vBias1); w(m.vLin2); w(m.vB2); w(m.vLin3); w(m.vB3); w(m.vLinM); w(m.vBM);
   fclose(f);
 }
 
+namespace {
+struct FileReader {
+  FILE* f;
+  bool ok = true;
+  void r(std::vector<float>& v, size_t n) {
+    v.resize(n);
+    if(fread(v.data(), 4, n, f) != n)
+      ok = false;
+  }
+  void block(ModelBlock& b, int k, int W, int Cg, int mid) {
+    b.kind = k;
+    if(k >= 2) {
+      r(b.bnPs, W); r(b.bnPb, W); r(b.convP, (size_t)mid * W);
+      b.inner.resize(2);
+      block(b.inner[0], k == 3 ? 1 : 0, mid, Cg, 0);
+      block(b.inner[1], 0, mid, Cg, 0);
+      r(b.bnQs, mid); r(b.bnQb, mid); r(b.convQ, (size_t)W * mid);
+      return;
+    }
+    const int Cr = W - Cg;
+    r(b.bn1s, W);
+    r(b.bn1b, W);
+    if(k == 0) {
+      r(b.conv1, (size_t)W * W * 9); r(b.bn2s, W); r(b.bn2b, W); r(b.conv2, (size_t)W * W * 9);
+    } else {
+      r(b.conv1, (size_t)Cr * W * 9); r(b.conv1g, (size_t)Cg * W * 9); r(b.bngs, Cg); r(b.bngb, Cg);
+      r(b.linG, (size_t)Cr * 3 * Cg); r(b.bn2s, Cr); r(b.bn2b, Cr); r(b.conv2, (size_t)W * Cr * 9);
+    }
+  }
+};
+}  // namespace
+
 ModelHost loadModel(const std::string& path) {
   FILE* f = fopen(path.c_str(), "rb");
   if(!f)
     throw std::runtime_error("cannot open model " + path);
   char magic[4];
-  int32_t ver = 0, hdr[9];
-  if(fread(magic, 1, 4, f) != 4 || memcmp(magic, "CFNN", 4) != 0 || fread(&ver, 4, 1, f) != 1 || ver != 1 ||
-     fread(hdr, 4, 9, f) != 9 || hdr[8] < 1 || hdr[8] > 64) {
+  int32_t ver = 0, hdr[10] = {0};
+  if(fread(magic, 1, 4, f) != 4 || memcmp(magic, "CFNN", 4) != 0 || fread(&ver, 4, 1, f) != 1 ||
+     (ver != 1 && ver != 2) || fread(hdr, 4, ver == 1 ? 9 : 10, f) != (size_t)(ver == 1 ? 9 : 10) || hdr[8] < 1 ||
+     hdr[8] > 64) {
     fclose(f);
-    throw std::runtime_error("not a CFNN v1 model: " + path);
+    throw std::runtime_error("not a CFNN v1/v2 model: " + path);
   }
   ModelHost m;
   ModelCfg& c = m.cfg;
   c.cin = hdr[0]; c.gin = hdr[1]; c.C = hdr[2]; c.Cg = hdr[3]; c.p1 = hdr[4]; c.g1 = hdr[5]; c.v1 = hdr[6];
   c.v2 = hdr[7];
+  c.mid = ver == 2 ? hdr[9] : 0;
   c.kinds.resize(hdr[8]);
-  bool ok = fread(c.kinds.data(), 4, hdr[8], f) == (size_t)hdr[8];
-  auto r = [&](std::vector<float>& v, size_t n) {
-    v.resize(n);
-    if(fread(v.data(), 4, n, f) != n)
-      ok = false;
-  };
-  const int C = c.C, Cr = c.C - c.Cg;
-  r(m.convInit, (size_t)C * c.cin * 9);
-  r(m.globInit, (size_t)C * c.gin);
+  FileReader rd{f};
+  rd.ok = fread(c.kinds.data(), 4, hdr[8], f) == (size_t)hdr[8];
+  for(int k : c.kinds)
+    if(k < 0 || k > 3 || (k >= 2 && c.mid <= 0))
+      rd.ok = false;
+  if(!rd.ok) {
+    fclose(f);
+    throw std::runtime_error("bad block kinds in model " + path);
+  }
+  const int C = c.C;
+  rd.r(m.convInit, (size_t)C * c.cin * 9);
+  rd.r(m.globInit, (size_t)C * c.gin);
   for(int k : c.kinds) {
     ModelBlock b;
-    b.kind = k;
-    r(b.bn1s, C);
-    r(b.bn1b, C);
-    if(k == 0) {
-      r(b.conv1, (size_t)C * C * 9); r(b.bn2s, C); r(b.bn2b, C); r(b.conv2, (size_t)C * C * 9);
-    } else {
-      r(b.conv1, (size_t)Cr * C * 9); r(b.conv1g, (size_t)c.Cg * C * 9); r(b.bngs, c.Cg); r(b.bngb, c.Cg);
-      r(b.linG, (size_t)Cr * 3 * c.Cg); r(b.bn2s, Cr); r(b.bn2b, Cr); r(b.conv2, (size_t)C * Cr * 9);
-    }
+    rd.block(b, k, C, c.Cg, c.mid);
     m.blocks.push_back(std::move(b));
   }
-  r(m.tips, C); r(m.tipb, C);
-  r(m.pConv1, (size_t)c.p1 * C); r(m.pConvG, (size_t)c.g1 * C); r(m.pBiasG, c.g1);
-  r(m.pLinG, (size_t)c.p1 * 3 * c.g1); r(m.pBias2, c.p1); r(m.pConv2, (size_t)4 * c.p1);
-  r(m.vConv1, (size_t)c.v1 * C); r(m.vBias1, c.v1); r(m.vLin2, (size_t)c.v2 * 3 * c.v1); r(m.vB2, c.v2);
-  r(m.vLin3, (size_t)2 * c.v2); r(m.vB3, 2); r(m.vLinM, (size_t)2 * c.v2); r(m.vBM, 2);
+  rd.r(m.tips, C); rd.r(m.tipb, C);
+  rd.r(m.pConv1, (size_t)c.p1 * C); rd.r(m.pConvG, (size_t)c.g1 * C); rd.r(m.pBiasG, c.g1);
+  rd.r(m.pLinG, (size_t)c.p1 * 3 * c.g1); rd.r(m.pBias2, c.p1); rd.r(m.pConv2, (size_t)4 * c.p1);
+  rd.r(m.vConv1, (size_t)c.v1 * C); rd.r(m.vBias1, c.v1); rd.r(m.vLin2, (size_t)c.v2 * 3 * c.v1); rd.r(m.vB2, c.v2);
+  rd.r(m.vLin3, (size_t)2 * c.v2); rd.r(m.vB3, 2); rd.r(m.vLinM, (size_t)2 * c.v2); rd.r(m.vBM, 2);
+  const bool trailing = fgetc(f) != EOF;
   fclose(f);
-  if(!ok)
-    throw std::runtime_error("truncated model file " + path);
+  if(!rd.ok || trailing)
+    throw std::runtime_error("truncated or oversized model file " + path);
   return m;
 }
 
+static double blockMacs(int k, double A, double W, double Cg, double mid) {
+  if(k >= 2)
+    return A * W * mid + blockMacs(k == 3 ? 1 : 0, A, mid, Cg, 0) + blockMacs(0, A, mid, Cg, 0) + A * mid * W;
+  if(k == 0)
+    return 2.0 * A * W * W * 9.0;
+  const double Cr = W - Cg;
+  return A * W * W * 9.0 + Cr * 3.0 * Cg + A * W * Cr * 9.0;
+}
+
 double modelFlopsPerEval(const ModelCfg& c, int A) {
-  const double C = c.C, Cr = c.C - c.Cg;
+  const double C = c.C;
   double macs = A * C * c.cin * 9.0 + C * c.gin;
-  for(int k : c.kinds) {
-    if(k == 0)
-      macs += 2.0 * A * C * C * 9.0;
-    else
-      macs += A * C * C * 9.0 + Cr * 3.0 * c.Cg + A * C * Cr * 9.0;
-  }
+  for(int k : c.kinds)
+    macs += blockMacs(k, A, C, c.Cg, c.mid);
   macs += A * C * (c.p1 + c.g1) + 3.0 * c.g1 * c.p1 + A * 4.0 * c.p1;
   macs += A * C * c.v1 + 3.0 * c.v1 * c.v2 + 4.0 * c.v2;
   return 2.0 * macs;

@@ -14,9 +14,9 @@
 //    A = activations gathered from LDS by neighbour offset (fp16, NHWC, padded
 //    rows -> conflict-free ds_read_b128), B = weights pre-swizzled on the host
 //    into per-lane 16-byte fragments streamed from L2 (one dwordx4 per lane);
-//  * the residual trunk x lives in registers (fp16, accumulator layout) for the
-//    whole network; only the fp16 conv input is staged through LDS, so HBM sees
-//    the 48-byte packed input and the 416-byte output per board and nothing else;
+//  * the f32 residual trunk lives in the accumulators between blocks and is
+//    parked in a workgroup-private L2-resident scratch during each block's first
+//    conv; only the fp16 conv input is staged through LDS;
 //  * BN + ReLU, global pooling, the gpool bias and both heads are fused epilogues.
 // Waves: rg = wave>>1 owns a contiguous range of 16-row tiles, cg = wave&1 owns
 // half of the output channels.
@@ -264,23 +264,32 @@ KC_D void stageT96(float* __restrict__ dst, const float* __restrict__ src, int r
   }
 }
 
-// The residual trunk is kept in registers as fp16 (RNE) between blocks; the
-// oracle's GPU-emulation mode rounds at the same points.
+// The residual trunk is f32.  Between blocks it lives in the accumulators; while
+// a block's first convolution owns them it is parked in a workgroup-private global
+// scratch in accumulator-fragment order (1 KiB contiguous per wave and tile, an
+// L2-resident round trip per block), so trained nets keep f32 trunk precision
+// without the 24 VGPRs a register copy would cost.
 template <class G>
-KC_D void packX(f16x4 (&xh)[G::MAXT][G::NCT], const f32x4 (&a)[G::MAXT][G::NCT]) {
-#pragma unroll
-  for(int t = 0; t < G::MAXT; t++)
-#pragma unroll
-    for(int ct = 0; ct < G::NCT; ct++)
-      xh[t][ct] = __builtin_convertvector(a[t][ct], f16x4);
+KC_D f32x4* trunkBase(float* trunk, int wave, int lane) {
+  return reinterpret_cast<f32x4*>(trunk) + ((size_t)blockIdx.x * NN_WAVES + wave) * (G::MAXT * G::NCT * 64) + lane;
 }
 template <class G>
-KC_D void unpackX(f32x4 (&a)[G::MAXT][G::NCT], const f16x4 (&xh)[G::MAXT][G::NCT]) {
+KC_D void storeTrunk(float* trunk, const f32x4 (&a)[G::MAXT][G::NCT], int wave, int lane) {
+  f32x4* p = trunkBase<G>(trunk, wave, lane);
 #pragma unroll
   for(int t = 0; t < G::MAXT; t++)
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++)
-      a[t][ct] = __builtin_convertvector(xh[t][ct], f32x4);
+      p[(t * G::NCT + ct) * 64] = a[t][ct];
+}
+template <class G>
+KC_D void loadTrunk(f32x4 (&a)[G::MAXT][G::NCT], float* trunk, int wave, int lane) {
+  const f32x4* p = trunkBase<G>(trunk, wave, lane);
+#pragma unroll
+  for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++)
+      a[t][ct] = p[(t * G::NCT + ct) * 64];
 }
 
 template <class G>
@@ -459,7 +468,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
                const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
                const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
-               float* __restrict__ out) {
+               float* __restrict__ out, float* __restrict__ trunk) {
   using G = NNGeo<X, Y, C>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
@@ -504,8 +513,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   NN_PHASE(1);
   int ab[G::MAXT];
   aBases<G>(ab, rowPa, tstart, lane);
-  f16x4 x[G::MAXT][G::NCT];
-  f32x4 acc[G::MAXT][G::NCT];
+  f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   zeroAcc<G>(acc);
   convTiles<G, 9, 1, true>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                            L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL, L->nblocks > 0 ? 9 : 1);
@@ -523,7 +531,8 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       }
     }
   }
-  packX<G>(x, acc);
+  if(L->nblocks > 0)
+    storeTrunk<G>(trunk, acc, wave, lane);
   if(tid < G::NPRM)
     prm[tid] = pre;
   const int Cr = G::C - L->Cg;
@@ -532,7 +541,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     __syncthreads();  // previous conv finished reading act
     NN_PHASE(3 + 4 * blk);
     const float* P = prm + (blk & 1) * G::NPRM;
-    storeBnRelu<G>(act, rowPa, x, P, P + 96, tstart, cg, lane);
+    storeBnRelu<G>(act, rowPa, acc, P, P + 96, tstart, cg, lane);
     __syncthreads();
     zeroAcc<G>(acc);
     pre = loadParam(L, WF, blk + 1, tid);  // next slab: its latency hides behind conv1
@@ -548,12 +557,13 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     const int nextTaps = lastBlk ? 1 : 9;
     if(L->kinds[blk] == 0) {
       storeBnRelu<G>(act, rowPa, acc, P + 192, P + 288, tstart, cg, lane);
+      loadTrunk<G>(acc, trunk, wave, lane);  // lands during the barrier / stream wait below
       __syncthreads();
-      unpackX<G>(acc, x);
       NN_PHASE(6 + 4 * blk);
       convTiles<G, 9, G::C / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                         3 * G::NCT_ALL, nextTaps);
-      packX<G>(x, acc);
+      if(!lastBlk)
+        storeTrunk<G>(trunk, acc, wave, lane);
     } else {
       // g branch: BN-ReLU into scr (f32, aliases the dead conv input), then
       // KataGPool per board (model_pytorch.py:326-352)
@@ -613,19 +623,20 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
           }
         }
       }
+      loadTrunk<G>(acc, trunk, wave, lane);
       __syncthreads();
-      unpackX<G>(acc, x);
       NN_PHASE(6 + 4 * blk);
       convTiles<G, 9, (G::C - 32) / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                3 * G::NCT_ALL, nextTaps);
-      packX<G>(x, acc);
+      if(!lastBlk)
+        storeTrunk<G>(trunk, acc, wave, lane);
     }
   }
   // ---- trunk tip ----
   __syncthreads();
   NN_PHASE(40);
   const float* PT = prm + (L->nblocks & 1) * G::NPRM;  // tip slab
-  storeBnRelu<G>(act, rowPa, x, PT, PT + 96, tstart, cg, lane);
+  storeBnRelu<G>(act, rowPa, acc, PT, PT + 96, tstart, cg, lane);
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
@@ -809,15 +820,22 @@ static std::vector<uint16_t> rowTables() {
   return tab;
 }
 
-bool NNEngine::supported(const ModelCfg& c, int X, int Y) {
+bool NNEngine::fusedSupported(const ModelCfg& c, int X, int Y) {
+  for(int k : c.kinds)
+    if(k > 1)
+      return false;
   return X == 5 && Y == 5 && c.C == 96 && c.Cg == 32 && c.p1 == 32 && c.g1 == 32 && c.v1 == 32 && c.v2 <= 64 && c.v2 % 4 == 0 &&
          c.cin == NUM_SPATIAL && c.gin == 1 && (int)c.kinds.size() <= NN_MAX_BLOCKS;
 }
 
-NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W) : cfg_(m.cfg), X_(X), Y_(Y), W_(W) {
-  if(!supported(m.cfg, X, Y))
-    throw std::invalid_argument("NNEngine: unsupported architecture/geometry (round 1 ships b6c96 @ 5x5)");
+NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.cfg), X_(X), Y_(Y), W_(W) {
   flops_ = modelFlopsPerEval(cfg_, X * Y);
+  if(path != NN_FAST && path != NN_ACCURATE && path != NN_FAST_LAYERED)
+    throw std::invalid_argument("NNEngine: unknown precision/path");
+  if(path != NN_FAST || !fusedSupported(m.cfg, X, Y)) {
+    layered_.reset(new NNLayered(m, X, Y, W, path == NN_ACCURATE));
+    return;
+  }
   const int C = cfg_.C, Cr = C - cfg_.Cg;
   std::vector<uint16_t> wb;
   std::vector<float> wf;
@@ -894,13 +912,12 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W) : cfg_(m.cfg), X_(X)
   const std::vector<uint16_t> tab = rowTables<G>();
   KC_HIP(hipMalloc(&tabDev_, tab.size() * 2));
   KC_HIP(hipMemcpy(tabDev_, tab.data(), tab.size() * 2, hipMemcpyHostToDevice));
-  static std::once_flag once;
-  std::call_once(once, [] {
-    KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-  });
+  // function attributes are per device: every engine sets it on its own device
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
 }
 
 NNEngine::~NNEngine() {
+  (void)hipFree(trunk_);
   (void)hipFree(wHalf_);
   (void)hipFree(wF32_);
   (void)hipFree(layoutDev_);
@@ -911,11 +928,24 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
                        const int* rowIdx) {
   if(n <= 0)
     return;
+  if(layered_) {
+    layered_->forward(n, in, out, st, countDev, rowIdx);
+    return;
+  }
   using G = NNGeo<5, 5, 96>;
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
   int grid = (n + G::NB - 1) / G::NB;
+  if(grid > trunkCap_) {
+    // stream-ordered: a launch still using the old scratch finishes before the free
+    if(trunk_)
+      KC_HIP(hipStreamSynchronize(st));
+    (void)hipFree(trunk_);
+    trunk_ = nullptr;
+    KC_HIP(hipMalloc(&trunk_, (size_t)grid * NN_WAVES * G::MAXT * G::NCT * 64 * 16));
+    trunkCap_ = grid;
+  }
   hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_,
-                     (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out);
+                     (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
   KC_HIP(hipGetLastError());
 }
 

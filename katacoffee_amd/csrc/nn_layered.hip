@@ -1,0 +1,788 @@
+// Layered residual-network forward: one MFMA implicit-GEMM launch per convolution
+// over the whole leaf batch, for every CFNN architecture (b6c96, b10c128,
+// b18c384nbt nested bottlenecks, ...) and board geometry (5x5, 7x7, 9x9).
+//
+// Semantics: eigenbackend.cpp (ConvLayer :270-680, BatchNormLayer :684-734,
+// poolRowsGPool :141-166, poolRowsValueHead :168-186, ResidualBlock :888-931,
+// GlobalPoolingResidualBlock :935-1015, Trunk :1169-1227, PolicyHead :1229-1299,
+// ValueHead :1301-1377); nested bottleneck blocks model_pytorch.py:860-958.
+//
+// MI355X design (DESIGN.md §3 "kConvL"):
+//  * activations live in HBM, NHWC: the residual trunk(s) in f32, activated conv
+//    inputs in fp16 where an epilogue can produce them (BN-ReLU of a conv output);
+//    BN-ReLU of a trunk is fused into the next conv's prologue (f32 -> fp16 while
+//    staging into LDS), the residual add into the conv's epilogue;
+//  * a 512-thread workgroup owns BPW whole boards (~250 output rows, 16 row tiles)
+//    and 32*TN output channels per wave column; the K loop runs over 32-channel
+//    slices: each slice of the boards' activations is staged (with a one-cell zero
+//    border, so every 3x3 neighbour is a fixed LDS row offset) into a
+//    double-buffered LDS stage while the previous slice's 9 taps run on
+//    v_mfma_f32_16x16x32_f16 (computed transposed, weights x activations, so each
+//    lane holds 4 consecutive output channels of one row);
+//  * weights are pre-swizzled on the host into per-lane 16-byte B fragments in
+//    [slice][tap][col tile] order and prefetched two K steps ahead into registers
+//    straight from L2 (every workgroup reads the same few hundred KB);
+//  * SPLIT ("accurate" precision): every operand is carried as an fp16 pair
+//    hi + lo (lo = fp16(x - hi)), each product as hi*hi + lo*hi + hi*lo on three
+//    MFMAs -> ~22-bit operands, logits within 1e-3 of the fp32 reference for any
+//    net.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <set>
+#include <vector>
+
+#include "engine.h"
+
+namespace kc {
+
+typedef _Float16 lh16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 lh16x4 __attribute__((ext_vector_type(4)));
+typedef float lf32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int L_WAVES = 8, L_NT = L_WAVES * 64;
+constexpr int L_WM = 4, L_WN = 2;  // wave grid: 4 row groups x 2 column groups
+constexpr int L_STRIDE = 40;       // fp16 per staged row: 32 channels + 8 pad (80 B rows)
+
+enum LPro : int { PRO_BITS = 0, PRO_F16 = 1, PRO_BN = 2, PRO_BN_GB = 3 };
+enum LEpi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_BNRELU16 = 2, EPI_STEM = 3 };
+
+template <int X_, int Y_>
+struct LGeo {
+  static constexpr int X = X_, Y = Y_, A = X_ * Y_;
+  static constexpr int BPW = 256 / A < 1 ? 1 : 256 / A;  // boards per workgroup
+  static constexpr int ROWS = BPW * A;
+  static constexpr int RT = (ROWS + 15) / 16;
+  static constexpr int TM = (RT + L_WM - 1) / L_WM;  // row tiles per wave
+  static constexpr int PX = X + 2, PY = Y + 2, PA = PX * PY;
+  static constexpr int PROWS = BPW * PA;
+  static constexpr int STAGE = PROWS * L_STRIDE * 2;  // bytes per staged 32-channel slice
+};
+
+struct LConvArgs {
+  // prologue: the conv input, channels [0, cinReal) of cin (multiple of 32)
+  int pro, cin, cinReal;
+  const void* src;
+  int srcLd, srcOff;
+  const float* ps;  // BN scale / bias (PRO_BN, PRO_BN_GB)
+  const float* pb;
+  const float* gb;  // per-board bias [board][gbLd] (PRO_BN_GB)
+  int gbLd;
+  const uint64_t* bits;  // PRO_BITS: packed V1 rows
+  int inWords;
+  const int* rowIdx;
+  // weights: [cin/32][taps][coutPad/16][64] 16-byte fragments (hi, lo)
+  const lh16x8* w;
+  const lh16x8* wlo;
+  int coutTiles;
+  // epilogue: channels [0, cout)
+  int epi, cout;
+  void* dst;
+  int dstLd, dstOff;
+  const float* es;
+  const float* eb;
+  const float* glob;  // EPI_STEM: globInit [C] (gin == 1), times winLen
+  float winLen;
+  // batch
+  int n;
+  const int* countDev;
+};
+
+KC_D uint32_t packHalf2(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) |
+         ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+}
+
+// One 32-channel slice of the workgroup's boards into an LDS stage (hi and, for
+// SPLIT, lo planes).  Rows are padded cells; borders stay zero (set once).
+template <class G, bool SPLIT>
+KC_D void stageSlice(const LConvArgs& a, char* stHi, char* stLo, int cb, int base, int nb, const float* sS,
+                     const float* sB, const float* sG, int tid) {
+  constexpr int TASKS = G::ROWS * 4;  // (row, 8-channel chunk)
+  for(int t = tid; t < TASKS; t += L_NT) {
+    const int r = t >> 2, q = t & 3;
+    const int brd = r / G::A, p = r - brd * G::A;
+    const int pr = brd * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1;
+    const int c0 = cb * 32 + q * 8;
+    float v[8];
+    if(brd >= nb) {
+#pragma unroll
+      for(int j = 0; j < 8; j++)
+        v[j] = 0.0f;
+    } else if(a.pro == PRO_BITS) {
+      const int src = a.rowIdx ? a.rowIdx[base + brd] : base + brd;
+      const uint64_t* w = a.bits + (size_t)src * a.inWords;
+#pragma unroll
+      for(int j = 0; j < 8; j++) {
+        const int c = c0 + j;
+        float bit = 0.0f;
+        if(c < a.cinReal) {
+          const int i = c * G::A + p;
+          bit = (float)((w[i >> 6] >> (i & 63)) & 1ULL);
+        }
+        v[j] = bit;
+      }
+    } else {
+      const size_t g = (size_t)(base + brd) * G::A + p;
+      if(a.pro == PRO_F16) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(a.src) + g * a.srcLd + c0);
+        *reinterpret_cast<uint4*>(stHi + (pr * L_STRIDE + q * 8) * 2) = raw;
+        continue;
+      }
+      const float* s = reinterpret_cast<const float*>(a.src) + g * a.srcLd + a.srcOff + c0;
+      const float4 x0 = *reinterpret_cast<const float4*>(s);
+      const float4 x1 = *reinterpret_cast<const float4*>(s + 4);
+      float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for(int j = 0; j < 8; j++) {
+        const int c = c0 + j;
+        float x = xs[j];
+        if(a.pro == PRO_BN_GB && c < a.cinReal)
+          x += sG[brd * a.gbLd + c];
+        const float y = fmaxf(x * sS[c] + sB[c], 0.0f);
+        v[j] = c < a.cinReal ? y : 0.0f;
+      }
+    }
+    uint4 hi;
+    hi.x = packHalf2(v[0], v[1]);
+    hi.y = packHalf2(v[2], v[3]);
+    hi.z = packHalf2(v[4], v[5]);
+    hi.w = packHalf2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(stHi + (pr * L_STRIDE + q * 8) * 2) = hi;
+    if constexpr(SPLIT) {
+      float lo[8];
+#pragma unroll
+      for(int j = 0; j < 8; j++)
+        lo[j] = v[j] - (float)(_Float16)v[j];
+      uint4 l4;
+      l4.x = packHalf2(lo[0], lo[1]);
+      l4.y = packHalf2(lo[2], lo[3]);
+      l4.z = packHalf2(lo[4], lo[5]);
+      l4.w = packHalf2(lo[6], lo[7]);
+      *reinterpret_cast<uint4*>(stLo + (pr * L_STRIDE + q * 8) * 2) = l4;
+    }
+  }
+}
+
+template <int X, int Y, int KT, int TN, bool SPLIT>
+__global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
+  using G = LGeo<X, Y>;
+  constexpr int T = KT * KT;
+  constexpr int NCT = TN * L_WN;  // column tiles per workgroup
+  constexpr int PLANES = SPLIT ? 2 : 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int count = a.countDev ? min(*a.countDev, a.n) : a.n;
+  const int base = blockIdx.x * G::BPW;
+  if(base >= count)
+    return;
+  const int nb = min(G::BPW, count - base);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ctBase = blockIdx.y * NCT + wn * TN;  // this wave's first global column tile
+  char* stage = smem;                                        // [2][PLANES][STAGE]
+  float* sS = reinterpret_cast<float*>(smem + 2 * PLANES * G::STAGE);  // [cin]
+  float* sB = sS + a.cin;
+  float* sG = sB + a.cin;  // [BPW][gbLd]
+  // zero both stages (borders and boards past the batch stay zero), parameters to LDS
+  for(int i = tid; i < 2 * PLANES * G::STAGE / 16; i += L_NT)
+    reinterpret_cast<uint4*>(smem)[i] = uint4{0u, 0u, 0u, 0u};
+  if(a.pro == PRO_BN || a.pro == PRO_BN_GB)
+    for(int i = tid; i < a.cin; i += L_NT) {
+      sS[i] = i < a.cinReal ? a.ps[i] : 0.0f;
+      sB[i] = i < a.cinReal ? a.pb[i] : 0.0f;
+    }
+  if(a.pro == PRO_BN_GB)
+    for(int i = tid; i < nb * a.gbLd; i += L_NT)
+      sG[i] = a.gb[(size_t)base * a.gbLd + i];
+  __syncthreads();
+  const int NCB = a.cin / 32;
+  stageSlice<G, SPLIT>(a, stage, stage + G::STAGE, 0, base, nb, sS, sB, sG, tid);
+
+  // per-lane A row bases (bytes, shifted to the (-r,-r) neighbour), padding rows -> row 0
+  int ab[G::TM];
+#pragma unroll
+  for(int t = 0; t < G::TM; t++) {
+    int r = (wm * G::TM + t) * 16 + (lane & 15);
+    if(r >= G::ROWS)
+      r = 0;
+    const int brd = r / G::A, p = r - brd * G::A;
+    const int pr = brd * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1;
+    const int shift = KT == 3 ? G::PX + 1 : 0;
+    ab[t] = ((pr - shift) * L_STRIDE) * 2 + 16 * (lane >> 4);
+  }
+  lf32x4 acc[G::TM][TN];
+#pragma unroll
+  for(int t = 0; t < G::TM; t++)
+#pragma unroll
+    for(int c = 0; c < TN; c++)
+      acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  // B fragments: step s = cb*T + tap; a ring of R register slots loaded R-1 steps
+  // ahead (3x3: R = 3, slot = tap % 3 since 9 % 3 == 0; 1x1: R = 2, slot = cb & 1)
+  constexpr int R = T % 3 == 0 ? 3 : 2;
+  const lh16x8* wl = a.w + (size_t)ctBase * 64 + lane;
+  const lh16x8* wlo = SPLIT ? a.wlo + (size_t)ctBase * 64 + lane : nullptr;
+  const size_t stepStride = (size_t)a.coutTiles * 64;
+  lh16x8 bh[R][TN], bl[R][SPLIT ? TN : 1];
+  auto loadB = [&](int s, int slot) {
+#pragma unroll
+    for(int c = 0; c < TN; c++) {
+      bh[slot][c] = wl[(size_t)s * stepStride + c * 64];
+      if constexpr(SPLIT)
+        bl[slot][c] = wlo[(size_t)s * stepStride + c * 64];
+    }
+  };
+  const int S = NCB * T;
+#pragma unroll
+  for(int i = 0; i < R - 1; i++)
+    if(i < S)
+      loadB(i, i);
+  __syncthreads();
+
+  // one K step: tap of slice cb from the stage at stHi/stLo, B slot `slot`
+  auto step = [&](int cb, int tap, int slot, const char* stHi, const char* stLo) {
+    const int s = cb * T + tap;
+    if(s + R - 1 < S)
+      loadB(s + R - 1, (slot + R - 1) % R);
+    const int dy = KT == 3 ? tap / 3 : 0, dx = KT == 3 ? tap % 3 : 0;
+    const int aoff = (dy * G::PX + dx) * L_STRIDE * 2;
+    lh16x8 ah[G::TM], al[SPLIT ? G::TM : 1];
+#pragma unroll
+    for(int t = 0; t < G::TM; t++) {
+      ah[t] = *reinterpret_cast<const lh16x8*>(stHi + ab[t] + aoff);
+      if constexpr(SPLIT)
+        al[t] = *reinterpret_cast<const lh16x8*>(stLo + ab[t] + aoff);
+    }
+#pragma unroll
+    for(int t = 0; t < G::TM; t++)
+#pragma unroll
+      for(int c = 0; c < TN; c++) {
+        acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[slot][c], ah[t], acc[t][c], 0, 0, 0);
+        if constexpr(SPLIT) {
+          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[slot][c], ah[t], acc[t][c], 0, 0, 0);
+          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[slot][c], al[t], acc[t][c], 0, 0, 0);
+        }
+      }
+  };
+  // one slice: its taps, then stage the next slice into the other buffer
+  auto slice = [&](int cb, int parity) {
+    const char* stHi = stage + (cb & 1) * PLANES * G::STAGE;
+    const char* stLo = stHi + G::STAGE;
+    if constexpr(T % 3 == 0) {
+#pragma unroll
+      for(int tap = 0; tap < T; tap++)
+        step(cb, tap, tap % 3, stHi, stLo);
+    } else {
+      step(cb, 0, parity, stHi, stLo);
+    }
+    if(cb + 1 < NCB) {
+      char* nHi = stage + ((cb + 1) & 1) * PLANES * G::STAGE;
+      stageSlice<G, SPLIT>(a, nHi, nHi + G::STAGE, cb + 1, base, nb, sS, sB, sG, tid);
+    }
+    __syncthreads();
+  };
+  int cb = 0;
+  for(; cb + 1 < NCB; cb += 2) {
+    slice(cb, 0);
+    slice(cb + 1, 1);
+  }
+  if(cb < NCB)
+    slice(cb, 0);
+
+  // ---- epilogue: lane holds channels ch..ch+3 of row (lane & 15) of each tile ----
+  const int rowsValid = nb * G::A;
+#pragma unroll
+  for(int t = 0; t < G::TM; t++) {
+    const int r = (wm * G::TM + t) * 16 + (lane & 15);
+    if(r >= rowsValid)
+      continue;
+    const size_t g = (size_t)base * G::A + r;
+#pragma unroll
+    for(int c = 0; c < TN; c++) {
+      const int ch = (ctBase + c) * 16 + 4 * (lane >> 4);
+      if(ch >= a.cout)
+        continue;
+      const lf32x4 v = acc[t][c];
+      if(a.epi == EPI_BNRELU16) {
+        const float4 s4 = *reinterpret_cast<const float4*>(a.es + ch);
+        const float4 b4 = *reinterpret_cast<const float4*>(a.eb + ch);
+        uint2 h;
+        h.x = packHalf2(fmaxf(v[0] * s4.x + b4.x, 0.0f), fmaxf(v[1] * s4.y + b4.y, 0.0f));
+        h.y = packHalf2(fmaxf(v[2] * s4.z + b4.z, 0.0f), fmaxf(v[3] * s4.w + b4.w, 0.0f));
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.dst) + g * a.dstLd + a.dstOff + ch) = h;
+      } else {
+        float* d = reinterpret_cast<float*>(a.dst) + g * a.dstLd + a.dstOff + ch;
+        float4 o = float4{v[0], v[1], v[2], v[3]};
+        if(a.epi == EPI_ADD) {
+          const float4 old = *reinterpret_cast<const float4*>(d);
+          o = float4{old.x + o.x, old.y + o.y, old.z + o.z, old.w + o.w};
+        } else if(a.epi == EPI_STEM) {
+          const float4 g4 = *reinterpret_cast<const float4*>(a.glob + ch);
+          o = float4{o.x + g4.x * a.winLen, o.y + g4.y * a.winLen, o.z + g4.z * a.winLen, o.w + g4.w * a.winLen};
+        }
+        *reinterpret_cast<float4*>(d) = o;
+      }
+    }
+  }
+}
+
+// Gpool branch of a gpool block: g = relu(T[:, Cr:Cr+Cg] * s + b), KataGPool
+// (mean, mean*(sqrt(A)-14)/10, max), bias[Cr] = linG x pooled.  One workgroup per board.
+__global__ void __launch_bounds__(256) kGpoolBias(const float* __restrict__ T, int ld, int A, int Cr, int Cg,
+                                                  const float* __restrict__ gs, const float* __restrict__ gbias,
+                                                  const float* __restrict__ linGT /*[3Cg][Cr]*/, float* __restrict__ out,
+                                                  int n, const int* __restrict__ countDev) {
+  __shared__ float pooled[3 * 128];
+  const int count = countDev ? min(*countDev, n) : n;
+  const int b = blockIdx.x;
+  if(b >= count)
+    return;
+  const float sqOff = sqrtf((float)A) - 14.0f;
+  const float* Tb = T + (size_t)b * A * ld + Cr;
+  for(int c = threadIdx.x; c < Cg; c += blockDim.x) {
+    float s = 0.0f, m = 0.0f;
+    for(int p = 0; p < A; p++) {
+      const float v = fmaxf(Tb[(size_t)p * ld + c] * gs[c] + gbias[c], 0.0f);
+      s += v;
+      m = fmaxf(m, v);
+    }
+    const float mean = s / (float)A;
+    pooled[c] = mean;
+    pooled[Cg + c] = mean * (sqOff / 10.0f);
+    pooled[2 * Cg + c] = m;
+  }
+  __syncthreads();
+  for(int o = threadIdx.x; o < Cr; o += blockDim.x) {
+    float s = 0.0f;
+    for(int k = 0; k < 3 * Cg; k++)
+      s += linGT[(size_t)k * Cr + o] * pooled[k];
+    out[(size_t)b * Cr + o] = s;
+  }
+}
+
+struct LHeadW {
+  const float *pBiasG, *pLinGT, *pBias2, *pConv2, *vBias1, *vLin2T, *vB2, *vLin3, *vB3, *vLinM, *vBM;
+  int p1, g1, v1, v2;
+};
+
+// Policy and value heads from T = [p | g | v] (raw 1x1 conv outputs of the tip),
+// PolicyHead::apply :1265-1299 / ValueHead::apply :1341-1377 with Coffee outputs:
+// out[dst] = policy [4][A] (direction-major), value (2), misc (2).  One workgroup per board.
+__global__ void __launch_bounds__(256) kHeadsL(const float* __restrict__ T, int ld, int A, LHeadW h,
+                                               float* __restrict__ out, const int* __restrict__ rowIdx, int n,
+                                               const int* __restrict__ countDev) {
+  __shared__ float pp[3 * 64], vp[3 * 128], pb[64], vh[256];
+  const int count = countDev ? min(*countDev, n) : n;
+  const int b = blockIdx.x;
+  if(b >= count)
+    return;
+  const float sqOff = sqrtf((float)A) - 14.0f;
+  const float* Tb = T + (size_t)b * A * ld;
+  const int tid = threadIdx.x;
+  for(int c = tid; c < h.g1 + h.v1; c += blockDim.x) {
+    const bool isG = c < h.g1;
+    const int cc = isG ? c : c - h.g1;
+    const int col = isG ? h.p1 + cc : h.p1 + h.g1 + cc;
+    const float bias = isG ? h.pBiasG[cc] : h.vBias1[cc];
+    float s = 0.0f, m = 0.0f;
+    for(int p = 0; p < A; p++) {
+      const float v = fmaxf(Tb[(size_t)p * ld + col] + bias, 0.0f);
+      s += v;
+      m = fmaxf(m, v);
+    }
+    const float mean = s / (float)A;
+    if(isG) {
+      pp[cc] = mean;
+      pp[h.g1 + cc] = mean * (sqOff / 10.0f);
+      pp[2 * h.g1 + cc] = m;
+    } else {
+      vp[cc] = mean;
+      vp[h.v1 + cc] = mean * (sqOff / 10.0f);
+      vp[2 * h.v1 + cc] = mean * ((sqOff * sqOff) / 100.0f - 0.1f);
+    }
+  }
+  __syncthreads();
+  for(int o = tid; o < h.p1 + h.v2; o += blockDim.x) {
+    if(o < h.p1) {
+      float s = 0.0f;
+      for(int k = 0; k < 3 * h.g1; k++)
+        s += h.pLinGT[(size_t)k * h.p1 + o] * pp[k];
+      pb[o] = s + h.pBias2[o];
+    } else {
+      const int q = o - h.p1;
+      float s = h.vB2[q];
+      for(int k = 0; k < 3 * h.v1; k++)
+        s += h.vLin2T[(size_t)k * h.v2 + q] * vp[k];
+      vh[q] = fmaxf(s, 0.0f);
+    }
+  }
+  __syncthreads();
+  float* o = out + (size_t)(rowIdx ? rowIdx[b] : b) * (4 * A + 4);
+  for(int i = tid; i < 4 * A; i += blockDim.x) {
+    const int d = i / A, p = i - d * A;
+    const float* tp = Tb + (size_t)p * ld;
+    float s = 0.0f;
+    for(int k = 0; k < h.p1; k++)
+      s += h.pConv2[d * h.p1 + k] * fmaxf(tp[k] + pb[k], 0.0f);
+    o[i] = s;
+  }
+  if(tid < 4) {
+    const float* w = tid < 2 ? h.vLin3 + tid * h.v2 : h.vLinM + (tid - 2) * h.v2;
+    float s = tid < 2 ? h.vB3[tid] : h.vBM[tid - 2];
+    for(int k = 0; k < h.v2; k++)
+      s += w[k] * vh[k];
+    o[4 * A + tid] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+
+namespace {
+
+uint16_t lf2h(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+
+template <int X, int Y, int KT, int TN, bool SPLIT>
+void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
+  using G = LGeo<X, Y>;
+  const size_t lds = 2 * (SPLIT ? 2 : 1) * G::STAGE + (2 * a.cin + G::BPW * (a.gbLd > 0 ? a.gbLd : 0)) * 4;
+  auto fn = kConvL<X, Y, KT, TN, SPLIT>;
+  static std::mutex mu;
+  static std::set<int> done;  // devices whose attribute is set (per device)
+  int dev = 0;
+  KC_HIP(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if(!done.count(dev)) {
+      KC_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      done.insert(dev);
+    }
+  }
+  const int gy = (a.coutTiles + TN * L_WN - 1) / (TN * L_WN);
+  hipLaunchKernelGGL(fn, dim3(grid, gy), dim3(L_NT), lds, st, a);
+  KC_HIP(hipGetLastError());
+}
+
+template <int X, int Y, bool SPLIT>
+void launchConvG(const LConvArgs& a, int kt, int tn, int grid, hipStream_t st) {
+  if(kt == 3) {
+    if(tn == 2) launchConvT<X, Y, 3, 2, SPLIT>(a, grid, st);
+    else if(tn == 3) launchConvT<X, Y, 3, 3, SPLIT>(a, grid, st);
+    else launchConvT<X, Y, 3, 4, SPLIT>(a, grid, st);
+  } else {
+    if(tn == 2) launchConvT<X, Y, 1, 2, SPLIT>(a, grid, st);
+    else if(tn == 3) launchConvT<X, Y, 1, 3, SPLIT>(a, grid, st);
+    else launchConvT<X, Y, 1, 4, SPLIT>(a, grid, st);
+  }
+}
+
+int lBoardsPerWG(int X, int Y) {
+  if(X == 5 && Y == 5) return LGeo<5, 5>::BPW;
+  if(X == 7 && Y == 7) return LGeo<7, 7>::BPW;
+  return LGeo<9, 9>::BPW;
+}
+
+}  // namespace
+
+bool NNLayered::supportedGeometry(int X, int Y) { return (X == 5 && Y == 5) || (X == 7 && Y == 7) || (X == 9 && Y == 9); }
+
+// Column tiles per wave for a conv with `cout` outputs: the widest of 4/3/2 that
+// tiles the (padded) output channels in 32*TN-wide workgroup columns.
+static int chooseTN(int cout) {
+  if(cout % 128 == 0) return 4;
+  if(cout % 96 == 0) return 3;
+  return 2;
+}
+
+NNLayered::NNLayered(const ModelHost& m, int X, int Y, int W, bool split)
+    : cfg_(m.cfg), X_(X), Y_(Y), W_(W), split_(split) {
+  if(!supportedGeometry(X, Y))
+    throw std::invalid_argument("NNLayered: board geometry must be 5x5, 7x7 or 9x9");
+  if(cfg_.gin != 1 || cfg_.cin > 32 || cfg_.p1 > 64 || cfg_.g1 > 64 || cfg_.v1 > 128 || cfg_.v2 > 256 ||
+     cfg_.Cg > 128)
+    throw std::invalid_argument("NNLayered: head/gpool widths out of range");
+  const int A = X * Y;
+  std::vector<uint16_t> wh, wl;  // fragments (8 fp16 each), hi / lo
+  std::vector<float> wf;
+  auto f32 = [&](const std::vector<float>& v) {
+    const int off = (int)wf.size();
+    wf.insert(wf.end(), v.begin(), v.end());
+    while(wf.size() % 4)
+      wf.push_back(0.0f);
+    return off;
+  };
+  auto transpose = [](const std::vector<float>& w, int O, int I) {  // [O][I] -> [I][O]
+    std::vector<float> t((size_t)O * I);
+    for(int o = 0; o < O; o++)
+      for(int i = 0; i < I; i++)
+        t[(size_t)i * O + o] = w[(size_t)o * I + i];
+    return t;
+  };
+  // Conv weights W(co, ci, tap) -> fragments [cb][tap][ct][lane][8]
+  auto packConvL = [&](int kt, int cin, int cout, const std::function<float(int, int, int)>& Wf) {
+    Conv c;
+    c.kt = kt;
+    c.cinReal = cin;
+    c.cin = (cin + 31) / 32 * 32;
+    c.cout = cout;
+    c.tn = chooseTN(cout);
+    const int ncw = 32 * c.tn;
+    c.coutTiles = (cout + ncw - 1) / ncw * ncw / 16;
+    c.wOff = (long)(wh.size() / 8);
+    const int taps = kt * kt;
+    for(int cb = 0; cb < c.cin / 32; cb++)
+      for(int tap = 0; tap < taps; tap++)
+        for(int ct = 0; ct < c.coutTiles; ct++)
+          for(int l = 0; l < 64; l++)
+            for(int j = 0; j < 8; j++) {
+              const int co = ct * 16 + (l & 15), ci = cb * 32 + 8 * (l >> 4) + j;
+              const float v = (co < cout && ci < cin) ? Wf(co, ci, tap) : 0.0f;
+              const uint16_t h = lf2h(v);
+              _Float16 hf;
+              memcpy(&hf, &h, 2);
+              wh.push_back(h);
+              wl.push_back(lf2h(v - (float)hf));
+            }
+    return c;
+  };
+  auto conv3 = [&](const std::vector<float>& w, int cin, int cout) {
+    return packConvL(3, cin, cout, [&](int co, int ci, int tap) { return w[((size_t)co * cin + ci) * 9 + tap]; });
+  };
+  auto conv1 = [&](const std::vector<float>& w, int cin, int cout) {
+    return packConvL(1, cin, cout, [&](int co, int ci, int) { return w[(size_t)co * cin + ci]; });
+  };
+  // regular / gpool block at trunk width Wd
+  std::function<void(const ModelBlock&, int, Block&)> buildBlock = [&](const ModelBlock& b, int Wd, Block& o) {
+    o.kind = b.kind;
+    o.width = Wd;
+    if(b.kind >= 2) {
+      const int mid = cfg_.mid;
+      o.bnPs = f32(b.bnPs);
+      o.bnPb = f32(b.bnPb);
+      o.convP = conv1(b.convP, Wd, mid);
+      o.inner.resize(2);
+      buildBlock(b.inner[0], mid, o.inner[0]);
+      buildBlock(b.inner[1], mid, o.inner[1]);
+      o.bnQs = f32(b.bnQs);
+      o.bnQb = f32(b.bnQb);
+      o.convQ = conv1(b.convQ, mid, Wd);
+      return;
+    }
+    o.bn1s = f32(b.bn1s);
+    o.bn1b = f32(b.bn1b);
+    if(b.kind == 0) {
+      o.conv1 = conv3(b.conv1, Wd, Wd);
+      o.bn2s = f32(b.bn2s);
+      o.bn2b = f32(b.bn2b);
+      o.conv2 = conv3(b.conv2, Wd, Wd);
+    } else {
+      const int Cg = cfg_.Cg, Cr = Wd - Cg;
+      o.conv1 = packConvL(3, Wd, Wd, [&](int co, int ci, int tap) {
+        return co < Cr ? b.conv1[((size_t)co * Wd + ci) * 9 + tap] : b.conv1g[((size_t)(co - Cr) * Wd + ci) * 9 + tap];
+      });
+      o.bngs = f32(b.bngs);
+      o.bngb = f32(b.bngb);
+      o.linGT = f32(transpose(b.linG, Cr, 3 * Cg));
+      o.bn2s = f32(b.bn2s);
+      o.bn2b = f32(b.bn2b);
+      o.conv2 = conv3(b.conv2, Cr, Wd);
+    }
+  };
+  const int C = cfg_.C;
+  stem_ = packConvL(3, cfg_.cin, C, [&](int co, int ci, int tap) {
+    return m.convInit[((size_t)co * cfg_.cin + ci) * 9 + tap];
+  });
+  globInit_ = f32(m.globInit);
+  blocks_.resize(cfg_.kinds.size());
+  for(size_t i = 0; i < blocks_.size(); i++)
+    buildBlock(m.blocks[i], C, blocks_[i]);
+  tips_ = f32(m.tips);
+  tipb_ = f32(m.tipb);
+  const int HWd = cfg_.p1 + cfg_.g1 + cfg_.v1;
+  head_ = packConvL(1, C, HWd, [&](int co, int ci, int) {
+    if(co < cfg_.p1)
+      return m.pConv1[(size_t)co * C + ci];
+    if(co < cfg_.p1 + cfg_.g1)
+      return m.pConvG[(size_t)(co - cfg_.p1) * C + ci];
+    return m.vConv1[(size_t)(co - cfg_.p1 - cfg_.g1) * C + ci];
+  });
+  hw_.pBiasG = f32(m.pBiasG);
+  hw_.pLinGT = f32(transpose(m.pLinG, cfg_.p1, 3 * cfg_.g1));
+  hw_.pBias2 = f32(m.pBias2);
+  hw_.pConv2 = f32(m.pConv2);
+  hw_.vBias1 = f32(m.vBias1);
+  hw_.vLin2T = f32(transpose(m.vLin2, cfg_.v2, 3 * cfg_.v1));
+  hw_.vB2 = f32(m.vB2);
+  hw_.vLin3 = f32(m.vLin3);
+  hw_.vB3 = f32(m.vB3);
+  hw_.vLinM = f32(m.vLinM);
+  hw_.vBM = f32(m.vBM);
+  // widest activation buffers
+  maxW_ = C;
+  if(cfg_.mid > maxW_)
+    maxW_ = cfg_.mid;
+  tW_ = std::max(maxW_, HWd);
+  // pad T / H widths so every column tile of the widest conv stays in bounds
+  tW_ = (tW_ + 127) / 128 * 128;
+  hW_ = (maxW_ + 127) / 128 * 128;
+  KC_HIP(hipMalloc(&wHi_, wh.size() * 2));
+  KC_HIP(hipMemcpy(wHi_, wh.data(), wh.size() * 2, hipMemcpyHostToDevice));
+  if(split_) {
+    KC_HIP(hipMalloc(&wLo_, wl.size() * 2));
+    KC_HIP(hipMemcpy(wLo_, wl.data(), wl.size() * 2, hipMemcpyHostToDevice));
+  }
+  KC_HIP(hipMalloc(&wF_, wf.size() * 4));
+  KC_HIP(hipMemcpy(wF_, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+  flops_ = modelFlopsPerEval(cfg_, A);
+}
+
+NNLayered::~NNLayered() {
+  (void)hipFree(wHi_);
+  (void)hipFree(wLo_);
+  (void)hipFree(wF_);
+  (void)hipFree(act_);
+}
+
+void NNLayered::ensure(int n) {
+  if(n <= cap_)
+    return;
+  (void)hipFree(act_);
+  act_ = nullptr;
+  const int bpw = lBoardsPerWG(X_, Y_);
+  const int nPad = (n + bpw - 1) / bpw * bpw;
+  const size_t rows = (size_t)nPad * X_ * Y_;
+  // X f32 [rows][C] | Y f32 [rows][mid] | T f32 [rows][tW] | H f16 [rows][hW] | gb f32 [nPad][C]
+  const size_t bytes = rows * (cfg_.C + cfg_.mid + tW_) * 4 + rows * hW_ * 2 + (size_t)nPad * maxW_ * 4 + 256;
+  KC_HIP(hipMalloc(&act_, bytes));
+  char* p = reinterpret_cast<char*>(act_);
+  bufX_ = reinterpret_cast<float*>(p);
+  p += rows * cfg_.C * 4;
+  bufY_ = reinterpret_cast<float*>(p);
+  p += rows * cfg_.mid * 4;
+  bufT_ = reinterpret_cast<float*>(p);
+  p += rows * tW_ * 4;
+  bufH_ = reinterpret_cast<uint16_t*>(p);
+  p += rows * hW_ * 2;
+  bufGB_ = reinterpret_cast<float*>(p);
+  cap_ = nPad;
+}
+
+void NNLayered::conv(const Conv& c, int pro, const void* src, int srcLd, int srcOff, int psOff, int pbOff,
+                     const float* gb, int gbLd, int epi, void* dst, int dstLd, int esOff, int ebOff, int n,
+                     const int* countDev, const uint64_t* bits, const int* rowIdx, hipStream_t st) {
+  LConvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.pro = pro;
+  a.cin = c.cin;
+  a.cinReal = c.cinReal;
+  a.src = src;
+  a.srcLd = srcLd;
+  a.srcOff = srcOff;
+  a.ps = psOff >= 0 ? wF_ + psOff : nullptr;
+  a.pb = pbOff >= 0 ? wF_ + pbOff : nullptr;
+  a.gb = gb;
+  a.gbLd = gb ? gbLd : 0;
+  a.bits = bits;
+  a.inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
+  a.rowIdx = rowIdx;
+  a.w = reinterpret_cast<const lh16x8*>(wHi_) + c.wOff;
+  a.wlo = split_ ? reinterpret_cast<const lh16x8*>(wLo_) + c.wOff : nullptr;
+  a.coutTiles = c.coutTiles;
+  a.epi = epi;
+  a.cout = c.cout;
+  a.dst = dst;
+  a.dstLd = dstLd;
+  a.dstOff = 0;
+  a.es = esOff >= 0 ? wF_ + esOff : nullptr;
+  a.eb = ebOff >= 0 ? wF_ + ebOff : nullptr;
+  a.glob = wF_ + globInit_;
+  a.winLen = (float)W_;
+  a.n = n;
+  a.countDev = countDev;
+  const int bpw = lBoardsPerWG(X_, Y_);
+  const int grid = (n + bpw - 1) / bpw;
+  const bool sp = split_;
+  if(X_ == 5)
+    sp ? launchConvG<5, 5, true>(a, c.kt, c.tn, grid, st) : launchConvG<5, 5, false>(a, c.kt, c.tn, grid, st);
+  else if(X_ == 7)
+    sp ? launchConvG<7, 7, true>(a, c.kt, c.tn, grid, st) : launchConvG<7, 7, false>(a, c.kt, c.tn, grid, st);
+  else
+    sp ? launchConvG<9, 9, true>(a, c.kt, c.tn, grid, st) : launchConvG<9, 9, false>(a, c.kt, c.tn, grid, st);
+}
+
+// x: trunk (f32, width = block width) updated in place.
+void NNLayered::runBlock(const Block& b, float* x, int n, const int* countDev, hipStream_t st) {
+  const int Wd = b.width;
+  if(b.kind >= 2) {
+    const int mid = cfg_.mid;
+    conv(b.convP, PRO_BN, x, Wd, 0, b.bnPs, b.bnPb, nullptr, 0, EPI_STORE, bufY_, mid, -1, -1, n, countDev, nullptr,
+         nullptr, st);
+    for(const Block& in : b.inner)
+      runBlock(in, bufY_, n, countDev, st);
+    conv(b.convQ, PRO_BN, bufY_, mid, 0, b.bnQs, b.bnQb, nullptr, 0, EPI_ADD, x, Wd, -1, -1, n, countDev, nullptr,
+         nullptr, st);
+    return;
+  }
+  if(b.kind == 0 && !split_) {
+    // mid activation BN2-ReLU'd in conv1's epilogue, stored fp16 (the conv2 operand)
+    conv(b.conv1, PRO_BN, x, Wd, 0, b.bn1s, b.bn1b, nullptr, 0, EPI_BNRELU16, bufH_, hW_, b.bn2s, b.bn2b, n,
+         countDev, nullptr, nullptr, st);
+    conv(b.conv2, PRO_F16, bufH_, hW_, 0, -1, -1, nullptr, 0, EPI_ADD, x, Wd, -1, -1, n, countDev, nullptr, nullptr,
+         st);
+  } else if(b.kind == 0) {
+    // split precision: the mid activation stays f32 so conv2's prologue can form hi + lo
+    conv(b.conv1, PRO_BN, x, Wd, 0, b.bn1s, b.bn1b, nullptr, 0, EPI_STORE, bufT_, tW_, -1, -1, n, countDev, nullptr,
+         nullptr, st);
+    conv(b.conv2, PRO_BN, bufT_, tW_, 0, b.bn2s, b.bn2b, nullptr, 0, EPI_ADD, x, Wd, -1, -1, n, countDev, nullptr,
+         nullptr, st);
+  } else {
+    const int Cg = cfg_.Cg, Cr = Wd - Cg;
+    conv(b.conv1, PRO_BN, x, Wd, 0, b.bn1s, b.bn1b, nullptr, 0, EPI_STORE, bufT_, tW_, -1, -1, n, countDev, nullptr,
+         nullptr, st);
+    hipLaunchKernelGGL(kGpoolBias, dim3(n), dim3(256), 0, st, bufT_, tW_, X_ * Y_, Cr, Cg, wF_ + b.bngs,
+                       wF_ + b.bngb, wF_ + b.linGT, bufGB_, n, countDev);
+    KC_HIP(hipGetLastError());
+    conv(b.conv2, PRO_BN_GB, bufT_, tW_, 0, b.bn2s, b.bn2b, bufGB_, Cr, EPI_ADD, x, Wd, -1, -1, n, countDev, nullptr,
+         nullptr, st);
+  }
+}
+
+void NNLayered::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev, const int* rowIdx) {
+  if(n <= 0)
+    return;
+  ensure(n);
+  const int C = cfg_.C;
+  conv(stem_, PRO_BITS, nullptr, 0, 0, -1, -1, nullptr, 0, EPI_STEM, bufX_, C, -1, -1, n, countDev, in, rowIdx, st);
+  for(const Block& b : blocks_)
+    runBlock(b, bufX_, n, countDev, st);
+  conv(head_, PRO_BN, bufX_, C, 0, tips_, tipb_, nullptr, 0, EPI_STORE, bufT_, tW_, -1, -1, n, countDev, nullptr,
+       nullptr, st);
+  LHeadW h;
+  h.pBiasG = wF_ + hw_.pBiasG;
+  h.pLinGT = wF_ + hw_.pLinGT;
+  h.pBias2 = wF_ + hw_.pBias2;
+  h.pConv2 = wF_ + hw_.pConv2;
+  h.vBias1 = wF_ + hw_.vBias1;
+  h.vLin2T = wF_ + hw_.vLin2T;
+  h.vB2 = wF_ + hw_.vB2;
+  h.vLin3 = wF_ + hw_.vLin3;
+  h.vB3 = wF_ + hw_.vB3;
+  h.vLinM = wF_ + hw_.vLinM;
+  h.vBM = wF_ + hw_.vBM;
+  h.p1 = cfg_.p1;
+  h.g1 = cfg_.g1;
+  h.v1 = cfg_.v1;
+  h.v2 = cfg_.v2;
+  hipLaunchKernelGGL(kHeadsL, dim3(n), dim3(256), 0, st, bufT_, tW_, X_ * Y_, h, out, rowIdx, n, countDev);
+  KC_HIP(hipGetLastError());
+}
+
+}  // namespace kc

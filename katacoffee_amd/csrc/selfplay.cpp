@@ -129,8 +129,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     if(!c.model_path)
       throw std::invalid_argument("model_path required unless use_fake_net");
     ModelHost m = loadModel(c.model_path);
-    nn_.reset(new NNEngine(m, c.x, c.y, c.win_len));
+    nn_.reset(new NNEngine(m, c.x, c.y, c.win_len, c.nn_precision));
   }
+  nnPath_ = c.nn_precision;
   xLen_ = c.x;
   yLen_ = c.y;
   winLen_ = c.win_len;
@@ -199,7 +200,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     int dev = 0, cus = 0;
     KC_HIP(hipGetDevice(&dev));
     KC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    d.nnCap = std::max(1, cus) * NN_BOARDS_PER_WG;
+    d.nnCap = nn_ ? std::min(G, nn_->batchCap(std::max(1, cus))) : std::max(1, cus) * NN_BOARDS_PER_WG;
   }
   d.nnIdx = devAlloc<int32_t>(owned_, G);
   d.nnCount = devAlloc<int32_t>(owned_, 1);
@@ -330,6 +331,7 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
     out.nn_evals += x.nnEvals;
     out.moves += x.moves;
     out.games_finished += x.gamesFinished;
+    out.errors += x.err != 0 ? 1 : 0;
   }
   unsigned long long cnt = 0, dropped = 0;
   KC_HIP(hipMemcpy(&cnt, hd_.rCount, 8, hipMemcpyDeviceToHost));
@@ -340,6 +342,9 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
   unsigned long long gdrop = 0;
   KC_HIP(hipMemcpy(&gdrop, hd_.gDropped, 8, hipMemcpyDeviceToHost));
   out.games_dropped = gdrop;
+  if(out.errors)
+    throw InternalError("self-play device invariant violated in " + std::to_string(out.errors) +
+                        " game slot(s) (node pool exhausted or no move candidate; raise node_cap)");
 }
 
 int SelfplayEngine::drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, float* gt, int8_t* val,
@@ -421,7 +426,7 @@ void SelfplayEngine::setModel(const char* path) {
   if(!nn_)
     throw std::invalid_argument("engine runs the stand-in network (use_fake_net)");
   ModelHost m = loadModel(path);  // throws on a bad file; the current network stays
-  std::unique_ptr<NNEngine> next(new NNEngine(m, xLen_, yLen_, winLen_));
+  std::unique_ptr<NNEngine> next(new NNEngine(m, xLen_, yLen_, winLen_, nnPath_));
   sync();
   nn_ = std::move(next);
   // cached evaluations belong to the previous network (the reference builds a new

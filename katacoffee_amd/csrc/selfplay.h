@@ -33,6 +33,7 @@ class SelfplayEngine {
   void kernelTime(int which, double& ms, uint64_t& launches);
   uint64_t timedNNEvals();
   const SearchDev& dev() const { return hd_; }
+  bool nnFused() const { return nn_ && nn_->fused(); }
 
  private:
   struct PendingTiming {
@@ -53,6 +54,7 @@ class SelfplayEngine {
   hipStream_t stream_ = nullptr;
   int commitInterval_ = 8;
   int xLen_ = 0, yLen_ = 0, winLen_ = 0;
+  int nnPath_ = 0;  // NNPath of the network (kept across hot reloads)
   uint64_t rounds_ = 0;
   uint64_t rowsDrained_ = 0;
   int timingEvery_ = 0;

@@ -13,7 +13,7 @@ replacement:
   oracle's fp32 forward (oracle/ora_nn.cpp, eigenbackend.cpp semantics): fixup-style
   per-channel affine norms (the merged BatchNorm of the file), KataGPool, gpool bias,
   a 4-direction policy head and a 2-logit value head;
-* ``save_cfnn`` / ``load_cfnn`` write and read CFNN v1, so a trained net goes straight
+* ``save_cfnn`` / ``load_cfnn`` write and read CFNN v1/v2, so a trained net goes straight
   back into ``katago selfplay -models-dir`` (hot reload) or ``coffee_nn_create``;
 * ``losses`` / ``train_step``: policy cross-entropy against the normalised visit
   target, value cross-entropy against the final outcome (draws split evenly between
@@ -31,6 +31,9 @@ import torch.nn.functional as F
 # csrc/model.cpp modelCfgByName (modelconfigs.py:129-180 for the two named nets)
 ARCHS = {
     "b6c96": dict(C=96, Cg=32, p1=32, g1=32, v1=32, v2=64, kinds=[0, 0, 1, 0, 1, 0]),
+    "b18c384nbt": dict(C=384, mid=192, Cg=64, p1=48, g1=48, v1=96, v2=128,
+                       kinds=[2, 2, 3, 2, 2, 3, 2, 2, 3, 2, 2, 3, 2, 2, 3, 2, 2, 2]),
+    "b2c32nbt": dict(C=64, mid=32, Cg=16, p1=16, g1=16, v1=16, v2=32, kinds=[3, 2]),
     "b10c128": dict(C=128, Cg=32, p1=32, g1=32, v1=32, v2=80, kinds=[0, 0, 0, 0, 1, 0, 0, 1, 0, 0]),
     "b2c32": dict(C=32, Cg=16, p1=16, g1=16, v1=16, v2=32, kinds=[0, 1]),
 }
@@ -53,9 +56,20 @@ def _gpool(x, value_head=False):
 
 
 class _Block(nn.Module):
-    def __init__(self, kind, C, Cg):
+    """kind 0 regular / 1 gpool (ResBlock, model_pytorch.py:678-746) at trunk width C;
+    kind 2 / 3 nested bottleneck (NestedBottleneckResBlock :860-958): 1x1 C->mid,
+    two inner blocks at width mid (the first a gpool block for kind 3), 1x1 mid->C."""
+
+    def __init__(self, kind, C, Cg, mid=0):
         super().__init__()
         self.kind = kind
+        if kind >= 2:
+            self.bnPs, self.bnPb = _affine(C)
+            self.convP = nn.Parameter(torch.empty(mid, C))
+            self.inner = nn.ModuleList([_Block(1 if kind == 3 else 0, mid, Cg), _Block(0, mid, Cg)])
+            self.bnQs, self.bnQb = _affine(mid)
+            self.convQ = nn.Parameter(torch.empty(C, mid))
+            return
         Cr = C - Cg if kind == 1 else C
         self.bn1s, self.bn1b = _affine(C)
         self.conv1 = nn.Parameter(torch.empty(Cr, C, 3, 3))
@@ -67,6 +81,13 @@ class _Block(nn.Module):
         self.conv2 = nn.Parameter(torch.empty(C, Cr, 3, 3))
 
     def forward(self, x):
+        if self.kind >= 2:
+            a = F.relu(x * self.bnPs[:, None, None] + self.bnPb[:, None, None])
+            y = torch.einsum("nchw,oc->nohw", a, self.convP)
+            for b in self.inner:
+                y = b(y)
+            aq = F.relu(y * self.bnQs[:, None, None] + self.bnQb[:, None, None])
+            return x + torch.einsum("nchw,oc->nohw", aq, self.convQ)
         a = F.relu(x * self.bn1s[:, None, None] + self.bn1b[:, None, None])
         h = F.conv2d(a, self.conv1, padding=1)
         if self.kind == 1:
@@ -74,6 +95,16 @@ class _Block(nn.Module):
             h = h + (_gpool(g) @ self.linG.t())[:, :, None, None]
         a2 = F.relu(h * self.bn2s[:, None, None] + self.bn2b[:, None, None])
         return x + F.conv2d(a2, self.conv2, padding=1)
+
+    def tensors(self):
+        """CFNN tensor order (csrc/model.h)."""
+        if self.kind >= 2:
+            return ([self.bnPs, self.bnPb, self.convP] + self.inner[0].tensors() + self.inner[1].tensors() +
+                    [self.bnQs, self.bnQb, self.convQ])
+        if self.kind == 0:
+            return [self.bn1s, self.bn1b, self.conv1, self.bn2s, self.bn2b, self.conv2]
+        return [self.bn1s, self.bn1b, self.conv1, self.conv1g, self.bngs, self.bngb, self.linG, self.bn2s, self.bn2b,
+                self.conv2]
 
 
 class CoffeeNet(nn.Module):
@@ -86,7 +117,7 @@ class CoffeeNet(nn.Module):
         C, Cg, p1, g1, v1, v2 = (cfg[k] for k in ("C", "Cg", "p1", "g1", "v1", "v2"))
         self.convInit = nn.Parameter(torch.empty(C, cin, 3, 3))
         self.globInit = nn.Parameter(torch.empty(C, gin))
-        self.blocks = nn.ModuleList(_Block(k, C, Cg) for k in cfg["kinds"])
+        self.blocks = nn.ModuleList(_Block(k, C, Cg, cfg.get("mid", 0)) for k in cfg["kinds"])
         self.tips, self.tipb = _affine(C)
         self.pConv1 = nn.Parameter(torch.empty(p1, C))
         self.pConvG = nn.Parameter(torch.empty(g1, C))
@@ -111,7 +142,7 @@ class CoffeeNet(nn.Module):
         for name, p in self.named_parameters():
             if p.dim() >= 2:
                 fan_in = p[0].numel()
-                scale = 0.5 if name.endswith("conv2") else 1.0
+                scale = 0.5 if name.endswith("conv2") or name.endswith("convQ") else 1.0
                 p.copy_(torch.randn(p.shape, generator=g) * (scale * np.sqrt(2.0 / fan_in)))
 
     def forward(self, binp, glob):
@@ -135,22 +166,22 @@ class CoffeeNet(nn.Module):
         """The file's tensor sequence."""
         out = [self.convInit, self.globInit]
         for b in self.blocks:
-            out += [b.bn1s, b.bn1b]
-            if b.kind == 0:
-                out += [b.conv1, b.bn2s, b.bn2b, b.conv2]
-            else:
-                out += [b.conv1, b.conv1g, b.bngs, b.bngb, b.linG, b.bn2s, b.bn2b, b.conv2]
+            out += b.tensors()
         out += [self.tips, self.tipb, self.pConv1, self.pConvG, self.pBiasG, self.pLinG, self.pBias2, self.pConv2,
                 self.vConv1, self.vBias1, self.vLin2, self.vB2, self.vLin3, self.vB3, self.vLinM, self.vBM]
         return out
 
 
 def save_cfnn(net, path):
-    """Writes CFNN v1 (written to path + '.tmp' then renamed, like the row files)."""
+    """Writes CFNN v1 (v2 when a block is a nested bottleneck), to path + '.tmp' then
+    renamed, like the row files."""
     import os
     c = net.cfg
-    hdr = struct.pack("<4si9i", b"CFNN", 1, c["cin"], c["gin"], c["C"], c["Cg"], c["p1"], c["g1"], c["v1"], c["v2"],
-                      len(c["kinds"]))
+    fields = [c["cin"], c["gin"], c["C"], c["Cg"], c["p1"], c["g1"], c["v1"], c["v2"], len(c["kinds"])]
+    if any(k >= 2 for k in c["kinds"]):
+        hdr = struct.pack("<4si10i", b"CFNN", 2, *fields, c["mid"])
+    else:
+        hdr = struct.pack("<4si9i", b"CFNN", 1, *fields)
     body = [np.asarray(c["kinds"], "<i4").tobytes()]
     body += [t.detach().cpu().to(torch.float32).contiguous().numpy().astype("<f4").tobytes() for t in net.tensors()]
     tmp = path + ".tmp"
@@ -162,17 +193,22 @@ def save_cfnn(net, path):
 
 
 def load_cfnn(path):
-    """Reads CFNN v1 into a CoffeeNet (raises ValueError on a malformed file)."""
+    """Reads CFNN v1/v2 into a CoffeeNet (raises ValueError on a malformed file)."""
     with open(path, "rb") as f:
         data = f.read()
-    if len(data) < 44 or data[:4] != b"CFNN" or struct.unpack_from("<i", data, 4)[0] != 1:
-        raise ValueError("not a CFNN v1 model: %s" % path)
+    ver = struct.unpack_from("<i", data, 4)[0] if len(data) >= 8 else 0
+    if len(data) < 44 or data[:4] != b"CFNN" or ver not in (1, 2):
+        raise ValueError("not a CFNN v1/v2 model: %s" % path)
     cin, gin, C, Cg, p1, g1, v1, v2, nb = struct.unpack_from("<9i", data, 8)
+    mid = struct.unpack_from("<i", data, 44)[0] if ver == 2 else 0
+    hdr = 48 if ver == 2 else 44
     if not 1 <= nb <= 64:
         raise ValueError("bad block count in %s" % path)
-    kinds = list(struct.unpack_from("<%di" % nb, data, 44))
-    net = CoffeeNet(dict(C=C, Cg=Cg, p1=p1, g1=g1, v1=v1, v2=v2, kinds=kinds), cin=cin, gin=gin)
-    off = 44 + 4 * nb
+    kinds = list(struct.unpack_from("<%di" % nb, data, hdr))
+    if any(k < 0 or k > 3 or (k >= 2 and mid <= 0) for k in kinds):
+        raise ValueError("bad block kinds in %s" % path)
+    net = CoffeeNet(dict(C=C, Cg=Cg, p1=p1, g1=g1, v1=v1, v2=v2, kinds=kinds, mid=mid), cin=cin, gin=gin)
+    off = hdr + 4 * nb
     with torch.no_grad():
         for t in net.tensors():
             n = t.numel()

@@ -16,6 +16,7 @@
 //                                  §8c); pinned by SPEC decisions in DESIGN.md.
 // ============================================================================
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -78,31 +79,71 @@ int symCell(const Geom& g, int cell, int sym);
 int symDir(int dir, int sym);
 
 // --------------------------------------------------------------------------
-// Neural net (Coffee b-blocks x c-channels; eigenbackend.cpp:888-1377 semantics)
+// Neural net (Coffee b-blocks x c-channels; eigenbackend.cpp:888-1377 semantics,
+// nested bottleneck blocks model_pytorch.py:860-958).  CFNN v1/v2 file layout:
+// katacoffee_amd/csrc/model.h.
 struct ModelCfg {
   int cin = NUM_SPATIAL, gin = NUM_GLOBAL;
   int C = 96, Cg = 32, p1 = 32, g1 = 32, v1 = 32, v2 = 64;
+  int mid = 0;  // nested-bottleneck inner width (0: no bottleneck blocks)
   int nblocks = 6;
-  int kinds[32] = {0, 0, 1, 0, 1, 0};  // 0 regular, 1 gpool
+  int kinds[64] = {0, 0, 1, 0, 1, 0};  // 0 regular, 1 gpool, 2 bottleneck, 3 bottleneck (gpool inner 0)
+};
+// A convolution's weights [cout][cin][ky][kx] plus GEMM-packed copies (fp32 and
+// fp16-rounded) for the blocked CPU forward.
+struct PackedConv {
+  int ky = 0, kx = 0, cin = 0, cout = 0;
+  std::vector<float> w, p32, p16;
+  void pack();
 };
 struct Model {
   ModelCfg cfg;
-  // All tensors f32, layout documented in katacoffee_amd/csrc/model_format.h
-  std::vector<float> convInit, globInit;
+  PackedConv convInit;
+  std::vector<float> globInit;
   struct Block {
-    int kind;
-    std::vector<float> bn1s, bn1b, conv1, conv1g, bngs, bngb, linG, bn2s, bn2b, conv2;
+    int kind = 0;
+    // regular / gpool (width = the block's trunk width)
+    std::vector<float> bn1s, bn1b, bngs, bngb, linG, bn2s, bn2b;
+    PackedConv conv1;  // gpool blocks: the r and g output channels concatenated [r | g]
+    PackedConv conv2;
+    // nested bottleneck: p = 1x1 C->mid, two inner blocks at width mid, q = 1x1 mid->C
+    std::vector<float> bnPs, bnPb, bnQs, bnQb;
+    PackedConv convP, convQ;
+    std::vector<Block> inner;
   };
   std::vector<Block> blocks;
   std::vector<float> tips, tipb;
-  std::vector<float> pConv1, pConvG, pBiasG, pLinG, pBias2, pConv2;
-  std::vector<float> vConv1, vBias1, vLin2, vB2, vLin3, vB3, vLinM, vBM;
+  PackedConv head;  // 1x1 C -> [pConv1 | pConvG | vConv1]
+  std::vector<float> pBiasG, pLinG, pBias2, pConv2;
+  std::vector<float> vBias1, vLin2, vB2, vLin3, vB3, vLinM, vBM;
 };
 bool modelLoad(const char* path, Model& m);
 // n boards of size X*Y; bin NCHW [n][cin][A], glob [n][gin];
 // outputs: policy logits [n][4][A], value logits [n][2], misc [n][2].
-// mode 0: fp32; mode 1: emulate the GPU kernel's bf16 rounding points.
+// mode 0: fp32; mode 1: emulate the GPU kernels' fp16 rounding points (every
+// convolution weight and convolution input rounded to fp16, residual trunks f32).
 void nnForward(const Model& m, int X, int Y, int n, const float* bin, const float* glob,
                float* policy, float* value, float* misc, int mode, int threads);
+
+// Layer library (the forward above is built from these; tests pin them to the
+// reference's testnn.cpp known-answer vectors and model_pytorch.py blocks).
+// Activations NHWC [n][A][C]; mask [n][A] (nullptr = all cells on board).
+struct NNBatch {
+  int n, X, Y, A;
+  const float* mask;
+  bool fp16;
+  int threads;
+};
+void convApply(const NNBatch& b, const PackedConv& cv, const float* in, float* out, bool accumulate);
+// BatchNormLayer::apply (eigenbackend.cpp:717-734): (x [+ perBoard]) * s + b, act, mask
+void bnAct(const NNBatch& b, int C, const float* s, const float* bias, const float* in, int ldIn, float* out,
+           bool relu, const float* perBoard = nullptr);
+// poolRowsGPool / poolRowsValueHead (eigenbackend.cpp:141-186): out [n][3C]
+void gpoolRows(const NNBatch& b, int C, const float* in, int ldIn, float* out, bool valueHead);
+// residual blocks (ResidualBlock :888-931, GlobalPoolingResidualBlock :935-1015,
+// NestedBottleneckResBlock model_pytorch.py:943-958): x [n][A][width] updated in place
+void blockApply(const NNBatch& b, const Model::Block& blk, float* x);
+// One block from its CFNN tensor sequence (kind 0-3 at trunk width W).
+bool blockFromBlob(const float* blob, size_t count, int kind, int W, int Cg, int mid, Model::Block& b);
 
 }  // namespace ora

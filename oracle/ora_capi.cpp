@@ -1,5 +1,6 @@
 // ORACLE (test infrastructure only) — extern "C" surface for the Python test
 // harness (ctypes) and bench.py's cpu_baseline leg.  Never linked by the product.
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 
@@ -118,6 +119,86 @@ void ora_model_free(void* m) { delete(Model*)m; }
 int ora_nn_forward(void* m, int X, int Y, int n, const float* bin, const float* glob, float* policy, float* value,
                    float* misc, int mode, int threads) {
   nnForward(*(Model*)m, X, Y, n, bin, glob, policy, value, misc, mode, threads);
+  return 0;
+}
+
+// ---- NN layer library (tests/test_oracle_nn.py) ----
+// BatchNormLayer merge (eigenbackend.cpp:700-706): scale / sqrt(var + eps), bias - scale * mean.
+void ora_bn_merge(int C, float eps, const float* mean, const float* var, const float* scale, const float* bias,
+                  float* outS, float* outB) {
+  for(int c = 0; c < C; c++) {
+    outS[c] = scale[c] / sqrtf(var[c] + eps);
+    outB[c] = bias[c] - outS[c] * mean[c];
+  }
+}
+
+static PackedConv mkConv(int ky, int kx, int cin, int cout, const float* w) {
+  PackedConv c;
+  c.ky = ky;
+  c.kx = kx;
+  c.cin = cin;
+  c.cout = cout;
+  c.w.assign(w, w + (size_t)ky * kx * cin * cout);
+  c.pack();
+  return c;
+}
+
+int ora_conv_apply(int ky, int kx, int cin, int cout, const float* w, int n, int X, int Y, const float* in, float* out,
+                   int mode) {
+  NNBatch b{n, X, Y, X * Y, nullptr, mode == 1, 1};
+  convApply(b, mkConv(ky, kx, cin, cout, w), in, out, false);
+  return 0;
+}
+
+int ora_bn_apply(int C, const float* s, const float* bias, int relu, int n, int X, int Y, const float* in,
+                 const float* mask, float* out) {
+  NNBatch b{n, X, Y, X * Y, mask, false, 1};
+  bnAct(b, C, s, bias, in, C, out, relu != 0);
+  return 0;
+}
+
+int ora_gpool_apply(int C, int valueHead, int n, int X, int Y, const float* in, const float* mask, float* out) {
+  NNBatch b{n, X, Y, X * Y, mask, false, 1};
+  gpoolRows(b, C, in, C, out, valueHead != 0);
+  return 0;
+}
+
+// One residual block given its pieces (any kernel sizes): conv k = (ky, kx, cin, cout).
+// kind 0: preBN, conv1, midBN, conv2.  kind 1 (gpool): conv1 = [regular | gpool]
+// outputs concatenated, gS/gB the gpool BN, linG [Cr][3Cg] (Cr = conv2 cin).
+int ora_block_apply_parts(int kind, int n, int X, int Y, const float* mask, float* x, const float* preS,
+                          const float* preB, const int* k1, const float* w1, const float* gS, const float* gB,
+                          const float* linG, const float* midS, const float* midB, const int* k2, const float* w2,
+                          int mode) {
+  NNBatch b{n, X, Y, X * Y, mask, mode == 1, 1};
+  Model::Block blk;
+  blk.kind = kind;
+  blk.conv1 = mkConv(k1[0], k1[1], k1[2], k1[3], w1);
+  blk.conv2 = mkConv(k2[0], k2[1], k2[2], k2[3], w2);
+  const int W = k1[2], H = k1[3], M = k2[2];
+  blk.bn1s.assign(preS, preS + W);
+  blk.bn1b.assign(preB, preB + W);
+  blk.bn2s.assign(midS, midS + M);
+  blk.bn2b.assign(midB, midB + M);
+  if(kind == 1) {
+    const int Cg = H - M;
+    blk.bngs.assign(gS, gS + Cg);
+    blk.bngb.assign(gB, gB + Cg);
+    blk.linG.assign(linG, linG + (size_t)M * 3 * Cg);
+  }
+  blockApply(b, blk, x);
+  return 0;
+}
+
+// One block (kind 0-3; 2/3 = nested bottleneck, model_pytorch.py:860-958) from its
+// CFNN tensor sequence (csrc/model.h) at trunk width W, bottleneck width mid, gpool Cg.
+int ora_block_apply_blob(int kind, int W, int mid, int Cg, const float* blob, long long count, int n, int X, int Y,
+                         float* x, int mode) {
+  Model::Block blk;
+  if(!blockFromBlob(blob, (size_t)count, kind, W, Cg, mid, blk))
+    return 1;
+  NNBatch b{n, X, Y, X * Y, nullptr, mode == 1, 1};
+  blockApply(b, blk, x);
   return 0;
 }
 

@@ -1,0 +1,137 @@
+"""GPU parity of the network paths (NeuralNet::getOutput replacement, nninterface.h:31-171)
+against the CPU oracle (eigenbackend.cpp semantics, oracle/ora_nn.cpp) for every
+BASELINE architecture and board geometry:
+
+  C2  b6c96 @ 5x5        fused kernel and layered kernels
+  C3  b10c128 @ 5x5      layered kernels
+  C4  b10c128 @ 7x7      layered kernels
+  C5  b18c384nbt @ 9x9   layered kernels (nested bottleneck blocks)
+
+Tolerances (on policy/value/misc logits):
+  accurate precision vs the fp32 oracle: 1e-3 absolute (north star) for every net
+  fast precision     vs the oracle's fp16-emulation mode (same operand roundings,
+                     different f32 accumulation order, so an fp16 operand can round
+                     the other way and the flip propagates through the trunk):
+                     2e-3 x max(1, max|logit|);
+                     vs the fp32 oracle: 1e-3 absolute for the C2 benchmark net
+                     (b6c96 random init); deeper nets are printed (fp16 operand noise
+                     grows with depth, ~1e-3 of the largest logit for b18c384nbt)
+"""
+import os
+
+import numpy as np
+import pytest
+
+import katacoffee_amd as kc
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack_u64(planes):
+    """[n][15][A] {0,1} -> [n][ceil(15A/64)] u64, bit i of the flat index in word i>>6."""
+    n = planes.shape[0]
+    flat = planes.reshape(n, -1).astype(np.uint8)
+    words = (flat.shape[1] + 63) // 64
+    bits = np.zeros((n, words * 64), np.uint8)
+    bits[:, :flat.shape[1]] = flat
+    return np.packbits(bits, axis=1, bitorder="little").view("<u8").reshape(n, words)
+
+
+def _boards(n, X, Y, W, seed):
+    """Random legal-looking positions (random stones, up to 5 history moves, random
+    symmetry) encoded by the oracle's V1 encoder."""
+    rng = np.random.default_rng(seed)
+    A = X * Y
+    colors = np.zeros((n, A), np.uint8)
+    hc = np.full((n, 5), -1, np.int8)
+    hd = np.full((n, 5), 4, np.int8)
+    for i in range(n):
+        k = int(rng.integers(0, A // 2))
+        idx = rng.choice(A, size=k, replace=False)
+        colors[i, idx] = rng.integers(1, 3, size=k)
+        h = min(k, int(rng.integers(0, 6)))
+        hc[i, :h] = idx[:h]
+        hd[i, :h] = rng.integers(0, 4, size=h)
+    pla = rng.integers(1, 3, size=n).astype(np.uint8)
+    sym = rng.integers(0, 8, size=n).astype(np.int32)
+    binp, glob = oracle.encode_batch(X, Y, W, colors, hc, hd, pla, sym)
+    return binp, glob.reshape(n, 1).astype(np.float32)
+
+
+def _ref(path, X, Y, binp, glob, mode):
+    n = binp.shape[0]
+    pol, val, misc = oracle.Model(path).forward(X, Y, binp, glob, mode=mode, threads=8)
+    return np.concatenate([pol.reshape(n, -1), val, misc], axis=1)
+
+
+CASES = [
+    # arch, X, Y, W, boards (ragged: not a multiple of the boards per workgroup)
+    ("b6c96", 5, 5, 4, 203),
+    ("b10c128", 5, 5, 4, 131),
+    ("b10c128", 7, 7, 5, 67),
+    ("b2c32nbt", 5, 5, 4, 45),
+    ("b18c384nbt", 9, 9, 5, 13),
+]
+
+
+@pytest.fixture(scope="module")
+def models(tmp_path_factory):
+    d = tmp_path_factory.mktemp("nets")
+    out = {}
+    for arch in sorted({c[0] for c in CASES}):
+        p = str(d / ("%s.cfnn" % arch))
+        kc.write_random_model(arch, 0xC0FFEE, p)
+        out[arch] = p
+    return out
+
+
+@pytest.mark.parametrize("arch,X,Y,W,n", CASES, ids=["%s-%dx%d" % (c[0], c[1], c[2]) for c in CASES])
+@pytest.mark.parametrize("precision", ["fast", "fast-layered", "accurate"])
+def test_network_vs_oracle(models, arch, X, Y, W, n, precision):
+    path = models[arch]
+    binp, glob = _boards(n, X, Y, W, seed=n)
+    net = kc.Network(path, X, Y, W, precision=precision)
+    assert net.fused == (precision == "fast" and arch == "b6c96")
+    out = net.forward(_pack_u64(binp))
+    net.close()
+    ref32 = _ref(path, X, Y, binp, glob, 0)
+    err32 = float(np.abs(out - ref32).max())
+    if precision == "accurate":
+        print(arch, precision, "max |diff| vs fp32", err32, "max |ref|", np.abs(ref32).max())
+        assert err32 <= 1e-3
+    else:
+        ref16 = _ref(path, X, Y, binp, glob, 1)
+        err16 = float(np.abs(out - ref16).max())
+        print(arch, precision, "max |diff| vs fp16-emulation", err16, "vs fp32", err32, "max |ref|",
+              np.abs(ref32).max())
+        assert err16 <= 2e-3 * max(1.0, float(np.abs(ref32).max()))
+        if arch == "b6c96":
+            assert err32 <= 1e-3
+
+
+def test_layered_batch_indirection(models):
+    """count from the device and row indirection (the self-play batch protocol):
+    rows beyond the count are untouched, row r reads input rowIdx[r] and writes
+    output rowIdx[r] -- exercised by self-play below; here the plain batch equals
+    the per-board results of a bigger batch (no cross-board leakage)."""
+    path = models["b10c128"]
+    binp, glob = _boards(40, 7, 7, 5, seed=5)
+    packed = _pack_u64(binp)
+    net = kc.Network(path, 7, 7, 5, precision="fast-layered")
+    full = net.forward(packed)
+    part = net.forward(packed[7:19])
+    net.close()
+    np.testing.assert_array_equal(full[7:19], part)
+
+
+@pytest.mark.parametrize("arch,X,Y,W", [("b10c128", 7, 7, 5), ("b18c384nbt", 9, 9, 5)])
+def test_selfplay_runs_on_layered_network(models, arch, X, Y, W):
+    """Self-play on the C4 / C5 networks: games advance, rows appear, no device errors."""
+    sp = kc.Selfplay(X, Y, W, num_games=64, max_visits=8, seed=3, model_path=models[arch], node_cap=64,
+                     nn_cache_log2=12)
+    sp.step(400)
+    st = sp.stats()
+    sp.close()
+    assert st["errors"] == 0
+    assert st["moves"] > 0 and st["nn_evals"] > 0

@@ -1,10 +1,14 @@
 """GPU check of the training loop's hand-off: a net trained by the
 torch side on engine-format rows, written as CFNN, evaluates on the MI355X network
-kernel to the logits of the torch model.  Tolerances are relative to the largest
-logit: the kernel keeps the residual trunk in fp16, so one-ulp rounding flips of a
-trunk value of magnitude m move logits by about m·2^-11; the 1e-3 absolute north-star
-bound holds for the benchmark net's activation range (tests/test_gpu_parity.py), a
-trained net with larger activations sees ~1e-3 relative."""
+kernels to the logits of the torch model.
+
+  accurate precision (fp16 hi/lo operand pairs): within 1e-3 absolute of the torch
+      fp32 model -- the north-star bound, for a trained net;
+  fast precision (fp16 operands, f32 accumulation and trunk): within 2e-3 of the
+      largest logit of the oracle's fp16-emulation mode (same roundings, different
+      accumulation order, so single operands may round the other way).  Against fp32
+      its error is set by fp16 operand rounding (~1e-3 of the largest logit for this
+      net) and is printed, not asserted."""
 import os
 import tempfile
 
@@ -45,14 +49,20 @@ def test_trained_net_runs_on_device_kernel():
         pol, val, misc = net(batch["binp"], batch["glob"])
     ref = np.concatenate([pol.numpy(), val.numpy(), misc.numpy()], axis=1)
     planes = batch["binp"].numpy().reshape(len(ref), 15, 25)
-    dev = kc.Network(path, 5, 5, 4)
-    out = dev.forward(_pack_u64(planes))
-    dev.close()
+    packed = _pack_u64(planes)
+    acc = kc.Network(path, 5, 5, 4, precision="accurate")
+    out_acc = acc.forward(packed)
+    acc.close()
+    fast = kc.Network(path, 5, 5, 4)
+    assert fast.fused
+    out = fast.forward(packed)
+    fast.close()
     pol16, val16, misc16 = oracle.Model(path).forward(5, 5, planes, batch["glob"].numpy(), mode=1, threads=8)
     ref16 = np.concatenate([pol16.reshape(len(ref), -1), val16, misc16], axis=1)
-    err16 = np.abs(out - ref16).max()
-    err = np.abs(out - ref).max()
-    print("max |diff| vs fp16 oracle", err16, "vs torch fp32", err, "max |ref|", np.abs(ref).max())
-    scale = max(1.0, float(np.abs(ref).max()))
-    assert err16 <= 2e-3 * scale
-    assert err <= 2e-3 * scale
+    err_acc = float(np.abs(out_acc - ref).max())
+    err16 = float(np.abs(out - ref16).max())
+    err = float(np.abs(out - ref).max())
+    print("accurate vs torch fp32", err_acc, "| fast vs fp16 oracle", err16, "fast vs torch fp32", err,
+          "| max |ref|", np.abs(ref).max())
+    assert err_acc <= 1e-3
+    assert err16 <= 2e-3 * max(1.0, float(np.abs(ref).max()))

@@ -29,14 +29,15 @@ def _boards(n, X, Y, W, seed):
     return oracle.encode_batch(X, Y, W, colors, hc, hd, pla, sym)
 
 
-@pytest.mark.parametrize("arch,X,Y,W", [("b2c32", 5, 5, 4), ("b6c96", 5, 5, 4), ("b2c32", 7, 7, 5)])
+@pytest.mark.parametrize("arch,X,Y,W", [("b2c32", 5, 5, 4), ("b6c96", 5, 5, 4), ("b2c32", 7, 7, 5),
+                                        ("b2c32nbt", 5, 5, 4), ("b10c128", 7, 7, 5), ("b18c384nbt", 9, 9, 5)])
 def test_torch_net_matches_oracle_forward(arch, X, Y, W):
     d = tempfile.mkdtemp()
     path = os.path.join(d, "m.cfnn")
     kc.write_random_model(arch, 7, path)
     net = train.load_cfnn(path)
     binp, glob = _boards(24, X, Y, W, seed=3)
-    pol_o, val_o, misc_o = oracle.Model(path).forward(X, Y, binp, glob, mode=0)
+    pol_o, val_o, misc_o = oracle.Model(path).forward(X, Y, binp, glob, mode=0, threads=4)
     with torch.no_grad():
         pol, val, misc = net(torch.from_numpy(binp.reshape(24, 15, Y, X)), torch.from_numpy(glob.reshape(24, 1)))
     np.testing.assert_allclose(pol.numpy(), pol_o.reshape(24, -1), atol=2e-4, rtol=1e-4)
@@ -44,12 +45,14 @@ def test_torch_net_matches_oracle_forward(arch, X, Y, W):
     np.testing.assert_allclose(misc.numpy(), misc_o, atol=2e-4, rtol=1e-4)
 
 
-def test_cfnn_roundtrip_is_byte_exact():
+@pytest.mark.parametrize("arch", ["b6c96", "b2c32nbt", "b18c384nbt"])
+def test_cfnn_roundtrip_is_byte_exact(arch):
     d = tempfile.mkdtemp()
     a, b = os.path.join(d, "a.cfnn"), os.path.join(d, "b.cfnn")
-    kc.write_random_model("b6c96", 11, a)
+    kc.write_random_model(arch, 11, a)
     train.save_cfnn(train.load_cfnn(a), b)
     assert open(a, "rb").read() == open(b, "rb").read()
+    assert open(a, "rb").read()[4] == (2 if "nbt" in arch else 1)
     # a torch-initialised net is readable by the engine's loader (flops query parses it)
     c = os.path.join(d, "c.cfnn")
     train.save_cfnn(train.CoffeeNet("b10c128"), c)
