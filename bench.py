@@ -1,80 +1,64 @@
-"""Self-play benchmark: BASELINE.json config C2 (5x5 connect-4 Coffee, 4096 games per
-GPU, 600 visits, random-init b6c96; the network runs fp16 MFMA with f32 accumulation
--- same rate as bf16 on gfx950, more mantissa) on N GPUs of one node.
+"""Self-play benchmark (BASELINE.json): training rows/s + MCTS playouts/s of the
+MI355X Coffee self-play engine, one process per GPU.
 
-A "step" is `--rounds-per-step` (1000) rounds of the hot path over the whole batch of
-games (one round = select/expand for every game -> one batched network
-evaluation -> backup, plus the periodic move-commit launch).  Games shard across
-ranks (slot_base = rank * games); finished rows are drained each step and, for
-N > 1, gathered to rank 0 over RCCL (the only collective).
+Workloads (BASELINE.json configs; --config, default C2, the config the metric is
+quoted on):
+  C2  5x5 connect-4, 4096 games/GPU, 600 visits, b6c96       (fused network kernel)
+  C3  5x5 connect-4, 16384 games/GPU, 600 visits, b10c128    (layered network kernels)
+  C4  7x7 connect-5, 8192 games/GPU, 800 visits, b10c128     (layered)
+  C5  9x9 connect-5, 4096 games/GPU, 1600 visits, b18c384nbt (layered, nested bottlenecks)
+Networks are random-init (seed 0xC0FFEE); positions start from empty boards.  The
+network computes with fp16 MFMA operands, f32 accumulation and f32 residual trunk
+(--precision fast, the configs' bf16/fp16), or fp16 hi/lo pairs (--precision accurate).
 
-value = training rows/s over the timed steps for the whole job.  In benchmark mode
-(one row per move at full visits) a row is fixed the moment its move is
-committed; rows are emitted to the buffer when the game ends.  We count committed
-moves (= rows) in the window; rows actually drained in the window are reported too.
+A "step" is --rounds-per-step rounds of the hot path over every game of the GPU
+(one round = select/expand -> one batched network evaluation -> backup, plus the
+periodic move-commit launch).  Games shard across ranks (slot_base = rank * games);
+each step's finished rows are drained from the device and, for N > 1, gathered to
+rank 0 over RCCL (the only collective); a writer thread on rank 0 writes them to
+.npz files (the reference's trainingwrite row format) inside the timed region.
 
-Self-play clears the search tree before every move, as the reference does for
-self-play (play.cpp:1941-1946), so every row costs a full 600-visit search.
+value = training rows produced per second in the timed window, whole job: in the
+benchmark play settings (one row per move at full visits) every committed
+move is exactly one row, fixed at commit; its game's rows are written when the game
+ends.  rows_written_npz counts the rows the writer actually wrote in the window.
+Game starts are staggered over the warm-up (a seeded per-slot idle delay), so game
+ends and row bursts are spread over the run rather than arriving in phase.
 
-All games start together and stay roughly in phase (a 5x5 game at 600 visits lasts
-about 11000 rounds), so rates swing by up to 2x from one 1000-round chunk to the next
-(tools/steady_state.py prints the trajectory).  The defaults (20 warm-up steps =
-20k rounds, then 60 timed steps = 60k rounds, about 5 game cycles) average the swings
-out: over 100k+ rounds the long-run rate is within a few percent of this window's.
-Short --steps/--warmup values time a partial cycle and can be off by 30%.
-
-The network batch is capped at one full wave of network workgroups (compute units x
-8 boards = 2048 rows; coffee_selfplay_config.nn_batch_cap): a launch's cost steps with
-its number of workgroup waves, so rows past the cap wait one round (round-robin, so no
-row waits long) instead of paying for a mostly idle second wave.
-
-The NN evaluation cache is on at the reference's own selfplay1.cfg size
-(nnCacheSizePowerOfTwo = 21, nneval.cpp:611-623): a search leaf whose state was
-evaluated earlier, by any game, takes that evaluation instead of the network, as in
-the reference; nn_evals_per_sec counts only real network evaluations.  The CPU
-baseline runs the same cache.
+--gpus N without a torch.distributed launcher starts N ranks itself (one process per
+GPU, RCCL world size N); under torchrun the environment's WORLD_SIZE is used.
 """
 import argparse
 import json
 import os
+import queue
+import shutil
+import socket
+import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_F16_TFLOPS = 2500.0    # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
-PEAK_HBM_GBS = 8000.0
+PEAK_HBM_GBS = 8000.0       # HBM3E
+# SURVEY 8d canonical record sizes for the tree roofline: node stats 32 B, per child
+# a 16 B edge + the child's 32 B stats
+NODE_B, CHILD_B = 32, 48
 
-
-def parse():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--games", type=int, default=4096)
-    ap.add_argument("--visits", type=int, default=600)
-    ap.add_argument("--arch", default="b6c96")
-    ap.add_argument("--rounds-per-step", type=int, default=1000)
-    ap.add_argument("--commit-interval", type=int, default=8)
-    ap.add_argument("--nn-cache-log2", type=int, default=21,
-                    help="NN evaluation cache entries = 2^k (selfplay1.cfg nnCacheSizePowerOfTwo = 21); 0 = off")
-    ap.add_argument("--nn-batch-cap", type=int, default=0,
-                    help="rows per network launch (0 = one full wave of network workgroups)")
-    ap.add_argument("--play", choices=["benchmark", "production"], default="benchmark",
-                    help="benchmark: SURVEY 8d (one row per move at full visits, the metric's mode); "
-                         "production: selfplay1.cfg play settings (configs/selfplay1_coffee5.cfg)")
-    ap.add_argument("--seed", type=int, default=20250217)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP event timing")
-    ap.add_argument("--timing-every", type=int, default=16,
-                    help="time every N-th launch of each kernel group (an event pair costs a few us of stream gap)")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
-                    help="per-launch HBM bytes of the network kernel from a PMC pass (see profiles/)")
-    return ap.parse_args()
-
+CONFIGS = {
+    "C2": dict(X=5, Y=5, W=4, games=4096, visits=600, arch="b6c96", rounds=1000,
+               label="C2: 5x5 connect-4, 4096 games/GPU, 600 visits, b6c96"),
+    "C3": dict(X=5, Y=5, W=4, games=16384, visits=600, arch="b10c128", rounds=200,
+               label="C3: 5x5 connect-4, 16384 games/GPU, 600 visits, b10c128"),
+    "C4": dict(X=7, Y=7, W=5, games=8192, visits=800, arch="b10c128", rounds=200,
+               label="C4: 7x7 connect-5, 8192 games/GPU, 800 visits, b10c128"),
+    "C5": dict(X=9, Y=9, W=5, games=4096, visits=1600, arch="b18c384nbt", rounds=40,
+               label="C5: 9x9 connect-5, 4096 games/GPU, 1600 visits, b18c384nbt"),
+}
 
 # selfplay1.cfg play settings (cpp/configs/training/selfplay1.cfg lines 24-76)
 PRODUCTION = dict(init_games_with_policy=1, policy_init_area_prop=0.04, side_position_prob=0.02,
@@ -85,42 +69,186 @@ PRODUCTION = dict(init_games_with_policy=1, policy_init_area_prop=0.04, side_pos
                   fork_game_min_choices=3, early_fork_game_max_choices=12, fork_game_max_choices=36)
 
 
-def cpu_baseline(model_path, visits, seconds, cache_log2):
-    """The oracle (C++ CPU restatement: same rules/search/rows, fp32 Eigen-semantics
-    network) on this host's cores: a bounded sample of the same workload."""
-    import numpy as np  # noqa: F401
-    from oracle import oracle
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="C2")
+    ap.add_argument("--games", type=int, default=0, help="games per GPU (0 = the config's)")
+    ap.add_argument("--visits", type=int, default=0, help="visits per move (0 = the config's)")
+    ap.add_argument("--rounds-per-step", type=int, default=0, help="0 = the config's")
+    ap.add_argument("--precision", choices=["fast", "accurate", "fast-layered"], default="fast")
+    ap.add_argument("--commit-interval", type=int, default=8)
+    ap.add_argument("--nn-cache-log2", type=int, default=21,
+                    help="NN evaluation cache entries = 2^k (selfplay1.cfg nnCacheSizePowerOfTwo = 21); 0 = off")
+    ap.add_argument("--nn-batch-cap", type=int, default=0,
+                    help="rows per network launch (0 = engine default: one workgroup wave for the fused kernel)")
+    ap.add_argument("--play", choices=["benchmark", "production"], default="benchmark",
+                    help="benchmark: SURVEY 8d (one row per move at full visits, the metric's mode); "
+                         "production: selfplay1.cfg play settings")
+    ap.add_argument("--stagger", type=int, default=-1,
+                    help="per-slot start delay range in rounds (-1 = min(one game, 90%% of the warm-up))")
+    ap.add_argument("--seed", type=int, default=20250217)
+    ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
+    ap.add_argument("--cpu-c1-seconds", type=float, default=30.0, help="timed CPU-baseline window (C1 run)")
+    ap.add_argument("--cpu-warmup-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP event timing")
+    ap.add_argument("--timing-every", type=int, default=16,
+                    help="time every N-th launch of each kernel group (an event pair costs a few us of stream gap)")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                    help="per-launch HBM bytes per kernel from a PMC pass (see profiles/)")
+    return ap.parse_args()
 
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
-    games = 2 * cores
-    model = oracle.Model(model_path)
-    sp = oracle.Selfplay(5, 5, 4, games=games, max_visits=visits, node_cap=max(2048, 3 * visits), seed=1,
-                         nn_mode=1, model=model, nn_threads=cores, nn_cache_log2=cache_log2)
-    sp.rounds(8)  # warm-up: root evaluations
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, script=None, argv=None):
+    """One process per GPU (torch.distributed.run's environment contract: RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT), started as children before anything
+    here touches the GPU; rank 0 prints the JSON line.  Returns the worst exit code."""
+    port = free_port()
+    script = script or os.path.abspath(__file__)
+    argv = sys.argv[1:] if argv is None else argv
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def cpu_info():
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if cores <= 0:
+        cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return cores, model
+
+
+def cpu_run(oracle, model, X, Y, W, games, visits, threads, warm_s, timed_s, cache_log2):
+    sp = oracle.Selfplay(X, Y, W, games=games, max_visits=visits, node_cap=max(2048, 3 * visits), seed=1, nn_mode=1,
+                         model=model, nn_threads=threads, nn_cache_log2=cache_log2)
+    if threads > 1 and games > 1:
+        sp.set_parallel(threads)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        sp.rounds(8)
     i0 = [sp.info(g) for g in range(games)]
     t0 = time.perf_counter()
     rounds = 0
-    while time.perf_counter() - t0 < seconds:
-        sp.rounds(16)
-        rounds += 16
+    while time.perf_counter() - t0 < timed_s:
+        sp.rounds(8)
+        rounds += 8
     dt = time.perf_counter() - t0
     i1 = [sp.info(g) for g in range(games)]
-    moves = sum(b["movesMade"] - a["movesMade"] for a, b in zip(i0, i1))
-    playouts = sum(b["playouts"] - a["playouts"] for a, b in zip(i0, i1))
-    return {
-        "value": moves / dt,
-        "unit": "rows/s",
-        "playouts_per_sec": playouts / dt,
-        "cores": cores,
-        "kind": "port",
-        "sample": "oracle C++ self-play, %d games x %d visits, b6c96 fp32, %d rounds in %.1f s (%d moves, %d playouts)"
-                  % (games, visits, rounds, dt, moves, playouts),
+    d = lambda k: sum(b[k] - a[k] for a, b in zip(i0, i1))
+    return dict(rows_per_sec=d("movesMade") / dt, playouts_per_sec=d("playouts") / dt, nn_evals_per_sec=d("nnEvals") / dt,
+                rounds=rounds, seconds=dt, moves=d("movesMade"), playouts=d("playouts"))
+
+
+def cpu_baseline(args, cfg, model_path):
+    """The oracle (C++ restatement: same rules / search / rows, fp32 forward with
+    eigenbackend.cpp semantics, convolutions as im2col + a register-blocked AVX2
+    SGEMM) on this host: C1 (1 game, 200 visits) and the GPU's workload saturated
+    (4 x cores games, threads over games and inside the forward, NN cache on)."""
+    from oracle import oracle
+    cores, model_name = cpu_info()
+    model = oracle.Model(model_path)
+    c1 = None
+    if cfg["arch"] == "b6c96" and (cfg["X"], cfg["Y"]) == (5, 5):
+        c1 = cpu_run(oracle, model, 5, 5, 4, 1, 200, 1, args.cpu_warmup_seconds, args.cpu_c1_seconds,
+                     args.nn_cache_log2)
+    sat = cpu_run(oracle, model, cfg["X"], cfg["Y"], cfg["W"], 4 * cores, args.visits or cfg["visits"], cores,
+                  args.cpu_warmup_seconds, args.cpu_seconds, args.nn_cache_log2)
+    out = {
+        "value": sat["rows_per_sec"], "unit": "rows/s", "cores": cores, "kind": "port",
+        "playouts_per_sec": sat["playouts_per_sec"], "nn_evals_per_sec": sat["nn_evals_per_sec"],
+        "cpu_model": model_name,
+        "sample": "oracle C++ self-play (fp32 im2col+SGEMM forward), %s workload on %d threads: %d games x %d visits, "
+                  "%.0f s warm-up then %d rounds in %.1f s (%d moves, %d playouts)"
+                  % (cfg["label"].split(":")[0], cores, 4 * cores, args.visits or cfg["visits"],
+                     args.cpu_warmup_seconds, sat["rounds"], sat["seconds"], sat["moves"], sat["playouts"]),
     }
+    if c1:
+        out["C1"] = {"rows_per_sec": c1["rows_per_sec"], "playouts_per_sec": c1["playouts_per_sec"], "threads": 1,
+                     "sample": "1 game x 200 visits, b6c96 fp32, %.0f s warm-up then %.1f s (%d moves, %d playouts)"
+                               % (args.cpu_warmup_seconds, c1["seconds"], c1["moves"], c1["playouts"])}
+    return out
+
+
+class NpzWriter:
+    """Writes row blocks to .npz files on a background thread (trainingwrite.cpp
+    writeToZipFile :566-587 then rename :765-769, via the native coffee_write_npz)."""
+
+    def __init__(self, kc, X, Y, outdir):
+        self.kc, self.X, self.Y, self.dir = kc, X, Y, outdir
+        self.q = queue.Queue()
+        self.rows = 0
+        self.files = 0
+        self.err = None
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            rows = self.q.get()
+            if rows is None:
+                return
+            try:
+                n = len(rows["meta"])
+                if n:
+                    path = os.path.join(self.dir, "rows%06d.npz" % self.files)
+                    self.kc.write_npz(path + ".tmp", rows, self.X, self.Y)
+                    os.replace(path + ".tmp", path)
+                    self.files += 1
+                    self.rows += n
+            except Exception as e:  # surfaced by close()
+                self.err = e
+
+    def put(self, rows):
+        self.q.put(rows)
+
+    def close(self):
+        self.q.put(None)
+        self.t.join()
+        if self.err:
+            raise self.err
+
+
+def load_traffic(path):
+    try:
+        return json.load(open(path))
+    except Exception:
+        return {}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    cfg = CONFIGS[args.config]
+    X, Y, W = cfg["X"], cfg["Y"], cfg["W"]
+    games = args.games or cfg["games"]
+    visits = args.visits or cfg["visits"]
+    rps = args.rounds_per_step or cfg["rounds"]
+    import numpy as np  # noqa: F401
     import torch
 
     import katacoffee_amd as kc
@@ -130,27 +258,42 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    kc.check(kc.lib().coffee_set_device(local))
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
     tmpdir = tempfile.mkdtemp(prefix="kcbench%d_" % rank)
-    model_path = os.path.join(tmpdir, "%s.cfnn" % args.arch)
-    kc.write_random_model(args.arch, 0xC0FFEE, model_path)
-    flops_per_eval = kc.model_flops(model_path, 25)
+    model_path = os.path.join(tmpdir, "%s.cfnn" % cfg["arch"])
+    kc.write_random_model(cfg["arch"], 0xC0FFEE, model_path)
+    flops_per_eval = kc.model_flops(model_path, X * Y)
 
-    sp = kc.Selfplay(5, 5, 4, num_games=args.games, max_visits=args.visits, seed=args.seed,
-                     slot_base=rank * args.games, model_path=model_path, commit_interval=args.commit_interval,
-                     nn_cache_log2=args.nn_cache_log2, nn_batch_cap=args.nn_batch_cap)
+    warm_rounds = args.warmup * rps
+    game_rounds = visits * X * Y // 2
+    stagger = args.stagger if args.stagger >= 0 else min(game_rounds, int(0.9 * warm_rounds))
+    play = PRODUCTION if args.play == "production" else {}
+    # benchmark mode clears the tree before every move: a search holds at
+    # most visits + 1 nodes; production's cheap searches reuse the tree
+    node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
+    sp = kc.Selfplay(X, Y, W, num_games=games, max_visits=visits, seed=args.seed, slot_base=rank * games,
+                     model_path=model_path, commit_interval=args.commit_interval, nn_cache_log2=args.nn_cache_log2,
+                     nn_batch_cap=args.nn_batch_cap, nn_precision=args.precision, start_stagger=stagger,
+                     node_cap=node_cap, **play)
     for _ in range(args.warmup):
-        sp.step(args.rounds_per_step)
+        sp.step(rps)
         sp.sync()  # bounded launch queue (a profiler's per-dispatch state stays small)
-    s0 = sp.stats()
     sp.drain_rows()
+    sp.drain_games()
     if not args.no_timing:
         sp.enable_timing(args.timing_every)
+    s0 = sp.stats()
     base_ms = [sp.kernel_time(i) for i in range(4)]
     base_timed_evals = sp.timed_nn_evals()
+    writer = None
+    if rank == 0 and not args.no_npz:
+        os.makedirs(os.path.join(tmpdir, "tdata"), exist_ok=True)
+        writer = NpzWriter(kc, X, Y, os.path.join(tmpdir, "tdata"))
 
     def barrier():
         if dist is not None:
@@ -158,37 +301,44 @@ def main():
         torch.cuda.synchronize()
 
     rows_gathered = 0
+    per_rank_rows = 0
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sp.step(args.rounds_per_step)
+        sp.step(rps)
         rows = sp.drain_rows()
-        n = len(rows["meta"])
+        sp.drain_games()
+        per_rank_rows += len(rows["meta"])
         if dist is not None:
             # RCCL gather of this step's finished rows to rank 0 (the writer rank)
-            got = kcrows.gather_to_rank0(rows, 5, 5, dist, torch.device("cuda", local))
-            if rank == 0:
-                rows_gathered += len(got["meta"])
-        else:
-            rows_gathered += n
+            rows = kcrows.gather_to_rank0(rows, X, Y, dist, torch.device("cuda", local))
+        if rank == 0:
+            rows_gathered += len(rows["meta"])
+            if writer:
+                writer.put(rows)
     sp.sync()
+    if writer:
+        writer.close()  # every drained row is on disk before the clock stops
     barrier()
     elapsed = time.perf_counter() - t0
     s1 = sp.stats()
-    moves = s1["moves"] - s0["moves"]
-    playouts = s1["playouts"] - s0["playouts"]
-    evals = s1["nn_evals"] - s0["nn_evals"]
+    d = {k: s1[k] - s0[k] for k in ("moves", "playouts", "nn_evals", "tree_levels", "tree_children")}
     kt = [sp.kernel_time(i) for i in range(4)]
     timed_evals = sp.timed_nn_evals() - base_timed_evals
+    rank_rows = [per_rank_rows]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([moves, playouts, evals], dtype=torch.float64, device="cuda")
+        keys = ["moves", "playouts", "nn_evals"]
+        c = torch.tensor([d[k] for k in keys], dtype=torch.float64, device="cuda")
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        moves, playouts, evals = [float(v) for v in c.tolist()]
-    rows_per_sec = moves / elapsed
-    out = None
+        for k, v in zip(keys, c.tolist()):
+            d[k] = v
+        pr = torch.tensor([per_rank_rows], dtype=torch.int64, device="cuda")
+        allr = [torch.zeros_like(pr) for _ in range(world)]
+        dist.all_gather(allr, pr)
+        rank_rows = [int(x.item()) for x in allr]
     if rank == 0:
         names = ["select", "network", "backup", "commit"]
         kernels = {}
@@ -196,27 +346,49 @@ def main():
             ms = kt[i][0] - base_ms[i][0]
             n = kt[i][1] - base_ms[i][1]
             kernels[nm] = {"ms_timed": ms, "launches_timed": n, "avg_us": 1000.0 * ms / n if n else None}
+        rounds_run = args.steps * rps
+        traffic = load_traffic(args.traffic_json)
+        roof_all = {}
         net = kernels["network"]
-        roof = None
         if net["launches_timed"]:
-            # the timed launches' own batch sizes (kCompact sums them on the device)
             per_launch = timed_evals / net["launches_timed"]
-            avg_s = net["avg_us"] * 1e-6
-            achieved = per_launch * flops_per_eval / avg_s / 1e12
-            traffic = None
-            if os.path.exists(args.traffic_json):
-                try:
-                    traffic = json.load(open(args.traffic_json)).get("network_bytes_per_launch")
-                except Exception:
-                    traffic = None
-            roof = {"kernel": "kNNForward (fused b6c96 forward)", "bound": "mfma", "achieved": achieved,
-                    "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_F16_TFLOPS,
-                    "traffic": traffic, "evals_per_launch": per_launch, "flops_per_eval": flops_per_eval,
-                    "avg_launch_us": net["avg_us"], "timed_launches": net["launches_timed"],
-                    "timing": "HIP events on the engine stream around every %d-th launch" % args.timing_every}
+            achieved = per_launch * flops_per_eval / (net["avg_us"] * 1e-6) / 1e12
+            fused = args.precision == "fast" and cfg["arch"] == "b6c96"
+            mfma_factor = 3 if args.precision == "accurate" else 1
+            roof_all["network"] = {
+                "kernel": "kNNForward (fused %s forward)" % cfg["arch"] if fused else
+                          "kConvL/kGpoolBias/kHeadsL (layered %s forward, one launch group)" % cfg["arch"],
+                "bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_F16_TFLOPS,
+                "traffic": traffic.get("network_bytes_per_launch") if fused and args.config == "C2" else None,
+                "evals_per_launch": per_launch, "flops_per_eval": flops_per_eval,
+                "mfma_per_product": mfma_factor, "avg_launch_us": net["avg_us"],
+                "timed_launches": net["launches_timed"]}
+        # tree roofline: per descent, sum over path nodes of 32 B + k * 48 B,
+        # counted on the device (tree_levels, tree_children)
+        tree_bytes = NODE_B * d["tree_levels"] + CHILD_B * d["tree_children"]
+        for nm in ("select", "backup"):
+            k = kernels[nm]
+            if k["launches_timed"] and rounds_run:
+                per_launch_b = tree_bytes / rounds_run
+                ach = per_launch_b / (k["avg_us"] * 1e-6) / 1e9
+                roof_all[nm] = {"kernel": "kSelect" if nm == "select" else "kBackup", "bound": "hbm",
+                                "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                                "traffic": traffic.get("%s_bytes_per_launch" % nm) if args.config == "C2" else None,
+                                "algorithmic_bytes_per_launch": per_launch_b,
+                                "path_nodes_per_playout": d["tree_levels"] / max(1, d["playouts"]),
+                                "children_per_path_node": d["tree_children"] / max(1, d["tree_levels"]),
+                                "avg_launch_us": k["avg_us"]}
+        total_ms = {nm: (kernels[nm]["avg_us"] or 0.0) * (1 if nm != "commit" else 1.0 / args.commit_interval)
+                    for nm in names}
+        dominant = max(("network", "select", "backup"), key=lambda nm: total_ms[nm] if nm in roof_all else -1)
+        roof = dict(roof_all.get(dominant, {}))
+        if roof:
+            roof["timing"] = "HIP events on the engine stream around every %d-th launch" % args.timing_every
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(model_path, args.visits, args.cpu_seconds, args.nn_cache_log2)
+            cpu = cpu_baseline(args, cfg, model_path)
+        rows_per_sec = d["moves"] / elapsed
         out = {
             "metric": "self-play training rows/sec + MCTS playouts/sec, 5x5 Coffee b6c96 @600 visits",
             "value": rows_per_sec,
@@ -228,26 +400,36 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp16",
-            "data": "synthetic: self-play from empty 5x5 boards, random-init b6c96 (seed 0xC0FFEE)",
-            "config": {"workload": "C2: 5x5 connect-4, %d games/GPU, %d visits, b6c96 (fp16 MFMA)" % (args.games, args.visits),
-                       "games_per_gpu": args.games, "visits": args.visits, "rounds_per_step": args.rounds_per_step,
-                       "commit_interval": args.commit_interval, "nn_cache_log2": args.nn_cache_log2,
-                       "nn_batch_cap": args.nn_batch_cap or "one workgroup wave",
-                       "play_settings": args.play,
-                       "parallelism": "game-sharded x%d" % world},
-            "playouts_per_sec": playouts / elapsed,
-            "moves_per_sec": moves / elapsed,
-            "nn_evals_per_sec": evals / elapsed,
+            "dtype": "fp16" if args.precision != "accurate" else "fp16x2 (split hi/lo)",
+            "data": "synthetic: self-play from empty %dx%d boards, random-init %s (seed 0xC0FFEE)" % (X, Y, cfg["arch"]),
+            "config": {"workload": cfg["label"] + (" (%d games, %d visits)" % (games, visits)
+                                                   if (games, visits) != (cfg["games"], cfg["visits"]) else ""),
+                       "config": args.config, "games_per_gpu": games, "visits": visits, "arch": cfg["arch"],
+                       "board": "%dx%d win %d" % (X, Y, W), "precision": args.precision,
+                       "network_path": "fused" if args.precision == "fast" and cfg["arch"] == "b6c96" else "layered",
+                       "rounds_per_step": rps, "commit_interval": args.commit_interval,
+                       "nn_cache_log2": args.nn_cache_log2, "nn_batch_cap": args.nn_batch_cap or "engine default",
+                       "play_settings": args.play, "start_stagger_rounds": stagger, "node_cap": node_cap or "default",
+                       "parallelism": "game-sharded x%d (RCCL row gather)" % world if world > 1 else "1 GPU"},
+            "rccl_world_size": world,
+            "rows_per_rank": rank_rows,
+            "playouts_per_sec": d["playouts"] / elapsed,
+            "moves_per_sec": d["moves"] / elapsed,
+            "nn_evals_per_sec": d["nn_evals"] / elapsed,
             "rows_drained": rows_gathered,
+            "rows_written_npz": writer.rows if writer else None,
+            "rows_written_npz_per_sec": (writer.rows / elapsed) if writer else None,
+            "npz_files": writer.files if writer else None,
             "kernels": kernels,
-            "roofline": roof,
+            "roofline": roof or None,
+            "roofline_all": roof_all,
             "cpu_baseline": cpu,
         }
-        if cpu:
-            out["speedup_vs_cpu"] = rows_per_sec / cpu["value"] if cpu["value"] > 0 else None
-        print(json.dumps(out))
+        if cpu and cpu["value"] > 0:
+            out["speedup_vs_cpu"] = rows_per_sec / cpu["value"]
+        print(json.dumps(out), flush=True)
     sp.close()
+    shutil.rmtree(tmpdir, ignore_errors=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -197,6 +197,9 @@ typedef struct coffee_selfplay_config {
                             (compute units x 8 boards: 2048 on MI355X) for the fused
                             kernel, unbounded for the layered kernels */
   int32_t nn_precision;  /* COFFEE_NN_FAST / _ACCURATE / _FAST_LAYERED (0 = fast) */
+  int32_t start_stagger; /* > 0: each slot idles a seeded number of rounds in [0, start_stagger)
+                            before its first game (benchmarks: spreads game ends over the
+                            run); 0 = all games start in round 0 */
 } coffee_selfplay_config;
 
 typedef struct coffee_selfplay coffee_selfplay;
@@ -212,7 +215,10 @@ typedef struct coffee_selfplay_stats {
   uint64_t rows_dropped;    /* rows lost to a full row buffer (drain more often) */
   uint64_t games_dropped;   /* game records lost to a full record buffer (2 x num_games) */
   uint64_t errors;          /* device invariant violations (node pool exhausted, no move
-                               candidate); nonzero makes step/stats return COFFEE_EINTERNAL */
+                               candidate); nonzero makes stats return COFFEE_EINTERNAL */
+  uint64_t tree_levels;     /* tree levels descended by all playouts (path nodes) */
+  uint64_t tree_children;   /* children scanned at those path nodes (select reads each
+                               path node and its k children; backup re-aggregates them) */
 } coffee_selfplay_stats;
 
 int coffee_selfplay_create(const coffee_selfplay_config* cfg, coffee_selfplay** out);

@@ -85,13 +85,14 @@ class SelfplayConfig(ctypes.Structure):
         ("nn_cache_log2", ctypes.c_int32),
         ("nn_batch_cap", ctypes.c_int32),
         ("nn_precision", ctypes.c_int32),
+        ("start_stagger", ctypes.c_int32),
     ]
 
 
 class SelfplayStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ["rounds", "playouts", "nn_evals", "moves", "games_finished", "rows_written", "rows_pending",
-                 "rows_dropped", "games_dropped", "errors"]]
+                 "rows_dropped", "games_dropped", "errors", "tree_levels", "tree_children"]]
 
 
 # Every symbol include/katacoffee.h declares (checked by tests/test_abi.py).
@@ -355,7 +356,7 @@ class Selfplay:
 
     def __init__(self, X=5, Y=5, W=4, num_games=4096, max_visits=600, seed=1, slot_base=0, model_path=None,
                  node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, nn_batch_cap=0, nn_precision="fast",
-                 **search_over):
+                 start_stagger=0, **search_over):
         _torch_cuda()
         self.X, self.Y, self.W = X, Y, W
         self.A, self.P = X * Y, 4 * X * Y
@@ -372,6 +373,7 @@ class Selfplay:
         cfg.nn_cache_log2 = nn_cache_log2
         cfg.nn_batch_cap = nn_batch_cap
         cfg.nn_precision = PRECISIONS[nn_precision]
+        cfg.start_stagger = start_stagger
         self._model = model_path.encode() if model_path else None
         cfg.model_path = self._model
         cfg.search = default_search_params(max_visits=max_visits, **search_over)

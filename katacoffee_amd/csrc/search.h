@@ -175,6 +175,9 @@ struct GameDev {
   uint64_t rngSeed, rngCtr;
   uint64_t gameHash0, gameHash1;
   uint64_t playouts, nnEvals, moves, gamesFinished;
+  // measurement (SURVEY §8d tree roofline): tree levels descended and children
+  // scanned at those levels, summed over this slot's descents
+  uint64_t treeLevels, treeChildren;
   int32_t phase, rootK;
   uint32_t syms;                  // four root symmetries, 4 bits each
   int32_t cSlot;                  // NN-cache slot of the leaf (hit or bid)
@@ -187,7 +190,7 @@ struct GameDev {
   int32_t gameMode;               // FinishedGameData mode: 0 normal, 2 fork (trainingwrite.h:97-104)
   int32_t sideCount, sideNext;    // queued side positions of this game, the one being searched
   int32_t sideMode;               // 1 while the finished game's side positions are searched
-  int32_t pad3;
+  int32_t startDelay;             // rounds this slot idles before its first game (bench stagger)
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
@@ -200,6 +203,7 @@ struct SearchDev {
   SP spCheap;            // cheapSearchSP(sp): parameters of games with noNoise set
   int G, cap, ttCap, svbCap, P, A, inWords, maxTurns;
   int rowCap, slotBase;
+  int startStagger;      // first games start after a per-slot delay in [0, startStagger) rounds
   uint64_t seed;
   GameDev* games;
   Node* nodes;

@@ -636,6 +636,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
   s.pathLen = 0;
   DBoard b = s.root;
   int ni = s.rootIdx;
+  uint32_t scanned = 0;  // children of the path nodes (tree-roofline accounting)
   while(true) {
     // the first SPEC_EDGES child slots (two cache lines) are read speculatively,
     // together with the node record (slots past numChildren are ignored), saving
@@ -651,6 +652,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
     const bool isRoot = ni == s.rootIdx;
     const float* pol = isRoot ? v.rootNoised() : v.pol(ni);
     int newPos = -1;
+    scanned += n.numChildren;
     const unsigned long long tSel = SPROF_NOW();
     int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits, e0);
     SPROF_ADD(5, SPROF_NOW() - tSel);
@@ -741,6 +743,8 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
     }
     ni = child;
   }
+  s.treeLevels += (uint64_t)s.pathLen;
+  s.treeChildren += scanned;
 }
 
 // ---------------------------------------------------------------------------
@@ -764,10 +768,12 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     return;
   }
   loadGame(v, s);
-  if(s.phase == PH_COMMIT) {
+  if(s.phase == PH_COMMIT || s.startDelay > 0) {
     s.leafKind = LEAF_NONE;
     if(v.lane == 0) {
       d.games[g].leafKind = LEAF_NONE;
+      if(s.startDelay > 0)
+        d.games[g].startDelay = s.startDelay - 1;
       d.nnNeed[g] = 0;
     }
     return;
@@ -2884,6 +2890,13 @@ __global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp, co
   s.svbSel = 0;
   s.gameNum = 0;
   startGame(v, s);
+  // benchmark stagger: idle rounds before the slot's first game, so game ends (and
+  // row bursts) spread over the run instead of arriving in phase; own stream, so
+  // the games themselves are unchanged
+  s.startDelay = d.startStagger > 0
+                     ? (int32_t)(mix64(d.seed ^ 0x5a5a5a5a5a5a5a5aULL ^ (uint64_t)(d.slotBase + g)) %
+                                 (uint64_t)d.startStagger)
+                     : 0;
   waveSync();
   storeGame(v, s);
 }

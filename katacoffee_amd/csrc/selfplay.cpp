@@ -150,6 +150,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.maxTurns = A + 1;
   d.rowCap = rowCap;
   d.slotBase = c.slot_base;
+  if(c.start_stagger < 0)
+    throw std::invalid_argument("start_stagger must be >= 0");
+  d.startStagger = c.start_stagger;
   d.seed = c.seed;
   d.games = devAlloc<GameDev>(owned_, G);
   d.nodes = devAlloc<Node>(owned_, (size_t)G * cap, false);
@@ -332,6 +335,8 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
     out.moves += x.moves;
     out.games_finished += x.gamesFinished;
     out.errors += x.err != 0 ? 1 : 0;
+    out.tree_levels += x.treeLevels;
+    out.tree_children += x.treeChildren;
   }
   unsigned long long cnt = 0, dropped = 0;
   KC_HIP(hipMemcpy(&cnt, hd_.rCount, 8, hipMemcpyDeviceToHost));

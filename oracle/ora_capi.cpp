@@ -254,6 +254,8 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
   return s;
 }
 void ora_sp_free(void* h) { delete(Selfplay*)h; }
+// CPU baseline: threads over games in select / backup (numGameThreads, selfplay.cpp:90)
+void ora_sp_set_parallel(void* h, int threads) { ((Selfplay*)h)->cfg.parallelGames = threads; }
 
 int ora_sp_rounds(void* h, int n) {
   Selfplay* s = (Selfplay*)h;

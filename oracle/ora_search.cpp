@@ -1663,7 +1663,10 @@ void selfplayRound(Selfplay& s) {
   std::vector<int> need(G, 0);
   const bool cacheOn = s.cfg.cacheLog2 > 0;
   const uint32_t cacheMask = cacheOn ? (uint32_t)((1u << s.cfg.cacheLog2) - 1) : 0u;
-  // ---- select ----
+  // ---- select (games are independent: threads over games for the CPU baseline,
+  // cfg.parallelGames; the tests run it serially) ----
+  const int par = s.cfg.parallelGames;
+#pragma omp parallel for schedule(dynamic, 4) num_threads(par > 1 ? par : 1) if(par > 1)
   for(int i = 0; i < G; i++) {
     Game& gm = s.games[i];
     Ctx cx(s, gm);
@@ -1769,29 +1772,34 @@ void selfplayRound(Selfplay& s) {
     std::vector<float> pol;
     float w, l;
   };
-  std::vector<CacheWrite> cacheWrites;  // fresh evaluations, in game order
+  std::vector<CacheWrite> cacheWrites(G);  // fresh evaluations, by game (written in game order)
+  std::vector<char> cacheWritten(G, 0);
+  // moves, game ends and side/fork steps append to the shared row buffer: serialised
+  // (in parallel mode the row order is thread order; the counts are the same)
+#pragma omp parallel for schedule(dynamic, 4) num_threads(par > 1 ? par : 1) if(par > 1)
   for(int i = 0; i < G; i++) {
     Game& gm = s.games[i];
     if(gm.nnDeferred)  // backed up in the round its row is evaluated
       continue;
     Ctx cx(s, gm);
     const float* o = &out[(size_t)i * (g.P + 4)];
-    if(gm.leafKind == LEAF_INIT) {
-      if(cx.initMove(o)) {  // the opening ended the game: nothing searched, no rows
-        cx.finishGame();
-        gm.gamesFinished++;
-        gm.gameNum++;
-        gm.sideNext = 0;
-        cx.afterGame();
+    if(gm.leafKind == LEAF_INIT || gm.leafKind == LEAF_FORK || gm.leafKind == LEAF_SIDE) {
+#pragma omp critical(ora_rows)
+      {
+        if(gm.leafKind == LEAF_INIT) {
+          if(cx.initMove(o)) {  // the opening ended the game: nothing searched, no rows
+            cx.finishGame();
+            gm.gamesFinished++;
+            gm.gameNum++;
+            gm.sideNext = 0;
+            cx.afterGame();
+          }
+        } else if(gm.leafKind == LEAF_FORK) {
+          cx.forkEval(o);
+        } else {
+          cx.sideEval(o);
+        }
       }
-      continue;
-    }
-    if(gm.leafKind == LEAF_FORK) {
-      cx.forkEval(o);
-      continue;
-    }
-    if(gm.leafKind == LEAF_SIDE) {
-      cx.sideEval(o);
       continue;
     }
     if(gm.leafKind == LEAF_ROOTEVAL) {
@@ -1829,8 +1837,10 @@ void selfplayRound(Selfplay& s) {
           cx.addLeafValue(gm.rootIdx, r.nnWin - r.nnLoss, false, true);
         cx.noiseAndTemp(rp, gm.rootNoised.data());
         gm.phase = PH_SEARCH;
-        if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit)
+        if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit) {
+#pragma omp critical(ora_rows)
           cx.commitMove();
+        }
       }
       continue;
     }
@@ -1847,7 +1857,8 @@ void selfplayRound(Selfplay& s) {
         cx.postprocess(gm.leafBoard, gm.leafSym, o, pol, w, l);
         if(cacheOn) {  // staged now: commitMove below may compact the node pool
           const uint32_t slot = cacheSlotOf(n.key0, n.key1, cacheMask);
-          cacheWrites.push_back({slot, n.key0, n.key1, std::vector<float>(pol, pol + g.P), w, l});
+          cacheWrites[i] = {slot, n.key0, n.key1, std::vector<float>(pol, pol + g.P), w, l};
+          cacheWritten[i] = 1;
         }
       }
       n.nnWin = w;
@@ -1868,12 +1879,17 @@ void selfplayRound(Selfplay& s) {
       cx.recompute(pn, 1, pn == gm.rootIdx);
     }
     gm.playouts++;
-    if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit)
+    if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit) {
+#pragma omp critical(ora_rows)
       cx.commitMove();
+    }
   }
   // ---- cache write: after every read of this round; in game order, so a slot ends
   // up holding its highest-numbered evaluator (the device's atomicMax bid) ----
-  for(const CacheWrite& c : cacheWrites) {
+  for(int i = 0; i < G; i++) {
+    if(!cacheWritten[i])
+      continue;
+    const CacheWrite& c = cacheWrites[i];
     s.cacheKey[2 * c.slot] = c.k0;
     s.cacheKey[2 * c.slot + 1] = c.k1;
     memcpy(&s.cachePol[(size_t)c.slot * g.P], c.pol.data(), sizeof(float) * g.P);

@@ -116,6 +116,7 @@ struct SelfplayCfg {
   int nnThreads = 1;
   int cacheLog2 = 0;       // NN evaluation cache of 2^cacheLog2 entries, 0 = off (SPEC a7)
   int nnCap = 1 << 30;     // rows per network batch; the rest wait for the next round (device kCompact)
+  int parallelGames = 0;   // > 1: select / backup threads over games (CPU baseline only)
 };
 
 struct Game {

@@ -42,6 +42,7 @@ def lib():
         L.ora_sp_rows.argtypes = [P, P, P, P, P, P, P]
         L.ora_sp_game_tree.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P]
         L.ora_sp_free.argtypes = [P]
+        L.ora_sp_set_parallel.argtypes = [P, ctypes.c_int]
         L.ora_model_free.argtypes = [P]
         _load_tables(L)
         _lib = L
@@ -170,6 +171,11 @@ class Selfplay:
 
     def rounds(self, n):
         lib().ora_sp_rounds(self.h, n)
+
+    def set_parallel(self, threads):
+        """CPU baseline only: threads over games in select/backup (row order then
+        follows thread timing; counts and per-game results are unchanged)."""
+        lib().ora_sp_set_parallel(self.h, int(threads))
 
     def info(self, slot):
         a = np.zeros(16, np.int64)
