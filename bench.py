@@ -89,6 +89,9 @@ def parse():
                          "production: selfplay1.cfg play settings")
     ap.add_argument("--stagger", type=int, default=-1,
                     help="per-slot start delay range in rounds (-1 = min(one game, 90%% of the warm-up))")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="independent game groups per GPU, each on its own stream (overlaps one group's network "
+                         "with another's search kernels)")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
@@ -232,6 +235,59 @@ class NpzWriter:
             raise self.err
 
 
+class Groups:
+    """K independent engines over disjoint game slots, each on its own HIP stream
+    (the engine's), stepped in interleaved chunks so one group's network launch
+    overlaps another group's select / backup kernels.  Each group keeps its own NN
+    cache, so every group is as deterministic as a single engine."""
+
+    def __init__(self, kc, k, games, slot_base, **kw):
+        assert games % k == 0
+        self.g = [kc.Selfplay(num_games=games // k, slot_base=slot_base + i * (games // k), **kw) for i in range(k)]
+
+    def step(self, rounds, chunk=8):
+        done = 0
+        while done < rounds:
+            n = min(chunk, rounds - done)
+            for e in self.g:
+                e.step(n)
+            done += n
+
+    def sync(self):
+        for e in self.g:
+            e.sync()
+
+    def stats(self):
+        out = {}
+        for e in self.g:
+            for k, v in e.stats().items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def drain_rows(self):
+        parts = [e.drain_rows() for e in self.g]
+        return {k: __import__("numpy").concatenate([p[k] for p in parts]) for k in parts[0]}
+
+    def drain_games(self):
+        for e in self.g:
+            e.drain_games()
+
+    def enable_timing(self, every):
+        for e in self.g:
+            e.enable_timing(every)
+
+    def kernel_time(self, i):
+        t = [e.kernel_time(i) for e in self.g]
+        return sum(a for a, _ in t), sum(b for _, b in t)
+
+    def timed_nn_evals(self):
+        return sum(e.timed_nn_evals() for e in self.g)
+
+    def close(self):
+        for e in self.g:
+            e.close()
+
+
 def load_traffic(path):
     try:
         return json.load(open(path))
@@ -276,10 +332,14 @@ def main():
     # benchmark mode clears the tree before every move: a search holds at
     # most visits + 1 nodes; production's cheap searches reuse the tree
     node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
-    sp = kc.Selfplay(X, Y, W, num_games=games, max_visits=visits, seed=args.seed, slot_base=rank * games,
-                     model_path=model_path, commit_interval=args.commit_interval, nn_cache_log2=args.nn_cache_log2,
-                     nn_batch_cap=args.nn_batch_cap, nn_precision=args.precision, start_stagger=stagger,
-                     node_cap=node_cap, **play)
+    cap = args.nn_batch_cap
+    if cap == 0 and args.groups > 1:
+        # the groups' network launches share one wave of workgroups
+        cap = torch.cuda.get_device_properties(local).multi_processor_count * 8
+    sp = Groups(kc, args.groups, games, rank * games, X=X, Y=Y, W=W, max_visits=visits, seed=args.seed,
+                model_path=model_path, commit_interval=args.commit_interval, nn_cache_log2=args.nn_cache_log2,
+                nn_batch_cap=cap // args.groups, nn_precision=args.precision, start_stagger=stagger,
+                node_cap=node_cap, **play)
     for _ in range(args.warmup):
         sp.step(rps)
         sp.sync()  # bounded launch queue (a profiler's per-dispatch state stays small)
@@ -409,7 +469,7 @@ def main():
                        "network_path": "fused" if args.precision == "fast" and cfg["arch"] == "b6c96" else "layered",
                        "rounds_per_step": rps, "commit_interval": args.commit_interval,
                        "nn_cache_log2": args.nn_cache_log2, "nn_batch_cap": args.nn_batch_cap or "engine default",
-                       "play_settings": args.play, "start_stagger_rounds": stagger, "node_cap": node_cap or "default",
+                       "play_settings": args.play, "start_stagger_rounds": stagger, "groups": args.groups, "node_cap": node_cap or "default",
                        "parallelism": "game-sharded x%d (RCCL row gather)" % world if world > 1 else "1 GPU"},
             "rccl_world_size": world,
             "rows_per_rank": rank_rows,

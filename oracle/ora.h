@@ -10,7 +10,11 @@
 //   rules / zobrist / state hash : bit-exact vs tests/golden/rules_*.npz, produced
 //                                  by the reference's own cpp/game (oracle/_ref)
 //   Rand / t-dist CDF table      : tests/golden/rand_kat.npz, tdist3.npz (reference)
-//   NN layers                    : tests/golden/nnlayers_*.npz (reference testnn.cpp KATs)
+//   NN layers                    : tests/golden/nnlayers_kat.npz (the reference's
+//                                  cpp/tests/testnn.cpp layer KATs) and
+//                                  tests/golden/nnblocks_pytorch.npz (python/model_pytorch.py
+//                                  ResBlock / gpool / nested-bottleneck blocks), see
+//                                  tests/test_oracle_nn.py
 //   encoder / search / rows      : "parity unpinned" by any reference test — the
 //                                  reference does not compile for these (SURVEY §0,
 //                                  §8c); pinned by SPEC decisions in DESIGN.md.
@@ -105,6 +109,7 @@ struct Model {
     // regular / gpool (width = the block's trunk width)
     std::vector<float> bn1s, bn1b, bngs, bngb, linG, bn2s, bn2b;
     PackedConv conv1;  // gpool blocks: the r and g output channels concatenated [r | g]
+    PackedConv conv1g; // optional separate gpool conv (then conv1 holds only r)
     PackedConv conv2;
     // nested bottleneck: p = 1x1 C->mid, two inner blocks at width mid, q = 1x1 mid->C
     std::vector<float> bnPs, bnPb, bnQs, bnQb;

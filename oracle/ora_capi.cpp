@@ -164,18 +164,20 @@ int ora_gpool_apply(int C, int valueHead, int n, int X, int Y, const float* in, 
 }
 
 // One residual block given its pieces (any kernel sizes): conv k = (ky, kx, cin, cout).
-// kind 0: preBN, conv1, midBN, conv2.  kind 1 (gpool): conv1 = [regular | gpool]
-// outputs concatenated, gS/gB the gpool BN, linG [Cr][3Cg] (Cr = conv2 cin).
+// kind 0: preBN, conv1, midBN, conv2.  kind 1 (gpool): conv1 the regular conv, kg/wg
+// the gpool conv, gS/gB the gpool BN, linG [Cr][3Cg] (Cr = conv2 cin).
 int ora_block_apply_parts(int kind, int n, int X, int Y, const float* mask, float* x, const float* preS,
-                          const float* preB, const int* k1, const float* w1, const float* gS, const float* gB,
-                          const float* linG, const float* midS, const float* midB, const int* k2, const float* w2,
-                          int mode) {
+                          const float* preB, const int* k1, const float* w1, const int* kg, const float* wg,
+                          const float* gS, const float* gB, const float* linG, const float* midS, const float* midB,
+                          const int* k2, const float* w2, int mode) {
   NNBatch b{n, X, Y, X * Y, mask, mode == 1, 1};
   Model::Block blk;
   blk.kind = kind;
   blk.conv1 = mkConv(k1[0], k1[1], k1[2], k1[3], w1);
   blk.conv2 = mkConv(k2[0], k2[1], k2[2], k2[3], w2);
-  const int W = k1[2], H = k1[3], M = k2[2];
+  if(kind == 1)
+    blk.conv1g = mkConv(kg[0], kg[1], kg[2], kg[3], wg);
+  const int W = k1[2], H = k1[3] + (kind == 1 ? kg[3] : 0), M = k2[2];
   blk.bn1s.assign(preS, preS + W);
   blk.bn1b.assign(preB, preB + W);
   blk.bn2s.assign(midS, midS + M);

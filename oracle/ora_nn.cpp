@@ -247,19 +247,30 @@ void blockApply(const NNBatch& b, const Model::Block& blk, float* x) {
     convApply(b, blk.convQ, aq.data(), x, true);
     return;
   }
-  const int W = blk.conv1.cin, H = blk.conv1.cout, M = blk.conv2.cin;
-  std::vector<float> a(rows * W), h(rows * H), a2(rows * M);
+  const int W = blk.conv1.cin, M = blk.conv2.cin;
+  const bool split = blk.conv1g.cout > 0;  // separate gpool conv (any kernel sizes: testnn.cpp KAT)
+  const int H = blk.conv1.cout + (split ? blk.conv1g.cout : 0);
+  std::vector<float> a(rows * W), h(rows * blk.conv1.cout), a2(rows * M), hg;
   bnAct(b, W, blk.bn1s.data(), blk.bn1b.data(), x, W, a.data(), true);
   convApply(b, blk.conv1, a.data(), h.data(), false);
   if(blk.kind == 0) {
     bnAct(b, M, blk.bn2s.data(), blk.bn2b.data(), h.data(), H, a2.data(), true);
   } else {
     const int Cr = M, Cg = H - M;
+    const float* graw = h.data() + Cr;
+    int gld = H;
+    if(split) {
+      hg.resize(rows * Cg);
+      convApply(b, blk.conv1g, a.data(), hg.data(), false);
+      graw = hg.data();
+      gld = Cg;
+    }
+    const int rld = split ? Cr : H;
     std::vector<float> g(rows * Cg), pooled((size_t)b.n * 3 * Cg), bias((size_t)b.n * Cr);
-    bnAct(b, Cg, blk.bngs.data(), blk.bngb.data(), h.data() + Cr, H, g.data(), true);
+    bnAct(b, Cg, blk.bngs.data(), blk.bngb.data(), graw, gld, g.data(), true);
     gpoolRows(b, Cg, g.data(), Cg, pooled.data(), false);
     matmulRows(b.n, 3 * Cg, Cr, pooled.data(), blk.linG.data(), nullptr, bias.data());
-    bnAct(b, Cr, blk.bn2s.data(), blk.bn2b.data(), h.data(), H, a2.data(), true, bias.data());
+    bnAct(b, Cr, blk.bn2s.data(), blk.bn2b.data(), h.data(), rld, a2.data(), true, bias.data());
   }
   convApply(b, blk.conv2, a2.data(), x, true);
 }

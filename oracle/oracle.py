@@ -42,6 +42,9 @@ def lib():
         L.ora_sp_rows.argtypes = [P, P, P, P, P, P, P]
         L.ora_sp_game_tree.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P]
         L.ora_sp_free.argtypes = [P]
+        L.ora_bn_merge.argtypes = [ctypes.c_int, ctypes.c_float] + [P] * 6
+        L.ora_block_apply_blob.argtypes = [ctypes.c_int] * 4 + [P, ctypes.c_longlong] + [ctypes.c_int] * 3 + [P,
+                                                                                                            ctypes.c_int]
         L.ora_sp_set_parallel.argtypes = [P, ctypes.c_int]
         L.ora_model_free.argtypes = [P]
         _load_tables(L)
@@ -113,6 +116,72 @@ def fake_net(X, Y, W, binp):
     out = np.zeros((n, 4 * X * Y + 4), np.float32)
     lib().ora_fake_net(X, Y, W, n, ptr(np.ascontiguousarray(binp, np.float32)), ptr(out))
     return out
+
+
+# ---- NN layer library (ora_nn.cpp), NHWC activations ----
+def _f32(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def conv_apply(w, x, mode=0):
+    """ConvLayer: w [cout][cin][ky][kx], x [n][Y][X][cin] -> [n][Y][X][cout]."""
+    cout, cin, ky, kx = w.shape
+    n, Y, X, _ = x.shape
+    out = np.zeros((n, Y, X, cout), np.float32)
+    w, x = _f32(w), _f32(x)
+    lib().ora_conv_apply(ky, kx, cin, cout, ptr(w), n, X, Y, ptr(x), ptr(out), mode)
+    return out
+
+
+def bn_merge(eps, mean, var, scale, bias):
+    C = len(mean)
+    s, b = np.zeros(C, np.float32), np.zeros(C, np.float32)
+    a = [_f32(v) for v in (mean, var, scale, bias)]
+    lib().ora_bn_merge(C, ctypes.c_float(eps), *[ptr(v) for v in a], ptr(s), ptr(b))
+    return s, b
+
+
+def bn_apply(s, b, x, mask=None, relu=False):
+    n, Y, X, C = x.shape
+    out = np.zeros_like(x, dtype=np.float32)
+    s, b, x = _f32(s), _f32(b), _f32(x)
+    m = _f32(mask) if mask is not None else None
+    lib().ora_bn_apply(C, ptr(s), ptr(b), int(relu), n, X, Y, ptr(x), ptr(m) if m is not None else None, ptr(out))
+    return out
+
+
+def block_apply_parts(x, mask, pre, conv1, mid, conv2, gconv=None, gbn=None, linG=None, mode=0):
+    """One residual block from its pieces (ResidualBlock / GlobalPoolingResidualBlock,
+    eigenbackend.cpp:888-1015): pre/mid/gbn = merged (scale, bias); convs [cout][cin][ky][kx];
+    linG [Cr][3Cg].  x NHWC is updated and returned."""
+    n, Y, X, _ = x.shape
+    x = _f32(x).copy()
+    kind = 1 if gconv is not None else 0
+    k1 = np.array([conv1.shape[2], conv1.shape[3], conv1.shape[1], conv1.shape[0]], np.int32)
+    k2 = np.array([conv2.shape[2], conv2.shape[3], conv2.shape[1], conv2.shape[0]], np.int32)
+    arrs = [_f32(pre[0]), _f32(pre[1]), _f32(conv1), _f32(mid[0]), _f32(mid[1]), _f32(conv2)]
+    if kind:
+        kg = np.array([gconv.shape[2], gconv.shape[3], gconv.shape[1], gconv.shape[0]], np.int32)
+        g = [_f32(gconv), _f32(gbn[0]), _f32(gbn[1]), _f32(linG)]
+    else:
+        kg = np.zeros(4, np.int32)
+        g = [np.zeros(1, np.float32)] * 4
+    m = _f32(mask) if mask is not None else None
+    lib().ora_block_apply_parts(kind, n, X, Y, ptr(m) if m is not None else None, ptr(x), ptr(arrs[0]), ptr(arrs[1]),
+                                ptr(k1), ptr(arrs[2]), ptr(kg), ptr(g[0]), ptr(g[1]), ptr(g[2]), ptr(g[3]),
+                                ptr(arrs[3]), ptr(arrs[4]), ptr(k2), ptr(arrs[5]), mode)
+    return x
+
+
+def block_apply_blob(kind, W, mid, Cg, blob, x, mode=0):
+    """One block from its CFNN tensor sequence (kinds 0-3); x NHWC updated and returned."""
+    n, Y, X, _ = x.shape
+    x = _f32(x).copy()
+    blob = _f32(blob)
+    rc = lib().ora_block_apply_blob(kind, W, mid, Cg, ptr(blob), ctypes.c_longlong(blob.size), n, X, Y, ptr(x), mode)
+    if rc != 0:
+        raise ValueError("block tensors do not match kind %d at width %d" % (kind, W))
+    return x
 
 
 class Model:
