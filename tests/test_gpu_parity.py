@@ -273,3 +273,64 @@ def test_game_records_match_rows_and_rules(model_path):
         sp.set_model(model_path + ".missing")
     sp.step(10)
     sp.sync()
+
+
+def _compare_game(gpu, ora, g, og, done):
+    gi, oi = gpu.game_info(g), ora.info(og)
+    for a, b in INFO_KEYS:
+        assert gi[a] == oi[b], (done, g, a, gi[a], oi[b])
+    gn, ge = gpu.game_tree(g)
+    on, oe = ora.game_tree(og)
+    np.testing.assert_array_equal(gn, on, err_msg="round %d game %d nodes" % (done, g))
+    np.testing.assert_array_equal(ge, oe, err_msg="round %d game %d edges" % (done, g))
+    if gi["phase"] == 1:
+        np.testing.assert_array_equal(gpu.root_policy(g), ora.root_noised(og))
+
+
+# The NI = 4 (7x7, P = 196) and NI = 6 (9x9, P = 324) instantiations of the search
+# kernels: game state, trees, root priors and rows bit-exact vs the oracle.
+@pytest.mark.parametrize("X,Y,W,games,visits,rounds,seed,cache_log2,play",
+                         [(7, 7, 5, 6, 32, 1500, 3, 0, {}), (7, 7, 5, 8, 24, 1500, 5, 12, PRODUCTION),
+                          (9, 9, 5, 4, 24, 1500, 7, 0, {}), (9, 9, 5, 6, 20, 1500, 11, 12,
+                                                             dict(PRODUCTION, side_position_prob=0.2, **FORKS))],
+                         ids=["7x7-bench", "7x7-production", "9x9-bench", "9x9-everything"])
+def test_selfplay_geometries_bit_exact_vs_oracle(X, Y, W, games, visits, rounds, seed, cache_log2, play):
+    cap = 128
+    gpu = kc.Selfplay(X, Y, W, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,
+                      nn_cache_log2=cache_log2, **play)
+    ora = oracle.Selfplay(X, Y, W, games=games, max_visits=visits, node_cap=cap, seed=seed,
+                          nn_cache_log2=cache_log2, **play)
+    done = 0
+    for chunk in [1, 7, 200, rounds]:
+        gpu.step(chunk - done)
+        ora.rounds(chunk - done)
+        done = chunk
+        for g in range(games):
+            _compare_game(gpu, ora, g, g, done)
+    st = gpu.stats()
+    assert st["errors"] == 0 and st["rows_dropped"] == 0 and st["moves"] > 0
+    gr = _sorted_rows(gpu.drain_rows())
+    orr = _sorted_rows(ora.rows())
+    assert len(gr["meta"]) == len(orr["meta"])
+    for k in orr:
+        np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
+    gpu.close()
+
+
+def test_selfplay_full_scale_sampled_slots_bit_exact():
+    """C2 scale on the device (4096 games, 600 visits, node_cap 2048, deep trees) with
+    the stand-in network; 12 sampled slots replayed one by one in the oracle from the
+    same per-slot streams (slot_base).  Games are independent once the NN cache is off
+    and the batch cap never binds (cap = games), so each slot must match exactly."""
+    G, visits, rounds, cap = 4096, 600, 2600, 2048
+    gpu = kc.Selfplay(5, 5, 4, num_games=G, max_visits=visits, seed=2025, node_cap=cap, commit_interval=1,
+                      nn_cache_log2=0, nn_batch_cap=G)
+    gpu.step(rounds)
+    st = gpu.stats()
+    assert st["errors"] == 0 and st["moves"] >= G  # every game committed moves
+    slots = [0, 1, 17, 511, 777, 1024, 2047, 2048, 3000, 3333, 4000, 4095]
+    for s in slots:
+        ora = oracle.Selfplay(5, 5, 4, games=1, max_visits=visits, node_cap=cap, seed=2025, slot_base=s)
+        ora.rounds(rounds)
+        _compare_game(gpu, ora, s, 0, rounds)
+    gpu.close()
