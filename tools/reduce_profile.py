@@ -10,8 +10,8 @@ import sys
 
 
 def short(name):
-    for k in ["kNNForward", "kSelect", "kBackup", "kCommit", "kRows", "kCacheWrite", "kCompact", "kFakeNet", "kInit",
-              "fillBuffer", "copyBuffer"]:
+    for k in ["kNNForward", "kConvL", "kGpoolBias", "kHeadsL", "kSelect", "kBackup", "kCommit", "kRows", "kCacheWrite",
+              "kCompact", "kFakeNet", "kInit", "fillBuffer", "copyBuffer"]:
         if k in name:
             return k
     return name[:40]
