@@ -97,16 +97,57 @@ KC_D uint32_t packHalf2(float a, float b) {
 }
 
 // One 32-channel slice of the workgroup's boards into an LDS stage (hi and, for
-// SPLIT, lo planes).  Rows are padded cells; borders stay zero (set once).
+// SPLIT, lo planes).  Rows are padded cells; borders stay zero (set once).  Split in
+// two so the next slice's global loads are in flight while the current slice's
+// MFMAs run: stageLoad issues a thread's (row, 8-channel) tasks into registers,
+// stageStore applies the prologue (BN-ReLU, gpool bias) and writes fp16 to LDS.
+template <class G>
+struct StageRegs {
+  static constexpr int TPT = (G::ROWS * 4 + L_NT - 1) / L_NT;  // tasks per thread
+  float4 x0[TPT], x1[TPT];  // f32 source (PRO_BN*), or raw fp16 bits in x0 (PRO_F16)
+};
+
+template <class G>
+KC_D void stageLoad(const LConvArgs& a, StageRegs<G>& R, int cb, int base, int nb, int tid) {
+#pragma unroll
+  for(int k = 0; k < StageRegs<G>::TPT; k++) {
+    const int t = tid + k * L_NT;
+    R.x0[k] = R.x1[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    if(t >= G::ROWS * 4 || a.pro == PRO_BITS)
+      continue;
+    const int r = t >> 2, q = t & 3;
+    const int brd = r / G::A;
+    if(brd >= nb)
+      continue;
+    const size_t g = (size_t)base * G::A + r;
+    const int c0 = cb * 32 + q * 8;
+    if(a.pro == PRO_F16) {
+      R.x0[k] = *reinterpret_cast<const float4*>(reinterpret_cast<const uint16_t*>(a.src) + g * a.srcLd + c0);
+    } else {
+      const float* sp = reinterpret_cast<const float*>(a.src) + g * a.srcLd + a.srcOff + c0;
+      R.x0[k] = *reinterpret_cast<const float4*>(sp);
+      R.x1[k] = *reinterpret_cast<const float4*>(sp + 4);
+    }
+  }
+}
+
 template <class G, bool SPLIT>
-KC_D void stageSlice(const LConvArgs& a, char* stHi, char* stLo, int cb, int base, int nb, const float* sS,
-                     const float* sB, const float* sG, int tid) {
-  constexpr int TASKS = G::ROWS * 4;  // (row, 8-channel chunk)
-  for(int t = tid; t < TASKS; t += L_NT) {
+KC_D void stageStore(const LConvArgs& a, const StageRegs<G>& R, char* stHi, char* stLo, int cb, int base, int nb,
+                     const float* sS, const float* sB, const float* sG, int tid) {
+#pragma unroll
+  for(int k = 0; k < StageRegs<G>::TPT; k++) {
+    const int t = tid + k * L_NT;
+    if(t >= G::ROWS * 4)
+      continue;
     const int r = t >> 2, q = t & 3;
     const int brd = r / G::A, p = r - brd * G::A;
     const int pr = brd * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1;
     const int c0 = cb * 32 + q * 8;
+    char* dHi = stHi + (pr * L_STRIDE + q * 8) * 2;
+    if(a.pro == PRO_F16) {
+      *reinterpret_cast<float4*>(dHi) = R.x0[k];  // already fp16 (zeros past the batch)
+      continue;
+    }
     float v[8];
     if(brd >= nb) {
 #pragma unroll
@@ -126,16 +167,7 @@ KC_D void stageSlice(const LConvArgs& a, char* stHi, char* stLo, int cb, int bas
         v[j] = bit;
       }
     } else {
-      const size_t g = (size_t)(base + brd) * G::A + p;
-      if(a.pro == PRO_F16) {
-        const uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(a.src) + g * a.srcLd + c0);
-        *reinterpret_cast<uint4*>(stHi + (pr * L_STRIDE + q * 8) * 2) = raw;
-        continue;
-      }
-      const float* s = reinterpret_cast<const float*>(a.src) + g * a.srcLd + a.srcOff + c0;
-      const float4 x0 = *reinterpret_cast<const float4*>(s);
-      const float4 x1 = *reinterpret_cast<const float4*>(s + 4);
-      float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      const float xs[8] = {R.x0[k].x, R.x0[k].y, R.x0[k].z, R.x0[k].w, R.x1[k].x, R.x1[k].y, R.x1[k].z, R.x1[k].w};
 #pragma unroll
       for(int j = 0; j < 8; j++) {
         const int c = c0 + j;
@@ -151,7 +183,7 @@ KC_D void stageSlice(const LConvArgs& a, char* stHi, char* stLo, int cb, int bas
     hi.y = packHalf2(v[2], v[3]);
     hi.z = packHalf2(v[4], v[5]);
     hi.w = packHalf2(v[6], v[7]);
-    *reinterpret_cast<uint4*>(stHi + (pr * L_STRIDE + q * 8) * 2) = hi;
+    *reinterpret_cast<uint4*>(dHi) = hi;
     if constexpr(SPLIT) {
       float lo[8];
 #pragma unroll
@@ -163,6 +195,47 @@ KC_D void stageSlice(const LConvArgs& a, char* stHi, char* stLo, int cb, int bas
       l4.z = packHalf2(lo[4], lo[5]);
       l4.w = packHalf2(lo[6], lo[7]);
       *reinterpret_cast<uint4*>(stLo + (pr * L_STRIDE + q * 8) * 2) = l4;
+    }
+  }
+}
+
+// Epilogue shared by the conv kernels: lane holds channels ch..ch+3 of row
+// (lane & 15) of each of its tiles.
+template <class G, int TN>
+KC_D void convEpilogue(const LConvArgs& a, const lf32x4 (&acc)[G::TM][TN], int base, int nb, int wm, int ctBase,
+                       int lane) {
+  const int rowsValid = nb * G::A;
+#pragma unroll
+  for(int t = 0; t < G::TM; t++) {
+    const int r = (wm * G::TM + t) * 16 + (lane & 15);
+    if(r >= rowsValid)
+      continue;
+    const size_t g = (size_t)base * G::A + r;
+#pragma unroll
+    for(int c = 0; c < TN; c++) {
+      const int ch = (ctBase + c) * 16 + 4 * (lane >> 4);
+      if(ch >= a.cout)
+        continue;
+      const lf32x4 v = acc[t][c];
+      if(a.epi == EPI_BNRELU16) {
+        const float4 s4 = *reinterpret_cast<const float4*>(a.es + ch);
+        const float4 b4 = *reinterpret_cast<const float4*>(a.eb + ch);
+        uint2 h;
+        h.x = packHalf2(fmaxf(v[0] * s4.x + b4.x, 0.0f), fmaxf(v[1] * s4.y + b4.y, 0.0f));
+        h.y = packHalf2(fmaxf(v[2] * s4.z + b4.z, 0.0f), fmaxf(v[3] * s4.w + b4.w, 0.0f));
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.dst) + g * a.dstLd + a.dstOff + ch) = h;
+      } else {
+        float* d = reinterpret_cast<float*>(a.dst) + g * a.dstLd + a.dstOff + ch;
+        float4 o = float4{v[0], v[1], v[2], v[3]};
+        if(a.epi == EPI_ADD) {
+          const float4 old = *reinterpret_cast<const float4*>(d);
+          o = float4{old.x + o.x, old.y + o.y, old.z + o.z, old.w + o.w};
+        } else if(a.epi == EPI_STEM) {
+          const float4 g4 = *reinterpret_cast<const float4*>(a.glob + ch);
+          o = float4{o.x + g4.x * a.winLen, o.y + g4.y * a.winLen, o.z + g4.z * a.winLen, o.w + g4.w * a.winLen};
+        }
+        *reinterpret_cast<float4*>(d) = o;
+      }
     }
   }
 }
@@ -199,7 +272,9 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
       sG[i] = a.gb[(size_t)base * a.gbLd + i];
   __syncthreads();
   const int NCB = a.cin / 32;
-  stageSlice<G, SPLIT>(a, stage, stage + G::STAGE, 0, base, nb, sS, sB, sG, tid);
+  StageRegs<G> sr;
+  stageLoad<G>(a, sr, 0, base, nb, tid);
+  stageStore<G, SPLIT>(a, sr, stage, stage + G::STAGE, 0, base, nb, sS, sB, sG, tid);
 
   // per-lane A row bases (bytes, shifted to the (-r,-r) neighbour), padding rows -> row 0
   int ab[G::TM];
@@ -267,10 +342,13 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
         }
       }
   };
-  // one slice: its taps, then stage the next slice into the other buffer
+  // one slice: the next slice's global loads, its taps, then the next slice's
+  // prologue into the other stage buffer
   auto slice = [&](int cb, int parity) {
     const char* stHi = stage + (cb & 1) * PLANES * G::STAGE;
     const char* stLo = stHi + G::STAGE;
+    if(cb + 1 < NCB)
+      stageLoad<G>(a, sr, cb + 1, base, nb, tid);
     if constexpr(T % 3 == 0) {
 #pragma unroll
       for(int tap = 0; tap < T; tap++)
@@ -280,7 +358,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     }
     if(cb + 1 < NCB) {
       char* nHi = stage + ((cb + 1) & 1) * PLANES * G::STAGE;
-      stageSlice<G, SPLIT>(a, nHi, nHi + G::STAGE, cb + 1, base, nb, sS, sB, sG, tid);
+      stageStore<G, SPLIT>(a, sr, nHi, nHi + G::STAGE, cb + 1, base, nb, sS, sB, sG, tid);
     }
     __syncthreads();
   };
@@ -292,74 +370,199 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   if(cb < NCB)
     slice(cb, 0);
 
-  // ---- epilogue: lane holds channels ch..ch+3 of row (lane & 15) of each tile ----
-  const int rowsValid = nb * G::A;
+  convEpilogue<G, TN>(a, acc, base, nb, wm, ctBase, lane);
+}
+
+// 1x1 convolutions (bottleneck in / out, heads): no halo, so a stage holds 128
+// channels of the workgroup's rows unpadded (four 32-channel K steps per stage,
+// staged synchronously with all of a thread's loads in flight), the stage count is
+// a quarter of the 32-channel slices and a stage's load latency is paid once per
+// four K steps.  Same wave grid, fragments, prologues and epilogues as kConvL.
+constexpr int L1_SW = 4;                  // 32-channel slices per stage
+constexpr int L1_STRIDE = 32 * L1_SW + 8;  // fp16 per staged row (272 B)
+
+template <class G>
+constexpr int l1StageBytes() {
+  return G::ROWS * L1_STRIDE * 2;
+}
+
+template <int X, int Y, int TN, bool SPLIT>
+__global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
+  using G = LGeo<X, Y>;
+  constexpr int NCT = TN * L_WN;
+  constexpr int SB = l1StageBytes<G>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int count = a.countDev ? min(*a.countDev, a.n) : a.n;
+  const int base = blockIdx.x * G::BPW;
+  if(base >= count)
+    return;
+  const int nb = min(G::BPW, count - base);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ctBase = blockIdx.y * NCT + wn * TN;
+  char* stHi = smem;
+  char* stLo = smem + SB;
+  float* sS = reinterpret_cast<float*>(smem + (SPLIT ? 2 : 1) * SB);
+  float* sB = sS + a.cin;
+  for(int i = tid; i < a.cin; i += L_NT) {
+    sS[i] = i < a.cinReal ? a.ps[i] : 0.0f;
+    sB[i] = i < a.cinReal ? a.pb[i] : 0.0f;
+  }
+  int ab[G::TM];
 #pragma unroll
   for(int t = 0; t < G::TM; t++) {
-    const int r = (wm * G::TM + t) * 16 + (lane & 15);
-    if(r >= rowsValid)
-      continue;
-    const size_t g = (size_t)base * G::A + r;
+    int r = (wm * G::TM + t) * 16 + (lane & 15);
+    if(r >= G::ROWS)
+      r = 0;
+    ab[t] = r * L1_STRIDE * 2 + 16 * (lane >> 4);
+  }
+  lf32x4 acc[G::TM][TN];
+#pragma unroll
+  for(int t = 0; t < G::TM; t++)
+#pragma unroll
+    for(int c = 0; c < TN; c++)
+      acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const lh16x8* wl = a.w + (size_t)ctBase * 64 + lane;
+  const lh16x8* wlo = SPLIT ? a.wlo + (size_t)ctBase * 64 + lane : nullptr;
+  const size_t stepStride = (size_t)a.coutTiles * 64;
+  const int NCB = a.cin / 32;
+  lh16x8 bh[2][TN], bl[2][SPLIT ? TN : 1];
+  auto loadB = [&](int s, int slot) {
 #pragma unroll
     for(int c = 0; c < TN; c++) {
-      const int ch = (ctBase + c) * 16 + 4 * (lane >> 4);
-      if(ch >= a.cout)
-        continue;
-      const lf32x4 v = acc[t][c];
-      if(a.epi == EPI_BNRELU16) {
-        const float4 s4 = *reinterpret_cast<const float4*>(a.es + ch);
-        const float4 b4 = *reinterpret_cast<const float4*>(a.eb + ch);
-        uint2 h;
-        h.x = packHalf2(fmaxf(v[0] * s4.x + b4.x, 0.0f), fmaxf(v[1] * s4.y + b4.y, 0.0f));
-        h.y = packHalf2(fmaxf(v[2] * s4.z + b4.z, 0.0f), fmaxf(v[3] * s4.w + b4.w, 0.0f));
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.dst) + g * a.dstLd + a.dstOff + ch) = h;
-      } else {
-        float* d = reinterpret_cast<float*>(a.dst) + g * a.dstLd + a.dstOff + ch;
-        float4 o = float4{v[0], v[1], v[2], v[3]};
-        if(a.epi == EPI_ADD) {
-          const float4 old = *reinterpret_cast<const float4*>(d);
-          o = float4{old.x + o.x, old.y + o.y, old.z + o.z, old.w + o.w};
-        } else if(a.epi == EPI_STEM) {
-          const float4 g4 = *reinterpret_cast<const float4*>(a.glob + ch);
-          o = float4{o.x + g4.x * a.winLen, o.y + g4.y * a.winLen, o.z + g4.z * a.winLen, o.w + g4.w * a.winLen};
-        }
-        *reinterpret_cast<float4*>(d) = o;
+      bh[slot][c] = wl[(size_t)s * stepStride + c * 64];
+      if constexpr(SPLIT)
+        bl[slot][c] = wlo[(size_t)s * stepStride + c * 64];
+    }
+  };
+  loadB(0, 0);
+  constexpr int TASKS = G::ROWS * 4 * L1_SW;  // (row, 8-channel chunk) of a stage
+  for(int st = 0; st * L1_SW < NCB; st++) {
+    __syncthreads();  // previous stage consumed
+    // stage: channels [128 st, 128 st + 128) of every row, prologue BN-ReLU -> fp16;
+    // every load of the stage is issued before the first conversion
+    constexpr int TPT = (TASKS + L_NT - 1) / L_NT;
+    float4 x0[TPT], x1[TPT];
+#pragma unroll
+    for(int k = 0; k < TPT; k++) {
+      const int t = tid + k * L_NT;
+      const int r = t / (4 * L1_SW), q = t - r * (4 * L1_SW);
+      const int c0 = st * 32 * L1_SW + q * 8;
+      x0[k] = x1[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+      if(t < TASKS && r / G::A < nb && c0 < a.cin) {
+        const float* sp = reinterpret_cast<const float*>(a.src) + ((size_t)base * G::A + r) * a.srcLd + a.srcOff + c0;
+        x0[k] = *reinterpret_cast<const float4*>(sp);
+        x1[k] = *reinterpret_cast<const float4*>(sp + 4);
       }
     }
+#pragma unroll
+    for(int k = 0; k < TPT; k++) {
+      const int t = tid + k * L_NT;
+      if(t >= TASKS)
+        continue;
+      const int r = t / (4 * L1_SW), q = t - r * (4 * L1_SW);
+      const int brd = r / G::A;
+      const int c0 = st * 32 * L1_SW + q * 8;
+      float v[8];
+      const float xs[8] = {x0[k].x, x0[k].y, x0[k].z, x0[k].w, x1[k].x, x1[k].y, x1[k].z, x1[k].w};
+#pragma unroll
+      for(int j = 0; j < 8; j++)
+        v[j] = (brd < nb && c0 + j < a.cinReal) ? fmaxf(xs[j] * sS[c0 + j] + sB[c0 + j], 0.0f) : 0.0f;
+      uint4 hi;
+      hi.x = packHalf2(v[0], v[1]);
+      hi.y = packHalf2(v[2], v[3]);
+      hi.z = packHalf2(v[4], v[5]);
+      hi.w = packHalf2(v[6], v[7]);
+      *reinterpret_cast<uint4*>(stHi + (r * L1_STRIDE + q * 8) * 2) = hi;
+      if constexpr(SPLIT) {
+        float lo[8];
+#pragma unroll
+        for(int j = 0; j < 8; j++)
+          lo[j] = v[j] - (float)(_Float16)v[j];
+        uint4 l4;
+        l4.x = packHalf2(lo[0], lo[1]);
+        l4.y = packHalf2(lo[2], lo[3]);
+        l4.z = packHalf2(lo[4], lo[5]);
+        l4.w = packHalf2(lo[6], lo[7]);
+        *reinterpret_cast<uint4*>(stLo + (r * L1_STRIDE + q * 8) * 2) = l4;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for(int j = 0; j < L1_SW; j++) {
+      const int s = st * L1_SW + j;
+      if(s >= NCB)
+        break;
+      if(s + 1 < NCB)
+        loadB(s + 1, (j + 1) & 1);
+      lh16x8 ah[G::TM], al[SPLIT ? G::TM : 1];
+#pragma unroll
+      for(int t = 0; t < G::TM; t++) {
+        ah[t] = *reinterpret_cast<const lh16x8*>(stHi + ab[t] + 64 * j);
+        if constexpr(SPLIT)
+          al[t] = *reinterpret_cast<const lh16x8*>(stLo + ab[t] + 64 * j);
+      }
+#pragma unroll
+      for(int t = 0; t < G::TM; t++)
+#pragma unroll
+        for(int c = 0; c < TN; c++) {
+          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j & 1][c], ah[t], acc[t][c], 0, 0, 0);
+          if constexpr(SPLIT) {
+            acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j & 1][c], ah[t], acc[t][c], 0, 0, 0);
+            acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j & 1][c], al[t], acc[t][c], 0, 0, 0);
+          }
+        }
+    }
   }
+  convEpilogue<G, TN>(a, acc, base, nb, wm, ctBase, lane);
 }
 
 // Gpool branch of a gpool block: g = relu(T[:, Cr:Cr+Cg] * s + b), KataGPool
-// (mean, mean*(sqrt(A)-14)/10, max), bias[Cr] = linG x pooled.  One workgroup per board.
+// (mean, mean*(sqrt(A)-14)/10, max), bias[Cr] = linG x pooled.  One workgroup per
+// board; the pooling splits the cells over 256/Cg thread groups (consecutive lanes
+// read consecutive channels of a row).
 __global__ void __launch_bounds__(256) kGpoolBias(const float* __restrict__ T, int ld, int A, int Cr, int Cg,
                                                   const float* __restrict__ gs, const float* __restrict__ gbias,
                                                   const float* __restrict__ linGT /*[3Cg][Cr]*/, float* __restrict__ out,
                                                   int n, const int* __restrict__ countDev) {
-  __shared__ float pooled[3 * 128];
+  __shared__ float pooled[3 * 128], ps[256], pm[256];
   const int count = countDev ? min(*countDev, n) : n;
   const int b = blockIdx.x;
   if(b >= count)
     return;
   const float sqOff = sqrtf((float)A) - 14.0f;
   const float* Tb = T + (size_t)b * A * ld + Cr;
-  for(int c = threadIdx.x; c < Cg; c += blockDim.x) {
-    float s = 0.0f, m = 0.0f;
-    for(int p = 0; p < A; p++) {
-      const float v = fmaxf(Tb[(size_t)p * ld + c] * gs[c] + gbias[c], 0.0f);
-      s += v;
-      m = fmaxf(m, v);
+  const int parts = 256 / Cg, tid = threadIdx.x;
+  const int c = tid % Cg, part = tid / Cg;
+  float sum = 0.0f, mx = 0.0f;
+  if(part < parts) {
+    const float sc = gs[c], bi = gbias[c];
+    for(int p = part; p < A; p += parts) {
+      const float v = fmaxf(Tb[(size_t)p * ld + c] * sc + bi, 0.0f);
+      sum += v;
+      mx = fmaxf(mx, v);
     }
-    const float mean = s / (float)A;
-    pooled[c] = mean;
-    pooled[Cg + c] = mean * (sqOff / 10.0f);
-    pooled[2 * Cg + c] = m;
+  }
+  ps[tid] = sum;
+  pm[tid] = mx;
+  __syncthreads();
+  if(tid < Cg) {
+    float s2 = 0.0f, m2 = 0.0f;
+    for(int k = 0; k < parts; k++) {
+      s2 += ps[k * Cg + tid];
+      m2 = fmaxf(m2, pm[k * Cg + tid]);
+    }
+    const float mean = s2 / (float)A;
+    pooled[tid] = mean;
+    pooled[Cg + tid] = mean * (sqOff / 10.0f);
+    pooled[2 * Cg + tid] = m2;
   }
   __syncthreads();
-  for(int o = threadIdx.x; o < Cr; o += blockDim.x) {
-    float s = 0.0f;
+  for(int o = tid; o < Cr; o += blockDim.x) {
+    float s3 = 0.0f;
     for(int k = 0; k < 3 * Cg; k++)
-      s += linGT[(size_t)k * Cr + o] * pooled[k];
-    out[(size_t)b * Cr + o] = s;
+      s3 += linGT[(size_t)k * Cr + o] * pooled[k];
+    out[(size_t)b * Cr + o] = s3;
   }
 }
 
@@ -374,7 +577,7 @@ struct LHeadW {
 __global__ void __launch_bounds__(256) kHeadsL(const float* __restrict__ T, int ld, int A, LHeadW h,
                                                float* __restrict__ out, const int* __restrict__ rowIdx, int n,
                                                const int* __restrict__ countDev) {
-  __shared__ float pp[3 * 64], vp[3 * 128], pb[64], vh[256];
+  __shared__ float pp[3 * 64], vp[3 * 128], pb[64], vh[256], ps[256], pm[256];
   const int count = countDev ? min(*countDev, n) : n;
   const int b = blockIdx.x;
   if(b >= count)
@@ -382,22 +585,35 @@ __global__ void __launch_bounds__(256) kHeadsL(const float* __restrict__ T, int 
   const float sqOff = sqrtf((float)A) - 14.0f;
   const float* Tb = T + (size_t)b * A * ld;
   const int tid = threadIdx.x;
-  for(int c = tid; c < h.g1 + h.v1; c += blockDim.x) {
-    const bool isG = c < h.g1;
-    const int cc = isG ? c : c - h.g1;
+  // pooled g (policy) and v (value) channels: 256 / (g1 + v1) thread groups split the cells
+  const int NCH = h.g1 + h.v1, parts = 256 / NCH;
+  const int c = tid % NCH, part = tid / NCH;
+  const bool isG = c < h.g1;
+  const int cc = isG ? c : c - h.g1;
+  float sum = 0.0f, mx = 0.0f;
+  if(part < parts) {
     const int col = isG ? h.p1 + cc : h.p1 + h.g1 + cc;
     const float bias = isG ? h.pBiasG[cc] : h.vBias1[cc];
-    float s = 0.0f, m = 0.0f;
-    for(int p = 0; p < A; p++) {
+    for(int p = part; p < A; p += parts) {
       const float v = fmaxf(Tb[(size_t)p * ld + col] + bias, 0.0f);
-      s += v;
-      m = fmaxf(m, v);
+      sum += v;
+      mx = fmaxf(mx, v);
     }
-    const float mean = s / (float)A;
+  }
+  ps[tid] = sum;
+  pm[tid] = mx;
+  __syncthreads();
+  if(tid < NCH) {
+    float s2 = 0.0f, m2 = 0.0f;
+    for(int k = 0; k < parts; k++) {
+      s2 += ps[k * NCH + tid];
+      m2 = fmaxf(m2, pm[k * NCH + tid]);
+    }
+    const float mean = s2 / (float)A;
     if(isG) {
       pp[cc] = mean;
       pp[h.g1 + cc] = mean * (sqOff / 10.0f);
-      pp[2 * h.g1 + cc] = m;
+      pp[2 * h.g1 + cc] = m2;
     } else {
       vp[cc] = mean;
       vp[h.v1 + cc] = mean * (sqOff / 10.0f);
@@ -453,8 +669,19 @@ uint16_t lf2h(float f) {
 template <int X, int Y, int KT, int TN, bool SPLIT>
 void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
   using G = LGeo<X, Y>;
-  const size_t lds = 2 * (SPLIT ? 2 : 1) * G::STAGE + (2 * a.cin + G::BPW * (a.gbLd > 0 ? a.gbLd : 0)) * 4;
-  auto fn = kConvL<X, Y, KT, TN, SPLIT>;
+  size_t lds;
+  const void* fnp;
+  if constexpr(KT == 1) {
+    if(a.pro != PRO_BN)
+      throw std::invalid_argument("1x1 convolutions take a BN-ReLU prologue");
+    lds = (SPLIT ? 2 : 1) * l1StageBytes<G>() + 2 * (size_t)a.cin * 4;
+    fnp = (const void*)kConv1L<X, Y, TN, SPLIT>;
+  } else {
+    lds = 2 * (SPLIT ? 2 : 1) * G::STAGE + (2 * a.cin + G::BPW * (a.gbLd > 0 ? a.gbLd : 0)) * 4;
+    fnp = (const void*)kConvL<X, Y, KT, TN, SPLIT>;
+  }
+  if(lds > 160 * 1024)
+    throw std::invalid_argument("layered conv: LDS budget exceeded");
   static std::mutex mu;
   static std::set<int> done;  // devices whose attribute is set (per device)
   int dev = 0;
@@ -462,12 +689,15 @@ void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
   {
     std::lock_guard<std::mutex> lk(mu);
     if(!done.count(dev)) {
-      KC_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      KC_HIP(hipFuncSetAttribute(fnp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       done.insert(dev);
     }
   }
   const int gy = (a.coutTiles + TN * L_WN - 1) / (TN * L_WN);
-  hipLaunchKernelGGL(fn, dim3(grid, gy), dim3(L_NT), lds, st, a);
+  if constexpr(KT == 1)
+    hipLaunchKernelGGL((kConv1L<X, Y, TN, SPLIT>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+  else
+    hipLaunchKernelGGL((kConvL<X, Y, KT, TN, SPLIT>), dim3(grid, gy), dim3(L_NT), lds, st, a);
   KC_HIP(hipGetLastError());
 }
 

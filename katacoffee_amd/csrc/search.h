@@ -139,7 +139,8 @@ struct TurnRec {
   float targetWeight;          // limits.targetWeight, surprise-weighted at the game's end
   int8_t cell, dir;
   uint8_t rows;                // resolved integer weight: copies of this turn's row
-  int8_t pad[5];
+  uint8_t gen;                 // network generation (hot reloads so far, mod 256) at the move's commit
+  int8_t pad[4];
 };
 static_assert(sizeof(TurnRec) == 56, "TurnRec layout");
 
@@ -166,7 +167,9 @@ struct FinRec {
   unsigned long long rowBase;
   int32_t numMoves, winner, gameNum, pending;  // pending 1: rows reserved at rowBase
   int32_t numRows, startTurn;                  // startTurn: unsearched moves before the searched ones
-  int32_t gameMode, pad;
+  int32_t gameMode;
+  int32_t genStart, genEnd;  // network generations at the game's start / end (rows' [49], [50])
+  int32_t pad;
 };
 
 struct GameDev {
@@ -191,6 +194,7 @@ struct GameDev {
   int32_t sideCount, sideNext;    // queued side positions of this game, the one being searched
   int32_t sideMode;               // 1 while the finished game's side positions are searched
   int32_t startDelay;             // rounds this slot idles before its first game (bench stagger)
+  int32_t startGen;               // network generation when the game started
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
@@ -204,6 +208,7 @@ struct SearchDev {
   int G, cap, ttCap, svbCap, P, A, inWords, maxTurns;
   int rowCap, slotBase;
   int startStagger;      // first games start after a per-slot delay in [0, startStagger) rounds
+  int32_t* modelGen;     // network generation: hot reloads so far (coffee_selfplay_set_model)
   uint64_t seed;
   GameDev* games;
   Node* nodes;

@@ -1149,6 +1149,7 @@ KC_D bool initMove(const GV& v, GameDev& s, const float* o, float* scratch /* LD
   if(v.lane == 0) {
     TurnRec rec;
     memset(&rec, 0, sizeof(rec));
+    rec.gen = (uint8_t)*v.d.modelGen;
     rec.cell = (int8_t)(chosen % A);
     rec.dir = (int8_t)(chosen / A);
     v.turns()[s.numTurns] = rec;
@@ -1917,6 +1918,7 @@ KC_D bool setMoveLimits(const GV& v, GameDev& s, DRng& rng, float lastWL) {
 KC_D void startGame(const GV& v, GameDev& s) {
   s.rngSeed = mix64(v.d.seed ^ mix64(((uint64_t)(v.d.slotBase + v.g) << 32) | (uint32_t)s.gameNum));
   s.rngCtr = 0;
+  s.startGen = *v.d.modelGen;
   boardInit(v.T, s.root);
   clearTables(v, s);
   s.numTurns = 0;
@@ -1956,6 +1958,7 @@ KC_D void startGame(const GV& v, GameDev& s) {
 KC_D void startForkGame(const GV& v, GameDev& s, const DBoard& b, int prefix, int move) {
   s.rngSeed = mix64(v.d.seed ^ mix64(((uint64_t)(v.d.slotBase + v.g) << 32) | (uint32_t)s.gameNum));
   s.rngCtr = 0;
+  s.startGen = *v.d.modelGen;
   s.root = b;
   clearTables(v, s);
   TurnRec* tr = v.turns();
@@ -1964,6 +1967,7 @@ KC_D void startForkGame(const GV& v, GameDev& s, const DBoard& b, int prefix, in
     const int8_t dir = t < prefix ? tr[t].dir : (int8_t)(move / v.T.A);
     TurnRec rec;
     memset(&rec, 0, sizeof(rec));
+    rec.gen = (uint8_t)*v.d.modelGen;
     rec.cell = cell;
     rec.dir = dir;
     tr[t] = rec;
@@ -2249,6 +2253,8 @@ KC_D void emitSideRow(const GV& v, const GameDev& s, const TurnRec& rec, DRng& r
     gval = (float)b.turn;
   else if(li == 53)
     gval = (float)s.startTurn;
+  else if(li == 49)
+    gval = *d.modelGen != s.startGen ? 1.0f : 0.0f;  // [50]: 0 (searched with the current network)
   else if(li == 55)
     gval = (float)s.gameMode;
   else if(li == 57)
@@ -2415,6 +2421,8 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scra
     f->numRows = numRows;
     f->startTurn = s.startTurn;
     f->gameMode = s.gameMode;
+    f->genStart = s.startGen;
+    f->genEnd = *d.modelGen;
     f->winner = s.root.winner;
     f->gameNum = s.gameNum;
     f->pending = fits && numRows > 0 ? 1 : 0;
@@ -2565,6 +2573,12 @@ __global__ void __launch_bounds__(64 * ROWS_WAVES) kRows(const SearchDev* __rest
       gval = (float)t;
     } else if(li == 53) {
       gval = (float)f.startTurn;
+    } else if(li == 49) {
+      // earlier-network metadata (trainingwrite.cpp:459-461, :844-850): the game saw a
+      // hot reload; reloads after this turn's commit
+      gval = f.genEnd != f.genStart ? 1.0f : 0.0f;
+    } else if(li == 50) {
+      gval = (float)(uint8_t)((uint32_t)f.genEnd - (uint32_t)tr[t].gen);
     } else if(li == 55) {
       gval = (float)f.gameMode;
     } else if(li == 57) {
@@ -2659,6 +2673,7 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     rec.rootNNLoss = r.nnLoss;
     rec.targetWeight = s.moveWeight;
     rec.rows = 0;
+    rec.gen = (uint8_t)*v.d.modelGen;
   }
   const int t = s.numTurns;
   int16_t* pt = side ? d.sidePol + (size_t)g * P : v.turnPol(t);

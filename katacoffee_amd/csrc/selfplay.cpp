@@ -206,6 +206,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     d.nnCap = nn_ ? std::min(G, nn_->batchCap(std::max(1, cus))) : std::max(1, cus) * NN_BOARDS_PER_WG;
   }
   d.nnIdx = devAlloc<int32_t>(owned_, G);
+  d.modelGen = devAlloc<int32_t>(owned_, 1);
   d.nnCount = devAlloc<int32_t>(owned_, 1);
   if(c.nn_cache_log2 < 0 || c.nn_cache_log2 > 26)
     throw std::invalid_argument("nn_cache_log2 must be in 0..26");
@@ -434,6 +435,10 @@ void SelfplayEngine::setModel(const char* path) {
   std::unique_ptr<NNEngine> next(new NNEngine(m, xLen_, yLen_, winLen_, nnPath_));
   sync();
   nn_ = std::move(next);
+  // network generation: rows of games that span the switch carry it in [49] / [50]
+  // (ChangedNeuralNet, play.cpp:1210-1226; trainingwrite.cpp:459-461)
+  modelGen_++;
+  KC_HIP(hipMemcpy(hd_.modelGen, &modelGen_, sizeof(int32_t), hipMemcpyHostToDevice));
   // cached evaluations belong to the previous network (the reference builds a new
   // NNEvaluator, and with it a new cache, per model: cpp/command/selfplay.cpp:150-200)
   if(hd_.cacheOn)

@@ -55,6 +55,7 @@ class SelfplayEngine {
   int commitInterval_ = 8;
   int xLen_ = 0, yLen_ = 0, winLen_ = 0;
   int nnPath_ = 0;  // NNPath of the network (kept across hot reloads)
+  int32_t modelGen_ = 0;  // hot reloads so far
   uint64_t rounds_ = 0;
   uint64_t rowsDrained_ = 0;
   int timingEvery_ = 0;

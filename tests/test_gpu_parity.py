@@ -334,3 +334,32 @@ def test_selfplay_full_scale_sampled_slots_bit_exact():
         ora.rounds(rounds)
         _compare_game(gpu, ora, s, 0, rounds)
     gpu.close()
+
+
+def test_rows_record_network_switch(model_path):
+    """Hot reload mid-game (switchNetsMidGame, play.cpp:1210-1226): rows of games that
+    span the switch carry globalTargets[49] = 1 and [50] = reloads after the row's turn
+    (trainingwrite.cpp:459-461, :844-850); games entirely on one network carry 0, 0."""
+    sp = kc.Selfplay(5, 5, 4, num_games=32, max_visits=16, seed=41, model_path=model_path, commit_interval=1)
+    sp.step(150)
+    other = model_path.replace(".cfnn", "-switch.cfnn")
+    kc.write_random_model("b6c96", 78, other)
+    sp.set_model(other)
+    sp.step(1500)
+    rows = sp.drain_rows()
+    assert sp.stats()["errors"] == 0
+    gt, meta = rows["globalTargetsNC"], rows["meta"]
+    spanning = 0
+    for key in sorted({(int(m[0]), int(m[1])) for m in meta}):
+        sel = [i for i, m in enumerate(meta) if (int(m[0]), int(m[1])) == key]
+        sel.sort(key=lambda i: int(meta[i][2]))
+        f49 = gt[sel, 49]
+        f50 = gt[sel, 50]
+        assert np.all(f49 == f49[0]) and f49[0] in (0.0, 1.0)
+        if f49[0] == 0.0:
+            assert np.all(f50 == 0.0)
+        else:
+            assert set(np.unique(f50)) <= {0.0, 1.0} and np.all(np.diff(f50) <= 0)
+            spanning += int(f50[0] == 1.0 and f50[-1] == 0.0)
+    assert spanning > 0
+    sp.close()

@@ -1,0 +1,13 @@
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/tnn.log 2>&1 || { tail -30 gpurun_out/tnn.log; exit 1; }
+tail -2 gpurun_out/tnn.log
+t() { timeout -k 10 200 python -u tools/nn_bench.py "$@" || exit 1; }
+t --arch b6c96 --precision fast-layered --n 512,2048,8192
+t --arch b10c128 --precision fast --n 977,4096,16384
+t --arch b10c128 --board 7 --n 600,4096
+t --arch b18c384nbt --board 9 --n 484,4096 --iters 5
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nn2 -o nn --output-format csv -- python tools/nn_bench.py --arch b18c384nbt --board 9 --n 484 --iters 5 > gpurun_out/prof_nn2.log 2>&1 || exit 1
+python3 -c "
+import csv
+for r in list(csv.DictReader(open('gpurun_out/prof_nn2/nn_kernel_stats.csv')))[:7]: print(r['Name'][:40], r['Calls'], round(float(r['AverageNs'])/1000,1), 'us', r['Percentage'])"
