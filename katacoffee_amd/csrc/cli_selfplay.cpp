@@ -179,6 +179,7 @@ struct Settings {
   int x = 5, y = 5, winLen = 4, games = 4096, gpus = 1, maxRowsPerFile = 10000;
   float modelPollSeconds = 10.0f;
   int nnCacheLog2 = 21;  // selfplay1.cfg:121 nnCacheSizePowerOfTwo
+  int nnPrecision = COFFEE_NN_FAST;  // nnPrecision = fast | accurate | fastLayered (the reference's useFP16)
   int64_t maxGamesTotal = -1;
   uint64_t seed = 0;
   coffee_search_params sp;
@@ -214,6 +215,17 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   getf("modelPollSeconds", s.modelPollSeconds);
   geti("nnCacheSizePowerOfTwo", s.nnCacheLog2);  // setup.cpp:268; <= 0 disables the cache
   s.nnCacheLog2 = std::max(0, s.nnCacheLog2);
+  it = kv.find("nnPrecision");
+  if(it != kv.end()) {
+    if(it->second == "fast")
+      s.nnPrecision = COFFEE_NN_FAST;
+    else if(it->second == "accurate")
+      s.nnPrecision = COFFEE_NN_ACCURATE;
+    else if(it->second == "fastLayered")
+      s.nnPrecision = COFFEE_NN_FAST_LAYERED;
+    else
+      throw std::runtime_error("nnPrecision must be fast, accurate or fastLayered");
+  }
   coffee_search_params& p = s.sp;
   geti("maxVisits", p.max_visits);
   getf("cpuctExploration", p.cpuct_exploration);
@@ -383,6 +395,7 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
   c.model_path = model.c_str();
   c.search = s.sp;
   c.nn_cache_log2 = s.nnCacheLog2;
+  c.nn_precision = s.nnPrecision;
   coffee_selfplay* h = nullptr;
   check(coffee_selfplay_create(&c, &h), "create engine");
   std::mt19937_64 fileRng(s.seed ^ (0x9E3779B97F4A7C15ULL * (gpu + 1)));
