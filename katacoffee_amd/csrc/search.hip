@@ -90,8 +90,18 @@ KC_D unsigned long long* sprofLds() {
 #define SPROF_FLUSH()                                                           \
   do {                                                                          \
     __syncthreads();                                                            \
-    if(laneId() < SPROF_N && blockIdx.x < SPROF_MAXG)                           \
+    if(laneId() < SPROF_N && blockIdx.x < SPROF_MAXG && laneId() < 24)          \
       g_searchProf[blockIdx.x * SPROF_N + laneId()] += sprofLds()[laneId()];    \
+  } while(0)
+// per-block maximum of a value over launches (slots 24..31; no contention)
+#define SPROF_MAX(i, v)                                                                   \
+  do {                                                                                    \
+    if(laneId() == 0 && blockIdx.x < SPROF_MAXG) {                                        \
+      unsigned long long* q_ = &g_searchProf[blockIdx.x * SPROF_N + (i)];                 \
+      const unsigned long long v_ = (unsigned long long)(v);                              \
+      if(v_ > *q_)                                                                        \
+        *q_ = v_;                                                                         \
+    }                                                                                     \
   } while(0)
 #else
 #define SPROF_NOW() 0ull
@@ -99,6 +109,9 @@ KC_D unsigned long long* sprofLds() {
   do {               \
   } while(0)
 #define SPROF_ADD(i, v) \
+  do {                  \
+  } while(0)
+#define SPROF_MAX(i, v) \
   do {                  \
   } while(0)
 #define SPROF_FLUSH() \
@@ -851,6 +864,8 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   waveSync();
   storeGame(v, s);
   SPROF_ADD(0, 1);
+  SPROF_MAX(24, SPROF_NOW() - t0);
+  SPROF_MAX(25, s.pathLen);
   SPROF_ADD(1, SPROF_NOW() - t0);
   SPROF_ADD(2, t1 - t0);
   SPROF_ADD(3, t2 - t1);
@@ -1342,6 +1357,7 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
   waveSync();
   storeGame(v, s);
   SPROF_ADD(10, 1);
+  SPROF_MAX(26, SPROF_NOW() - t0);
   SPROF_ADD(11, SPROF_NOW() - t0);
   SPROF_ADD(12, tPost);
   SPROF_ADD(13, tPath);
@@ -1367,8 +1383,17 @@ extern "C" void coffee_debug_search_profile(unsigned long long* out, int reset) 
   KC_HIP(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(g_searchProf), all.size() * 8));
   for(int i = 0; i < SPROF_N; i++)
     out[i] = 0;
-  for(size_t k = 0; k < all.size(); k++)
-    out[k % SPROF_N] += all[k];
+  for(size_t k = 0; k < all.size(); k++) {
+    const int i = (int)(k % SPROF_N);
+    if(i < 24)
+      out[i] += all[k];
+    else if(i <= 26)
+      out[i] = std::max(out[i], all[k]);
+    if(i == 24)
+      out[27] += all[k];  // sum of per-block maxima (their mean: the typical slowest descent)
+    if(i == 26)
+      out[28] += all[k];
+  }
   if(reset) {
     std::fill(all.begin(), all.end(), 0ull);
     KC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_searchProf), all.data(), all.size() * 8));

@@ -45,6 +45,9 @@ def main():
                     ("encode+slot", 7)]:
         print("  %-14s %8.0f cycles/block" % (name, p[i] / nb))
     print("  path levels    %8.2f per block" % (p[4] / nb))
+    print("  slowest select block %d cycles (mean of per-slot maxima %.0f), deepest path %d" %
+          (p[24], p[27] / max(1, a.games), p[25]))
+    print("  slowest backup block %d cycles (mean of per-slot maxima %.0f)" % (p[26], p[28] / max(1, a.games)))
     if a.probe:
         print("NN-cache bound: %d of %d evaluated leaves repeat an earlier state (%.1f%%)" %
               (p[9], p[10], 100.0 * p[9] / max(1, p[10])))
