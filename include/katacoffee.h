@@ -174,6 +174,15 @@ typedef struct coffee_search_params {
    * probability a refutation position (the root policy's alternative to the played
    * move) is queued and searched after the game; one row each */
   float side_position_prob;              /* 0.02 */
+  /* tree positions (recordTreePositions play.cpp:710-860, :1347-1361, :1612-1628): after
+   * a searched move (or side position), positions of its search tree up to 5 moves deep
+   * reached only through the mover's most-visited moves, from nodes with at least
+   * record_tree_threshold visits, are written as side rows with weight
+   * record_tree_target_weight (<= 1).  PlaySettings fields with these defaults
+   * (playsettings.cpp:14); the reference's selfplay config loader does not read them */
+  int32_t record_tree_positions;         /* 0 */
+  int32_t record_tree_threshold;         /* 0 */
+  float record_tree_target_weight;       /* 0.0 */
 } coffee_search_params;
 
 void coffee_search_params_default(coffee_search_params* p);

@@ -71,6 +71,8 @@ class SearchParams(ctypes.Structure):
         ("fork_game_prob", ctypes.c_float), ("fork_game_min_choices", ctypes.c_int32),
         ("early_fork_game_max_choices", ctypes.c_int32), ("fork_game_max_choices", ctypes.c_int32),
         ("side_position_prob", ctypes.c_float),
+        ("record_tree_positions", ctypes.c_int32), ("record_tree_threshold", ctypes.c_int32),
+        ("record_tree_target_weight", ctypes.c_float),
     ]
 
 

@@ -86,7 +86,7 @@ static void checkGeom(int x, int y, int w) {
 extern "C" {
 
 const char* coffee_last_error(void) { return gLastError.c_str(); }
-int coffee_abi_version(void) { return 103; }
+int coffee_abi_version(void) { return 104; }
 
 int coffee_device_count(int* count) {
   return guarded([&] {
@@ -286,6 +286,9 @@ void coffee_search_params_default(coffee_search_params* p) {
   p->early_fork_game_max_choices = 12;
   p->fork_game_max_choices = 36;
   p->side_position_prob = 0.0f;
+  p->record_tree_positions = 0;
+  p->record_tree_threshold = 0;
+  p->record_tree_target_weight = 0.0f;
 }
 
 struct coffee_selfplay {

@@ -278,6 +278,11 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   geti("earlyForkGameMaxChoices", p.early_fork_game_max_choices);
   geti("forkGameMaxChoices", p.fork_game_max_choices);
   getf("sidePositionProb", p.side_position_prob);
+  // PlaySettings fields the reference's loader never reads (playsettings.cpp:14): accepted
+  // here so the recording can be switched on from a config
+  getb("recordTreePositions", p.record_tree_positions);
+  geti("recordTreeThreshold", p.record_tree_threshold);
+  getf("recordTreeTargetWeight", p.record_tree_target_weight);
 }
 
 struct RowSink {

@@ -77,6 +77,8 @@ struct SP {
   float earlyForkProb, earlyForkMoveProp, forkProb;  // earlyForkGameProb, earlyForkGameExpectedMoveProp, forkGameProb
   int forkMinChoices, earlyForkMaxChoices, forkMaxChoices;
   float sideProb;            // sidePositionProb
+  int recordTree, recordTreeThreshold;  // recordTreePositions, recordTreeThreshold
+  float recordTreeWeight;               // recordTreeTargetWeight
 };
 
 // The parameters of a cheap search whose rows are not recorded (runBotWithLimits

@@ -1428,15 +1428,14 @@ KC_D void lcbAndRadius(const SP& sp, int pla, uint32_t cVisits, float cWs, float
   lcb = selfU - radius;
 }
 
-// oracle playSelectionValues (getPlaySelectionValues searchresults.cpp:63-309).
-// posOut/vals are LDS arrays [P]; returns the count (uniform).
+// oracle playSelectionValuesAt (getPlaySelectionValues searchresults.cpp:63-309) on node
+// ri with policy pol; the over-explored-children reduction and direct policy moves are
+// root-only.  posOut/vals are LDS arrays [P]; returns the count (uniform).
 template <int NI>
-KC_D int playSelectionValues(const GV& v, const SP& sp, const GameDev& s, float scaleMaxToAtLeast, bool allowDirect,
-                             int* posOut, float* vals, bool useLcb) {
-  const int ri = s.rootIdx;
+KC_D int playSelectionValuesAt(const GV& v, const SP& sp, const GameDev& s, int ri, const float* pol, bool isRoot,
+                               float scaleMaxToAtLeast, bool allowDirect, int* posOut, float* vals, bool useLcb) {
   const Node& n = v.nodes()[ri];
   const int k = n.numChildren;
-  const float* pol = v.rootNoised();
   const int pla = n.nextPla;
   const Edge* E = v.edges(ri);
   float cw[NI], val[NI];
@@ -1496,7 +1495,7 @@ KC_D int playSelectionValues(const GV& v, const SP& sp, const GameDev& s, float 
         bw = cw[j];
     bestWeight = __shfl(bw, bestLane, 64);
   }
-  if(k > 0) {
+  if(isRoot && k > 0) {
     const float fpu = fpuValue(sp, n, pla, true, 1.0f);
     const float scaling = exploreScaling(sp, total);
     float bp = 0.0f, bu = 0.0f;
@@ -1602,7 +1601,7 @@ KC_D int playSelectionValues(const GV& v, const SP& sp, const GameDev& s, float 
   }
   waveSync();
   if(numChildren == 0) {
-    if(!allowDirect)
+    if(!allowDirect || !isRoot)
       return 0;
     const int P = v.d.P;
     for(int base = 0; base < P; base += 64) {
@@ -1644,6 +1643,14 @@ KC_D int playSelectionValues(const GV& v, const SP& sp, const GameDev& s, float 
   }
   waveSync();
   return numChildren;
+}
+
+// oracle playSelectionValues: the root with its noised policy.
+template <int NI>
+KC_D int playSelectionValues(const GV& v, const SP& sp, const GameDev& s, float scaleMaxToAtLeast, bool allowDirect,
+                             int* posOut, float* vals, bool useLcb) {
+  return playSelectionValuesAt<NI>(v, sp, s, s.rootIdx, v.rootNoised(), true, scaleMaxToAtLeast, allowDirect, posOut,
+                                   vals, useLcb);
 }
 
 // oracle chooseIndex (chooseIndexWithTemperature searchhelpers.cpp:11-49)
@@ -2214,7 +2221,7 @@ KC_D void afterGame(const GV& v, GameDev& s, DRng& rng, uint16_t* scratch) {
 // (the search's root value), no next-move policy, no ownership / future boards /
 // final run lengths (the reference passes NULL for them; its finalMaxLength
 // dereference is B15, here zeros).  History masks from the game stream.
-KC_D void emitSideRow(const GV& v, const GameDev& s, const TurnRec& rec, DRng& rng) {
+KC_D void emitSideRow(const GV& v, const GameDev& s, const TurnRec& rec, DRng& rng, const DBoard& b, int gameNumMeta) {
   const SearchDev& d = v.d;
   const DTables& T = v.T;
   const int A = T.A, P = T.P, pb = (A + 7) / 8;
@@ -2237,7 +2244,6 @@ KC_D void emitSideRow(const GV& v, const GameDev& s, const TurnRec& rec, DRng& r
   r = ((unsigned long long)hi << 32) | lo;
   if(r == ~0ull)
     return;
-  const DBoard& b = s.root;
   const int pla = b.pla;
   packRowBinWave(T, b, d.rBin + r * NUM_SPATIAL * pb);
   if(v.lane == 0)
@@ -2293,9 +2299,179 @@ KC_D void emitSideRow(const GV& v, const GameDev& s, const TurnRec& rec, DRng& r
   for(int i = v.lane; i < 5 * A; i += 64)
     vt[i] = 0;
   if(v.lane < 4) {
-    const int m = v.lane == 0 ? d.slotBase + v.g : (v.lane == 1 ? s.gameNum - 1 : (v.lane == 2 ? b.turn : s.numTurns));
+    const int m = v.lane == 0 ? d.slotBase + v.g : (v.lane == 1 ? gameNumMeta : (v.lane == 2 ? b.turn : s.numTurns));
     d.rMeta[r * 4 + v.lane] = m;
   }
+}
+
+// oracle searchTargets: extractPolicyTarget (play.cpp:635-672; scaleMaxToAtLeast 10, no
+// direct policy moves) into pt (global [P]) and getPolicySurpriseAndEntropy
+// (searchresults.cpp:486-550) at node ni with policy pol.
+template <int NI>
+KC_D void searchTargets(const GV& v, const SP& sp, const GameDev& s, int ni, const float* pol, bool isRoot,
+                        int16_t* pt, TurnRec& rec, int* posv, float* vals, float* tmp, float* tmp2) {
+  const int P = v.d.P;
+  for(int p = v.lane; p < P; p += 64)
+    pt[p] = 0;
+  {
+    int m = playSelectionValuesAt<NI>(v, sp, s, ni, pol, isRoot, 10.0f, false, posv, vals, sp.useLcb);
+    float mx = 0.0f;
+    for(int i = v.lane; i < m; i += 64)
+      mx = vals[i] > mx ? vals[i] : mx;
+    mx = waveMax(mx);
+    float factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
+    waveSync();
+    for(int i = v.lane; i < m; i += 64)
+      pt[posv[i]] = (int16_t)roundf(vals[i] * factor);
+  }
+  waveSync();
+  int m = playSelectionValuesAt<NI>(v, sp, s, ni, pol, isRoot, 1.0f, true, posv, vals, sp.useLcb);
+  const float sumV = seqSum(vals, m, v.lane);
+  // per-child terms (0 where the oracle skips), summed in order on lane 0
+  waveSync();
+  for(int i = v.lane; i < m; i += 64) {
+    float p = fmaxf(pol[posv[i]], 1e-30f);
+    float tt = vals[i] / sumV;
+    float st = 0.0f, et = 0.0f;
+    if(tt > 1e-30f) {
+      float lt = dlog(tt), lp = dlog(p);
+      st = tt * (lt - lp);
+      et = -tt * lt;
+    }
+    tmp[i] = st;
+    tmp2[i] = et;
+  }
+  const float surprise = seqSum(tmp, m, v.lane);
+  const float searchEnt = seqSum(tmp2, m, v.lane);
+  waveSync();
+  for(int p = v.lane; p < P; p += 64) {
+    float q = pol[p];
+    tmp[p] = q > 1e-30f ? -q * dlog(q) : 0.0f;
+  }
+  float polEnt = seqSum(tmp, P, v.lane);
+  rec.policySurprise = fmaxf(0.0f, surprise);
+  rec.searchEntropy = fmaxf(0.0f, searchEnt);
+  rec.policyEntropy = fmaxf(0.0f, polEnt);
+  waveSync();
+}
+
+// oracle valueTargets (extractValueTargets play.cpp:674-682, reportedsearchvalues.cpp:10-50)
+KC_D void valueTargets(const Node& n, TurnRec& rec) {
+  float wl = fmaxf(-1.0f, fminf(1.0f, n.winLossAvg));
+  rec.whiteWin = fmaxf(0.0f, fminf(1.0f, 0.5f * (wl + 1.0f)));
+  rec.whiteLoss = fmaxf(0.0f, fminf(1.0f, 0.5f * (-wl + 1.0f)));
+  rec.rootWL = wl;
+}
+
+// oracle rawStats (computeNNRawStats play.cpp:684-704) from a stored evaluation
+KC_D void rawStats(const GV& v, float win, float loss, const float* pol, TurnRec& rec, float* tmp) {
+  rec.rawWhiteWL = win - loss;
+  for(int p = v.lane; p < v.d.P; p += 64) {
+    float q = pol[p];
+    tmp[p] = q >= 1e-30f ? -q * dlog(q) : 0.0f;
+  }
+  // in-order sum of only the q >= 1e-30 terms: zero terms are exact no-ops
+  rec.rawPolicyEntropy = seqSum(tmp, v.d.P, v.lane);
+  waveSync();
+}
+
+// oracle recordTreeRec (recordTreePositionsRec play.cpp:710-814, maxDepth 5), as a
+// pre-order walk with an explicit stack: a side row at every non-root node reached
+// only through the best moves of the player to move there; excl0/excl1 skipped at the
+// root.  Frames and boards live in LDS; every lane walks the same path.
+template <int NI>
+KC_D void recordTreePositions(const GV& v, const SP& sp, const GameDev& s, DRng& rng, int excl0, int excl1,
+                              uint32_t rootVisits, int gameNumMeta, int* posv, float* vals, float* tmp, float* tmp2) {
+  constexpr int MAXD = 5;
+  __shared__ DBoard tb[MAXD + 1];
+  __shared__ int fNode[MAXD + 1], fNext[MAXD + 1], fBest[MAXD + 1], fFlags[MAXD + 1];
+  const SearchDev& d = v.d;
+  const int A = d.A;
+  int16_t* pt = d.sidePol + (size_t)v.g * d.P;
+  tb[0] = s.root;
+  fNode[0] = s.rootIdx;
+  fFlags[0] = 3;  // bit 0: the player to move has played best so far; bit 1: the opponent
+  waveSync();
+  int depth = 0;
+  bool enter = true;
+  while(depth >= 0) {
+    const int ni = fNode[depth];
+    const int k = v.nodes()[ni].numChildren;
+    const Edge* E = v.edges(ni);
+    if(enter) {
+      enter = false;
+      if(k <= 0) {
+        depth--;
+        continue;
+      }
+      if((fFlags[depth] & 1) && ni != s.rootIdx) {
+        TurnRec rec;
+        searchTargets<NI>(v, sp, s, ni, v.pol(ni), false, pt, rec, posv, vals, tmp, tmp2);
+        const Node& n = v.nodes()[ni];
+        rawStats(v, n.nnWin, n.nnLoss, v.pol(ni), rec, tmp);
+        valueTargets(n, rec);
+        rec.visits = rootVisits;
+        // resolveWeight (play.cpp:1683-1696) when the position is recorded
+        const float w = sp.recordTreeWeight;
+        const float fl = floorf(w);
+        const int copies = (int)fl + (rng.uni() < w - fl ? 1 : 0);
+        for(int c = 0; c < copies; c++)
+          emitSideRow(v, s, rec, rng, tb[depth], gameNumMeta);
+        waveSync();
+      }
+      if(depth >= MAXD) {
+        depth--;
+        continue;
+      }
+      // the most-visited child; children[0]'s count is not consulted (:757-769)
+      float bv = -1.0f;
+      int bi = BIG;
+      for(int i = 1 + v.lane; i < k; i += 64) {
+        const float cv = (float)v.nodes()[E[i].child].visits;
+        if(cv > bv) {
+          bv = cv;
+          bi = i;
+        }
+      }
+      waveArgmax(bv, bi);
+      fBest[depth] = bv > 0.0f ? bi : 0;
+      fNext[depth] = 0;
+      waveSync();
+    }
+    const int flags = fFlags[depth], best = fBest[depth];
+    const bool plaB = (flags & 1) != 0, oppB = (flags & 2) != 0;
+    int found = -1, foundFlags = 0;
+    for(int i = fNext[depth]; i < k; i++) {
+      const bool np = oppB, no = plaB && i == best;
+      if(!np && !no)
+        continue;
+      const Edge e = E[i];
+      const int mv = (int)e.move;
+      if(depth == 0 && (mv == excl0 || mv == excl1))
+        continue;
+      if((long long)v.nodes()[e.child].visits < (long long)sp.recordTreeThreshold)
+        continue;
+      found = i;
+      foundFlags = (np ? 1 : 0) | (no ? 2 : 0);
+      break;
+    }
+    if(found < 0) {
+      depth--;
+      continue;
+    }
+    const Edge e = E[found];
+    waveSync();
+    fNext[depth] = found + 1;
+    tb[depth + 1] = tb[depth];
+    waveSync();
+    playMoveWave(v.T, tb[depth + 1], (int)e.move % A, (int)e.move / A);
+    fNode[depth + 1] = (int)e.child;
+    fFlags[depth + 1] = foundFlags;
+    waveSync();
+    depth++;
+    enter = true;
+  }
+  waveSync();
 }
 
 // oracle sideEval: the network's policy at a side position's continuation picks a
@@ -2688,78 +2864,25 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   const int chosen = posv[ci];
   const Node& r = v.nodes()[s.rootIdx];
   TurnRec rec;
-  {
-    float wl = fmaxf(-1.0f, fminf(1.0f, r.winLossAvg));
-    rec.whiteWin = fmaxf(0.0f, fminf(1.0f, 0.5f * (wl + 1.0f)));
-    rec.whiteLoss = fmaxf(0.0f, fminf(1.0f, 0.5f * (-wl + 1.0f)));
-    rec.visits = r.visits;
-    rec.rootWL = wl;
-    rec.rootNNWin = r.nnWin;
-    rec.rootNNLoss = r.nnLoss;
-    rec.targetWeight = s.moveWeight;
-    rec.rows = 0;
-    rec.gen = (uint8_t)*v.d.modelGen;
-  }
+  valueTargets(r, rec);
+  rec.visits = r.visits;
+  rec.rootNNWin = r.nnWin;
+  rec.rootNNLoss = r.nnLoss;
+  rec.targetWeight = s.moveWeight;
+  rec.rows = 0;
+  rec.gen = (uint8_t)*v.d.modelGen;
   const int t = s.numTurns;
   int16_t* pt = side ? d.sidePol + (size_t)g * P : v.turnPol(t);
   waveSync();
-  {
-    for(int p = v.lane; p < P; p += 64)
-      pt[p] = 0;
-    // the targets run after runBotWithLimits restored the base parameters (play.cpp:1066, :1307-1320)
-    int m = playSelectionValues<NI>(v, sp, s, 10.0f, false, posv, vals, sp.useLcb);
-    float mx = 0.0f;
-    for(int i = v.lane; i < m; i += 64)
-      mx = vals[i] > mx ? vals[i] : mx;
-    mx = waveMax(mx);
-    float factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
-    waveSync();
-    for(int i = v.lane; i < m; i += 64)
-      pt[posv[i]] = (int16_t)roundf(vals[i] * factor);
-  }
-  rec.rawWhiteWL = s.rawWin - s.rawLoss;
-  {
-    const float* rp = v.rawPolicy();
-    for(int p = v.lane; p < P; p += 64) {
-      float q = rp[p];
-      tmp[p] = q >= 1e-30f ? -q * dlog(q) : 0.0f;
-    }
-    // in-order sum of only the q >= 1e-30 terms: zero terms are exact no-ops
-    rec.rawPolicyEntropy = seqSum(tmp, P, v.lane);
-  }
-  {
-    waveSync();
-    int m = playSelectionValues<NI>(v, sp, s, 1.0f, true, posv, vals, sp.useLcb);
-    const float* pol = v.rootNoised();
-    const float sumV = seqSum(vals, m, v.lane);
-    // per-child terms (0 where the oracle skips), summed in order on lane 0
-    waveSync();
-    for(int i = v.lane; i < m; i += 64) {
-      float p = fmaxf(pol[posv[i]], 1e-30f);
-      float tt = vals[i] / sumV;
-      float st = 0.0f, et = 0.0f;
-      if(tt > 1e-30f) {
-        float lt = dlog(tt), lp = dlog(p);
-        st = tt * (lt - lp);
-        et = -tt * lt;
-      }
-      tmp[i] = st;
-      tmp2[i] = et;
-    }
-    const float surprise = seqSum(tmp, m, v.lane);
-    const float searchEnt = seqSum(tmp2, m, v.lane);
-    waveSync();
-    for(int p = v.lane; p < P; p += 64) {
-      float q = pol[p];
-      tmp[p] = q > 1e-30f ? -q * dlog(q) : 0.0f;
-    }
-    float polEnt = seqSum(tmp, P, v.lane);
-    rec.policySurprise = fmaxf(0.0f, surprise);
-    rec.searchEntropy = fmaxf(0.0f, searchEnt);
-    rec.policyEntropy = fmaxf(0.0f, polEnt);
-  }
+  // the targets run after runBotWithLimits restored the base parameters (play.cpp:1066, :1307-1320)
+  searchTargets<NI>(v, sp, s, s.rootIdx, v.rootNoised(), true, pt, rec, posv, vals, tmp, tmp2);
+  rawStats(v, s.rawWin, s.rawLoss, v.rawPolicy(), rec, tmp);
+  const bool recordTree = sp.recordTree != 0 && sp.recordTreeWeight > 0.0f;
   if(side) {
-    emitSideRow(v, s, rec, rng);
+    emitSideRow(v, s, rec, rng, s.root, s.gameNum - 1);
+    // its subtree positions (play.cpp:1612-1628)
+    if(recordTree)
+      recordTreePositions<NI>(v, sp, s, rng, -1, -1, r.visits, s.gameNum - 1, posv, vals, tmp, tmp2);
     // occasionally continue: the response, then a forking move from the network's
     // policy there becomes another side position (play.cpp:1632-1656)
     if(rng.uni() < 0.25f) {
@@ -2781,13 +2904,21 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
     return;
   }
   // a side position: the root policy's alternative to the move (play.cpp:1328-1345)
+  int forkMove = -1;
   if(sp.sideProb > 0.0f && rng.uni() < sp.sideProb) {
     const int fm = forkingMove(v, rng, v.pol(s.rootIdx), s.root, chosen, posv, vals, tmp);
+    forkMove = fm;
     if(fm >= 0) {
       DBoard b2 = s.root;
       playMoveWave(v.T, b2, fm % A, fm / A);
       pushSide(v, s, b2);
     }
+  }
+  // subtree positions of this search, except the played and the forked branches
+  // (play.cpp:1347-1361)
+  if(recordTree) {
+    waveSync();
+    recordTreePositions<NI>(v, sp, s, rng, chosen, forkMove, r.visits, s.gameNum, posv, vals, tmp, tmp2);
   }
   rec.cell = (int8_t)(chosen % A);
   rec.dir = (int8_t)(chosen / A);

@@ -68,6 +68,9 @@ SP toSP(const coffee_search_params& p) {
   s.earlyForkMaxChoices = p.early_fork_game_max_choices;
   s.forkMaxChoices = p.fork_game_max_choices;
   s.sideProb = p.side_position_prob;
+  s.recordTree = p.record_tree_positions;
+  s.recordTreeThreshold = p.record_tree_threshold;
+  s.recordTreeWeight = p.record_tree_target_weight;
   return s;
 }
 
@@ -113,6 +116,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     throw std::invalid_argument("fork settings: probabilities in [0, 0.5], min <= max choices <= 100");
   if(!unit(sp.side_position_prob))
     throw std::invalid_argument("side_position_prob must be in [0, 1]");
+  // play.cpp:1349-1350
+  if(sp.record_tree_positions && sp.record_tree_target_weight > 1.0f)
+    throw std::invalid_argument("record_tree_target_weight > 1");
   const DTables& ht = hostTables(c.x, c.y, c.win_len);
   T_ = deviceTables(c.x, c.y, c.win_len);
   commitInterval_ = c.commit_interval > 0 ? c.commit_interval : 8;

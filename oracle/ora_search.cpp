@@ -628,10 +628,17 @@ struct Ctx {
   // at the call (self-play turns it off for the move choice only, play.cpp:1040-1046, :1073-1076).
   int playSelectionValues(float scaleMaxToAtLeast, bool allowDirectPolicyMoves, int* posOut, float* vals,
                           bool useLcb) {
-    int ri = gm.rootIdx;
+    return playSelectionValuesAt(gm.rootIdx, gm.rootNoised.data(), true, scaleMaxToAtLeast, allowDirectPolicyMoves,
+                                 posOut, vals, useLcb);
+  }
+
+  // The same on any node (tree positions, play.cpp:736-745): the node's own network
+  // policy (getPolicyProbsMaybeNoised: noise only at the root); the reduction of
+  // over-explored children (:136-186) and direct policy moves (:242-276) are root-only.
+  int playSelectionValuesAt(int ri, const float* pol, bool isRoot, float scaleMaxToAtLeast,
+                            bool allowDirectPolicyMoves, int* posOut, float* vals, bool useLcb) {
     const Node& n = N(ri);
     const int k = n.numChildren;
-    const float* pol = gm.rootNoised.data();
     int pla = n.nextPla;
     float cw[MAX_P];
     for(int i = 0; i < k; i++) {
@@ -656,7 +663,7 @@ struct Ctx {
         }
       }
     }
-    if(k > 0) {
+    if(isRoot && k > 0) {
       float fpu = fpuValue(ri, pla, true, 1.0f);
       float scaling = exploreScaling(total);
       // getExploreSelectionValueOfChild for the best child, isDuringSearch = false
@@ -725,7 +732,7 @@ struct Ctx {
       }
     }
     if(numChildren == 0) {
-      if(!allowDirectPolicyMoves)
+      if(!allowDirectPolicyMoves || !isRoot)
         return 0;
       for(int p = 0; p < g.P; p++) {
         if(!isLegal(g, gm.root, p % g.A, p / g.A) || pol[p] < 0.0f)
@@ -1198,8 +1205,11 @@ struct Ctx {
       startGame();
   }
 
-  // writeGame's side rows (trainingwrite.cpp:894-937, addRow with isSidePosition).
-  void emitSideRow(const TurnRec& tr) {
+  // writeGame's side rows (trainingwrite.cpp:894-937, addRow with isSidePosition):
+  // a searched side position (board = its root, after the game: gameNumMeta = the
+  // finished game's number) or a tree position (board = the node's position).
+  void emitSideRow(const TurnRec& tr) { emitSideRow(tr, gm.root, (int32_t)gm.gameNum - 1); }
+  void emitSideRow(const TurnRec& tr, const Board& b, int32_t gameNumMeta) {
     const int A = g.A, P = g.P, pb = (A + 7) / 8;
     float hmv[5];
     bool h = true;
@@ -1208,7 +1218,6 @@ struct Ctx {
       hmv[i] = h ? 1.0f : 0.0f;
     }
     Rows& R = s.rows;
-    const Board& b = gm.root;
     const int pla = b.pla;
     float bin[NUM_SPATIAL * MAX_AREA], glob[1];
     encodeV1(g, b, 0, bin, glob);
@@ -1221,7 +1230,7 @@ struct Ctx {
     R.value.resize((size_t)R.n * 5 * A);
     R.meta.resize((size_t)R.n * 4);
     R.meta[r * 4 + 0] = s.cfg.slotBase + gm.slot;
-    R.meta[r * 4 + 1] = (int32_t)gm.gameNum - 1;
+    R.meta[r * 4 + 1] = gameNumMeta;
     R.meta[r * 4 + 2] = b.turn;
     R.meta[r * 4 + 3] = (int32_t)gm.turns.size();
     for(int ch = 0; ch < NUM_SPATIAL; ch++)
@@ -1262,6 +1271,119 @@ struct Ctx {
       R.value[r * 5 * A + i] = 0;
   }
 
+  // A search's targets at node ni with policy pol: extractPolicyTarget (play.cpp:635-672,
+  // scaleMaxToAtLeast 10, no direct policy moves) and getPolicySurpriseAndEntropy
+  // (searchresults.cpp:486-550, scaleMaxToAtLeast 1).
+  void searchTargets(int ni, const float* pol, bool isRoot, TurnRec& tr) {
+    int posv[MAX_P];
+    float vals[MAX_P];
+    tr.policyTarget.assign(g.P, 0);
+    {
+      int m = playSelectionValuesAt(ni, pol, isRoot, 10.0f, false, posv, vals, sp.useLcbForSelection);
+      float mx = 0.0f;
+      for(int i = 0; i < m; i++)
+        if(vals[i] > mx)
+          mx = vals[i];
+      float factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
+      for(int i = 0; i < m; i++)
+        tr.policyTarget[posv[i]] = (int16_t)roundf(vals[i] * factor);
+    }
+    int m = playSelectionValuesAt(ni, pol, isRoot, 1.0f, true, posv, vals, sp.useLcbForSelection);
+    float sumV = 0.0f;
+    for(int i = 0; i < m; i++)
+      sumV = sumV + vals[i];
+    float surprise = 0.0f, searchEnt = 0.0f, polEnt = 0.0f;
+    for(int i = 0; i < m; i++) {
+      float p = std::max(pol[posv[i]], 1e-30f);
+      float t = vals[i] / sumV;
+      if(t > 1e-30f) {
+        float lt = kLogf(t), lp = kLogf(p);
+        surprise = surprise + t * (lt - lp);
+        searchEnt = searchEnt + (-t * lt);
+      }
+    }
+    for(int p = 0; p < g.P; p++)
+      if(pol[p] > 1e-30f)
+        polEnt = polEnt + (-pol[p] * kLogf(pol[p]));
+    tr.policySurprise = std::max(0.0f, surprise);
+    tr.searchEntropy = std::max(0.0f, searchEnt);
+    tr.policyEntropy = std::max(0.0f, polEnt);
+  }
+
+  // extractValueTargets (play.cpp:674-682) via ReportedSearchValues (reportedsearchvalues.cpp:10-50).
+  void valueTargets(int ni, TurnRec& tr) {
+    float wl = std::max(-1.0f, std::min(1.0f, N(ni).winLossAvg));
+    tr.whiteWin = std::max(0.0f, std::min(1.0f, 0.5f * (wl + 1.0f)));
+    tr.whiteLoss = std::max(0.0f, std::min(1.0f, 0.5f * (-wl + 1.0f)));
+    tr.rootWL = wl;
+  }
+
+  // computeNNRawStats (play.cpp:684-704) from a stored evaluation.
+  void rawStats(float win, float loss, const float* pol, TurnRec& tr) {
+    tr.rawWhiteWL = win - loss;
+    float ent = 0.0f;
+    for(int p = 0; p < g.P; p++) {
+      float q = pol[p];
+      if(q >= 1e-30f)
+        ent = ent + (-q * kLogf(q));
+    }
+    tr.rawPolicyEntropy = ent;
+  }
+
+  // recordTreePositionsRec (play.cpp:710-814, maxDepth 5 from :832): a pre-order walk of
+  // the finished search's tree that writes a side row at every non-root node reached
+  // only through best moves of the player to move there; excl0/excl1 (the played move
+  // and the side position's forking move) are skipped at the root.  SPEC: the raw
+  // network stats are the node's stored evaluation (the reference re-evaluates the
+  // position, :748); the weight resolves when the position is recorded
+  // (resolveWeight :1683-1696: floor + a draw on the excess) and the rows are written
+  // then (the tree is gone by the game's end), with the network-change fields of a
+  // searched side row.
+  void recordTreeRec(const Board& b, int ni, int depth, bool plaBest, bool oppBest, int excl0, int excl1,
+                     uint32_t rootVisits, int32_t gameNumMeta) {
+    const int k = N(ni).numChildren;
+    if(k <= 0)
+      return;
+    if(plaBest && ni != gm.rootIdx) {
+      TurnRec tr;
+      searchTargets(ni, POL(ni), false, tr);
+      valueTargets(ni, tr);
+      rawStats(N(ni).nnWin, N(ni).nnLoss, POL(ni), tr);
+      tr.visits = rootVisits;
+      const float w = sp.recordTreeTargetWeight;
+      const float fl = floorf(w);
+      const int copies = (int)fl + (gm.rng.uni() < w - fl ? 1 : 0);
+      for(int c = 0; c < copies; c++)
+        emitSideRow(tr, b, gameNumMeta);
+    }
+    if(depth >= 5)
+      return;
+    // the child with the most visits, children[0]'s count not consulted (:757-769)
+    int best = 0;
+    uint32_t bestVisits = 0;
+    for(int i = 1; i < k; i++) {
+      const uint32_t cv = N((int)EC(ni, i)).visits;
+      if(cv > bestVisits) {
+        bestVisits = cv;
+        best = i;
+      }
+    }
+    for(int i = 0; i < k; i++) {
+      const bool newPla = oppBest, newOpp = plaBest && i == best;
+      if(!newPla && !newOpp)
+        continue;
+      const int mv = EM(ni, i);
+      if(mv == excl0 || mv == excl1)
+        continue;
+      const int ci = (int)EC(ni, i);
+      if((int64_t)N(ci).visits < (int64_t)sp.recordTreeThreshold)
+        continue;
+      Board b2 = b;
+      playMove(g, b2, mv % g.A, mv / g.A);
+      recordTreeRec(b2, ci, depth + 1, newPla, newOpp, -1, -1, rootVisits, gameNumMeta);
+    }
+  }
+
   // The network's policy at a side position's continuation picks a forking move.
   void sideEval(const float* out) {
     float pol[MAX_P], w, l;
@@ -1297,67 +1419,23 @@ void Ctx::commitMove() {
   float temp = interpolateEarly(sp.chosenMoveTemperatureHalflife, sp.chosenMoveTemperatureEarly, sp.chosenMoveTemperature);
   int chosen = posv[chooseIndex(vals, n, temp)];
   const Node& r = N(gm.rootIdx);
-  // extractValueTargets play.cpp:674-682 via ReportedSearchValues reportedsearchvalues.cpp:10-50
-  float wl = std::max(-1.0f, std::min(1.0f, r.winLossAvg));
-  tr.whiteWin = std::max(0.0f, std::min(1.0f, 0.5f * (wl + 1.0f)));
-  tr.whiteLoss = std::max(0.0f, std::min(1.0f, 0.5f * (-wl + 1.0f)));
+  valueTargets(gm.rootIdx, tr);
   tr.visits = r.visits;
-  tr.rootWL = wl;
   tr.rootNNWin = r.nnWin;
   tr.rootNNLoss = r.nnLoss;
   tr.targetWeight = gm.moveWeight;
   // the targets below run after runBotWithLimits restored the base parameters
   // (play.cpp:1066, :1307-1320)
   Ctx base(s, gm, s.cfg.sp);
-  // extractPolicyTarget play.cpp:635-672
-  tr.policyTarget.assign(g.P, 0);
-  {
-    int m = base.playSelectionValues(10.0f, false, posv, vals, sp.useLcbForSelection);
-    float mx = 0.0f;
-    for(int i = 0; i < m; i++)
-      if(vals[i] > mx)
-        mx = vals[i];
-    float factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
-    for(int i = 0; i < m; i++)
-      tr.policyTarget[posv[i]] = (int16_t)roundf(vals[i] * factor);
-  }
+  base.searchTargets(gm.rootIdx, gm.rootNoised.data(), true, tr);
   // computeNNRawStats play.cpp:684-704 (first root-symmetry eval)
-  tr.rawWhiteWL = gm.rawWin - gm.rawLoss;
-  {
-    float ent = 0.0f;
-    for(int p = 0; p < g.P; p++) {
-      float q = gm.rawPolicy[p];
-      if(q >= 1e-30f)
-        ent = ent + (-q * kLogf(q));
-    }
-    tr.rawPolicyEntropy = ent;
-  }
-  // getPolicySurpriseAndEntropy searchresults.cpp:486-550
-  {
-    int m = base.playSelectionValues(1.0f, true, posv, vals, sp.useLcbForSelection);
-    const float* pol = gm.rootNoised.data();
-    float sumV = 0.0f;
-    for(int i = 0; i < m; i++)
-      sumV = sumV + vals[i];
-    float surprise = 0.0f, searchEnt = 0.0f, polEnt = 0.0f;
-    for(int i = 0; i < m; i++) {
-      float p = std::max(pol[posv[i]], 1e-30f);
-      float t = vals[i] / sumV;
-      if(t > 1e-30f) {
-        float lt = kLogf(t), lp = kLogf(p);
-        surprise = surprise + t * (lt - lp);
-        searchEnt = searchEnt + (-t * lt);
-      }
-    }
-    for(int p = 0; p < g.P; p++)
-      if(pol[p] > 1e-30f)
-        polEnt = polEnt + (-pol[p] * kLogf(pol[p]));
-    tr.policySurprise = std::max(0.0f, surprise);
-    tr.searchEntropy = std::max(0.0f, searchEnt);
-    tr.policyEntropy = std::max(0.0f, polEnt);
-  }
+  rawStats(gm.rawWin, gm.rawLoss, gm.rawPolicy.data(), tr);
+  const bool recordTree = s.cfg.sp.recordTreePositions != 0 && s.cfg.sp.recordTreeTargetWeight > 0.0f;
   if(side) {
     emitSideRow(tr);
+    // its subtree positions (play.cpp:1612-1628)
+    if(recordTree)
+      base.recordTreeRec(gm.root, gm.rootIdx, 0, true, true, -1, -1, r.visits, (int32_t)gm.gameNum - 1);
     // occasionally continue: the response, then a forking move (play.cpp:1632-1656)
     if(gm.rng.uni() < 0.25f) {
       Board b2 = gm.root;
@@ -1373,14 +1451,20 @@ void Ctx::commitMove() {
     return;
   }
   // a side position: the root policy's alternative to the move (play.cpp:1328-1345)
+  int forkMove = -1;
   if(s.cfg.sp.sidePositionProb > 0.0f && gm.rng.uni() < s.cfg.sp.sidePositionProb) {
     const int fm = forkingMove(POL(gm.rootIdx), gm.root, chosen);
+    forkMove = fm;
     if(fm >= 0) {
       Board b2 = gm.root;
       playMove(g, b2, fm % g.A, fm / g.A);
       pushSide(b2);
     }
   }
+  // subtree positions of this search, except the played and the forked branches
+  // (play.cpp:1347-1361)
+  if(recordTree)
+    base.recordTreeRec(gm.root, gm.rootIdx, 0, true, true, chosen, forkMove, r.visits, (int32_t)gm.gameNum);
   tr.cell = (int8_t)(chosen % g.A);
   tr.dir = (int8_t)(chosen / g.A);
   gm.turns.push_back(tr);

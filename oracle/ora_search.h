@@ -47,6 +47,11 @@ struct SearchParams {
   float forkGameProb = 0.0f;             // 0.01
   int forkGameMinChoices = 3, earlyForkGameMaxChoices = 12, forkGameMaxChoices = 36;
   float sidePositionProb = 0.0f;         // 0.02
+  // recordTreePositions (play.cpp:710-860): PlaySettings fields the selfplay config
+  // loader leaves at their defaults (playsettings.cpp:14)
+  int recordTreePositions = 0;
+  int recordTreeThreshold = 0;
+  float recordTreeTargetWeight = 0.0f;
 };
 
 // The search parameters of a cheap search whose rows are not recorded

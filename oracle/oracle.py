@@ -216,6 +216,7 @@ PLAY_SETTINGS = {
     "early_fork_game_prob": 0.0, "early_fork_game_expected_move_prop": 0.025, "fork_game_prob": 0.0,
     "fork_game_min_choices": 3, "early_fork_game_max_choices": 12, "fork_game_max_choices": 36,
     "side_position_prob": 0.0,
+    "record_tree_positions": 0, "record_tree_threshold": 0, "record_tree_target_weight": 0.0,
 }
 
 

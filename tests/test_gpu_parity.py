@@ -317,6 +317,43 @@ def test_selfplay_geometries_bit_exact_vs_oracle(X, Y, W, games, visits, rounds,
     gpu.close()
 
 
+# Tree positions (recordTreePositions play.cpp:710-860): side rows from the finished
+# searches' trees, bit-exact vs the oracle, alone and with every other variety feature.
+TREE = dict(record_tree_positions=1, record_tree_threshold=2, record_tree_target_weight=0.6)
+
+
+@pytest.mark.parametrize("X,Y,W,games,visits,rounds,seed,cache_log2,play",
+                         [(5, 5, 4, 8, 32, 1500, 61, 0, TREE),
+                          (5, 5, 4, 8, 24, 1800, 67, 12, dict(PRODUCTION, side_position_prob=0.3, **FORKS,
+                                                              record_tree_positions=1, record_tree_threshold=3,
+                                                              record_tree_target_weight=1.0)),
+                          (9, 9, 5, 4, 24, 1200, 71, 0, TREE)],
+                         ids=["5x5-tree", "5x5-tree-everything", "9x9-tree"])
+def test_selfplay_tree_positions_bit_exact_vs_oracle(X, Y, W, games, visits, rounds, seed, cache_log2, play):
+    cap = 128
+    gpu = kc.Selfplay(X, Y, W, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,
+                      nn_cache_log2=cache_log2, row_capacity=1 << 16, **play)
+    ora = oracle.Selfplay(X, Y, W, games=games, max_visits=visits, node_cap=cap, seed=seed,
+                          nn_cache_log2=cache_log2, **play)
+    done = 0
+    for chunk in [1, 7, 200, rounds]:
+        gpu.step(chunk - done)
+        ora.rounds(chunk - done)
+        done = chunk
+        for g in range(games):
+            _compare_game(gpu, ora, g, g, done)
+    st = gpu.stats()
+    assert st["errors"] == 0 and st["rows_dropped"] == 0 and st["moves"] > 0
+    gr = _sorted_rows(gpu.drain_rows())
+    orr = _sorted_rows(ora.rows())
+    assert len(gr["meta"]) == len(orr["meta"])
+    tree = orr["globalTargetsNC"][:, 27] == 0.0
+    assert tree.sum() > 0
+    for k in orr:
+        np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
+    gpu.close()
+
+
 def test_selfplay_full_scale_sampled_slots_bit_exact():
     """C2 scale on the device (4096 games, 600 visits, node_cap 2048, deep trees) with
     the stand-in network; 12 sampled slots replayed one by one in the oracle from the

@@ -194,3 +194,35 @@ def test_side_positions():
         np.testing.assert_array_equal(gt[side, 2 * f], gt[side, 0])
     np.testing.assert_array_equal(gt[:, 60], 16.0)
     np.testing.assert_array_equal(r["policyTargetsNCMove"][side, 1], 1)
+
+
+def test_tree_positions():
+    """Tree positions (recordTreePositions play.cpp:710-860): with no side positions and
+    no forks every row without ownership targets comes from the search trees: policy
+    targets of searched children, the root's visit count in gt[60], one value target."""
+    base = dict(games=6, max_visits=24, node_cap=128, seed=53)
+    plain = oracle.Selfplay(5, 5, 4, **base)
+    plain.rounds(1500)
+    assert np.all(plain.rows()["globalTargetsNC"][:, 27] != 0.0)
+    sp = oracle.Selfplay(5, 5, 4, record_tree_positions=1, record_tree_threshold=2, record_tree_target_weight=1.0,
+                         **base)
+    sp.rounds(1500)
+    r = sp.rows()
+    gt, val, pol = r["globalTargetsNC"], r["valueTargetsNCHW"], r["policyTargetsNCMove"]
+    tree = gt[:, 27] == 0.0
+    assert tree.sum() > (~tree).sum() > 0
+    np.testing.assert_array_equal(gt[:, 60], 24.0)
+    assert np.all(val[tree] == 0)
+    for f in range(1, 5):
+        np.testing.assert_array_equal(gt[tree, 2 * f], gt[tree, 0])
+    np.testing.assert_array_equal(pol[tree, 1], 1)
+    # a recorded node has children (>= threshold visits along the path): scaled to >= 10
+    assert np.all(pol[tree, 0].max(axis=1) >= 10)
+    # positions lie 1..5 moves past a searched turn
+    assert np.all(gt[tree, 51] >= 1)
+    # weight 0.5 resolves to 0 or 1 copies
+    half = oracle.Selfplay(5, 5, 4, record_tree_positions=1, record_tree_threshold=2, record_tree_target_weight=0.5,
+                           **base)
+    half.rounds(1500)
+    n_half = int((half.rows()["globalTargetsNC"][:, 27] == 0.0).sum())
+    assert 0 < n_half < tree.sum()
