@@ -118,37 +118,142 @@ struct DRng {
 
 KC_D int laneId() { return (int)(threadIdx.x & 63); }
 
+// Cross-lane exchanges of the xor butterfly without the LDS: lanes i and i^32 /
+// i^16 via v_permlane32_swap / v_permlane16_swap (both results of the swap hold
+// the two partners' values), i^8 / i^4 via DPP row_ror:8 / row_ror:4 (after the
+// wider levels a partial depends only on lane mod 16 / mod 8, so rotating a row
+// by 8 / 4 reaches the xor partner's value), i^2 / i^1 via DPP quad_perm.  Every
+// combine below is commutative, so each level pairs exactly the butterfly's
+// partials: the results are bit-identical to the shuffle butterfly (treeSum64).
+KC_D int bitsF(float x) { return __builtin_bit_cast(int, x); }
+KC_D float asF(int x) { return __builtin_bit_cast(float, x); }
+template <int CTRL>
+KC_D int dppMov(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+constexpr int DPP_ROR8 = 0x128, DPP_ROR4 = 0x124, DPP_X2 = 0x4e, DPP_X1 = 0xb1;
+// The partner value at butterfly level LVL (0: i^32, 1: i^16, 2: i^8, 3: i^4, 4: i^2,
+// 5: i^1) for the DPP levels; the permlane levels go through swapPair.
+template <int LVL>
+KC_D int partner(int x) {
+  static_assert(LVL >= 2 && LVL <= 5, "DPP levels");
+  if constexpr(LVL == 2)
+    return dppMov<DPP_ROR8>(x);
+  else if constexpr(LVL == 3)
+    return dppMov<DPP_ROR4>(x);
+  else if constexpr(LVL == 4)
+    return dppMov<DPP_X2>(x);
+  else
+    return dppMov<DPP_X1>(x);
+}
+// {own-half value, partner-half value} for levels 0/1 (order differs by half; the
+// combines are commutative).
+template <int LVL>
+KC_D void swapPair(int x, int& a, int& b) {
+  if constexpr(LVL == 0) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    a = r[0];
+    b = r[1];
+  } else {
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    a = r[0];
+    b = r[1];
+  }
+}
+
 // treeSum64 (oracle/ora_math.h): the lane's in-order partial, then xor butterfly.
 KC_D float waveSum(float s) {
-#pragma unroll
-  for(int off = 32; off >= 1; off >>= 1)
-    s = s + __shfl_xor(s, off, 64);
+  int a, b;
+  swapPair<0>(bitsF(s), a, b);
+  s = asF(a) + asF(b);
+  swapPair<1>(bitsF(s), a, b);
+  s = asF(a) + asF(b);
+  s = s + asF(partner<2>(bitsF(s)));
+  s = s + asF(partner<3>(bitsF(s)));
+  s = s + asF(partner<4>(bitsF(s)));
+  s = s + asF(partner<5>(bitsF(s)));
   return s;
 }
 KC_D float waveMax(float s) {
-#pragma unroll
-  for(int off = 32; off >= 1; off >>= 1)
-    s = fmaxf(s, __shfl_xor(s, off, 64));
+  int a, b;
+  swapPair<0>(bitsF(s), a, b);
+  s = fmaxf(asF(a), asF(b));
+  swapPair<1>(bitsF(s), a, b);
+  s = fmaxf(asF(a), asF(b));
+  s = fmaxf(s, asF(partner<2>(bitsF(s))));
+  s = fmaxf(s, asF(partner<3>(bitsF(s))));
+  s = fmaxf(s, asF(partner<4>(bitsF(s))));
+  s = fmaxf(s, asF(partner<5>(bitsF(s))));
   return s;
 }
 KC_D int waveMinI(int s) {
-#pragma unroll
-  for(int off = 32; off >= 1; off >>= 1)
-    s = min(s, __shfl_xor(s, off, 64));
+  int a, b;
+  swapPair<0>(s, a, b);
+  s = min(a, b);
+  swapPair<1>(s, a, b);
+  s = min(a, b);
+  s = min(s, partner<2>(s));
+  s = min(s, partner<3>(s));
+  s = min(s, partner<4>(s));
+  s = min(s, partner<5>(s));
   return s;
 }
 // argmax with "first strictly greater wins" semantics (lowest index on ties).
-KC_D void waveArgmax(float& v, int& idx) {
-#pragma unroll
-  for(int off = 32; off >= 1; off >>= 1) {
-    float ov = __shfl_xor(v, off, 64);
-    int oi = __shfl_xor(idx, off, 64);
-    if(ov > v || (ov == v && oi < idx)) {
-      v = ov;
-      idx = oi;
-    }
+KC_D void argmaxCombine(float& v, int& idx, float ov, int oi) {
+  if(ov > v || (ov == v && oi < idx)) {
+    v = ov;
+    idx = oi;
   }
 }
+template <int LVL>
+KC_D void argmaxSwapLevel(float& v, int& idx) {
+  int va, vb, ia, ib;
+  swapPair<LVL>(bitsF(v), va, vb);
+  swapPair<LVL>(idx, ia, ib);
+  v = asF(va);
+  idx = ia;
+  argmaxCombine(v, idx, asF(vb), ib);
+}
+template <int LVL>
+KC_D void argmaxDppLevel(float& v, int& idx) {
+  const float ov = asF(partner<LVL>(bitsF(v)));
+  const int oi = partner<LVL>(idx);
+  argmaxCombine(v, idx, ov, oi);
+}
+KC_D void waveArgmax(float& v, int& idx) {
+  argmaxSwapLevel<0>(v, idx);
+  argmaxSwapLevel<1>(v, idx);
+  argmaxDppLevel<2>(v, idx);
+  argmaxDppLevel<3>(v, idx);
+  argmaxDppLevel<4>(v, idx);
+  argmaxDppLevel<5>(v, idx);
+}
+// XOR of every lane's value (order-free), in every lane.
+KC_D uint64_t waveXor64(uint64_t h) {
+  int lo = (int)(uint32_t)h, hi = (int)(uint32_t)(h >> 32), a, b;
+  swapPair<0>(lo, a, b);
+  lo = a ^ b;
+  swapPair<0>(hi, a, b);
+  hi = a ^ b;
+  swapPair<1>(lo, a, b);
+  lo = a ^ b;
+  swapPair<1>(hi, a, b);
+  hi = a ^ b;
+  lo ^= partner<2>(lo);
+  hi ^= partner<2>(hi);
+  lo ^= partner<3>(lo);
+  hi ^= partner<3>(hi);
+  lo ^= partner<4>(lo);
+  hi ^= partner<4>(hi);
+  lo ^= partner<5>(lo);
+  hi ^= partner<5>(hi);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+// v of lane srcLane (uniform) in every lane, through a scalar register.
+KC_D int bcastLane(int v, int srcLane) {
+  return __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(srcLane));
+}
+KC_D float bcastLaneF(float v, int srcLane) { return asF(bcastLane(bitsF(v), srcLane)); }
 KC_D uint64_t ballot(bool b) { return __ballot(b); }
 
 }  // namespace kc

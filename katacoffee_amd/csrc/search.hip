@@ -183,7 +183,7 @@ KC_D float tsum(const float (&x)[NI], int n, int lane) {
   return waveSum(a);
 }
 
-KC_D int bcastI(int v, int srcLane) { return __shfl(v, srcLane, 64); }
+KC_D int bcastI(int v, int srcLane) { return bcastLane(v, srcLane); }
 
 // Child slots read speculatively with their node record (2 x 128-B lines of Edge).
 constexpr int SPEC_EDGES = 16;
@@ -195,56 +195,56 @@ KC_D float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeigh
 
 // ---------------------------------------------------------------------------
 // Transposition table (oracle ttFind / ttInsert): linear probing, 64 slots per step.
-KC_D int ttFind(const GV& v, uint64_t k0, uint64_t k1) {
+// The node of key (k0, k1) or -1; on a miss emptySlot is where ttInsert would put it
+// (the first free slot of the probe sequence; the table is not changed in between).
+// A window's slot and key loads are issued together.
+KC_D int ttFind(const GV& v, uint64_t k0, uint64_t k1, int& emptySlot) {
   const int mask = v.d.ttCap - 1;
   const int start = (int)(k0 & (uint64_t)mask);
   const uint64_t* key = v.ttKey();
   const int32_t* node = v.ttNode();
+  emptySlot = -1;
   for(int base = 0; base < v.d.ttCap; base += 64) {
     int s = (start + base + v.lane) & mask;
-    int nd = node[s];
-    bool match = nd >= 0 && key[2 * s] == k0 && key[2 * s + 1] == k1;
+    const int nd = node[s];
+    const uint64_t ka = key[2 * s], kb = key[2 * s + 1];
+    bool match = nd >= 0 && ka == k0 && kb == k1;
     uint64_t m = ballot(nd < 0 || match);
     if(m) {
       int f = firstLane(m);
+      emptySlot = bcastI(s, f);
       return bcastI(match ? nd : -1, f);
     }
   }
   return -1;
 }
 
-KC_D void ttInsert(const GV& v, uint64_t k0, uint64_t k1, int nodeIdx) {
-  const int mask = v.d.ttCap - 1;
-  const int start = (int)(k0 & (uint64_t)mask);
-  uint64_t* key = v.ttKey();
-  int32_t* node = v.ttNode();
-  for(int base = 0; base < v.d.ttCap; base += 64) {
-    int s = (start + base + v.lane) & mask;
-    uint64_t m = ballot(node[s] < 0);
-    if(m) {
-      if(v.lane == firstLane(m)) {
-        key[2 * s] = k0;
-        key[2 * s + 1] = k1;
-        node[s] = nodeIdx;
-      }
-      return;
-    }
+KC_D void ttInsertAt(const GV& v, int slot, uint64_t k0, uint64_t k1, int nodeIdx) {
+  if(slot >= 0 && v.lane == 0) {
+    v.ttKey()[2 * slot] = k0;
+    v.ttKey()[2 * slot + 1] = k1;
+    v.ttNode()[slot] = nodeIdx;
   }
 }
 
-// SVB table (oracle svbFindOrInsert), key 0 = empty.
-KC_D int svbFindOrInsert(const GV& v, int sel, uint64_t k) {
+// SVB table (oracle svbFindOrInsert), key 0 = empty.  first: this lane's key of the
+// first probe window, loaded ahead by svbProbe (its latency overlaps other work).
+KC_D uint64_t svbProbe(const GV& v, int sel, uint64_t k) {
+  const int mask = v.d.svbCap - 1;
+  return v.d.svbKey[v.svbBase(sel) + (((int)(k & (uint64_t)mask) + v.lane) & mask)];
+}
+KC_D int svbFindOrInsert(const GV& v, int sel, uint64_t k, uint64_t first) {
   const int mask = v.d.svbCap - 1;
   const size_t b = v.svbBase(sel);
   const int start = (int)(k & (uint64_t)mask);
   for(int base = 0; base < v.d.svbCap; base += 64) {
     int s = (start + base + v.lane) & mask;
-    uint64_t kk = v.d.svbKey[b + s];
+    uint64_t kk = base == 0 ? first : v.d.svbKey[b + s];
     uint64_t m = ballot(kk == 0 || kk == k);
     if(m) {
       int f = firstLane(m);
       int slot = bcastI(s, f);
-      bool empty = __shfl((int)(kk == 0), f, 64) != 0;
+      bool empty = bcastLane((int)(kk == 0), f) != 0;
       if(empty && v.lane == f) {
         v.d.svbKey[b + slot] = k;
         v.d.svbD[b + slot] = 0;
@@ -267,22 +267,19 @@ KC_D uint64_t svbKeyOf(const GV& v, const DBoard& before, int parentPrevPos, int
     int col = (xx >= 0 && xx < T.X && yy >= 0 && yy < T.Y) ? colorAt(before, yy * T.X + xx) : 3;
     h = T.svbZ[SVB_IDX_PAT + col * 25 + wy * 5 + wx];
   }
-#pragma unroll
-  for(int off = 32; off >= 1; off >>= 1) {
-    uint32_t lo = __shfl_xor((uint32_t)h, off, 64), hi = __shfl_xor((uint32_t)(h >> 32), off, 64);
-    h ^= ((uint64_t)hi << 32) | lo;
-  }
+  h = waveXor64(h);
   h ^= T.svbZ[parentPrevPos] ^ T.svbZ[SVB_IDX_MOVE1 + movePos] ^ T.svbZ[SVB_IDX_PLA + mover];
   return h != 0 ? h : 1;
 }
 
-KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k1, bool terminal) {
+// freeIdx: freeList[freeTop - 1] when the caller loaded it ahead, else -1.
+KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k1, bool terminal, int freeIdx = -1) {
   if(s.freeTop <= 0) {
     s.err = 1;
     return -1;
   }
   s.freeTop--;
-  int idx = (int)v.freeList()[s.freeTop];
+  int idx = freeIdx >= 0 ? freeIdx : (int)v.freeList()[s.freeTop];
   if(v.lane == 0) {
     Node n;
     n.visits = 0;
@@ -541,9 +538,11 @@ KC_D float exploreScaling(const SP& sp, float totalChildWeight) {
 }
 
 // oracle selectBest (selectBestChildToDescend searchexplorehelpers.cpp:304-451)
+// Also returns the chosen existing child's edge and the child's visits and flags,
+// broadcast from the lane that holds them (no reload of either after the choice).
 template <int NI>
 KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool isRoot, int& newPos,
-                    uint32_t* hasBits, const Edge& e0) {
+                    uint32_t* hasBits, const Edge& e0, Edge& ce, uint32_t& cVisits, uint32_t& cFlags) {
   const SP& sp = *v.sp;
   const int P = v.d.P;
   const int k = n.numChildren;
@@ -556,17 +555,21 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
   const Edge* E = v.edges(ni);
   const Node* NS = v.nodes();
   float probs[NI], cw[NI], pv[NI], cu[NI];
-  uint32_t cvis[NI];
+  uint32_t cvis[NI], cfl[NI];
+  Edge ev[NI];
 #pragma unroll
   for(int j = 0; j < NI; j++) {
     int i = v.lane + 64 * j;
     probs[j] = cw[j] = pv[j] = cu[j] = 0.0f;
-    cvis[j] = 0;
+    cvis[j] = cfl[j] = 0;
+    ev[j] = Edge{0u, 0u, 0.0f, 0u};
     if(i < k) {
       const Edge e = j == 0 && i < SPEC_EDGES ? e0 : E[i];
+      ev[j] = e;
       const Node& c = NS[e.child];
       float p = isRoot ? pol[e.move] : e.prior;
       cvis[j] = c.visits;
+      cfl[j] = c.flags;
       cu[j] = c.utilityAvg;
       pv[j] = p;
       probs[j] = p < 0.0f ? 0.0f : p;
@@ -605,6 +608,24 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
   }
   waveArgmax(best, bestIdx);
   int bestSlot = best > -__builtin_inff() ? bestIdx : -1;
+  if(bestSlot >= 0) {
+    Edge me{0u, 0u, 0.0f, 0u};
+    uint32_t mv = 0, mf = 0;
+#pragma unroll
+    for(int j = 0; j < NI; j++)
+      if(j == (bestSlot >> 6)) {
+        me = ev[j];
+        mv = cvis[j];
+        mf = cfl[j];
+      }
+    const int bl = bestSlot & 63;
+    ce.child = (uint32_t)bcastLane((int)me.child, bl);
+    ce.visits = (uint32_t)bcastLane((int)me.visits, bl);
+    ce.move = (uint32_t)bcastLane((int)me.move, bl);
+    ce.prior = 0.0f;
+    cVisits = (uint32_t)bcastLane((int)mv, bl);
+    cFlags = (uint32_t)bcastLane((int)mf, bl);
+  }
   float bp = -1.0f;
   int bpos = BIG;
   if(isRoot) {
@@ -643,19 +664,43 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
 // oracle descend (playoutDescend search.cpp:936-1165, allocateOrFindNode :704-759,
 // maybeCatchUpEdgeVisits :1169-1207)
 template <int NI>
-KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
+KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* LDS [P] */) {
   const SP& sp = *v.sp;
   const DTables& T = v.T;
   s.pathLen = 0;
   DBoard b = s.root;
   int ni = s.rootIdx;
   uint32_t scanned = 0;  // children of the path nodes (tree-roofline accounting)
+  // the first SPEC_EDGES child slots (two cache lines) are read speculatively,
+  // together with the node record (slots past numChildren are ignored), saving
+  // a dependent round trip; wider speculation would touch cold lines.  Each
+  // level's loads are issued before anything waits on the previous level.
+  auto loadE0 = [&](int node) {
+    return v.lane < SPEC_EDGES && v.lane < v.d.P ? v.edges(node)[v.lane] : Edge{0u, 0u, 0.0f, 0u};
+  };
+  Edge e0 = loadE0(ni);
+  Node n = v.nodes()[ni];
+  // the node an expansion will take (one expansion ends a descent)
+  const int freeIdx = s.freeTop > 0 ? (int)v.freeList()[s.freeTop - 1] : -1;
+  {
+    // the root's noised policy into LDS: the root selection gathers it per child and
+    // scans it for the best unexpanded move
+    const float* rn = v.rootNoised();
+    float pr[NI];
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      const int p = v.lane + 64 * j;
+      pr[j] = p < v.d.P ? rn[p] : 0.0f;
+    }
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      const int p = v.lane + 64 * j;
+      if(p < v.d.P)
+        rootPol[p] = pr[j];
+    }
+    waveSync();
+  }
   while(true) {
-    // the first SPEC_EDGES child slots (two cache lines) are read speculatively,
-    // together with the node record (slots past numChildren are ignored), saving
-    // a dependent round trip; wider speculation would touch cold lines
-    const Edge e0 = v.lane < SPEC_EDGES && v.lane < v.d.P ? v.edges(ni)[v.lane] : Edge{0u, 0u, 0.0f, 0u};
-    const Node& n = v.nodes()[ni];
     if(n.flags & 2) {
       s.leafKind = LEAF_TERMINAL;
       s.leafNode = ni;
@@ -663,11 +708,13 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
       break;
     }
     const bool isRoot = ni == s.rootIdx;
-    const float* pol = isRoot ? v.rootNoised() : v.pol(ni);
+    const float* pol = isRoot ? rootPol : v.pol(ni);
     int newPos = -1;
     scanned += n.numChildren;
     const unsigned long long tSel = SPROF_NOW();
-    int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits, e0);
+    Edge ce{0u, 0u, 0.0f, 0u};
+    uint32_t cVisits = 0, cFlags = 0;
+    int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits, e0, ce, cVisits, cFlags);
     SPROF_ADD(5, SPROF_NOW() - tSel);
     (void)tSel;
     if(slot < 0) {
@@ -687,28 +734,32 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
       // SVB key of the expansion (needs the board before the move); computed
       // up front so no second board copy stays live across playMoveWave.
       const bool svbKeyed = sp.svbFactor != 0.0f && hCell(b, 0) >= 0;
-      uint64_t svbKey = 0;
-      if(svbKeyed)
+      uint64_t svbKey = 0, svbFirst = 0;
+      if(svbKeyed) {
         svbKey = svbKeyOf(v, b, hDir(b, 0) * T.A + hCell(b, 0), newPos, b.pla);
+        svbFirst = svbProbe(v, s.svbSel, svbKey);
+      }
       playMoveWave(T, b, cell, dir);
       uint64_t k0, k1;
       stateHash(T, b, k0, k1);
-      int child = sp.useGraph ? ttFind(v, k0, k1) : -1;
-      if(child < 0) {
-        child = allocNode(v, s, b.pla, k0, k1, b.finished != 0);
+      int ttSlot = -1;
+      int child = sp.useGraph ? ttFind(v, k0, k1, ttSlot) : -1;
+      const bool fresh = child < 0;
+      if(fresh) {
+        child = allocNode(v, s, b.pla, k0, k1, b.finished != 0, freeIdx);
         if(child < 0) {
           s.leafKind = LEAF_NOCHILD;
           s.leafNode = ni;
           break;
         }
         if(svbKeyed) {
-          int e = svbFindOrInsert(v, s.svbSel, svbKey);
+          int e = svbFindOrInsert(v, s.svbSel, svbKey, svbFirst);
           waveSync();
           if(v.lane == 0)
             v.nodes()[child].svbEntry = e;
         }
         if(sp.useGraph)
-          ttInsert(v, k0, k1, child);
+          ttInsertAt(v, ttSlot, k0, k1, child);
       }
       waveSync();
       if(v.lane == 0) {
@@ -724,37 +775,41 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits) {
       s.pathLen++;
       waveSync();
       SPROF_ADD(6, SPROF_NOW() - tExp);
-      const Node& c = v.nodes()[child];
-      if(c.visits > 0) {
+      // a fresh node has no visits and the terminal flag of b; a transposition's
+      // record is read
+      const uint32_t cv = fresh ? 0u : v.nodes()[child].visits;
+      const uint32_t cf = fresh ? (b.finished ? 2u : 0u) : (uint32_t)v.nodes()[child].flags;
+      if(cv > 0) {
         s.leafKind = LEAF_CATCHUP;
         s.leafNode = child;
         break;
       }
       s.leafNode = child;
       s.leaf = b;
-      s.leafKind = (c.flags & 2) ? LEAF_TERMINAL : LEAF_NN;
+      s.leafKind = (cf & 2) ? LEAF_TERMINAL : LEAF_NN;
       break;
     }
-    const Edge e = v.edges(ni)[slot];
-    const int child = (int)e.child;
+    const int child = (int)ce.child;
     if(v.lane == 0) {
       v.pathNode()[s.pathLen] = ni;
       v.pathSlot()[s.pathLen] = slot;
     }
     s.pathLen++;
-    if(e.visits < v.nodes()[child].visits) {
+    if(ce.visits < cVisits) {
       s.leafKind = LEAF_CATCHUP;
       s.leafNode = child;
       break;
     }
     // existing child: its terminal flag already says whether the move ends the game
-    const int mv = (int)e.move, mover = b.pla;
+    const int mv = (int)ce.move, mover = b.pla;
     applyMove(T, b, mv % T.A, mv / T.A);
-    if(v.nodes()[child].flags & 2) {
+    if(cFlags & 2) {
       b.finished = 1;
       b.winner = maxRun(T, b, mv % T.A) >= T.W ? mover : 0;
     }
     ni = child;
+    e0 = loadE0(ni);
+    n = v.nodes()[ni];
   }
   s.treeLevels += (uint64_t)s.pathLen;
   s.treeChildren += scanned;
@@ -829,7 +884,8 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     s.leafSym = (int)((s.syms >> (4 * s.rootK)) & 15u);
     s.leaf = s.root;
   } else {
-    descend<NI>(v, s, hasBits);
+    __shared__ float rootPol[MAX_P];
+    descend<NI>(v, s, hasBits, rootPol);
     if(s.leafKind == LEAF_NN && d.cacheOn) {
       // NN evaluation cache (SPEC a7): a state evaluated in an earlier round by any
       // game is taken from the cache instead of the network
@@ -967,7 +1023,7 @@ KC_D float seqSum(float* lds, int n, int lane) {
   if(lane == 0)
     for(int i = 0; i < n; i++)
       acc = acc + lds[i];
-  return __shfl(acc, 0, 64);
+  return bcastLaneF(acc, 0);
 }
 
 // oracle noiseAndTemp (maybeAddPolicyNoiseAndTemp searchhelpers.cpp:122-222)
@@ -1339,8 +1395,8 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
     // the path in registers (lane j holds level j; levels >= 64 re-read), one load
     const int myNode = v.lane < s.pathLen ? pn[v.lane] : 0, mySlot = v.lane < s.pathLen ? ps[v.lane] : 0;
     for(int j = s.pathLen - 1; j >= 0; j--) {
-      const int node = j < 64 ? __shfl(myNode, j, 64) : pn[j];
-      const int slot = j < 64 ? __shfl(mySlot, j, 64) : ps[j];
+      const int node = j < 64 ? bcastLane(myNode, j) : pn[j];
+      const int slot = j < 64 ? bcastLane(mySlot, j) : ps[j];
       waveSync();
       recompute<NI>(v, s, node, slot, 1, node == s.rootIdx);
     }
@@ -1493,7 +1549,7 @@ KC_D int playSelectionValuesAt(const GV& v, const SP& sp, const GameDev& s, int 
     for(int j = 0; j < NI; j++)
       if(j == bestJ)
         bw = cw[j];
-    bestWeight = __shfl(bw, bestLane, 64);
+    bestWeight = bcastLaneF(bw, bestLane);
   }
   if(isRoot && k > 0) {
     const float fpu = fpuValue(sp, n, pla, true, 1.0f);
@@ -1507,9 +1563,9 @@ KC_D int playSelectionValuesAt(const GV& v, const SP& sp, const GameDev& s, int 
         bu = cu[j];
         bvis = cvis[j];
       }
-    bp = __shfl(bp, bestLane, 64);
-    bu = __shfl(bu, bestLane, 64);
-    bvis = (uint32_t)__shfl((int)bvis, bestLane, 64);
+    bp = bcastLaneF(bp, bestLane);
+    bu = bcastLaneF(bu, bestLane);
+    bvis = (uint32_t)bcastLane((int)bvis, bestLane);
     const float bw = bestWeight;
     const float buu = (bvis == 0 || bw <= 0.0f) ? fpu : bu;
     const float bestValue = bp < 0.0f ? -__builtin_inff() : (scaling * bp) / (1.0f + bw) + (pla == 2 ? buu : -buu);
@@ -1568,7 +1624,7 @@ KC_D int playSelectionValuesAt(const GV& v, const SP& sp, const GameDev& s, int 
       for(int j = 0; j < NI; j++)
         if(j == (bestLcbIdx >> 6))
           adj = val[j];
-      adj = __shfl(adj, bestLcbIdx & 63, 64);
+      adj = bcastLaneF(adj, bestLcbIdx & 63);
       float lb = adj;
 #pragma unroll
       for(int j = 0; j < NI; j++) {
@@ -2240,7 +2296,7 @@ KC_D void emitSideRow(const GV& v, const GameDev& s, const TurnRec& rec, DRng& r
       r = ~0ull;
     }
   }
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)r, 0, 64), hi = (uint32_t)__shfl((int)(uint32_t)(r >> 32), 0, 64);
+  const uint32_t lo = (uint32_t)bcastLane((int)(uint32_t)r, 0), hi = (uint32_t)bcastLane((int)(uint32_t)(r >> 32), 0);
   r = ((unsigned long long)hi << 32) | lo;
   if(r == ~0ull)
     return;
@@ -2589,7 +2645,7 @@ KC_D void finishGameRecord(const GV& v, const GameDev& s, DRng& rng, float* scra
         atomicAdd(d.gDropped, 1ull);
       }
     }
-    gi = (unsigned long long)(uint32_t)__shfl((int)(uint32_t)gi, 0, 64);
+    gi = (unsigned long long)(uint32_t)bcastLane((int)(uint32_t)gi, 0);
     if(gi < (unsigned long long)d.gCap) {
       GameRec* gr = d.gRec + gi;
       if(v.lane == 0) {

@@ -448,7 +448,7 @@ void SelfplayEngine::setModel(const char* path) {
   // cached evaluations belong to the previous network (the reference builds a new
   // NNEvaluator, and with it a new cache, per model: cpp/command/selfplay.cpp:150-200)
   if(hd_.cacheOn)
-    KC_HIP(hipMemset(hd_.cKey, 0, sizeof(uint64_t) * 2 * ((size_t)hd_.cacheMask + 1)));
+    KC_HIP(hipMemsetAsync(hd_.cKey, 0, sizeof(uint64_t) * 2 * ((size_t)hd_.cacheMask + 1), stream_));
 }
 
 void SelfplayEngine::gameInfo(int slot, int64_t* info) {
@@ -468,9 +468,14 @@ int SelfplayEngine::gameTree(int slot, int maxNodes, uint32_t* nodes, uint32_t* 
     throw std::invalid_argument("slot/max_nodes out of range");
   sync();
   std::vector<void*> tmp;
-  uint32_t* dn = devAlloc<uint32_t>(tmp, (size_t)maxNodes * 24);
-  uint32_t* de = devAlloc<uint32_t>(tmp, (size_t)maxNodes * hd_.P * 3);
-  int32_t* dc = devAlloc<int32_t>(tmp, 1);
+  // zeroed on the engine stream: a null-stream hipMemset is not ordered before work
+  // on the non-blocking engine stream
+  uint32_t* dn = devAlloc<uint32_t>(tmp, (size_t)maxNodes * 24, false);
+  uint32_t* de = devAlloc<uint32_t>(tmp, (size_t)maxNodes * hd_.P * 3, false);
+  int32_t* dc = devAlloc<int32_t>(tmp, 1, false);
+  KC_HIP(hipMemsetAsync(dn, 0, (size_t)maxNodes * 24 * 4, stream_));
+  KC_HIP(hipMemsetAsync(de, 0, (size_t)maxNodes * hd_.P * 3 * 4, stream_));
+  KC_HIP(hipMemsetAsync(dc, 0, 4, stream_));
   launchGameTree(dd_, slot, maxNodes, dn, de, dc, stream_);
   KC_HIP(hipStreamSynchronize(stream_));
   int n = 0;

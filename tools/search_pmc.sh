@@ -6,7 +6,7 @@ mkdir -p gpurun_out/spmc
 i=0
 for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" "SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set -d gpurun_out/spmc/p$i -o p --output-format csv -- python bench.py --steps 2 --warmup 1 --rounds-per-step 50 --cpu-seconds 0 > gpurun_out/spmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/spmc/p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $set -d gpurun_out/spmc/p$i -o p --output-format csv -- python bench.py --steps 2 --warmup 1 --rounds-per-step 50 --no-cpu-baseline --no-npz > gpurun_out/spmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/spmc/p$i.log; exit 1; }
 done
 python - <<'PY'
 import csv, glob, collections
