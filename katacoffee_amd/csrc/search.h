@@ -203,75 +203,100 @@ struct GameDev {
   float accWin, accLoss, rawWin, rawLoss;
 };
 
+// Device array pointer of SearchDev: on the device every access goes through a
+// global-address-space pointer, so the compiler emits global_load/store (ordered,
+// vmcnt-only waits) instead of flat accesses, which it must assume may hit LDS and
+// drain with vmcnt(0) lgkmcnt(0).  Same layout as a raw pointer.
+// (The empty asm keeps the generic->global->generic cast pair from being folded
+// away, so address-space inference sees a global pointer.)
+template <class T>
+KC_HD T* asGlobal(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __attribute__((address_space(1))) T* q = (__attribute__((address_space(1))) T*)p;
+  asm volatile("" : "+s"(q));
+  return (T*)q;
+#else
+  return p;
+#endif
+}
+template <class T>
+struct DPtr {
+  T* p;
+  DPtr() = default;
+  KC_HD DPtr(T* q) : p(q) {}
+  KC_HD operator T*() const { return asGlobal(p); }
+  KC_HD T* operator->() const { return asGlobal(p); }
+};
+
 struct SearchDev {
-  const DTables* T;
+  DPtr<const DTables> T;
   SP sp;
   SP spCheap;            // cheapSearchSP(sp): parameters of games with noNoise set
   int G, cap, ttCap, svbCap, P, A, inWords, maxTurns;
   int rowCap, slotBase;
   int startStagger;      // first games start after a per-slot delay in [0, startStagger) rounds
-  int32_t* modelGen;     // network generation: hot reloads so far (coffee_selfplay_set_model)
+  DPtr<int32_t> modelGen;     // network generation: hot reloads so far (coffee_selfplay_set_model)
   uint64_t seed;
-  GameDev* games;
-  Node* nodes;
-  Edge* edges;
-  OrderEnt* order;
-  uint64_t* nodeKey;     // [G][cap][2] transposition key of each node (TT rebuild after reuse)
-  float* policy;
-  uint32_t* freeList;
-  uint32_t* allocBits;
-  uint64_t* ttKey;
-  int32_t* ttNode;
-  uint64_t* svbKey;
-  int64_t* svbD;
-  int64_t* svbW;
-  float* accPolicy;
-  float* rawPolicy;
-  float* rootNoised;
-  int32_t* pathNode;
-  int32_t* pathSlot;
-  TurnRec* turns;
-  int16_t* turnPol;
+  DPtr<GameDev> games;
+  DPtr<Node> nodes;
+  DPtr<Edge> edges;
+  DPtr<OrderEnt> order;
+  DPtr<uint64_t> nodeKey;     // [G][cap][2] transposition key of each node (TT rebuild after reuse)
+  DPtr<float> policy;
+  DPtr<uint32_t> freeList;
+  DPtr<uint32_t> allocBits;
+  DPtr<uint64_t> ttKey;
+  DPtr<int32_t> ttNode;
+  DPtr<uint64_t> svbKey;
+  DPtr<int64_t> svbD;
+  DPtr<int64_t> svbW;
+  DPtr<float> accPolicy;
+  DPtr<float> rawPolicy;
+  DPtr<float> rootNoised;
+  DPtr<int32_t> pathNode;
+  DPtr<int32_t> pathSlot;
+  DPtr<TurnRec> turns;
+  DPtr<int16_t> turnPol;
   // network batch
-  uint64_t* nnIn;        // [G][inWords]
-  float* nnOut;          // [G][P+4]
-  int32_t* nnNeed;       // [G] 1 when the game's row needs the network this round
-  int32_t* nnIdx;        // [G] compacted rows to evaluate (kCompact)
-  int32_t* nnCount;      // rows in nnIdx
-  int32_t* nnDefer;      // [G] 1: the row did not fit this round's batch (kCompact); the game waits
+  DPtr<uint64_t> nnIn;        // [G][inWords]
+  DPtr<float> nnOut;          // [G][P+4]
+  DPtr<int32_t> nnNeed;       // [G] 1 when the game's row needs the network this round
+  DPtr<int32_t> nnIdx;        // [G] compacted rows to evaluate (kCompact)
+  DPtr<int32_t> nnCount;      // rows in nnIdx
+  DPtr<int32_t> nnDefer;      // [G] 1: the row did not fit this round's batch (kCompact); the game waits
   int nnCap;             // rows per network launch (batch cap: one full wave of network workgroups)
-  int32_t* nnRR;         // round-robin start of the next batch (kCompact)
-  unsigned long long* nnTimedEvals;  // summed nnCount of the rounds whose network launch was timed
+  DPtr<int32_t> nnRR;         // round-robin start of the next batch (kCompact)
+  DPtr<unsigned long long> nnTimedEvals;  // summed nnCount of the rounds whose network launch was timed
   // NN evaluation cache (SPEC a7): direct-mapped by state key, written between rounds
   uint32_t cacheMask;    // entries - 1 (0 with cacheOn == 0)
   int32_t cacheOn;
-  uint64_t* cKey;        // [entries][2]
-  float* cPol;           // [entries][P] post-processed policy (illegal = -1)
-  float* cVal;           // [entries][2] white win / loss
-  uint32_t* cTag;        // [entries] this round's highest bidding game + 1 (0 = none)
-  float* cStage;         // [G][P+2] a bidding game's payload
-  uint64_t* cStageKey;   // [G][2]
+  DPtr<uint64_t> cKey;        // [entries][2]
+  DPtr<float> cPol;           // [entries][P] post-processed policy (illegal = -1)
+  DPtr<float> cVal;           // [entries][2] white win / loss
+  DPtr<uint32_t> cTag;        // [entries] this round's highest bidding game + 1 (0 = none)
+  DPtr<float> cStage;         // [G][P+2] a bidding game's payload
+  DPtr<uint64_t> cStageKey;   // [G][2]
   // commit queue
-  FinRec* fin;           // [G] games finished by the current commit (kRows)
-  ForkRec* fork;         // [G] fork state (PH_FORK)
-  DBoard* side;          // [G][MAX_SIDE] queued side positions
-  int16_t* sidePol;      // [G][P] the policy target of the side position being written
-  int32_t* commitList;   // [G]
-  int32_t* commitCount;
+  DPtr<FinRec> fin;           // [G] games finished by the current commit (kRows)
+  DPtr<ForkRec> fork;         // [G] fork state (PH_FORK)
+  DPtr<DBoard> side;          // [G][MAX_SIDE] queued side positions
+  DPtr<int16_t> sidePol;      // [G][P] the policy target of the side position being written
+  DPtr<int32_t> commitList;   // [G]
+  DPtr<int32_t> commitCount;
   // rows
-  uint8_t* rBin;         // [rowCap][15][pb]
-  float* rGlob;          // [rowCap]
-  int16_t* rPol;         // [rowCap][2][P]
-  float* rGt;            // [rowCap][64]
-  int8_t* rVal;          // [rowCap][5][A]
-  int32_t* rMeta;        // [rowCap][4]
-  unsigned long long* rCount;
-  unsigned long long* rDropped;
+  DPtr<uint8_t> rBin;         // [rowCap][15][pb]
+  DPtr<float> rGlob;          // [rowCap]
+  DPtr<int16_t> rPol;         // [rowCap][2][P]
+  DPtr<float> rGt;            // [rowCap][64]
+  DPtr<int8_t> rVal;          // [rowCap][5][A]
+  DPtr<int32_t> rMeta;        // [rowCap][4]
+  DPtr<unsigned long long> rCount;
+  DPtr<unsigned long long> rDropped;
   // finished-game records (drained by the host for SGF files)
   int gCap;
-  GameRec* gRec;               // [gCap]
-  unsigned long long* gCount;
-  unsigned long long* gDropped;
+  DPtr<GameRec> gRec;               // [gCap]
+  DPtr<unsigned long long> gCount;
+  DPtr<unsigned long long> gDropped;
 };
 
 // Kernel launchers (search.hip).

@@ -303,8 +303,14 @@ KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k
 }
 
 // ---------------------------------------------------------------------------
-// oracle addLeafValue (searchupdatehelpers.cpp:12-82)
-KC_D void addLeafValue(const GV& v, const GameDev& s, int ni, float wl, bool isTerminal, bool assumeNoExisting) {
+// A node's statistics after an update (what its parent's recompute reads).
+struct NStats {
+  uint32_t visits;
+  float weightSum, weightSqSum, utilityAvg, utilitySqAvg, winLossAvg;
+};
+
+// oracle addLeafValue (searchupdatehelpers.cpp:12-82); returns the new statistics.
+KC_D NStats addLeafValue(const GV& v, const GameDev& s, int ni, float wl, bool isTerminal, bool assumeNoExisting) {
   const SP& sp = *v.sp;
   Node* np = &v.nodes()[ni];
   const int svbEntry = np->svbEntry;
@@ -345,6 +351,7 @@ KC_D void addLeafValue(const GV& v, const GameDev& s, int ni, float wl, bool isT
     np->winLossAvg = winLossAvg;
   }
   waveSync();
+  return NStats{visits, weightSum, weightSqSum, utilityAvg, utilitySqAvg, winLossAvg};
 }
 
 KC_D float cdfT(const DTables& T, float z) {
@@ -360,28 +367,103 @@ KC_D float cdfT(const DTables& T, float z) {
 }
 
 // oracle recompute (recomputeNodeStats searchupdatehelpers.cpp:151-328 +
-// downweightBadChildrenAndNormalizeWeight :330-419), after the path edge `slot` gained
-// a visit (the oracle's EV(pn, slot) += 1): the lane holding that edge adds it and
-// stores it back, so the increment rides on the edge load instead of costing a
-// dependent round trip of its own.  The node's SVB sums are loaded with the node.
+// downweightBadChildrenAndNormalizeWeight :330-419) for one path level, after the path
+// edge `slot` gained a visit (the oracle's EV(pn, slot) += 1).  Split in three so the
+// backup can run the levels as a pipeline: loadLevel (the node record and its first 64
+// edges), loadKids (child records, remaining edges, the node's SVB sums), computeLevel
+// (arithmetic and stores).  A level's loads are issued while the level below it is
+// computed, so the path child's record and (when the two levels share an SVB entry)
+// the SVB sums can be stale: computeLevel takes both from the level below (`below`),
+// which is exactly what the sequential order would read.
 template <int NI>
-KC_D void recompute(const GV& v, const GameDev& s, int ni, int slot, int numVisitsToAdd, bool isRoot) {
+struct PathLevel {
+  int ni, slot, k, nextPla, svbEntry;
+  float nnWin, nnLoss, lastSvbDelta, lastSvbWeight;
+  uint32_t visits0;
+  uint32_t ech[NI], evis[NI];  // edge child and visits
+  uint32_t cv[NI];
+  float cws[NI], cwsq[NI], cu[NI], cusq[NI], cwl[NI];
+  int64_t svbD0, svbW0;
+};
+// What a computed level hands to the level above it.
+struct LevelOut {
+  NStats st;
+  int svbEntry;  // -1: the SVB sums were not written
+  int64_t svbD, svbW;
+};
+
+template <int NI>
+KC_D void loadLevel(const GV& v, int ni, int slot, PathLevel<NI>& L) {
+  const Node nd = v.nodes()[ni];
+  const Edge* E = v.edges(ni);
+  // the first SPEC_EDGES slots speculatively with the record (slots past numChildren
+  // are ignored); the rest once the record says how many there are
+  const Edge e0 = v.lane < SPEC_EDGES && v.lane < v.d.P ? E[v.lane] : Edge{0u, 0u, 0.0f, 0u};
+  L.ech[0] = e0.child;
+  L.evis[0] = e0.visits;
+  L.ni = ni;
+  L.slot = slot;
+  L.k = nd.numChildren;
+  L.nextPla = nd.nextPla;
+  L.svbEntry = nd.svbEntry;
+  L.nnWin = nd.nnWin;
+  L.nnLoss = nd.nnLoss;
+  L.lastSvbDelta = nd.lastSvbDelta;
+  L.lastSvbWeight = nd.lastSvbWeight;
+  L.visits0 = nd.visits;
+}
+
+template <int NI>
+KC_D void loadKids(const GV& v, const GameDev& s, PathLevel<NI>& L) {
   const SP& sp = *v.sp;
-  Node* np = &v.nodes()[ni];
-  const int k = np->numChildren;
-  const int nextPla = np->nextPla;
-  const int svbEntry = np->svbEntry;
-  const float nnWin = np->nnWin, nnLoss = np->nnLoss;
-  const float lastSvbDelta = np->lastSvbDelta, lastSvbWeight = np->lastSvbWeight;
-  const uint32_t visits0 = np->visits;
-  Edge* E = v.edges(ni);
+  const Edge* E = v.edges(L.ni);
   const Node* NS = v.nodes();
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    const int i = v.lane + 64 * j;
+    L.cv[j] = 0;
+    L.cws[j] = L.cwsq[j] = L.cu[j] = L.cusq[j] = L.cwl[j] = 0.0f;
+    if(j > 0 || i >= SPEC_EDGES)
+      L.ech[j] = L.evis[j] = 0u;
+    if(i < L.k) {
+      if(j > 0 || i >= SPEC_EDGES) {
+        const Edge e = E[i];
+        L.ech[j] = e.child;
+        L.evis[j] = e.visits;
+      }
+      const Node& c = NS[L.ech[j]];
+      L.cv[j] = c.visits;
+      L.cws[j] = c.weightSum;
+      L.cwsq[j] = c.weightSqSum;
+      L.cu[j] = c.utilityAvg;
+      L.cusq[j] = c.utilitySqAvg;
+      L.cwl[j] = c.winLossAvg;
+    }
+  }
+  // unconditional (entry 0 when the node has none; ignored then): no branch between
+  // the pipeline's loads and the waits on them
+  const size_t e = v.svbBase(s.svbSel) + (L.svbEntry >= 0 ? L.svbEntry : 0);
+  L.svbD0 = v.d.svbD[e];
+  L.svbW0 = v.d.svbW[e];
+  (void)sp;
+}
+
+// issueNext() issues the next levels' loads; it runs right after this level's t-CDF
+// table reads, the last loads the level waits on (vmcnt counts in issue order, so a
+// wait on a load also waits on every older one).
+template <int NI, class F>
+KC_D LevelOut computeLevel(const GV& v, const GameDev& s, PathLevel<NI>& L, const LevelOut& below, bool haveBelow,
+                           int numVisitsToAdd, bool isRoot, F&& issueNext) {
+  const SP& sp = *v.sp;
+  const int k = L.k, slot = L.slot;
+  const int nextPla = L.nextPla;
+  const int svbEntry = L.svbEntry;
+  Edge* E = v.edges(L.ni);
   const bool svbOn = sp.svbFactor != 0.0f && svbEntry >= 0;
-  const size_t svbE = v.svbBase(s.svbSel) + (svbOn ? svbEntry : 0);
-  int64_t svbD0 = 0, svbW0 = 0;
-  if(svbOn) {
-    svbD0 = v.d.svbD[svbE];
-    svbW0 = v.d.svbW[svbE];
+  int64_t svbD0 = L.svbD0, svbW0 = L.svbW0;
+  if(svbOn && haveBelow && below.svbEntry == svbEntry) {
+    svbD0 = below.svbD;
+    svbW0 = below.svbW;
   }
   bool good[NI];
   float wAdj[NI], selfU[NI], cU[NI], cUsq[NI], cWl[NI], cWs[NI], cWsq[NI], tmp[NI];
@@ -393,23 +475,30 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int slot, int numVisi
     good[j] = false;
     wAdj[j] = selfU[j] = cU[j] = cUsq[j] = cWl[j] = cWs[j] = cWsq[j] = 0.0f;
     if(i < k) {
-      Edge e = E[i];
+      uint32_t evis = L.evis[j];
+      uint32_t cv = L.cv[j];
+      float ws = L.cws[j], wsq = L.cwsq[j], u = L.cu[j], usq = L.cusq[j], wl = L.cwl[j];
       if(i == slot) {
-        e.visits += 1;
-        E[i].visits = e.visits;
+        evis += 1;
+        E[i].visits = evis;
+        if(haveBelow) {
+          cv = below.st.visits;
+          ws = below.st.weightSum;
+          wsq = below.st.weightSqSum;
+          u = below.st.utilityAvg;
+          usq = below.st.utilitySqAvg;
+          wl = below.st.winLossAvg;
+        }
       }
-      const Node& c = NS[e.child];
-      uint32_t cv = c.visits;
-      float ws = c.weightSum;
-      good[j] = cv > 0 && ws > 0.0f && e.visits > 0;
+      good[j] = cv > 0 && ws > 0.0f && evis > 0;
       if(good[j]) {
-        cU[j] = c.utilityAvg;
-        cUsq[j] = c.utilitySqAvg;
-        cWl[j] = c.winLossAvg;
+        cU[j] = u;
+        cUsq[j] = usq;
+        cWl[j] = wl;
         cWs[j] = ws;
-        cWsq[j] = c.weightSqSum;
+        cWsq[j] = wsq;
         selfU[j] = nextPla == 2 ? cU[j] : -cU[j];
-        wAdj[j] = childWeight(e.visits, cv, ws);
+        wAdj[j] = childWeight(evis, cv, ws);
         maxW = wAdj[j] > maxW ? wAdj[j] : maxW;
       }
     }
@@ -427,21 +516,56 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int slot, int numVisi
     float stdev[NI];
 #pragma unroll
     for(int j = 0; j < NI; j++) {
+      if(j > 0 && 64 * j >= k) {  // uniform: no lane has an item here
+        stdev[j] = tmp[j] = 0.0f;
+        continue;
+      }
       stdev[j] = good[j] ? sqrtf(1e-8f + 1.0f / (1.5f * sqrtf(wAdj[j]))) : 0.0f;
       tmp[j] = good[j] ? selfU[j] * wAdj[j] : 0.0f;
     }
     const float simpleValue = tsum<NI>(tmp, k, v.lane) / currentTotal;
+    // cdfT split: the table reads of every item first, then the next levels' loads,
+    // then the interpolation (same arithmetic)
+    float y0[NI], y1[NI], lam[NI], pc[NI];
+    int mode[NI];  // 0 skip, 1 table, 2 constant pc
 #pragma unroll
     for(int j = 0; j < NI; j++) {
-      if(!good[j] || wAdj[j] < amountToPrune) {
+      mode[j] = 0;
+      y0[j] = y1[j] = lam[j] = pc[j] = 0.0f;
+      if(j > 0 && 64 * j >= k)
+        continue;
+      if(!good[j] || wAdj[j] < amountToPrune)
+        continue;
+      float z = (selfU[j] - simpleValue) / stdev[j];
+      float dd = (1999.0f * (z - (-50.0f))) / 100.0f;
+      if(dd <= 0.0f) {
+        mode[j] = 2;
+        pc[j] = 0.0f;
+        continue;
+      }
+      int idx = (int)dd;
+      if(idx >= 1999) {
+        mode[j] = 2;
+        pc[j] = 1.0f;
+        continue;
+      }
+      mode[j] = 1;
+      lam[j] = dd - (float)idx;
+      y0[j] = v.T.cdf[idx];
+      y1[j] = v.T.cdf[idx + 1];
+    }
+    issueNext();
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      if((j > 0 && 64 * j >= k) || mode[j] == 0) {
         tmp[j] = 0.0f;
         continue;
       }
       float nw = wAdj[j] - amountToSubtract;
       if(nw <= 0.0f)
         nw = 0.0f;
-      float z = (selfU[j] - simpleValue) / stdev[j];
-      float p = cdfT(v.T, z) + 0.0001f;
+      const float c = mode[j] == 1 ? y0[j] + lam[j] * (y1[j] - y0[j]) : pc[j];
+      float p = c + 0.0001f;
       float f = sp.valueWeightExp == 0.5f ? sqrtf(p) : dpow(p, sp.valueWeightExp);
       tmp[j] = nw * f;
     }
@@ -450,11 +574,13 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int slot, int numVisi
 #pragma unroll
     for(int j = 0; j < NI; j++)
       wAdj[j] = tmp[j] * factor;
+  } else {
+    issueNext();
   }
   float wlv[NI], uv[NI], usqv[NI], wsqv[NI];
 #pragma unroll
   for(int j = 0; j < NI; j++) {
-    if(!good[j]) {
+    if((j > 0 && 64 * j >= k) || !good[j]) {
       wlv[j] = uv[j] = usqv[j] = wsqv[j] = 0.0f;
       continue;
     }
@@ -469,25 +595,31 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int slot, int numVisi
   float utilitySqSum = tsum<NI>(usqv, k, v.lane);
   float weightSqSum = tsum<NI>(wsqv, k, v.lane);
   float weightSum = currentTotal;
-  float wl = nnWin - nnLoss;
+  float wl = L.nnWin - L.nnLoss;
   float utility = wl;
-  float newLastD = lastSvbDelta, newLastW = lastSvbWeight;
+  float newLastD = L.lastSvbDelta, newLastW = L.lastSvbWeight;
+  LevelOut out;
+  out.svbEntry = -1;
+  out.svbD = out.svbW = 0;
   if(svbOn) {
-    const size_t e = svbE;
     int64_t D = svbD0, Wt = svbW0;
     if(currentTotal > 1e-10f) {
       float utilityChildren = utilitySum / currentTotal;
       float svbWv = dpow(origTotal, sp.svbExp);
       float svbDv = (utilityChildren - utility) * svbWv;
-      D += svbQ(svbDv) - svbQ(lastSvbDelta);
-      Wt += svbQ(svbWv) - svbQ(lastSvbWeight);
+      D += svbQ(svbDv) - svbQ(L.lastSvbDelta);
+      Wt += svbQ(svbWv) - svbQ(L.lastSvbWeight);
       waveSync();
       if(v.lane == 0) {
+        const size_t e = v.svbBase(s.svbSel) + svbEntry;
         v.d.svbD[e] = D;
         v.d.svbW[e] = Wt;
       }
       newLastD = svbDv;
       newLastW = svbWv;
+      out.svbEntry = svbEntry;
+      out.svbD = D;
+      out.svbW = Wt;
     }
     float dd = svbF(D), ww = svbF(Wt);
     if(ww > 0.001f)
@@ -498,18 +630,81 @@ KC_D void recompute(const GV& v, const GameDev& s, int ni, int slot, int numVisi
   utilitySqSum = utilitySqSum + utility * utility;
   weightSqSum = weightSqSum + 1.0f;
   weightSum = weightSum + 1.0f;
+  out.st.winLossAvg = winLossSum / weightSum;
+  out.st.utilityAvg = utilitySum / weightSum;
+  out.st.utilitySqAvg = utilitySqSum / weightSum;
+  out.st.weightSqSum = weightSqSum;
+  out.st.weightSum = weightSum;
+  out.st.visits = L.visits0 + (uint32_t)numVisitsToAdd;
   waveSync();
   if(v.lane == 0) {
-    np->winLossAvg = winLossSum / weightSum;
-    np->utilityAvg = utilitySum / weightSum;
-    np->utilitySqAvg = utilitySqSum / weightSum;
-    np->weightSqSum = weightSqSum;
-    np->weightSum = weightSum;
-    np->visits = visits0 + (uint32_t)numVisitsToAdd;
+    Node* np = &v.nodes()[L.ni];
+    np->winLossAvg = out.st.winLossAvg;
+    np->utilityAvg = out.st.utilityAvg;
+    np->utilitySqAvg = out.st.utilitySqAvg;
+    np->weightSqSum = out.st.weightSqSum;
+    np->weightSum = out.st.weightSum;
+    np->visits = out.st.visits;
     np->lastSvbDelta = newLastD;
     np->lastSvbWeight = newLastW;
   }
   waveSync();
+  return out;
+}
+
+// The path from the deepest level to the root.  The loads of level j-1 (record and
+// first edges, then child records) and the record of level j-2 are issued before
+// level j is computed; with more than two items per lane (register budget) the
+// levels run one at a time.
+template <int NI>
+KC_D void backupPath(const GV& v, const GameDev& s, int pathLen, NStats leaf, bool haveLeaf) {
+  const int32_t* pn = v.pathNode();
+  const int32_t* ps = v.pathSlot();
+  // the path in registers (lane j holds level j; levels >= 64 re-read), one load
+  const int myNode = v.lane < pathLen ? pn[v.lane] : 0, mySlot = v.lane < pathLen ? ps[v.lane] : 0;
+  auto nodeAt = [&](int j) { return j < 64 ? bcastLane(myNode, j) : pn[j]; };
+  auto slotAt = [&](int j) { return j < 64 ? bcastLane(mySlot, j) : ps[j]; };
+  if(pathLen <= 0)
+    return;
+  LevelOut below;
+  bool haveBelow = haveLeaf;
+  below.st = leaf;
+  below.svbEntry = -1;
+  below.svbD = below.svbW = 0;
+  int j = pathLen - 1;
+  if constexpr(NI > 2) {
+    // wide levels (7x7, 9x9): one level at a time
+    for(; j >= 0; j--) {
+      PathLevel<NI> cur;
+      loadLevel<NI>(v, nodeAt(j), slotAt(j), cur);
+      loadKids<NI>(v, s, cur);
+      below = computeLevel<NI>(v, s, cur, below, haveBelow, 1, cur.ni == s.rootIdx, [] {});
+      haveBelow = true;
+    }
+    return;
+  }
+  PathLevel<NI> cur, nxt;
+  loadLevel<NI>(v, nodeAt(j), slotAt(j), cur);
+  if(j > 0)
+    loadLevel<NI>(v, nodeAt(j - 1), slotAt(j - 1), nxt);
+  loadKids<NI>(v, s, cur);
+  for(; j >= 0; j--) {
+    PathLevel<NI> nn;
+    // the child records of the level above and the record two levels up, issued
+    // while this level is computed
+    auto issueNext = [&] {
+      if(j > 0)
+        loadKids<NI>(v, s, nxt);
+      if(j > 1)
+        loadLevel<NI>(v, nodeAt(j - 2), slotAt(j - 2), nn);
+    };
+    below = computeLevel<NI>(v, s, cur, below, haveBelow, 1, cur.ni == s.rootIdx, issueNext);
+    haveBelow = true;
+    if(j > 0) {
+      cur = nxt;
+      nxt = nn;
+    }
+  }
 }
 
 // oracle fpuValue (searchexplorehelpers.cpp:245-301)
@@ -563,6 +758,8 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
     probs[j] = cw[j] = pv[j] = cu[j] = 0.0f;
     cvis[j] = cfl[j] = 0;
     ev[j] = Edge{0u, 0u, 0.0f, 0u};
+    if(j > 0 && 64 * j >= k)  // uniform: no lane has an item here
+      continue;
     if(i < k) {
       const Edge e = j == 0 && i < SPEC_EDGES ? e0 : E[i];
       ev[j] = e;
@@ -587,7 +784,7 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
 #pragma unroll
   for(int j = 0; j < NI; j++) {
     int i = v.lane + 64 * j;
-    if(i >= k)
+    if((j > 0 && 64 * j >= k) || i >= k)
       continue;
     float p = pv[j];
     float val;
@@ -1107,30 +1304,38 @@ KC_D void noiseAndTemp(const GV& v, GameDev& s, DRng& rng, const float* raw, flo
 template <int NI>
 KC_D void buildOrder(const GV& v, int ni, const float (&pv)[NI], float* lds) {
   const int P = v.d.P;
+  // one 64-bit key per entry ordering "higher prior first, then lower position":
+  // the prior's bits in an order-preserving form above the complemented position
+  // (priors are >= +0 or exactly -1, so float order is the key order)
+  uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
+  auto keyOf = [](float x, int p) {
+    const uint32_t b = __builtin_bit_cast(uint32_t, x);
+    const uint32_t o = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    return ((uint64_t)o << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
+  };
+  uint64_t myKey[NI];
   waveSync();
 #pragma unroll
-  for(int j = 0; j < NI; j++)
-    if(v.lane + 64 * j < P)
-      lds[v.lane + 64 * j] = pv[j];
+  for(int j = 0; j < NI; j++) {
+    const int p = v.lane + 64 * j;
+    myKey[j] = keyOf(pv[j], p);
+    if(p < P)
+      keys[p] = myKey[j];
+  }
   waveSync();
   OrderEnt* ord = v.order(ni);
   int nLegal = 0;
-  // rank of each of the lane's entries = entries ordered before it; 4 per LDS read
-  // (P = 4A is a multiple of 4)
+  // rank of each of the lane's entries = entries ordered before it (larger keys)
   int rank[NI];
 #pragma unroll
   for(int j = 0; j < NI; j++)
     rank[j] = 0;
-  for(int q = 0; q < P; q += 4) {
-    const float4 y = *reinterpret_cast<const float4*>(lds + q);
+  for(int q = 0; q < P; q += 2) {
+    const uint64_t k0 = keys[q], k1 = keys[q + 1];
 #pragma unroll
     for(int j = 0; j < NI; j++) {
-      const float x = pv[j];
-      const int p = v.lane + 64 * j;
-      rank[j] += (y.x > x || (y.x == x && q < p)) ? 1 : 0;
-      rank[j] += (y.y > x || (y.y == x && q + 1 < p)) ? 1 : 0;
-      rank[j] += (y.z > x || (y.z == x && q + 2 < p)) ? 1 : 0;
-      rank[j] += (y.w > x || (y.w == x && q + 3 < p)) ? 1 : 0;
+      rank[j] += k0 > myKey[j] ? 1 : 0;
+      rank[j] += k1 > myKey[j] ? 1 : 0;
     }
   }
 #pragma unroll
@@ -1139,8 +1344,9 @@ KC_D void buildOrder(const GV& v, int ni, const float (&pv)[NI], float* lds) {
     if(p < P && pv[j] >= 0.0f)
       ord[rank[j]] = OrderEnt{pv[j], (uint32_t)p};
   }
-  for(int base = 0; base < P; base += 64)
-    nLegal += __builtin_popcountll(ballot(base + v.lane < P && lds[base + v.lane] >= 0.0f));
+#pragma unroll
+  for(int j = 0; j < NI; j++)
+    nLegal += __builtin_popcountll(ballot(v.lane + 64 * j < P && pv[j] >= 0.0f));
   for(int r = nLegal + v.lane; r < P; r += 64)
     ord[r] = OrderEnt{-1.0f, 0xFFFFu};
   waveSync();
@@ -1243,7 +1449,7 @@ KC_D bool initMove(const GV& v, GameDev& s, const float* o, float* scratch /* LD
 }
 
 template <int NI>
-__global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
+__global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
   if(g >= d.G || d.nnDefer[g])  // a deferred leaf is backed up in a later round
@@ -1324,6 +1530,8 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
       needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)s.visitLimit;
     }
   } else {
+    NStats leafSt{0u, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    bool haveLeaf = false;
     if(s.leafKind == LEAF_NN || s.leafKind == LEAF_CACHED) {
       float w, l;
       float* pol = v.pol(s.leafNode);
@@ -1378,28 +1586,23 @@ __global__ void __launch_bounds__(64) kBackup(const SearchDev* __restrict__ dp, 
       waveSync();
       const unsigned long long tb = SPROF_NOW();
       (void)tb;
-      addLeafValue(v, s, s.leafNode, w - l, false, true);
+      leafSt = addLeafValue(v, s, s.leafNode, w - l, false, true);
+      haveLeaf = true;
       tPost = tb - ta;
       tLeaf = SPROF_NOW() - tb;
     } else if(s.leafKind == LEAF_TERMINAL) {
       float val = s.leaf.winner == 2 ? 1.0f : (s.leaf.winner == 1 ? -1.0f : 0.0f);
-      addLeafValue(v, s, s.leafNode, val, true, false);
+      leafSt = addLeafValue(v, s, s.leafNode, val, true, false);
+      haveLeaf = true;
     } else if(s.leafKind == LEAF_NOCHILD) {
       const Node& n = v.nodes()[s.leafNode];
-      addLeafValue(v, s, s.leafNode, n.nnWin - n.nnLoss, false, false);
+      leafSt = addLeafValue(v, s, s.leafNode, n.nnWin - n.nnLoss, false, false);
+      haveLeaf = true;
     }
-    const int32_t* pn = v.pathNode();
-    const int32_t* ps = v.pathSlot();
     const unsigned long long tp0 = SPROF_NOW();
     (void)tp0;
-    // the path in registers (lane j holds level j; levels >= 64 re-read), one load
-    const int myNode = v.lane < s.pathLen ? pn[v.lane] : 0, mySlot = v.lane < s.pathLen ? ps[v.lane] : 0;
-    for(int j = s.pathLen - 1; j >= 0; j--) {
-      const int node = j < 64 ? bcastLane(myNode, j) : pn[j];
-      const int slot = j < 64 ? bcastLane(mySlot, j) : ps[j];
-      waveSync();
-      recompute<NI>(v, s, node, slot, 1, node == s.rootIdx);
-    }
+    // an updated leaf is the deepest level's path child (a catch-up leaf is unchanged)
+    backupPath<NI>(v, s, s.pathLen, leafSt, haveLeaf);
     tPath = SPROF_NOW() - tp0;
     s.playouts++;
     needCommit = v.nodes()[s.rootIdx].visits >= (uint32_t)s.visitLimit;
