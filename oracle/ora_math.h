@@ -76,19 +76,24 @@ inline float kPowf(float x, float y) {
     return y > 0.0f ? 0.0f : (y == 0.0f ? 1.0f : INFINITY);
   return kExpf(y * kLogf(x));
 }
+// double overloads (liboracle_f64: the reference's <cmath> in double)
+inline double kLogf(double x) { return std::log(x); }
+inline double kExpf(double x) { return std::exp(x); }
+inline double kPowf(double x, double y) { return std::pow(x, y); }
 
 // 64-lane xor butterfly: lane l first accumulates v[l], v[l+64], v[l+128], ...
 // in order (lanes with l >= n start from +0), then xor-butterfly 32,16,..,1.
-inline float treeSum64(const float* v, int n) {
-  float s[64];
+template <class T>
+inline T treeSum64(const T* v, int n) {
+  T s[64];
   for(int l = 0; l < 64; l++) {
-    float a = l < n ? v[l] : 0.0f;
+    T a = l < n ? v[l] : T(0);
     for(int j = l + 64; j < n; j += 64)
       a = a + v[j];
     s[l] = a;
   }
   for(int off = 32; off >= 1; off >>= 1) {
-    float t[64];
+    T t[64];
     for(int l = 0; l < 64; l++)
       t[l] = s[l] + s[l ^ off];
     memcpy(s, t, sizeof(s));

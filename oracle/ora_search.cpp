@@ -24,12 +24,22 @@
 
 namespace ora {
 
+// std::min / std::max over the search's arithmetic type (mixed float / real operands)
+template <class A, class B>
+inline real rmin(A a, B b) {
+  return std::min<real>((real)a, (real)b);
+}
+template <class A, class B>
+inline real rmax(A a, B b) {
+  return std::max<real>((real)a, (real)b);
+}
+
 static const int SVB_CAP = 4096;
 
 // SPEC B27: subtree-value-bias sums are kept in 64-bit fixed point (2^-32 units)
 // so that concurrent/unordered updates are exact and order independent.
-inline int64_t svbQ(float x) { return llrintf(x * 4294967296.0f); }
-inline float svbF(int64_t v) { return (float)v * (1.0f / 4294967296.0f); }
+inline int64_t svbQ(real x) { return std::llrint(x * 4294967296.0f); }
+inline real svbF(int64_t v) { return (real)v * (1.0f / 4294967296.0f); }
 static const uint64_t SVB_SEED = 0x5b5b5b5b5b5b5b5bULL;
 
 // ---------------------------------------------------------------------------
@@ -158,21 +168,21 @@ struct Ctx {
     return i;
   }
 
-  static float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeight) {
+  static real childWeight(uint32_t edgeVisits, uint32_t childVisits, real rawWeight) {
     // NodeStats::childWeight searchnode.h:59-61
-    return rawWeight * ((float)edgeVisits / (float)std::max(childVisits, 1u));
+    return rawWeight * ((real)edgeVisits / (real)std::max(childVisits, 1u));
   }
 
   // --- addLeafValue searchupdatehelpers.cpp:12-82 (weight 1, Coffee utility = winLoss) ---
-  void addLeafValue(int ni, float wl, bool isTerminal, bool assumeNoExisting) {
+  void addLeafValue(int ni, real wl, bool isTerminal, bool assumeNoExisting) {
     Node& n = N(ni);
-    float utility = wl;
+    real utility = wl;
     if(sp.subtreeValueBiasFactor != 0.0f && !isTerminal && n.svbEntry >= 0) {
-      float d = svbF(gm.svbDelta[n.svbEntry]), w = svbF(gm.svbWeight[n.svbEntry]);
+      real d = svbF(gm.svbDelta[n.svbEntry]), w = svbF(gm.svbWeight[n.svbEntry]);
       if(w > 0.001f)
         utility = utility + (sp.subtreeValueBiasFactor * d) / w;
     }
-    float usq = utility * utility;
+    real usq = utility * utility;
     if(assumeNoExisting) {
       n.winLossAvg = wl;
       n.utilityAvg = utility;
@@ -181,7 +191,7 @@ struct Ctx {
       n.weightSum = 1.0f;
       n.visits += 1;
     } else {
-      float oldW = n.weightSum, newW = oldW + 1.0f;
+      real oldW = n.weightSum, newW = oldW + 1.0f;
       n.winLossAvg = (n.winLossAvg * oldW + wl) / newW;
       n.utilityAvg = (n.utilityAvg * oldW + utility) / newW;
       n.utilitySqAvg = (n.utilitySqAvg * oldW + usq) / newW;
@@ -191,16 +201,16 @@ struct Ctx {
     }
   }
 
-  float cdf(float z) {
+  real cdf(real z) {
     // DistributionTable::getCdf distributiontable.h (size 2000, [-50,50])
-    float d = (1999.0f * (z - (-50.0f))) / 100.0f;
+    real d = (1999.0f * (z - (-50.0f))) / 100.0f;
     if(d <= 0.0f)
       return 0.0f;
     int idx = (int)d;
     if(idx >= 1999)
       return 1.0f;
-    float lambda = d - (float)idx;
-    float y0 = T.cdf[idx], y1 = T.cdf[idx + 1];
+    real lambda = d - (real)idx;
+    real y0 = T.cdf[idx], y1 = T.cdf[idx + 1];
     return y0 + lambda * (y1 - y0);
   }
 
@@ -208,10 +218,10 @@ struct Ctx {
   void recompute(int ni, int numVisitsToAdd, bool isRoot) {
     Node& n = N(ni);
     const int k = n.numChildren;
-    float wAdj[MAX_P], selfU[MAX_P], wlv[MAX_P], uv[MAX_P], usqv[MAX_P], wsqv[MAX_P], tmp[MAX_P];
+    real wAdj[MAX_P], selfU[MAX_P], wlv[MAX_P], uv[MAX_P], usqv[MAX_P], wsqv[MAX_P], tmp[MAX_P];
     bool good[MAX_P];
     int numGood = 0;
-    float maxW = 0.0f;
+    real maxW = 0.0f;
     for(int i = 0; i < k; i++) {
       const Node& c = N((int)EC(ni, i));
       uint32_t ev = EV(ni, i);
@@ -227,21 +237,21 @@ struct Ctx {
         wAdj[i] = 0.0f;
       }
     }
-    float origTotal = treeSum64(wAdj, k);
-    float currentTotal = origTotal;
-    float amountToSubtract = 0.0f, amountToPrune = 0.0f;
+    real origTotal = treeSum64(wAdj, k);
+    real currentTotal = origTotal;
+    real amountToSubtract = 0.0f, amountToPrune = 0.0f;
     if(isRoot && sp.rootNoiseEnabled) {
-      amountToSubtract = std::min(sp.chosenMoveSubtract, maxW / 64.0f);
-      amountToPrune = std::min(sp.chosenMovePrune, maxW / 64.0f);
+      amountToSubtract = rmin(sp.chosenMoveSubtract, maxW / 64.0f);
+      amountToPrune = rmin(sp.chosenMovePrune, maxW / 64.0f);
     }
     // downweightBadChildrenAndNormalizeWeight (valueWeightExponent != 0 branch)
     if(numGood > 0 && currentTotal > 0.0f) {
-      float stdev[MAX_P];
+      real stdev[MAX_P];
       for(int i = 0; i < k; i++) {
-        stdev[i] = good[i] ? sqrtf(1e-8f + 1.0f / (1.5f * sqrtf(wAdj[i]))) : 0.0f;
+        stdev[i] = good[i] ? std::sqrt(1e-8f + 1.0f / (1.5f * std::sqrt(wAdj[i]))) : 0.0f;
         tmp[i] = good[i] ? selfU[i] * wAdj[i] : 0.0f;
       }
-      float simpleValue = treeSum64(tmp, k) / currentTotal;
+      real simpleValue = treeSum64(tmp, k) / currentTotal;
       for(int i = 0; i < k; i++) {
         if(!good[i]) {
           tmp[i] = 0.0f;
@@ -251,16 +261,16 @@ struct Ctx {
           tmp[i] = 0.0f;
           continue;
         }
-        float nw = wAdj[i] - amountToSubtract;
+        real nw = wAdj[i] - amountToSubtract;
         if(nw <= 0.0f)
           nw = 0.0f;
-        float z = (selfU[i] - simpleValue) / stdev[i];
-        float p = cdf(z) + 0.0001f;
-        float f = sp.valueWeightExponent == 0.5f ? sqrtf(p) : kPowf(p, sp.valueWeightExponent);
+        real z = (selfU[i] - simpleValue) / stdev[i];
+        real p = cdf(z) + 0.0001f;
+        real f = sp.valueWeightExponent == 0.5f ? std::sqrt(p) : kPowf(p, (real)sp.valueWeightExponent);
         tmp[i] = nw * f;
       }
-      float totalNew = treeSum64(tmp, k);
-      float factor = currentTotal / totalNew;
+      real totalNew = treeSum64(tmp, k);
+      real factor = currentTotal / totalNew;
       for(int i = 0; i < k; i++)
         wAdj[i] = tmp[i] * factor;
     }
@@ -270,31 +280,31 @@ struct Ctx {
         continue;
       }
       const Node& c = N((int)EC(ni, i));
-      float ws = wAdj[i] / c.weightSum;
+      real ws = wAdj[i] / c.weightSum;
       wlv[i] = wAdj[i] * c.winLossAvg;
       uv[i] = wAdj[i] * c.utilityAvg;
       usqv[i] = wAdj[i] * c.utilitySqAvg;
       wsqv[i] = (ws * ws) * c.weightSqSum;
     }
-    float winLossSum = treeSum64(wlv, k);
-    float utilitySum = treeSum64(uv, k);
-    float utilitySqSum = treeSum64(usqv, k);
-    float weightSqSum = treeSum64(wsqv, k);
-    float weightSum = currentTotal;
-    float wl = n.nnWin - n.nnLoss;
-    float utility = wl;
+    real winLossSum = treeSum64(wlv, k);
+    real utilitySum = treeSum64(uv, k);
+    real utilitySqSum = treeSum64(usqv, k);
+    real weightSqSum = treeSum64(wsqv, k);
+    real weightSum = currentTotal;
+    real wl = n.nnWin - n.nnLoss;
+    real utility = wl;
     if(sp.subtreeValueBiasFactor != 0.0f && n.svbEntry >= 0) {
       int e = n.svbEntry;
       if(currentTotal > 1e-10f) {
-        float utilityChildren = utilitySum / currentTotal;
-        float svbW = kPowf(origTotal, sp.subtreeValueBiasWeightExponent);
-        float svbD = (utilityChildren - utility) * svbW;
+        real utilityChildren = utilitySum / currentTotal;
+        real svbW = kPowf(origTotal, (real)sp.subtreeValueBiasWeightExponent);
+        real svbD = (utilityChildren - utility) * svbW;
         gm.svbDelta[e] += svbQ(svbD) - svbQ(n.lastSvbDelta);
         gm.svbWeight[e] += svbQ(svbW) - svbQ(n.lastSvbWeight);
         n.lastSvbDelta = svbD;
         n.lastSvbWeight = svbW;
       }
-      float d = svbF(gm.svbDelta[e]), w = svbF(gm.svbWeight[e]);
+      real d = svbF(gm.svbDelta[e]), w = svbF(gm.svbWeight[e]);
       if(w > 0.001f)
         utility = utility + (sp.subtreeValueBiasFactor * d) / w;
     }
@@ -312,30 +322,30 @@ struct Ctx {
   }
 
   // --- getFpuValueForChildrenAssumeVisited searchexplorehelpers.cpp:245-301 ---
-  float fpuValue(int ni, int pla, bool isRoot, float probMass) {
+  real fpuValue(int ni, int pla, bool isRoot, real probMass) {
     const Node& n = N(ni);
-    float parentUtility = n.utilityAvg;
-    float forFpu = parentUtility;
+    real parentUtility = n.utilityAvg;
+    real forFpu = parentUtility;
     if(sp.fpuParentWeightByVisitedPolicy) {
-      float pw = sp.fpuParentWeightByVisitedPolicyPow == 2.0f ? probMass * probMass
-                                                              : kPowf(probMass, sp.fpuParentWeightByVisitedPolicyPow);
-      float avgWeight = std::min(1.0f, pw);
+      real pw = sp.fpuParentWeightByVisitedPolicyPow == 2.0f ? probMass * probMass
+                                                              : kPowf(probMass, (real)sp.fpuParentWeightByVisitedPolicyPow);
+      real avgWeight = rmin(1.0f, pw);
       forFpu = avgWeight * parentUtility + (1.0f - avgWeight) * (n.nnWin - n.nnLoss);
     }
-    float redMax = isRoot ? sp.rootFpuReductionMax : sp.fpuReductionMax;
-    float lossProp = isRoot ? sp.rootFpuLossProp : sp.fpuLossProp;
-    float reduction = redMax * sqrtf(probMass);
-    float fpu = pla == 2 ? forFpu - reduction : forFpu + reduction;
-    float lossValue = pla == 2 ? -1.0f : 1.0f;
+    real redMax = isRoot ? sp.rootFpuReductionMax : sp.fpuReductionMax;
+    real lossProp = isRoot ? sp.rootFpuLossProp : sp.fpuLossProp;
+    real reduction = redMax * std::sqrt(probMass);
+    real fpu = pla == 2 ? forFpu - reduction : forFpu + reduction;
+    real lossValue = pla == 2 ? -1.0f : 1.0f;
     fpu = fpu + (lossValue - fpu) * lossProp;
     return fpu;
   }
 
-  float exploreScaling(float totalChildWeight) {
-    float c = sp.cpuctExploration;
+  real exploreScaling(real totalChildWeight) {
+    real c = sp.cpuctExploration;
     if(sp.cpuctExplorationLog != 0.0f)
       c = c + sp.cpuctExplorationLog * kLogf((totalChildWeight + sp.cpuctExplorationBase) / sp.cpuctExplorationBase);
-    return c * sqrtf(totalChildWeight + 0.01f);
+    return c * std::sqrt(totalChildWeight + 0.01f);
   }
 
   // --- selectBestChildToDescend searchexplorehelpers.cpp:304-451 ---
@@ -344,33 +354,33 @@ struct Ctx {
     const Node& n = N(ni);
     const int k = n.numChildren;
     int pla = n.nextPla;
-    float probs[MAX_P], cw[MAX_P];
+    real probs[MAX_P], cw[MAX_P];
     bool hasChild[MAX_P];
     memset(hasChild, 0, sizeof(hasChild));
     for(int i = 0; i < k; i++) {
       const Node& c = N((int)EC(ni, i));
-      float p = pol[EM(ni, i)];
+      real p = pol[EM(ni, i)];
       probs[i] = p < 0.0f ? 0.0f : p;
       cw[i] = p < 0.0f ? 0.0f : childWeight(EV(ni, i), c.visits, c.weightSum);
       hasChild[EM(ni, i)] = true;
     }
-    float probMass = treeSum64(probs, k);
-    float total = treeSum64(cw, k);
-    float fpu = fpuValue(ni, pla, isRoot, probMass);
-    float scaling = exploreScaling(total);
-    float best = -INFINITY;
+    real probMass = treeSum64(probs, k);
+    real total = treeSum64(cw, k);
+    real fpu = fpuValue(ni, pla, isRoot, probMass);
+    real scaling = exploreScaling(total);
+    real best = -INFINITY;
     int bestSlot = -1;
     for(int i = 0; i < k; i++) {
       const Node& c = N((int)EC(ni, i));
-      float p = pol[EM(ni, i)];
-      float v;
+      real p = pol[EM(ni, i)];
+      real v;
       if(p < 0.0f)
         v = -INFINITY;  // POLICY_ILLEGAL_SELECTION_VALUE
       else {
-        float w = cw[i];
-        float u = (c.visits == 0 || w <= 0.0f) ? fpu : c.utilityAvg;
+        real w = cw[i];
+        real u = (c.visits == 0 || w <= 0.0f) ? fpu : c.utilityAvg;
         if(isRoot && sp.rootDesiredPerChildVisitsCoeff > 0.0f && p > 0.0f &&
-           w < sqrtf((p * total) * sp.rootDesiredPerChildVisitsCoeff))
+           w < std::sqrt((p * total) * sp.rootDesiredPerChildVisitsCoeff))
           v = 1e20f;
         else
           v = (scaling * p) / (1.0f + w) + (pla == 2 ? u : -u);
@@ -380,12 +390,12 @@ struct Ctx {
         bestSlot = i;
       }
     }
-    float bestNewProb = -1.0f;
+    real bestNewProb = -1.0f;
     int bestNew = -1;
     for(int pos = 0; pos < g.P; pos++) {
       if(hasChild[pos])
         continue;
-      float p = pol[pos];
+      real p = pol[pos];
       if(p < 0.0f)
         continue;
       if(p > bestNewProb) {
@@ -395,7 +405,7 @@ struct Ctx {
     }
     newPos = -1;
     if(bestNew >= 0) {
-      float v = (scaling * bestNewProb) / 1.0f + (pla == 2 ? fpu : -fpu);
+      real v = (scaling * bestNewProb) / 1.0f + (pla == 2 ? fpu : -fpu);
       if(v > best) {
         best = v;
         bestSlot = k;
@@ -480,36 +490,36 @@ struct Ctx {
   void postprocess(const Board& b, int sym, const float* out, float* pol, float& whiteWin, float& whiteLoss) {
     if(g.X != g.Y)
       sym &= 3;
-    float logit[MAX_P];
+    real logit[MAX_P];
     bool legal[MAX_P];
-    float mx = -1e25f;  // maxPolicy init nneval.cpp:709
+    real mx = -1e25f;  // maxPolicy init nneval.cpp:709
     for(int pos = 0; pos < g.P; pos++) {
       int d = pos / g.A, cell = pos % g.A;
       legal[pos] = isLegal(g, b, cell, d);
-      float v = legal[pos] ? out[symDir(d, sym) * g.A + symCell(g, cell, sym)] : -1e30f;
+      real v = legal[pos] ? out[symDir(d, sym) * g.A + symCell(g, cell, sym)] : -1e30f;
       logit[pos] = v;
       if(v > mx)
         mx = v;
     }
-    float e[MAX_P];
+    real e[MAX_P];
     for(int pos = 0; pos < g.P; pos++)
       e[pos] = kExpf(logit[pos] - mx);
-    float sum = treeSum64(e, g.P);
+    real sum = treeSum64(e, g.P);
     int legalCount = 0;
     for(int pos = 0; pos < g.P; pos++)
       legalCount += legal[pos] ? 1 : 0;
     if(sum <= 0.0f) {
-      float uniform = 1.0f / (float)legalCount;
+      real uniform = 1.0f / (real)legalCount;
       for(int pos = 0; pos < g.P; pos++)
         pol[pos] = legal[pos] ? uniform : -1.0f;
     } else {
       for(int pos = 0; pos < g.P; pos++)
         pol[pos] = legal[pos] ? e[pos] / sum : -1.0f;
     }
-    float wlg = out[g.P], llg = out[g.P + 1];
-    float m = std::max(wlg, llg);
-    float wp = kExpf(wlg - m), lp = kExpf(llg - m);
-    float ps = wp + lp;
+    real wlg = out[g.P], llg = out[g.P + 1];
+    real m = rmax(wlg, llg);
+    real wp = kExpf(wlg - m), lp = kExpf(llg - m);
+    real ps = wp + lp;
     wp = wp / ps;
     lp = lp / ps;
     if(b.pla == 2) {
@@ -521,11 +531,11 @@ struct Ctx {
     }
   }
 
-  float interpolateEarly(float halflife, float earlyValue, float value) {
+  real interpolateEarly(real halflife, real earlyValue, real value) {
     // Search::interpolateEarly searchhelpers.cpp:463-467
-    float rawHalflives = (float)gm.root.turn / halflife;
-    float halflives = rawHalflives * (19.0f / sqrtf((float)(g.X * g.Y)));
-    return value + (earlyValue - value) * kPowf(0.5f, halflives);
+    real rawHalflives = (real)gm.root.turn / halflife;
+    real halflives = rawHalflives * (19.0f / std::sqrt((real)(g.X * g.Y)));
+    return value + (earlyValue - value) * kPowf((real)0.5f, halflives);
   }
 
   // maybeAddPolicyNoiseAndTemp searchhelpers.cpp:122-222 (root only)
@@ -533,17 +543,17 @@ struct Ctx {
     for(int pos = 0; pos < g.P; pos++)
       out[pos] = raw[pos];
     if(sp.rootPolicyTemperature != 1.0f || sp.rootPolicyTemperatureEarly != 1.0f) {
-      float t = interpolateEarly(sp.chosenMoveTemperatureHalflife, sp.rootPolicyTemperatureEarly, sp.rootPolicyTemperature);
-      float mx = 0.0f;
+      real t = interpolateEarly(sp.chosenMoveTemperatureHalflife, sp.rootPolicyTemperatureEarly, sp.rootPolicyTemperature);
+      real mx = 0.0f;
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] > mx)
           mx = out[pos];
-      float logMax = kLogf(mx);
-      float invTemp = 1.0f / t;
-      float sum = 0.0f;
+      real logMax = kLogf(mx);
+      real invTemp = 1.0f / t;
+      real sum = 0.0f;
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] > 0.0f) {
-          float p = kExpf((kLogf(out[pos]) - logMax) * invTemp);
+          real p = kExpf((kLogf(out[pos]) - logMax) * invTemp);
           out[pos] = p;
           sum = sum + p;
         }
@@ -553,32 +563,32 @@ struct Ctx {
     }
     if(sp.rootNoiseEnabled) {
       // computeDirichletAlphaDistribution searchhelpers.cpp:51-91
-      float alpha[MAX_P];
+      real alpha[MAX_P];
       int legalCount = 0;
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] >= 0.0f)
           legalCount++;
-      float logSum = 0.0f;
+      real logSum = 0.0f;
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] >= 0.0f) {
-          alpha[pos] = kLogf(std::min(0.01f, out[pos]) + 1e-20f);
+          alpha[pos] = kLogf(rmin(0.01f, out[pos]) + 1e-20f);
           logSum = logSum + alpha[pos];
         }
-      float logMean = logSum / (float)legalCount;
-      float propSum = 0.0f;
+      real logMean = logSum / (real)legalCount;
+      real propSum = 0.0f;
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] >= 0.0f) {
-          alpha[pos] = std::max(0.0f, alpha[pos] - logMean);
+          alpha[pos] = rmax(0.0f, alpha[pos] - logMean);
           propSum = propSum + alpha[pos];
         }
-      float uniform = 1.0f / (float)legalCount;
+      real uniform = 1.0f / (real)legalCount;
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] >= 0.0f)
           alpha[pos] = propSum <= 0.0f ? uniform : 0.5f * (alpha[pos] / propSum + uniform);
       // addDirichletNoise searchhelpers.cpp:93-120.  SPEC a24: one draw from the
       // game stream seeds an independent sub-stream per move (parallel on device).
-      float r[MAX_P];
-      float rSum = 0.0f;
+      real r[MAX_P];
+      real rSum = 0.0f;
       const uint64_t base = gm.rng.next();
       for(int pos = 0; pos < g.P; pos++) {
         if(out[pos] >= 0.0f) {
@@ -592,7 +602,7 @@ struct Ctx {
       }
       for(int pos = 0; pos < g.P; pos++)
         r[pos] = r[pos] / rSum;
-      float w = sp.rootDirichletNoiseWeight;
+      real w = sp.rootDirichletNoiseWeight;
       for(int pos = 0; pos < g.P; pos++)
         if(out[pos] >= 0.0f)
           out[pos] = r[pos] * w + out[pos] * (1.0f - w);
@@ -600,25 +610,25 @@ struct Ctx {
   }
 
   // getSelfUtilityLCBAndRadius searchhelpers.cpp:469-521 (utilityRangeRadius = 1)
-  void lcbAndRadius(int pla, int ci, uint32_t ev, float& lcb, float& radius) {
+  void lcbAndRadius(int pla, int ci, uint32_t ev, real& lcb, real& radius) {
     const Node& c = N(ci);
     radius = 2.0f * 1.0f * sp.lcbStdevs;
     lcb = -radius;
-    float ws = childWeight(ev, c.visits, c.weightSum);
-    float wsq = childWeight(ev, c.visits, c.weightSqSum);
+    real ws = childWeight(ev, c.visits, c.weightSum);
+    real wsq = childWeight(ev, c.visits, c.weightSqSum);
     if(c.visits == 0 || ws <= 0.0f || wsq <= 0.0f)
       return;
-    float u = c.utilityAvg, usq = c.utilitySqAvg;
-    float ess = (ws * ws) / wsq;
-    float priorWeight = ws / ((ess * ess) * ess);
-    usq = std::max(usq, u * u + 1e-8f);
+    real u = c.utilityAvg, usq = c.utilitySqAvg;
+    real ess = (ws * ws) / wsq;
+    real priorWeight = ws / ((ess * ess) * ess);
+    usq = rmax(usq, u * u + 1e-8f);
     usq = (usq * ws + (usq + 1.0f) * priorWeight) / (ws + priorWeight);
     ws = ws + priorWeight;
     wsq = wsq + priorWeight * priorWeight;
     ess = (ws * ws) / wsq;
-    float selfU = pla == 2 ? u : -u;
-    float variance = usq - u * u;
-    float stdev = sqrtf(variance / ess);
+    real selfU = pla == 2 ? u : -u;
+    real variance = usq - u * u;
+    real stdev = std::sqrt(variance / ess);
     radius = stdev * sp.lcbStdevs;
     lcb = selfU - radius;
   }
@@ -626,7 +636,7 @@ struct Ctx {
   // getPlaySelectionValues searchresults.cpp:63-309 on the root.
   // Fills pos[] and vals[]; returns count (0 = failure).  useLcb: searchParams.useLcbForSelection
   // at the call (self-play turns it off for the move choice only, play.cpp:1040-1046, :1073-1076).
-  int playSelectionValues(float scaleMaxToAtLeast, bool allowDirectPolicyMoves, int* posOut, float* vals,
+  int playSelectionValues(real scaleMaxToAtLeast, bool allowDirectPolicyMoves, int* posOut, real* vals,
                           bool useLcb) {
     return playSelectionValuesAt(gm.rootIdx, gm.rootNoised.data(), true, scaleMaxToAtLeast, allowDirectPolicyMoves,
                                  posOut, vals, useLcb);
@@ -635,27 +645,27 @@ struct Ctx {
   // The same on any node (tree positions, play.cpp:736-745): the node's own network
   // policy (getPolicyProbsMaybeNoised: noise only at the root); the reduction of
   // over-explored children (:136-186) and direct policy moves (:242-276) are root-only.
-  int playSelectionValuesAt(int ri, const float* pol, bool isRoot, float scaleMaxToAtLeast,
-                            bool allowDirectPolicyMoves, int* posOut, float* vals, bool useLcb) {
+  int playSelectionValuesAt(int ri, const float* pol, bool isRoot, real scaleMaxToAtLeast,
+                            bool allowDirectPolicyMoves, int* posOut, real* vals, bool useLcb) {
     const Node& n = N(ri);
     const int k = n.numChildren;
     int pla = n.nextPla;
-    float cw[MAX_P];
+    real cw[MAX_P];
     for(int i = 0; i < k; i++) {
       const Node& c = N((int)EC(ri, i));
       cw[i] = childWeight(EV(ri, i), c.visits, c.weightSum);
       posOut[i] = EM(ri, i);
       vals[i] = cw[i];
     }
-    float total = treeSum64(cw, k);
+    real total = treeSum64(cw, k);
     int numChildren = k;
     int bestIdx = 0;
-    float bestWeight = -1e30f;
+    real bestWeight = -1e30f;
     {
-      float maxGood = -1e30f;
+      real maxGood = -1e30f;
       for(int i = 0; i < k; i++) {
-        float ev = (float)EV(ri, i);
-        float gdn = vals[i] * std::max(0.0f, ev - 1.0f) / std::max(1.0f, ev) + 2.0f * pol[posOut[i]];
+        real ev = (real)EV(ri, i);
+        real gdn = vals[i] * rmax(0.0f, ev - 1.0f) / rmax(1.0f, ev) + 2.0f * pol[posOut[i]];
         if(gdn > maxGood) {
           maxGood = gdn;
           bestWeight = vals[i];
@@ -664,32 +674,32 @@ struct Ctx {
       }
     }
     if(isRoot && k > 0) {
-      float fpu = fpuValue(ri, pla, true, 1.0f);
-      float scaling = exploreScaling(total);
+      real fpu = fpuValue(ri, pla, true, 1.0f);
+      real scaling = exploreScaling(total);
       // getExploreSelectionValueOfChild for the best child, isDuringSearch = false
       const Node& bc = N((int)EC(ri, bestIdx));
-      float bp = pol[posOut[bestIdx]];
-      float bw = cw[bestIdx];
-      float bu = (bc.visits == 0 || bw <= 0.0f) ? fpu : bc.utilityAvg;
-      float bestValue = bp < 0.0f ? -INFINITY : (scaling * bp) / (1.0f + bw) + (pla == 2 ? bu : -bu);
+      real bp = pol[posOut[bestIdx]];
+      real bw = cw[bestIdx];
+      real bu = (bc.visits == 0 || bw <= 0.0f) ? fpu : bc.utilityAvg;
+      real bestValue = bp < 0.0f ? -INFINITY : (scaling * bp) / (1.0f + bw) + (pla == 2 ? bu : -bu);
       for(int i = 0; i < k; i++) {
         if(i == bestIdx)
           continue;
         // getReducedPlaySelectionWeight searchexplorehelpers.cpp:209-243
         const Node& c = N((int)EC(ri, i));
-        float w = cw[i];
-        float reduced;
+        real w = cw[i];
+        real reduced;
         if(c.visits == 0 || w <= 0.0f)
           reduced = 0.0f;
         else {
-          float p = pol[posOut[i]];
-          float wanted;
+          real p = pol[posOut[i]];
+          real wanted;
           if(p < 0.0f)
             wanted = 0.0f;
           else {
-            float valueComponent = pla == 2 ? c.utilityAvg : -c.utilityAvg;
-            float exploreComponent = bestValue - valueComponent;
-            float exploreComponentScaling = scaling * p;
+            real valueComponent = pla == 2 ? c.utilityAvg : -c.utilityAvg;
+            real exploreComponent = bestValue - valueComponent;
+            real exploreComponentScaling = scaling * p;
             if(exploreComponent <= 0.0f)
               wanted = INFINITY;
             else {
@@ -700,31 +710,31 @@ struct Ctx {
           }
           reduced = w > wanted ? wanted : w;
         }
-        vals[i] = ceilf(reduced);
+        vals[i] = std::ceil(reduced);
       }
     }
     if(useLcb && k > 0) {
-      float lcb[MAX_P], rad[MAX_P];
-      float bestLcb = -1e10f;
+      real lcb[MAX_P], rad[MAX_P];
+      real bestLcb = -1e10f;
       int bestLcbIdx = -1;
       for(int i = 0; i < k; i++) {
         lcbAndRadius(pla, (int)EC(ri, i), EV(ri, i), lcb[i], rad[i]);
-        float w = vals[i];
+        real w = vals[i];
         if(w > 0.0f && w >= sp.minVisitPropForLCB * bestWeight && lcb[i] > bestLcb) {
           bestLcb = lcb[i];
           bestLcbIdx = i;
         }
       }
       if(bestLcbIdx >= 0) {
-        float adjusted = vals[bestLcbIdx];
+        real adjusted = vals[bestLcbIdx];
         for(int i = 0; i < k; i++) {
           if(i == bestLcbIdx)
             continue;
-          float excess = bestLcb - lcb[i];
+          real excess = bestLcb - lcb[i];
           if(excess < 0.0f)
             continue;
-          float rf = (rad[i] + excess) / (rad[i] + 0.20f * excess);
-          float lbound = (rf * rf) * vals[i];
+          real rf = (rad[i] + excess) / (rad[i] + 0.20f * excess);
+          real lbound = (rf * rf) * vals[i];
           if(lbound > adjusted)
             adjusted = lbound;
         }
@@ -744,15 +754,15 @@ struct Ctx {
       if(numChildren == 0)
         return 0;
     }
-    float mx = 0.0f;
+    real mx = 0.0f;
     for(int i = 0; i < numChildren; i++)
       if(vals[i] > mx)
         mx = vals[i];
     if(mx <= 0.0f)
       return 0;
-    float amountToSubtract = std::min(sp.chosenMoveSubtract, mx / 64.0f);
-    float amountToPrune = std::min(sp.chosenMovePrune, mx / 64.0f);
-    float newMax = mx - amountToSubtract;
+    real amountToSubtract = rmin(sp.chosenMoveSubtract, mx / 64.0f);
+    real amountToPrune = rmin(sp.chosenMovePrune, mx / 64.0f);
+    real newMax = mx - amountToSubtract;
     for(int i = 0; i < numChildren; i++) {
       if(vals[i] < amountToPrune)
         vals[i] = 0.0f;
@@ -769,13 +779,13 @@ struct Ctx {
   }
 
   // chooseIndexWithTemperature searchhelpers.cpp:11-49 with our stream.
-  int chooseIndex(const float* vals, int n, float temperature) {
-    float mx = 0.0f;
+  int chooseIndex(const real* vals, int n, real temperature) {
+    real mx = 0.0f;
     for(int i = 0; i < n; i++)
       if(vals[i] > mx)
         mx = vals[i];
     if(temperature <= 1.0e-4f) {
-      float best = vals[0];
+      real best = vals[0];
       int bi = 0;
       for(int i = 1; i < n; i++)
         if(vals[i] > best) {
@@ -784,15 +794,15 @@ struct Ctx {
         }
       return bi;
     }
-    float pr[MAX_P];
-    float logMax = kLogf(mx);
-    float sum = 0.0f;
+    real pr[MAX_P];
+    real logMax = kLogf(mx);
+    real sum = 0.0f;
     for(int i = 0; i < n; i++) {
       pr[i] = vals[i] <= 0.0f ? 0.0f : kExpf((kLogf(vals[i]) - logMax) / temperature);
       sum = sum + pr[i];
     }
-    float d = gm.rng.uni() * sum;  // Rand::nextUInt(relProbs) rand.h:244-262
-    float acc = 0.0f;
+    real d = gm.rng.uni() * sum;  // Rand::nextUInt(relProbs) rand.h:244-262
+    real acc = 0.0f;
     for(int i = 0; i < n; i++) {
       acc = acc + pr[i];
       if(acc > d)
@@ -932,20 +942,20 @@ struct Ctx {
         gm.noNoise = 1;
       }
     } else if(b.reduceVisits && (int)gm.turns.size() - gm.startTurn >= b.reduceVisitsThresholdLookback) {
-      float mn = 1e20f, mx = -1e20f;
+      real mn = 1e20f, mx = -1e20f;
       for(int j = 0; j < b.reduceVisitsThresholdLookback; j++) {
-        const float w = gm.turns[gm.turns.size() - 1 - j].rootWL;
+        const real w = gm.turns[gm.turns.size() - 1 - j].rootWL;
         mn = w < mn ? w : mn;
         mx = w > mx ? w : mx;
       }
-      float extreme = std::max(mn, -mx);
+      real extreme = rmax(mn, -mx);
       if(extreme > 1.0f)
         extreme = 1.0f;
-      const float through = extreme - b.reduceVisitsThreshold;
+      const real through = extreme - b.reduceVisitsThreshold;
       if(through > 0.0f) {
-        const float prop = through / (1.0f - b.reduceVisitsThreshold);
-        const float red = prop * prop;
-        const int v = (int)roundf((float)b.maxVisits + red * ((float)b.reducedVisitsMin - (float)b.maxVisits));
+        const real prop = through / (1.0f - b.reduceVisitsThreshold);
+        const real red = prop * prop;
+        const int v = (int)std::round((real)b.maxVisits + red * ((real)b.reducedVisitsMin - (real)b.maxVisits));
         gm.moveWeight = 1.0f + red * (b.reducedVisitsWeight - 1.0f);
         gm.visitLimit = std::max(v, b.reducedVisitsMin);
       }
@@ -971,10 +981,10 @@ struct Ctx {
     gm.initLeft = 0;
     const SearchParams& b = s.cfg.sp;
     if(b.initGamesWithPolicy && b.policyInitAreaProp > 0.0f) {
-      float u = gm.rng.uni();
+      real u = gm.rng.uni();
       while(u <= 0.0f)
         u = gm.rng.uni();
-      gm.initLeft = (int)floorf(-kLogf(u) * ((float)g.A * b.policyInitAreaProp));
+      gm.initLeft = (int)std::floor(-kLogf(u) * ((real)g.A * b.policyInitAreaProp));
     }
     if(gm.initLeft > 0) {
       gm.phase = PH_INIT;
@@ -995,25 +1005,25 @@ struct Ctx {
     float pol[MAX_P], w, l;
     postprocess(gm.root, gm.leafSym, out, pol, w, l);
     int cpos[MAX_P];
-    float cval[MAX_P];
+    real cval[MAX_P];
     int n = 0;
-    const float invT = 1.0f / b.policyInitAreaTemperature;
+    const real invT = 1.0f / b.policyInitAreaTemperature;
     for(int p = 0; p < g.P; p++)
       if(pol[p] > 0.0f) {
         cpos[n] = p;
-        cval[n] = b.policyInitAreaTemperature == 1.0f ? pol[p] : kPowf(pol[p], invT);
+        cval[n] = b.policyInitAreaTemperature == 1.0f ? pol[p] : kPowf((real)pol[p], (real)invT);
         n++;
       }
     int idx;
     if(gm.rng.uni() < 0.0002f) {
       idx = (int)gm.rng.below((uint32_t)n);
     } else {
-      float sum = 0.0f;
+      real sum = 0.0f;
       for(int i = 0; i < n; i++)
         sum = sum + cval[i];
-      const float dd = gm.rng.uni() * sum;
+      const real dd = gm.rng.uni() * sum;
       idx = n - 1;
-      float acc = 0.0f;
+      real acc = 0.0f;
       for(int i = 0; i < n; i++) {
         acc = acc + cval[i];
         if(acc > dd) {
@@ -1084,10 +1094,10 @@ struct Ctx {
     const int n = (int)gm.turns.size();
     int moveIdx;
     if(early) {
-      float u = gm.rng.uni();
+      real u = gm.rng.uni();
       while(u <= 0.0f)
         u = gm.rng.uni();
-      moveIdx = (int)floorf(-kLogf(u) * (b.earlyForkGameExpectedMoveProp * (float)g.A));
+      moveIdx = (int)std::floor(-kLogf(u) * (b.earlyForkGameExpectedMoveProp * (real)g.A));
     } else {
       moveIdx = n <= 0 ? 0 : (int)gm.rng.below((uint32_t)n);
     }
@@ -1125,7 +1135,7 @@ struct Ctx {
   void forkEval(const float* out) {
     float pol[MAX_P], w, l;
     postprocess(gm.leafBoard, gm.leafSym, out, pol, w, l);
-    const float wr = 0.5f * (w - l + 1.0f);
+    const real wr = 0.5f * (w - l + 1.0f);
     const int pla = gm.forkBoard.pla;
     if(gm.forkBest < 0 || (pla == 2 && wr > gm.forkBestWinrate) || (pla == 1 && wr < gm.forkBestWinrate)) {
       gm.forkBest = gm.forkNext;
@@ -1147,11 +1157,11 @@ struct Ctx {
   // (chooseRandomPolicyMove playutils.cpp:62-95, chooseRandomLegalMove :10-31).
   // Returns the policy position, or -1.
   int forkingMove(const float* pol, const Board& b, int ban) {
-    const float r = gm.rng.uni();
+    const real r = gm.rng.uni();
     if(r < 0.95f) {
-      const float temp = r < 0.70f ? 1.0f : 2.0f;
+      const real temp = r < 0.70f ? 1.0f : 2.0f;
       int cpos[MAX_P];
-      float cval[MAX_P];
+      real cval[MAX_P];
       int n = 0;
       for(int p = 0; p < g.P; p++)
         if(pol[p] > 0.0f && p != ban) {
@@ -1211,7 +1221,7 @@ struct Ctx {
   void emitSideRow(const TurnRec& tr) { emitSideRow(tr, gm.root, (int32_t)gm.gameNum - 1); }
   void emitSideRow(const TurnRec& tr, const Board& b, int32_t gameNumMeta) {
     const int A = g.A, P = g.P, pb = (A + 7) / 8;
-    float hmv[5];
+    real hmv[5];
     bool h = true;
     for(int i = 0; i < 5; i++) {
       h = h && gm.rng.uni() < 0.98f;
@@ -1254,18 +1264,18 @@ struct Ctx {
     gt[32] = tr.searchEntropy;
     for(int i = 0; i < 5; i++)
       gt[36 + i] = hmv[i];
-    gt[41] = (float)(gm.gameHash0 & 0x3FFFFF);
-    gt[42] = (float)((gm.gameHash0 >> 22) & 0x3FFFFF);
-    gt[43] = (float)((gm.gameHash0 >> 44) & 0xFFFFF);
-    gt[44] = (float)(gm.gameHash1 & 0x3FFFFF);
-    gt[45] = (float)((gm.gameHash1 >> 22) & 0x3FFFFF);
-    gt[46] = (float)((gm.gameHash1 >> 44) & 0xFFFFF);
-    gt[51] = (float)b.turn;
-    gt[53] = (float)gm.startTurn;
-    gt[55] = (float)gm.gameMode;
+    gt[41] = (real)(gm.gameHash0 & 0x3FFFFF);
+    gt[42] = (real)((gm.gameHash0 >> 22) & 0x3FFFFF);
+    gt[43] = (real)((gm.gameHash0 >> 44) & 0xFFFFF);
+    gt[44] = (real)(gm.gameHash1 & 0x3FFFFF);
+    gt[45] = (real)((gm.gameHash1 >> 22) & 0x3FFFFF);
+    gt[46] = (real)((gm.gameHash1 >> 44) & 0xFFFFF);
+    gt[51] = (real)b.turn;
+    gt[53] = (real)gm.startTurn;
+    gt[55] = (real)gm.gameMode;
     gt[57] = pla == 2 ? tr.rawWhiteWL : -tr.rawWhiteWL;
     gt[59] = tr.rawPolicyEntropy;
-    gt[60] = (float)tr.visits;
+    gt[60] = (real)tr.visits;
     gt[63] = 1.0f;
     for(int i = 0; i < 5 * A; i++)
       R.value[r * 5 * A + i] = 0;
@@ -1276,28 +1286,28 @@ struct Ctx {
   // (searchresults.cpp:486-550, scaleMaxToAtLeast 1).
   void searchTargets(int ni, const float* pol, bool isRoot, TurnRec& tr) {
     int posv[MAX_P];
-    float vals[MAX_P];
+    real vals[MAX_P];
     tr.policyTarget.assign(g.P, 0);
     {
       int m = playSelectionValuesAt(ni, pol, isRoot, 10.0f, false, posv, vals, sp.useLcbForSelection);
-      float mx = 0.0f;
+      real mx = 0.0f;
       for(int i = 0; i < m; i++)
         if(vals[i] > mx)
           mx = vals[i];
-      float factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
+      real factor = mx > 30000.0f ? 30000.0f / mx : 1.0f;
       for(int i = 0; i < m; i++)
-        tr.policyTarget[posv[i]] = (int16_t)roundf(vals[i] * factor);
+        tr.policyTarget[posv[i]] = (int16_t)std::round(vals[i] * factor);
     }
     int m = playSelectionValuesAt(ni, pol, isRoot, 1.0f, true, posv, vals, sp.useLcbForSelection);
-    float sumV = 0.0f;
+    real sumV = 0.0f;
     for(int i = 0; i < m; i++)
       sumV = sumV + vals[i];
-    float surprise = 0.0f, searchEnt = 0.0f, polEnt = 0.0f;
+    real surprise = 0.0f, searchEnt = 0.0f, polEnt = 0.0f;
     for(int i = 0; i < m; i++) {
-      float p = std::max(pol[posv[i]], 1e-30f);
-      float t = vals[i] / sumV;
+      real p = rmax(pol[posv[i]], 1e-30f);
+      real t = vals[i] / sumV;
       if(t > 1e-30f) {
-        float lt = kLogf(t), lp = kLogf(p);
+        real lt = kLogf(t), lp = kLogf(p);
         surprise = surprise + t * (lt - lp);
         searchEnt = searchEnt + (-t * lt);
       }
@@ -1305,25 +1315,25 @@ struct Ctx {
     for(int p = 0; p < g.P; p++)
       if(pol[p] > 1e-30f)
         polEnt = polEnt + (-pol[p] * kLogf(pol[p]));
-    tr.policySurprise = std::max(0.0f, surprise);
-    tr.searchEntropy = std::max(0.0f, searchEnt);
-    tr.policyEntropy = std::max(0.0f, polEnt);
+    tr.policySurprise = rmax(0.0f, surprise);
+    tr.searchEntropy = rmax(0.0f, searchEnt);
+    tr.policyEntropy = rmax(0.0f, polEnt);
   }
 
   // extractValueTargets (play.cpp:674-682) via ReportedSearchValues (reportedsearchvalues.cpp:10-50).
   void valueTargets(int ni, TurnRec& tr) {
-    float wl = std::max(-1.0f, std::min(1.0f, N(ni).winLossAvg));
-    tr.whiteWin = std::max(0.0f, std::min(1.0f, 0.5f * (wl + 1.0f)));
-    tr.whiteLoss = std::max(0.0f, std::min(1.0f, 0.5f * (-wl + 1.0f)));
+    real wl = rmax(-1.0f, rmin(1.0f, N(ni).winLossAvg));
+    tr.whiteWin = rmax(0.0f, rmin(1.0f, 0.5f * (wl + 1.0f)));
+    tr.whiteLoss = rmax(0.0f, rmin(1.0f, 0.5f * (-wl + 1.0f)));
     tr.rootWL = wl;
   }
 
   // computeNNRawStats (play.cpp:684-704) from a stored evaluation.
-  void rawStats(float win, float loss, const float* pol, TurnRec& tr) {
+  void rawStats(real win, real loss, const float* pol, TurnRec& tr) {
     tr.rawWhiteWL = win - loss;
-    float ent = 0.0f;
+    real ent = 0.0f;
     for(int p = 0; p < g.P; p++) {
-      float q = pol[p];
+      real q = pol[p];
       if(q >= 1e-30f)
         ent = ent + (-q * kLogf(q));
     }
@@ -1350,8 +1360,8 @@ struct Ctx {
       valueTargets(ni, tr);
       rawStats(N(ni).nnWin, N(ni).nnLoss, POL(ni), tr);
       tr.visits = rootVisits;
-      const float w = sp.recordTreeTargetWeight;
-      const float fl = floorf(w);
+      const real w = sp.recordTreeTargetWeight;
+      const real fl = std::floor(w);
       const int copies = (int)fl + (gm.rng.uni() < w - fl ? 1 : 0);
       for(int c = 0; c < copies; c++)
         emitSideRow(tr, b, gameNumMeta);
@@ -1404,7 +1414,7 @@ struct Ctx {
 
 void Ctx::commitMove() {
   int posv[MAX_P];
-  float vals[MAX_P];
+  real vals[MAX_P];
   TurnRec tr;
   // a side position's search (play.cpp:1576-1662) ends like a move search, but writes
   // one row and plays nothing
@@ -1416,7 +1426,7 @@ void Ctx::commitMove() {
     fprintf(stderr, "oracle: no move selectable\n");
     abort();
   }
-  float temp = interpolateEarly(sp.chosenMoveTemperatureHalflife, sp.chosenMoveTemperatureEarly, sp.chosenMoveTemperature);
+  real temp = interpolateEarly(sp.chosenMoveTemperatureHalflife, sp.chosenMoveTemperatureEarly, sp.chosenMoveTemperature);
   int chosen = posv[chooseIndex(vals, n, temp)];
   const Node& r = N(gm.rootIdx);
   valueTargets(gm.rootIdx, tr);
@@ -1500,60 +1510,60 @@ static void packBitsBE(const float* v, int len, uint8_t* out) {
 // Play::runGame row weights: value surprise (play.cpp:1470-1497), surprise-weighted
 // target weights (:1498-1574) and their probabilistic resolution (:1683-1697), in f32
 // with the loops' own order.  Fills turns[].rows.
-static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec>& turns, int t0, const float* tWin,
-                               const float* tLoss, Rng& rng) {
+static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec>& turns, int t0, const real* tWin,
+                               const real* tLoss, Rng& rng) {
   const int n = (int)turns.size();  // searched turns [t0, n)
   if(b.policySurpriseDataWeight > 0.0f || b.valueSurpriseDataWeight > 0.0f) {
-    std::vector<float> vs(n);
-    const float nowFactor = 1.0f / (1.0f + (float)A * 0.016f);
-    float winV = tWin[n], lossV = tLoss[n];
+    std::vector<real> vs(n);
+    const real nowFactor = 1.0f / (1.0f + (real)A * 0.016f);
+    real winV = tWin[n], lossV = tLoss[n];
     for(int i = n - 1; i >= t0; i--) {
       winV = winV + nowFactor * (tWin[i] - winV);
       lossV = lossV + nowFactor * (tLoss[i] - lossV);
-      float v = 0.0f;
+      real v = 0.0f;
       if(winV > 1e-30f)
-        v = v + winV * (kLogf(winV) - kLogf(std::max(turns[i].rootNNWin, 1e-30f)));
+        v = v + winV * (kLogf(winV) - kLogf(rmax(turns[i].rootNNWin, 1e-30f)));
       if(lossV > 1e-30f)
-        v = v + lossV * (kLogf(lossV) - kLogf(std::max(turns[i].rootNNLoss, 1e-30f)));
+        v = v + lossV * (kLogf(lossV) - kLogf(rmax(turns[i].rootNNLoss, 1e-30f)));
       if(v < 0.0f)
         v = 0.0f;
-      vs[i] = std::min(v, 1.0f);
+      vs[i] = rmin(v, 1.0f);
     }
-    float sumW = 0.0f, sumPS = 0.0f, sumVS = 0.0f;
+    real sumW = 0.0f, sumPS = 0.0f, sumVS = 0.0f;
     for(int i = t0; i < n; i++) {
-      const float tw = turns[i].targetWeight;
+      const real tw = turns[i].targetWeight;
       sumW = sumW + tw;
       sumPS = sumPS + turns[i].policySurprise * tw;
       sumVS = sumVS + vs[i] * tw;
     }
     if(sumW >= 1.0f) {
-      const float avgPS = sumPS / sumW, avgVS = sumVS / sumW;
-      float vsdw = b.valueSurpriseDataWeight;
+      const real avgPS = sumPS / sumW, avgVS = sumVS / sumW;
+      real vsdw = b.valueSurpriseDataWeight;
       if(avgVS < 0.010f)
         vsdw = vsdw * (avgVS / 0.010f);
-      const float thr = avgPS * 1.5f;
-      float sumPPV = 0.0f, sumVPV = 0.0f;
+      const real thr = avgPS * 1.5f;
+      real sumPPV = 0.0f, sumVPV = 0.0f;
       for(int i = t0; i < n; i++) {
-        const float tw = turns[i].targetWeight, ps = turns[i].policySurprise;
-        sumPPV = sumPPV + (tw * ps + (1.0f - tw) * std::max(0.0f, ps - thr));
+        const real tw = turns[i].targetWeight, ps = turns[i].policySurprise;
+        sumPPV = sumPPV + (tw * ps + (1.0f - tw) * rmax(0.0f, ps - thr));
         sumVPV = sumVPV + tw * vs[i];
       }
-      sumPPV = std::max(sumPPV, 1e-10f);
-      sumVPV = std::max(sumVPV, 1e-10f);
+      sumPPV = rmax(sumPPV, 1e-10f);
+      sumVPV = rmax(sumVPV, 1e-10f);
       for(int i = t0; i < n; i++) {
-        const float tw = turns[i].targetWeight, ps = turns[i].policySurprise;
-        const float ppv = tw * ps + (1.0f - tw) * std::max(0.0f, ps - thr);
-        const float vpv = tw * vs[i];
+        const real tw = turns[i].targetWeight, ps = turns[i].policySurprise;
+        const real ppv = tw * ps + (1.0f - tw) * rmax(0.0f, ps - thr);
+        const real vpv = tw * vs[i];
         turns[i].targetWeight = (1.0f - b.policySurpriseDataWeight - vsdw) * tw +
                                 b.policySurpriseDataWeight * ppv * sumW / sumPPV + vsdw * vpv * sumW / sumVPV;
       }
     }
   }
   for(int i = t0; i < n; i++) {
-    float w = turns[i].targetWeight;
+    real w = turns[i].targetWeight;
     if(w <= 0.0f)
       w = 0.0f;
-    const float fl = floorf(w), excess = w - fl;
+    const real fl = std::floor(w), excess = w - fl;
     turns[i].rows = (int)(rng.uni() < excess ? fl + 1.0f : fl);
   }
 }
@@ -1563,8 +1573,8 @@ static void resolveTurnWeights(const SearchParams& b, int A, std::vector<TurnRec
 void Ctx::finishGame() {
   const int numMoves = (int)gm.turns.size();
   const int A = g.A, P = g.P, pb = (A + 7) / 8;
-  float finalWin = gm.root.winner == 2 ? 1.0f : (gm.root.winner == 1 ? 0.0f : 0.5f);
-  std::vector<float> tWin(numMoves + 1), tLoss(numMoves + 1);
+  real finalWin = gm.root.winner == 2 ? 1.0f : (gm.root.winner == 1 ? 0.0f : 0.5f);
+  std::vector<real> tWin(numMoves + 1), tLoss(numMoves + 1);
   for(int t = 0; t < numMoves; t++) {
     tWin[t] = gm.turns[t].whiteWin;
     tLoss[t] = gm.turns[t].whiteLoss;
@@ -1621,12 +1631,12 @@ void Ctx::finishGame() {
     for(int i = 0; i < 64; i++)
       gt[i] = 0.0f;
     // fillValueTDTargets trainingwrite.cpp:286-314
-    const float nowFactors[5] = {0.0f, 1.0f / (1.0f + (float)A * 0.176f), 1.0f / (1.0f + (float)A * 0.056f),
-                                 1.0f / (1.0f + (float)A * 0.016f), 1.0f};
+    const real nowFactors[5] = {0.0f, 1.0f / (1.0f + (real)A * 0.176f), 1.0f / (1.0f + (real)A * 0.056f),
+                                 1.0f / (1.0f + (real)A * 0.016f), 1.0f};
     for(int f = 0; f < 5; f++) {
-      float win = 0.0f, loss = 0.0f, left = 1.0f;
+      real win = 0.0f, loss = 0.0f, left = 1.0f;
       for(int i = t; i <= numMoves; i++) {
-        float now;
+        real now;
         if(i == numMoves) {
           now = left;
           left = 0.0f;
@@ -1641,11 +1651,11 @@ void Ctx::finishGame() {
       gt[2 * f + 1] = loss;
     }
     {
-      float sum = 0.0f;
+      real sum = 0.0f;
       for(int i = t + 1; i <= numMoves; i++) {
-        float prevWL = tWin[i - 1] - tLoss[i - 1], nextWL = tWin[i] - tLoss[i];
-        float var = (nextWL - prevWL) * (nextWL - prevWL);
-        sum = sum + (float)(i - t) * var;
+        real prevWL = tWin[i - 1] - tLoss[i - 1], nextWL = tWin[i] - tLoss[i];
+        real var = (nextWL - prevWL) * (nextWL - prevWL);
+        sum = sum + (real)(i - t) * var;
       }
       gt[22] = sum;
     }
@@ -1662,18 +1672,18 @@ void Ctx::finishGame() {
       h = h && hmRng.uni() < 0.98f;
       gt[36 + i] = h ? 1.0f : 0.0f;
     }
-    gt[41] = (float)(gm.gameHash0 & 0x3FFFFF);
-    gt[42] = (float)((gm.gameHash0 >> 22) & 0x3FFFFF);
-    gt[43] = (float)((gm.gameHash0 >> 44) & 0xFFFFF);
-    gt[44] = (float)(gm.gameHash1 & 0x3FFFFF);
-    gt[45] = (float)((gm.gameHash1 >> 22) & 0x3FFFFF);
-    gt[46] = (float)((gm.gameHash1 >> 44) & 0xFFFFF);
-    gt[51] = (float)t;
-    gt[53] = (float)gm.startTurn;
-    gt[55] = (float)gm.gameMode;
+    gt[41] = (real)(gm.gameHash0 & 0x3FFFFF);
+    gt[42] = (real)((gm.gameHash0 >> 22) & 0x3FFFFF);
+    gt[43] = (real)((gm.gameHash0 >> 44) & 0xFFFFF);
+    gt[44] = (real)(gm.gameHash1 & 0x3FFFFF);
+    gt[45] = (real)((gm.gameHash1 >> 22) & 0x3FFFFF);
+    gt[46] = (real)((gm.gameHash1 >> 44) & 0xFFFFF);
+    gt[51] = (real)t;
+    gt[53] = (real)gm.startTurn;
+    gt[55] = (real)gm.gameMode;
     gt[57] = pla == 2 ? gm.turns[t].rawWhiteWL : -gm.turns[t].rawWhiteWL;
     gt[59] = gm.turns[t].rawPolicyEntropy;
-    gt[60] = (float)gm.turns[t].visits;
+    gt[60] = (real)gm.turns[t].visits;
     gt[63] = 1.0f;
     int8_t* vt = &R.value[r * 5 * A];
     const Board& b2 = boards[std::min(t + 2, numMoves)];
@@ -1906,7 +1916,7 @@ void selfplayRound(Selfplay& s) {
       }
       gm.rootK++;
       if(gm.rootK == cx.sp.rootNumSymmetriesToSample) {
-        float fl = (float)cx.sp.rootNumSymmetriesToSample;
+        real fl = (real)cx.sp.rootNumSymmetriesToSample;
         bool fresh = gm.rootIdx < 0;
         if(fresh)
           gm.rootIdx = cx.allocNode(gm.root.pla, stateHash(g, gm.root), false);
@@ -1951,7 +1961,7 @@ void selfplayRound(Selfplay& s) {
       cx.addLeafValue(gm.leafNode, w - l, false, true);
     } else if(gm.leafKind == LEAF_TERMINAL) {
       // search.cpp:943-953: value = 2*whiteWinsOfWinner - 1 (SPEC B16: draw = 0)
-      float v = gm.leafBoard.winner == 2 ? 1.0f : (gm.leafBoard.winner == 1 ? -1.0f : 0.0f);
+      real v = gm.leafBoard.winner == 2 ? 1.0f : (gm.leafBoard.winner == 1 ? -1.0f : 0.0f);
       cx.addLeafValue(gm.leafNode, v, true, false);
     } else if(gm.leafKind == LEAF_NOCHILD) {
       Node& n = cx.N(gm.leafNode);

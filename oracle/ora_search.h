@@ -7,6 +7,15 @@
 
 namespace ora {
 
+// Arithmetic type of the search statistics and selection values: float (the device's
+// SPEC restatement, the default) or double (-DORA_REAL=double, liboracle_f64.so: the
+// reference's own precision, searchnode.h:18-44; used to measure how far the f32
+// search drifts from f64 semantics, tests/test_f64_divergence.py).
+#ifndef ORA_REAL
+#define ORA_REAL float
+#endif
+typedef ORA_REAL real;
+
 // SearchParams (searchparams.h) restricted to what Coffee self-play reads, with
 // the values of cpp/configs/training/selfplay1.cfg (SURVEY §8d benchmark mode).
 struct SearchParams {
@@ -72,9 +81,9 @@ inline SearchParams cheapSearchParams(const SearchParams& p) {
 // pools can be compared bit-for-bit.
 struct Node {
   uint32_t visits;
-  float weightSum, weightSqSum, utilityAvg, utilitySqAvg, winLossAvg;
+  real weightSum, weightSqSum, utilityAvg, utilitySqAvg, winLossAvg;
   float nnWin, nnLoss;             // white-perspective NN probs (NNOutput::whiteWinProb/LossProb)
-  float lastSvbDelta, lastSvbWeight;
+  real lastSvbDelta, lastSvbWeight;
   int32_t svbEntry;                // -1 none
   uint16_t numChildren;
   uint8_t nextPla;

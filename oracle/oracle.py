@@ -12,9 +12,12 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+# the same restatement with f64 search statistics (ORA_REAL=double, ora_search.h)
+LIB_F64_PATH = os.path.join(HERE, "_build", "liboracle_f64.so")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 _lib = None
+_lib64 = None
 
 P = ctypes.c_void_p
 
@@ -23,12 +26,24 @@ def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib():
-    global _lib
+def lib(f64=False):
+    """The oracle library; f64=True: the variant with f64 search statistics."""
+    global _lib, _lib64
+    if f64:
+        if _lib64 is None:
+            if not os.path.exists(LIB_F64_PATH):
+                build()
+            _lib64 = _setup(ctypes.CDLL(LIB_F64_PATH))
+        return _lib64
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
-        L = ctypes.CDLL(LIB_PATH)
+        _lib = _setup(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+def _setup(L):
+    if True:
         L.ora_model_load.restype = P
         L.ora_sp_create.restype = P
         L.ora_sp_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
@@ -48,8 +63,7 @@ def lib():
         L.ora_sp_set_parallel.argtypes = [P, ctypes.c_int]
         L.ora_model_free.argtypes = [P]
         _load_tables(L)
-        _lib = L
-    return _lib
+    return L
 
 
 def ptr(a):
@@ -63,7 +77,7 @@ def _load_tables(L):
     go = np.ascontiguousarray(z["game_over"], np.uint64)
     cdf = np.ascontiguousarray(t["cdf"].astype(np.float32))
     L.ora_load_tables(*[ptr(a) for a in arrs], ptr(go), ptr(cdf))
-    _load_tables.keep = arrs + [go, cdf]
+    _load_tables.keep = getattr(_load_tables, "keep", []) + arrs + [go, cdf]
 
 
 NODE_DTYPE = np.dtype([
@@ -224,8 +238,12 @@ class Selfplay:
     """Round-synchronous self-play engine (select -> batched NN -> backup per round)."""
 
     def __init__(self, X, Y, W, games, max_visits, node_cap=2048, seed=1, slot_base=0, nn_mode=0, model=None,
-                 nn_threads=1, nn_cache_log2=0, nn_batch_cap=0, **play):
-        """play: PLAY_SETTINGS keywords (the device's coffee_search_params names)."""
+                 nn_threads=1, nn_cache_log2=0, nn_batch_cap=0, f64=False, **play):
+        """play: PLAY_SETTINGS keywords (the device's coffee_search_params names).
+        f64: search statistics in f64 (the reference's precision) instead of the
+        device's f32; node dumps (nodes/game_tree) are f32-layout only."""
+        self.L = lib(f64)
+        self.f64 = f64
         self.X, self.Y, self.W, self.games = X, Y, W, games
         self.A, self.P = X * Y, 4 * X * Y
         self.model = model
@@ -233,51 +251,53 @@ class Selfplay:
         if unknown:
             raise TypeError("unknown play settings: %s" % sorted(unknown))
         self._play = np.array([play.get(k, d) for k, d in PLAY_SETTINGS.items()], np.float32)
-        self.h = lib().ora_sp_create(X, Y, W, games, max_visits, node_cap, seed, slot_base, nn_mode,
+        self.h = self.L.ora_sp_create(X, Y, W, games, max_visits, node_cap, seed, slot_base, nn_mode,
                                      model.h if model is not None else None, nn_threads, nn_cache_log2,
                                      ptr(self._play), nn_batch_cap)
         if not self.h:
             raise RuntimeError("oracle selfplay create failed")
 
     def rounds(self, n):
-        lib().ora_sp_rounds(self.h, n)
+        self.L.ora_sp_rounds(self.h, n)
 
     def set_parallel(self, threads):
         """CPU baseline only: threads over games in select/backup (row order then
         follows thread timing; counts and per-game results are unchanged)."""
-        lib().ora_sp_set_parallel(self.h, int(threads))
+        self.L.ora_sp_set_parallel(self.h, int(threads))
 
     def info(self, slot):
         a = np.zeros(16, np.int64)
-        lib().ora_sp_game_info(self.h, slot, ptr(a))
+        self.L.ora_sp_game_info(self.h, slot, ptr(a))
         keys = ["phase", "rootK", "nodeCount", "rootIdx", "turn", "pla", "gameNum", "playouts", "nnEvals",
                 "movesMade", "gamesFinished", "rngCtr", "leafKind", "rootVisits", "lastCell", "lastDir"]
         return dict(zip(keys, a.tolist()))
 
     def nodes(self, slot, cap=4096):
+        if self.f64:
+            raise ValueError("raw node records have the f32 layout only")
         nodes = np.zeros(cap, NODE_DTYPE)
         ec = np.zeros(cap * self.P, np.uint32)
         ev = np.zeros(cap * self.P, np.uint32)
         em = np.zeros(cap * self.P, np.uint16)
         pol = np.zeros(cap * self.P, np.float32)
-        n = lib().ora_sp_game_nodes(self.h, slot, ptr(nodes), ptr(ec), ptr(ev), ptr(em), ptr(pol))
+        n = self.L.ora_sp_game_nodes(self.h, slot, ptr(nodes), ptr(ec), ptr(ev), ptr(em), ptr(pol))
         P = self.P
         return dict(nodes=nodes[:n], edge_child=ec[:n * P].reshape(n, P), edge_visits=ev[:n * P].reshape(n, P),
                     edge_move=em[:n * P].reshape(n, P), policy=pol[:n * P].reshape(n, P))
 
     def root_noised(self, slot):
         out = np.zeros(self.P, np.float32)
-        lib().ora_sp_root_noised(self.h, slot, ptr(out))
+        self.L.ora_sp_root_noised(self.h, slot, ptr(out))
         return out
 
     def rows(self):
-        n = lib().ora_sp_rows_count(self.h)
+        n = self.L.ora_sp_rows_count(self.h)
         A, P = self.A, self.P
         pb = (A + 7) // 8
         r = dict(binaryInputNCHWPacked=np.zeros((n, 15, pb), np.uint8), globalInputNC=np.zeros((n, 1), np.float32),
                  policyTargetsNCMove=np.zeros((n, 2, P), np.int16), globalTargetsNC=np.zeros((n, 64), np.float32),
                  valueTargetsNCHW=np.zeros((n, 5, self.Y, self.X), np.int8), meta=np.zeros((n, 4), np.int32))
-        lib().ora_sp_rows(self.h, ptr(r["binaryInputNCHWPacked"]), ptr(r["globalInputNC"]),
+        self.L.ora_sp_rows(self.h, ptr(r["binaryInputNCHWPacked"]), ptr(r["globalInputNC"]),
                           ptr(r["policyTargetsNCMove"]), ptr(r["globalTargetsNC"]), ptr(r["valueTargetsNCHW"]),
                           ptr(r["meta"]))
         return r
@@ -285,9 +305,9 @@ class Selfplay:
     def game_tree(self, slot, max_nodes=4096):
         nodes = np.zeros((max_nodes, 24), np.uint32)
         edges = np.zeros((max_nodes, self.P, 3), np.uint32)
-        n = lib().ora_sp_game_tree(self.h, slot, max_nodes, ptr(nodes), ptr(edges))
+        n = self.L.ora_sp_game_tree(self.h, slot, max_nodes, ptr(nodes), ptr(edges))
         return nodes[:n], edges[:n]
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().ora_sp_free(self.h)
+            self.L.ora_sp_free(self.h)
