@@ -249,19 +249,13 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
 
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
-// Copies a row-major [rows][96] f32 matrix (global, 16-B aligned) into LDS
-// transposed to [96][rows], so that threads of one wave (consecutive output
-// rows) read consecutive banks in the dot-product loops.
-KC_D void stageT96(float* __restrict__ dst, const float* __restrict__ src, int rows, int tid) {
+// Copies a [96][rows] f32 matrix (a [rows][96] linear layer the host stored
+// transposed; global, 16-B aligned) into LDS: consecutive output rows of one wave
+// read consecutive banks in the dot-product loops.  16-byte stores, no conflicts.
+KC_D void stage96(float* __restrict__ dst, const float* __restrict__ src, int rows, int tid) {
   const int n4 = rows * 24;
-  for(int q = tid; q < n4; q += NN_NT) {
-    const int o = q / 24, i4 = (q - o * 24) * 4;
-    const float4 v = reinterpret_cast<const float4*>(src)[q];
-    dst[(i4 + 0) * rows + o] = v.x;
-    dst[(i4 + 1) * rows + o] = v.y;
-    dst[(i4 + 2) * rows + o] = v.z;
-    dst[(i4 + 3) * rows + o] = v.w;
-  }
+  for(int q = tid; q < n4; q += NN_NT)
+    reinterpret_cast<float4*>(dst)[q] = reinterpret_cast<const float4*>(src)[q];
 }
 
 // The residual trunk is f32.  Between blocks it lives in the accumulators; while
@@ -382,10 +376,10 @@ KC_D void poolBoards(const float* scr, const float* vsrc, float* poolP, float* p
       if(vsrc)
         sv += vsrc[o];
     }
-    s = s + __shfl_xor(s, 1, 64);
-    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    s = s + asF(partner<5>(bitsF(s)));  // lane ^ 1 (DPP)
+    m = fmaxf(m, asF(partner<5>(bitsF(m))));
     if(vsrc)
-      sv = sv + __shfl_xor(sv, 1, 64);
+      sv = sv + asF(partner<5>(bitsF(sv)));
     if(half == 0) {
       const float mean = s / (float)G::A;
       poolP[b * 96 + c] = mean;
@@ -422,13 +416,15 @@ KC_D void linear96(const float* wT, int O, const float* in, float* out, int ostr
       s.z += w4.z * xv;
       s.w += w4.w * xv;
     }
-#pragma unroll
-    for(int m = 1; m < 4; m <<= 1) {
-      s.x += __shfl_xor(s.x, m, 64);
-      s.y += __shfl_xor(s.y, m, 64);
-      s.z += __shfl_xor(s.z, m, 64);
-      s.w += __shfl_xor(s.w, m, 64);
-    }
+    // quarters reduced over lanes ^1 then ^2 (DPP quad permutes)
+    s.x += asF(partner<5>(bitsF(s.x)));
+    s.y += asF(partner<5>(bitsF(s.y)));
+    s.z += asF(partner<5>(bitsF(s.z)));
+    s.w += asF(partner<5>(bitsF(s.w)));
+    s.x += asF(partner<4>(bitsF(s.x)));
+    s.y += asF(partner<4>(bitsF(s.y)));
+    s.z += asF(partner<4>(bitsF(s.z)));
+    s.w += asF(partner<4>(bitsF(s.w)));
     if(ks == 0) {
       float r[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
@@ -493,6 +489,14 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   h16x8* wl = reinterpret_cast<h16x8*>(smem + G::OFF_W);
   const float sqOff = sqrtf((float)G::A) - 14.0f;
 
+  // the stem's first two weight taps stream into the ring while the input is unpacked
+  {
+    constexpr int CH0 = G::NCT_ALL;  // 1-KiB pieces per stem tap (one 32-channel block)
+    const uint32_t ring = ldsAddr(wl);
+#pragma unroll
+    for(int tap = 0; tap < 2; tap++)
+      stageTapDma(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WBUF * 16, CH0, wave, lane);
+  }
   // ---- row tables; unpack the packed V1 planes into the zero-bordered act ----
   float pre = loadParam(L, WF, 0, tid);  // block 0's slab, stored after the stem conv
   for(int i = tid; i < G::NTAB; i += NN_NT)
@@ -500,13 +504,27 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   for(int idx = tid; idx < G::ACT_BYTES / 16; idx += NN_NT)
     reinterpret_cast<uint4*>(smem)[idx] = uint4{0u, 0u, 0u, 0u};
   __syncthreads();
-  for(int idx = tid; idx < nb * G::A * NUM_SPATIAL; idx += NN_NT) {
-    const int b = idx / (G::A * NUM_SPATIAL), i = idx - b * (G::A * NUM_SPATIAL);
-    const int c = i / G::A, p = i - c * G::A;
-    const int src = rowIdx ? rowIdx[base + b] : base + b;
-    const uint64_t word = in[(size_t)src * inWords + (i >> 6)];
-    if((word >> (i & 63)) & 1ULL)
-      act[padCell<G>(b, p) * G::ASTR + c] = (uint16_t)0x3c00;
+  {
+    // wave w unpacks board w: its row index and all its packed words are loaded up
+    // front (two round trips), then lane l sets bits l, l+64, ... (plane-major bits)
+    static_assert(G::NB == NN_WAVES, "one wave per board");
+    constexpr int NBITS = G::A * NUM_SPATIAL, NW = (NBITS + 63) / 64;
+    const int b = __builtin_amdgcn_readfirstlane(wave);
+    if(b < nb) {
+      const int src = rowIdx ? rowIdx[base + b] : base + b;
+      uint64_t words[NW];
+#pragma unroll
+      for(int k = 0; k < NW; k++)
+        words[k] = in[(size_t)src * inWords + k];
+#pragma unroll
+      for(int k = 0; k < NW; k++) {
+        const int i = k * 64 + lane;
+        if(i < NBITS && ((words[k] >> lane) & 1ULL)) {
+          const int c = i / G::A, p = i - c * G::A;
+          act[padCell<G>(b, p) * G::ASTR + c] = (uint16_t)0x3c00;
+        }
+      }
+    }
   }
   __syncthreads();
 
@@ -515,7 +533,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   aBases<G>(ab, rowPa, tstart, lane);
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1, true>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
+  convTiles<G, 9, 1, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                            L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL, L->nblocks > 0 ? 9 : 1);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
@@ -538,7 +556,9 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   const int Cr = G::C - L->Cg;
   NN_PHASE(2);
   for(int blk = 0; blk < L->nblocks; blk++) {
-    __syncthreads();  // previous conv finished reading act
+    // previous conv finished reading act; the parked trunk's stores (and the next
+    // conv's weight requests) stay in flight behind the epilogue below
+    barrierKeepDma();
     NN_PHASE(3 + 4 * blk);
     const float* P = prm + (blk & 1) * G::NPRM;
     storeBnRelu<G>(act, rowPa, acc, P, P + 96, tstart, cg, lane);
@@ -556,8 +576,15 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     const h16x8* nextW = lastBlk ? WB + L->wHead : WB + L->wConv1[lastBlk ? 0 : blk + 1];
     const int nextTaps = lastBlk ? 1 : 9;
     if(L->kinds[blk] == 0) {
+      // the parked trunk is requested before the epilogue, whose LDS work hides its latency
+      f32x4 tr[G::MAXT][G::NCT];
+      loadTrunk<G>(tr, trunk, wave, lane);
       storeBnRelu<G>(act, rowPa, acc, P + 192, P + 288, tstart, cg, lane);
-      loadTrunk<G>(acc, trunk, wave, lane);  // lands during the barrier / stream wait below
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+        for(int ct = 0; ct < G::NCT; ct++)
+          acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
       convTiles<G, 9, G::C / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
@@ -569,6 +596,18 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       // KataGPool per board (model_pytorch.py:326-352)
       const float* gs = P + 384;
       const float* gbias = P + 416;
+      // the gpool linear weights ([96][Cr] f32) are requested now and land in LDS
+      // after the epilogue's barrier
+      constexpr int LW = (96 * 64 / 4 + NN_NT - 1) / NN_NT;  // float4 per thread (Cr <= 64)
+      float4 lw[LW];
+      {
+        const float4* src = reinterpret_cast<const float4*>(WF + L->linG[blk]);
+#pragma unroll
+        for(int k = 0; k < LW; k++) {
+          const int q = tid + k * NN_NT;
+          lw[k] = q < Cr * 24 ? src[q] : float4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+      }
 #pragma unroll
       for(int ct = 0; ct < G::NCT; ct++) {
         const int ch = chOf<G>(cg, ct, lane);
@@ -590,12 +629,19 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       __syncthreads();
       NN_PHASE(50);
       float* lgT = actF;  // transposed linear weights in the idle front of act
-      stageT96(lgT, WF + L->linG[blk], Cr, tid);
+#pragma unroll
+      for(int k = 0; k < LW; k++) {
+        const int q = tid + k * NN_NT;
+        if(q < Cr * 24)
+          reinterpret_cast<float4*>(lgT)[q] = lw[k];
+      }
       poolBoards<G>(scr, nullptr, poolP, poolV, sqOff, tid);
       __syncthreads();
       NN_PHASE(51);
       linear96<G>(lgT, Cr, poolP, biasS, Cr, nullptr, false, tid);
       __syncthreads();
+      f32x4 tr[G::MAXT][G::NCT];  // the parked trunk, in flight during the epilogue
+      loadTrunk<G>(tr, trunk, wave, lane);
       zeroBorders<G>(act, tid);  // the f32 scratch overwrote border cells (disjoint from r-epi cells)
       NN_PHASE(52);
       {
@@ -623,7 +669,11 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
           }
         }
       }
-      loadTrunk<G>(acc, trunk, wave, lane);
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+        for(int ct = 0; ct < G::NCT; ct++)
+          acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
       convTiles<G, 9, (G::C - 32) / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
@@ -671,8 +721,8 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   float* plgT = reinterpret_cast<float*>(wl);
   float* l2T = plgT + 32 * 96;
   float* w3 = l2T + 96 * L->v2;  // value / misc output weights [4][v2], then their 4 biases
-  stageT96(plgT, WF + L->pLinG, 32, tid);
-  stageT96(l2T, WF + L->vLin2, L->v2, tid);
+  stage96(plgT, WF + L->pLinG, 32, tid);
+  stage96(l2T, WF + L->vLin2, L->v2, tid);
   {
     const int v2 = L->v2;
     for(int i = tid; i < 4 * v2 + 4; i += NN_NT) {
@@ -701,9 +751,12 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     float s = 0.0f;
     for(int i = k; i < v2; i += 16)
       s += w3[o * v2 + i] * vh[b * 64 + i];
-#pragma unroll
-    for(int m = 8; m >= 1; m >>= 1)
-      s += __shfl_xor(s, m, 64);
+    // lanes ^8, ^4, ^2, ^1 of the 16-lane group (DPP; after ^8 a partial depends only
+    // on lane mod 8, so the row rotation by 4 reaches the ^4 partner's value)
+    s += asF(partner<2>(bitsF(s)));
+    s += asF(partner<3>(bitsF(s)));
+    s += asF(partner<4>(bitsF(s)));
+    s += asF(partner<5>(bitsF(s)));
     if(k == 0 && b < nb) {
       const int dst = rowIdx ? rowIdx[base + b] : base + b;
       out[(size_t)dst * (G::P + 4) + G::P + o] = s + w3[4 * v2 + o];
@@ -735,8 +788,13 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
 #pragma unroll
         for(int j = 0; j < 4; j++)
           s += pv[j] * w2[d * 32 + c0 + j] + pv[4 + j] * w2[d * 32 + c1 + j];
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
+        {
+          int a0, a1;  // lanes ^16 then ^32 (permlane swaps)
+          swapPair<1>(bitsF(s), a0, a1);
+          s = asF(a0) + asF(a1);
+          swapPair<0>(bitsF(s), a0, a1);
+          s = asF(a0) + asF(a1);
+        }
         part[d] = s;
       }
       if((lane >> 4) == 0 && row < G::ROWS && brd < nb) {
@@ -850,6 +908,15 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
       wf.push_back(0.0f);
     return off;
   };
+  // a [rows][96] linear layer stored transposed ([96][rows]): the kernel copies it
+  // into LDS as is (stage96), the layout its dot products read
+  auto f32T = [&](const std::vector<float>& v, int rows) {
+    std::vector<float> t(v.size());
+    for(int r = 0; r < rows; r++)
+      for(int i = 0; i < 96; i++)
+        t[(size_t)i * rows + r] = v[(size_t)r * 96 + i];
+    return f32(t);
+  };
   auto bfOff = [&]() { return (int)(wb.size() / 8); };
   L.wInit = bfOff();
   packConv(wb, 9, 32, C, [&](int co, int ci, int tap) {
@@ -874,7 +941,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
       });
       L.bngs[i] = f32(b.bngs);
       L.bngb[i] = f32(b.bngb);
-      L.linG[i] = f32(b.linG);
+      L.linG[i] = f32T(b.linG, Cr);
       L.bn2s[i] = f32(b.bn2s);
       L.bn2b[i] = f32(b.bn2b);
       L.wConv2[i] = bfOff();
@@ -892,11 +959,11 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
     return m.vConv1[(size_t)(co - 64) * C + ci];
   });
   L.pBiasG = f32(m.pBiasG);
-  L.pLinG = f32(m.pLinG);
+  L.pLinG = f32T(m.pLinG, 32);
   L.pBias2 = f32(m.pBias2);
   L.pConv2 = f32(m.pConv2);
   L.vBias1 = f32(m.vBias1);
-  L.vLin2 = f32(m.vLin2);
+  L.vLin2 = f32T(m.vLin2, cfg_.v2);
   L.vB2 = f32(m.vB2);
   L.vLin3 = f32(m.vLin3);
   L.vB3 = f32(m.vB3);
