@@ -103,8 +103,10 @@ class NNEngine {
   // policy logits [4][A] in the symmetric frame, value logits (win, loss), misc[2].
   // rows [0, min(n, *countDev)) of the batch; with rowIdx, batch row r is game row rowIdx[r]
   // (input in[rowIdx[r]], output out[rowIdx[r]]), otherwise r.
+  // e0/e1 (optional): timing events, recorded by the fused kernel's dispatch itself
+  // (kernel-only time), around the layered kernels otherwise
   void forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev = nullptr,
-               const int* rowIdx = nullptr);
+               const int* rowIdx = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
   const ModelCfg& cfg() const { return cfg_; }
   double flopsPerEval() const { return flops_; }
   bool fused() const { return !layered_; }

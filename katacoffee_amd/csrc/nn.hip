@@ -21,6 +21,7 @@
 // Waves: rg = wave>>1 owns a contiguous range of 16-row tiles, cg = wave&1 owns
 // half of the output channels.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstring>
@@ -992,11 +993,15 @@ NNEngine::~NNEngine() {
 }
 
 void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev,
-                       const int* rowIdx) {
+                       const int* rowIdx, hipEvent_t e0, hipEvent_t e1) {
   if(n <= 0)
     return;
   if(layered_) {
+    if(e0)
+      KC_HIP(hipEventRecord(e0, st));
     layered_->forward(n, in, out, st, countDev, rowIdx);
+    if(e1)
+      KC_HIP(hipEventRecord(e1, st));
     return;
   }
   using G = NNGeo<5, 5, 96>;
@@ -1011,8 +1016,13 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
     KC_HIP(hipMalloc(&trunk_, (size_t)grid * NN_WAVES * G::MAXT * G::NCT * 64 * 16));
     trunkCap_ = grid;
   }
-  hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_,
-                     (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
+  if(e0)
+    hipExtLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, e0, e1, 0, layoutDev_,
+                          (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out,
+                          trunk_);
+  else
+    hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_,
+                       (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
   KC_HIP(hipGetLastError());
 }
 

@@ -301,11 +301,15 @@ struct SearchDev {
 
 // Kernel launchers (search.hip).
 void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
-void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+// e0/e1 (optional): events recorded at the kernel's start and end (hipExtLaunchKernel),
+// so the bench times the kernel itself, not the stream gaps around it
+void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
+                  hipEvent_t e1 = nullptr);
 // accumulate: add the batch size to *d.nnTimedEvals (rounds whose network launch is timed)
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate);
 void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st);
-void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st);
+void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
+                  hipEvent_t e1 = nullptr);
 void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);  // + kRows
 void launchGameTree(const SearchDev* dd, int slot, int maxNodes, uint32_t* nodesOut, uint32_t* edgesOut,
                     int32_t* count, hipStream_t st);

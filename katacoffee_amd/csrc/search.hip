@@ -14,6 +14,7 @@
 // functions are detmath.h's dlog/dexp/dpow, and the file is compiled with
 // -ffp-contract=off and correctly rounded division/sqrt.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "detmath.h"
 #include "engine.h"
@@ -3432,20 +3433,32 @@ void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   KC_HIP(hipGetLastError());
 }
 
-void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+// A launch, with start/end events recorded by the dispatch itself when given.
+template <class K, class... Args>
+static void launchEv(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, hipEvent_t e0, hipEvent_t e1,
+                     Args... args) {
+  if(e0)
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, st, e0, e1, 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+}
+
+void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const DTables* T = d.T;
   switch(laneItems(d.P)) {
-    case 2: hipLaunchKernelGGL(kSelect<2>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
-    case 4: hipLaunchKernelGGL(kSelect<4>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
-    default: hipLaunchKernelGGL(kSelect<7>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
+    case 2: launchEv(kSelect<2>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+    case 4: launchEv(kSelect<4>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+    default: launchEv(kSelect<7>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
   }
   KC_HIP(hipGetLastError());
 }
 
-void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const DTables* T = d.T;
   switch(laneItems(d.P)) {
-    case 2: hipLaunchKernelGGL(kBackup<2>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
-    case 4: hipLaunchKernelGGL(kBackup<4>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
-    default: hipLaunchKernelGGL(kBackup<7>, dim3(d.G), dim3(64), 0, st, dd, d.T); break;
+    case 2: launchEv(kBackup<2>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+    case 4: launchEv(kBackup<4>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+    default: launchEv(kBackup<7>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
   }
   KC_HIP(hipGetLastError());
 }

@@ -282,6 +282,16 @@ void SelfplayEngine::timed(int which, hipStream_t st, const std::function<void()
   pending_.push_back({which, a, b});
 }
 
+void SelfplayEngine::timedKernel(int which, bool on, const std::function<void(hipEvent_t, hipEvent_t)>& f) {
+  if(!on) {
+    f(nullptr, nullptr);
+    return;
+  }
+  hipEvent_t a = takeEvent(), b = takeEvent();
+  f(a, b);
+  pending_.push_back({which, a, b});
+}
+
 void SelfplayEngine::resolveTiming() {
   for(const PendingTiming& p : pending_) {
     KC_HIP(hipEventSynchronize(p.b));
@@ -301,21 +311,24 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
   const SearchDev& d = hd_;
   for(int r = 0; r < rounds; r++) {
     const bool t0 = sampleNow(0), t1 = sampleNow(1), t2 = sampleNow(2);
-    timed(0, st, [&] {
-      launchSelect(d, dd_, st);
-      launchCompact(d, dd_, st, t1);
-    }, t0);
-    timed(1, st, [&] {
+    // select, network and backup are timed by their own dispatches (kernel start to
+    // end, like rocprofv3); compact and cache write run untimed between them
+    timedKernel(0, t0, [&](hipEvent_t a, hipEvent_t b) { launchSelect(d, dd_, st, a, b); });
+    launchCompact(d, dd_, st, t1);
+    timedKernel(1, t1, [&](hipEvent_t a, hipEvent_t b) {
       const int rows = std::min(d.G, d.nnCap);  // grid bound; the batch is *d.nnCount rows
-      if(nn_)
-        nn_->forward(rows, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
-      else
+      if(nn_) {
+        nn_->forward(rows, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx, a, b);
+      } else {
+        if(a)
+          KC_HIP(hipEventRecord(a, st));
         launchFakeNet(T_, rows, d.nnIn, d.nnOut, st, d.nnCount, d.nnIdx);
-    }, t1);
-    timed(2, st, [&] {
-      launchBackup(d, dd_, st);
-      launchCacheWrite(d, dd_, st);
-    }, t2);
+        if(b)
+          KC_HIP(hipEventRecord(b, st));
+      }
+    });
+    timedKernel(2, t2, [&](hipEvent_t a, hipEvent_t b) { launchBackup(d, dd_, st, a, b); });
+    launchCacheWrite(d, dd_, st);
     rounds_++;
     if(rounds_ % (uint64_t)commitInterval_ == 0 || r == rounds - 1) {
       const bool t3 = sampleNow(3);

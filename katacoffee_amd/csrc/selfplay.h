@@ -41,6 +41,7 @@ class SelfplayEngine {
     hipEvent_t a, b;
   };
   void timed(int which, hipStream_t st, const std::function<void()>& f, bool on);
+  void timedKernel(int which, bool on, const std::function<void(hipEvent_t, hipEvent_t)>& f);
   bool sampleNow(int which) { return timingEvery_ > 0 && groupLaunches_[which]++ % (uint64_t)timingEvery_ == 0; }
   hipEvent_t takeEvent();
   void resolveTiming();
