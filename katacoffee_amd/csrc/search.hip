@@ -3227,31 +3227,40 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
 
 // kCacheWrite: the winning bidder of every cache slot stores its evaluation (runs
 // after kBackup, before the next kSelect reads the cache).
-__global__ void __launch_bounds__(64) kCacheWrite(const SearchDev* __restrict__ dp) {
+// One game per wave, four waves per block: a quarter of the blocks of one block per
+// game (the per-game work is a chain of a few dependent loads and one P-float copy,
+// so games are not serialised within a wave).
+constexpr int CW_GAMES_PER_WAVE = 1, CW_WAVES = 4;
+__global__ void __launch_bounds__(64 * CW_WAVES) kCacheWrite(const SearchDev* __restrict__ dp) {
   const SearchDev& d = *dp;
-  const int g = blockIdx.x;
-  if(g >= d.G || !d.games[g].cBid)
-    return;
   const int lane = laneId();
-  const uint32_t slot = (uint32_t)d.games[g].cSlot;
-  const bool won = d.cTag[slot] == (uint32_t)g + 1u;
-  if(won) {
-    const int P = d.P;
-    const float* st = d.cStage + (size_t)g * (P + 2);
-    for(int p = lane; p < P; p += 64)
-      d.cPol[(size_t)slot * P + p] = st[p];
-    if(lane == 0) {
-      d.cVal[2 * (size_t)slot] = st[P];
-      d.cVal[2 * (size_t)slot + 1] = st[P + 1];
-      d.cKey[2 * (size_t)slot] = d.cStageKey[2 * (size_t)g];
-      d.cKey[2 * (size_t)slot + 1] = d.cStageKey[2 * (size_t)g + 1];
+  const int wave = blockIdx.x * CW_WAVES + (int)(threadIdx.x >> 6);
+  for(int k = 0; k < CW_GAMES_PER_WAVE; k++) {
+    const int g = wave * CW_GAMES_PER_WAVE + k;
+    if(g >= d.G)
+      break;
+    if(!d.games[g].cBid)
+      continue;
+    const uint32_t slot = (uint32_t)d.games[g].cSlot;
+    const bool won = d.cTag[slot] == (uint32_t)g + 1u;
+    if(won) {
+      const int P = d.P;
+      const float* st = d.cStage + (size_t)g * (P + 2);
+      for(int p = lane; p < P; p += 64)
+        d.cPol[(size_t)slot * P + p] = st[p];
+      if(lane == 0) {
+        d.cVal[2 * (size_t)slot] = st[P];
+        d.cVal[2 * (size_t)slot + 1] = st[P + 1];
+        d.cKey[2 * (size_t)slot] = d.cStageKey[2 * (size_t)g];
+        d.cKey[2 * (size_t)slot + 1] = d.cStageKey[2 * (size_t)g + 1];
+      }
     }
-  }
-  __syncthreads();
-  if(lane == 0) {
-    if(won)
-      d.cTag[slot] = 0;
-    d.games[g].cBid = 0;
+    waveSync();
+    if(lane == 0) {
+      if(won)
+        d.cTag[slot] = 0;
+      d.games[g].cBid = 0;
+    }
   }
 }
 
@@ -3265,28 +3274,42 @@ __global__ void __launch_bounds__(64) kCacheWrite(const SearchDev* __restrict__ 
 // accumulate != 0: the count is also added to *d.nnTimedEvals (sampled kernel timing).
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
-  __shared__ int partHi[1024], partLo[1024];
-  const int t = threadIdx.x, per = (d.G + 1023) / 1024;
+  __shared__ uint32_t wsum[16], wpre[17];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = (d.G + 1023) / 1024;
   const int lo = t * per, hi = min(d.G, lo + per);
   const int p = *d.nnRR;
-  int ch = 0, cl = 0;
-  for(int i = lo; i < hi; i++) {
-    const int need = d.nnNeed[i];
-    ch += i >= p ? need : 0;
-    cl += i < p ? need : 0;
+  // needing games at or past the round-robin pointer count in the high half, the
+  // others (taken after them) in the low half: one scan of packed counts (G < 65536)
+  uint32_t c = 0;
+  for(int i = lo; i < hi; i++)
+    c += d.nnNeed[i] ? (i >= p ? 0x10000u : 1u) : 0u;
+  uint32_t incl = c;
+#pragma unroll
+  for(int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = (uint32_t)__shfl_up((int)incl, off, 64);
+    if(lane >= off)
+      incl += v;
   }
-  partHi[t] = ch;
-  partLo[t] = cl;
+  if(lane == 63)
+    wsum[w] = incl;
   __syncthreads();
-  for(int off = 1; off < 1024; off <<= 1) {  // inclusive scans
-    const int vh = t >= off ? partHi[t - off] : 0, vl = t >= off ? partLo[t - off] : 0;
-    __syncthreads();
-    partHi[t] += vh;
-    partLo[t] += vl;
-    __syncthreads();
+  if(t < 64) {
+    uint32_t x = t < 16 ? wsum[t] : 0u, xi = x;
+#pragma unroll
+    for(int off = 1; off < 16; off <<= 1) {
+      const uint32_t v = (uint32_t)__shfl_up((int)xi, off, 64);
+      if(t >= off)
+        xi += v;
+    }
+    if(t < 16)
+      wpre[t] = xi - x;
+    if(t == 15)
+      wpre[16] = xi;
   }
-  const int totalHi = partHi[1023], total = totalHi + partLo[1023], cap = d.nnCap;
-  int oh = partHi[t] - ch, ol = totalHi + partLo[t] - cl;
+  __syncthreads();
+  const uint32_t excl = wpre[w] + incl - c, all = wpre[16];
+  const int totalHi = (int)(all >> 16), total = totalHi + (int)(all & 0xFFFFu), cap = d.nnCap;
+  int oh = (int)(excl >> 16), ol = totalHi + (int)(excl & 0xFFFFu);
   for(int i = lo; i < hi; i++) {
     if(!d.nnNeed[i]) {
       d.nnDefer[i] = 0;
@@ -3429,7 +3452,8 @@ void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool
 void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   if(!d.cacheOn)
     return;
-  hipLaunchKernelGGL(kCacheWrite, dim3(d.G), dim3(64), 0, st, dd);
+  const int per = CW_GAMES_PER_WAVE * CW_WAVES;
+  hipLaunchKernelGGL(kCacheWrite, dim3((d.G + per - 1) / per), dim3(64 * CW_WAVES), 0, st, dd);
   KC_HIP(hipGetLastError());
 }
 

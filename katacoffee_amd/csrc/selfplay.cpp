@@ -88,6 +88,8 @@ static T* devAlloc(std::vector<void*>& owned, size_t count, bool zero = true) {
 SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   if(c.num_games <= 0)
     throw std::invalid_argument("num_games must be positive");
+  if(c.num_games > 65535)  // kCompact packs two per-device game counts into 16-bit halves
+    throw std::invalid_argument("num_games must be <= 65535 per device");
   const coffee_search_params& sp = c.search;
   if(sp.max_visits < 1 || sp.root_num_symmetries_to_sample < 1 || sp.root_num_symmetries_to_sample > 4)
     throw std::invalid_argument("search params: max_visits >= 1 and 1 <= root_num_symmetries_to_sample <= 4");
