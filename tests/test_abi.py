@@ -50,6 +50,9 @@ def test_abi_version_and_defaults(L):
     assert p.cheap_search_prob == 0.0 and p.reduce_visits == 0
     assert p.policy_surprise_data_weight == 0.0 and p.value_surprise_data_weight == 0.0
     assert p.cheap_search_visits == 100 and p.reduced_visits_min == 100
+    # PlaySettings defaults the reference's selfplay loader leaves in place (playsettings.cpp:14)
+    assert p.side_position_prob == 0.0
+    assert p.record_tree_positions == 0 and p.record_tree_threshold == 0 and p.record_tree_target_weight == 0.0
 
 
 def test_invalid_arguments_fail_loudly(L):

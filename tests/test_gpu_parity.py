@@ -354,6 +354,13 @@ def test_selfplay_tree_positions_bit_exact_vs_oracle(X, Y, W, games, visits, rou
     gpu.close()
 
 
+def test_tree_position_weight_above_one_rejected():
+    """play.cpp:1349-1350: recordTreeTargetWeight > 1 is an error."""
+    with pytest.raises(kc.CoffeeError):
+        kc.Selfplay(5, 5, 4, num_games=2, max_visits=8, node_cap=64, record_tree_positions=1,
+                    record_tree_target_weight=1.5)
+
+
 def test_selfplay_full_scale_sampled_slots_bit_exact():
     """C2 scale on the device (4096 games, 600 visits, node_cap 2048, deep trees) with
     the stand-in network; 12 sampled slots replayed one by one in the oracle from the
