@@ -1950,18 +1950,36 @@ KC_D int chooseIndex(const GV& v, DRng& rng, const float* vals, int n, float tem
   return bcastI(chosen, 0);
 }
 
+// 16-byte stores where the arrays allow (every per-game slice starts 16-B aligned when
+// its length is a multiple of 4 words), one word at a time otherwise.
+KC_D void fillWords(uint32_t* p, int n, uint32_t val, int lane) {
+  if((n & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    for(int i = lane; i < n / 4; i += 64)
+      q[i] = uint4{val, val, val, val};
+  } else {
+    for(int i = lane; i < n; i += 64)
+      p[i] = val;
+  }
+}
+
 KC_D void clearTables(const GV& v, GameDev& s) {
   const int cap = v.d.cap;
   uint32_t* fl = v.freeList();
-  for(int i = v.lane; i < cap; i += 64)
-    fl[i] = (uint32_t)(cap - 1 - i);  // pop order: 0, 1, 2, ...
-  for(int i = v.lane; i < cap / 32; i += 64)
-    v.allocBits()[i] = 0;
-  for(int i = v.lane; i < v.d.ttCap; i += 64)
-    v.ttNode()[i] = -1;
+  if((cap & 3) == 0 && (reinterpret_cast<uintptr_t>(fl) & 15) == 0) {
+    uint4* q = reinterpret_cast<uint4*>(fl);
+    for(int i = v.lane; i < cap / 4; i += 64) {
+      const uint32_t b = (uint32_t)(cap - 1 - 4 * i);  // pop order: 0, 1, 2, ...
+      q[i] = uint4{b, b - 1, b - 2, b - 3};
+    }
+  } else {
+    for(int i = v.lane; i < cap; i += 64)
+      fl[i] = (uint32_t)(cap - 1 - i);
+  }
+  fillWords(v.allocBits(), cap / 32, 0u, v.lane);
+  fillWords(reinterpret_cast<uint32_t*>(v.ttNode()), v.d.ttCap, 0xFFFFFFFFu, v.lane);
   const size_t sb = v.svbBase(s.svbSel);
-  for(int i = v.lane; i < v.d.svbCap; i += 64)
-    v.d.svbKey[sb + i] = 0;
+  fillWords(reinterpret_cast<uint32_t*>(&v.d.svbKey[sb]), 2 * v.d.svbCap, 0u, v.lane);
   s.freeTop = cap;
   s.liveCount = 0;
   s.rootIdx = -1;
