@@ -186,7 +186,7 @@ struct GameDev {
   int32_t phase, rootK;
   uint32_t syms;                  // four root symmetries, 4 bits each
   int32_t cSlot;                  // NN-cache slot of the leaf (hit or bid)
-  int32_t cBid;                   // 1: this round's evaluation bids for cSlot
+  float cHitWin, cHitLoss;        // a cache hit's values, read by kSelect with the key
   int32_t noNoise;                // this move is a cheap search without recorded rows
   int32_t visitLimit;             // this move's maxVisits (getSearchLimitsThisMove)
   float moveWeight;               // this move's target weight
@@ -264,6 +264,7 @@ struct SearchDev {
   DPtr<int32_t> nnIdx;        // [G] compacted rows to evaluate (kCompact)
   DPtr<int32_t> nnCount;      // rows in nnIdx
   DPtr<int32_t> nnDefer;      // [G] 1: the row did not fit this round's batch (kCompact); the game waits
+  DPtr<uint32_t> nnBid;       // [G] cache slot the row's evaluation bids for (~0u: none), kCompact bids
   int nnCap;             // rows per network launch (batch cap: one full wave of network workgroups)
   DPtr<int32_t> nnRR;         // round-robin start of the next batch (kCompact)
   DPtr<unsigned long long> nnTimedEvals;  // summed nnCount of the rounds whose network launch was timed
@@ -274,8 +275,6 @@ struct SearchDev {
   DPtr<float> cPol;           // [entries][P] post-processed policy (illegal = -1)
   DPtr<float> cVal;           // [entries][2] white win / loss
   DPtr<uint32_t> cTag;        // [entries] this round's highest bidding game + 1 (0 = none)
-  DPtr<float> cStage;         // [G][P+2] a bidding game's payload
-  DPtr<uint64_t> cStageKey;   // [G][2]
   // commit queue
   DPtr<FinRec> fin;           // [G] games finished by the current commit (kRows)
   DPtr<ForkRec> fork;         // [G] fork state (PH_FORK)
@@ -307,7 +306,6 @@ void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEv
                   hipEvent_t e1 = nullptr);
 // accumulate: add the batch size to *d.nnTimedEvals (rounds whose network launch is timed)
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate);
-void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
                   hipEvent_t e1 = nullptr);
 void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);  // + kRows

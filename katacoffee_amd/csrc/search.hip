@@ -1086,12 +1086,32 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     descend<NI>(v, s, hasBits, rootPol);
     if(s.leafKind == LEAF_NN && d.cacheOn) {
       // NN evaluation cache (SPEC a7): a state evaluated in an earlier round by any
-      // game is taken from the cache instead of the network
+      // game is taken from the cache instead of the network.  The payload is loaded
+      // with the key and a hit copies it into the leaf's policy here: this round's
+      // kBackup writes the winning bidders' evaluations into the table.
       const uint64_t k0 = v.nodeKey(s.leafNode)[0], k1 = v.nodeKey(s.leafNode)[1];
       const uint32_t slot = cacheSlot(k0, k1, d.cacheMask);
+      const int P = d.P;
+      const float* cp = d.cPol + (size_t)slot * P;
+      float pv[NI];
+#pragma unroll
+      for(int j = 0; j < NI; j++) {
+        const int pos = v.lane + 64 * j;
+        pv[j] = pos < P ? cp[pos] : 0.0f;
+      }
+      const float cw = d.cVal[2 * (size_t)slot], cl = d.cVal[2 * (size_t)slot + 1];
+      s.cSlot = (int32_t)slot;
       if(d.cKey[2 * (size_t)slot] == k0 && d.cKey[2 * (size_t)slot + 1] == k1) {
         s.leafKind = LEAF_CACHED;
-        s.cSlot = (int32_t)slot;
+        s.cHitWin = cw;
+        s.cHitLoss = cl;
+        float* pol = v.pol(s.leafNode);
+#pragma unroll
+        for(int j = 0; j < NI; j++) {
+          const int pos = v.lane + 64 * j;
+          if(pos < P)
+            pol[pos] = pv[j];
+        }
       }
     }
     if(s.leafKind == LEAF_NN)
@@ -1103,8 +1123,11 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   const bool needNN =
       s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT || s.leafKind == LEAF_FORK ||
       s.leafKind == LEAF_SIDE;
-  if(v.lane == 0)
+  if(v.lane == 0) {
     d.nnNeed[g] = needNN ? 1 : 0;
+    if(needNN)
+      d.nnBid[g] = s.leafKind == LEAF_NN && d.cacheOn ? (uint32_t)s.cSlot : ~0u;
+  }
   if(needNN) {
     // the game's own batch row: no shared counter (a same-address atomic from
     // every block serialises at L2); kCompact lists the rows the network evaluates
@@ -1544,37 +1567,36 @@ __global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* 
         probeLeafKey(v.nodeKey(s.leafNode)[0], v.nodeKey(s.leafNode)[1]);
 #endif
       if(s.leafKind == LEAF_CACHED) {
-        const float* cp = d.cPol + (size_t)s.cSlot * P;
+        // copied from the cache into the leaf's policy by kSelect
 #pragma unroll
         for(int j = 0; j < NI; j++) {
           const int pos = v.lane + 64 * j;
-          pv[j] = pos < P ? cp[pos] : -1.0f;
-          if(pos < P)
-            pol[pos] = pv[j];
+          pv[j] = pos < P ? pol[pos] : -1.0f;
         }
-        w = d.cVal[2 * (size_t)s.cSlot];
-        l = d.cVal[2 * (size_t)s.cSlot + 1];
+        w = s.cHitWin;
+        l = s.cHitLoss;
       } else {
         postprocess<NI>(v, s.leaf, s.leafSym, o, pol, w, l, scratch, pv);
         if(d.cacheOn) {
-          // bid for the state's cache slot; kCacheWrite stores the highest bidder's
-          // payload after this kernel (deterministic whatever the block order)
-          const uint64_t k0 = v.nodeKey(s.leafNode)[0], k1 = v.nodeKey(s.leafNode)[1];
-          const uint32_t slot = cacheSlot(k0, k1, d.cacheMask);
-          float* st = d.cStage + (size_t)g * (P + 2);
+          // kCompact bid this evaluation for the state's cache slot (atomicMax of
+          // game + 1 over the round's batch); the highest bidder stores its payload
+          // and clears the tag, deterministic whatever the block order.  Nothing
+          // reads the table in this kernel (hits were copied by kSelect).
+          const uint32_t slot = (uint32_t)s.cSlot;
+          if(d.cTag[slot] == (uint32_t)g + 1u) {
+            float* cp = d.cPol + (size_t)slot * P;
 #pragma unroll
-          for(int j = 0; j < NI; j++)
-            if(v.lane + 64 * j < P)
-              st[v.lane + 64 * j] = pv[j];
-          if(v.lane == 0) {
-            st[P] = w;
-            st[P + 1] = l;
-            d.cStageKey[2 * (size_t)g] = k0;
-            d.cStageKey[2 * (size_t)g + 1] = k1;
-            atomicMax(&d.cTag[slot], (uint32_t)g + 1u);
+            for(int j = 0; j < NI; j++)
+              if(v.lane + 64 * j < P)
+                cp[v.lane + 64 * j] = pv[j];
+            if(v.lane == 0) {
+              d.cVal[2 * (size_t)slot] = w;
+              d.cVal[2 * (size_t)slot + 1] = l;
+              d.cKey[2 * (size_t)slot] = v.nodeKey(s.leafNode)[0];
+              d.cKey[2 * (size_t)slot + 1] = v.nodeKey(s.leafNode)[1];
+              d.cTag[slot] = 0;
+            }
           }
-          s.cSlot = (int32_t)slot;
-          s.cBid = 1;
         }
       }
       buildOrder<NI>(v, s.leafNode, pv, scratch);
@@ -3243,45 +3265,6 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   SPROF_FLUSH();
 }
 
-// kCacheWrite: the winning bidder of every cache slot stores its evaluation (runs
-// after kBackup, before the next kSelect reads the cache).
-// One game per wave, four waves per block: a quarter of the blocks of one block per
-// game (the per-game work is a chain of a few dependent loads and one P-float copy,
-// so games are not serialised within a wave).
-constexpr int CW_GAMES_PER_WAVE = 1, CW_WAVES = 4;
-__global__ void __launch_bounds__(64 * CW_WAVES) kCacheWrite(const SearchDev* __restrict__ dp) {
-  const SearchDev& d = *dp;
-  const int lane = laneId();
-  const int wave = blockIdx.x * CW_WAVES + (int)(threadIdx.x >> 6);
-  for(int k = 0; k < CW_GAMES_PER_WAVE; k++) {
-    const int g = wave * CW_GAMES_PER_WAVE + k;
-    if(g >= d.G)
-      break;
-    if(!d.games[g].cBid)
-      continue;
-    const uint32_t slot = (uint32_t)d.games[g].cSlot;
-    const bool won = d.cTag[slot] == (uint32_t)g + 1u;
-    if(won) {
-      const int P = d.P;
-      const float* st = d.cStage + (size_t)g * (P + 2);
-      for(int p = lane; p < P; p += 64)
-        d.cPol[(size_t)slot * P + p] = st[p];
-      if(lane == 0) {
-        d.cVal[2 * (size_t)slot] = st[P];
-        d.cVal[2 * (size_t)slot + 1] = st[P + 1];
-        d.cKey[2 * (size_t)slot] = d.cStageKey[2 * (size_t)g];
-        d.cKey[2 * (size_t)slot + 1] = d.cStageKey[2 * (size_t)g + 1];
-      }
-    }
-    waveSync();
-    if(lane == 0) {
-      if(won)
-        d.cTag[slot] = 0;
-      d.games[g].cBid = 0;
-    }
-  }
-}
-
 // kCompact: the list of games whose row the network evaluates this round, at most
 // d.nnCap rows (one full wave of network workgroups: a launch's cost steps with its
 // number of workgroup waves).  The needing games are taken in cyclic game order from
@@ -3290,17 +3273,41 @@ __global__ void __launch_bounds__(64 * CW_WAVES) kCacheWrite(const SearchDev* __
 // are deferred (nnDefer): their games keep their leaf and skip the next select.  The
 // oracle applies the same rule (ora_search.cpp selfplayRound).
 // accumulate != 0: the count is also added to *d.nnTimedEvals (sampled kernel timing).
+// The thread's need flags and cache bids are loaded once, before the scan (16-byte
+// loads when its G / 1024 games are a multiple of 4, up to CP_VEC), so the kernel
+// waits for one round of loads instead of one per game.
+constexpr int CP_VEC = 16;
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
   __shared__ uint32_t wsum[16], wpre[17];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = (d.G + 1023) / 1024;
   const int lo = t * per, hi = min(d.G, lo + per);
   const int p = *d.nnRR;
+  const bool vec = per <= CP_VEC && (per & 3) == 0 && (d.G & 3) == 0;
+  uint64_t need = 0;  // bit k: game lo + k needs the network (per <= 64)
+  uint32_t bids[CP_VEC];
+  if(vec) {
+#pragma unroll
+    for(int q = 0; q < CP_VEC / 4; q++) {
+      bids[4 * q] = bids[4 * q + 1] = bids[4 * q + 2] = bids[4 * q + 3] = ~0u;
+      if(4 * q < per && lo + 4 * q < d.G) {
+        const int4 a = *reinterpret_cast<const int4*>(&d.nnNeed[lo + 4 * q]);
+        const uint4 b = *reinterpret_cast<const uint4*>(&d.nnBid[lo + 4 * q]);
+        need |= (uint64_t)((a.x ? 1u : 0u) | (a.y ? 2u : 0u) | (a.z ? 4u : 0u) | (a.w ? 8u : 0u)) << (4 * q);
+        bids[4 * q] = b.x;
+        bids[4 * q + 1] = b.y;
+        bids[4 * q + 2] = b.z;
+        bids[4 * q + 3] = b.w;
+      }
+    }
+  } else {
+    for(int i = lo; i < hi; i++)
+      need |= (uint64_t)(d.nnNeed[i] ? 1u : 0u) << (i - lo);
+  }
   // needing games at or past the round-robin pointer count in the high half, the
   // others (taken after them) in the low half: one scan of packed counts (G < 65536)
-  uint32_t c = 0;
-  for(int i = lo; i < hi; i++)
-    c += d.nnNeed[i] ? (i >= p ? 0x10000u : 1u) : 0u;
+  const uint64_t atOrPast = p <= lo ? ~0ull : (p - lo >= 64 ? 0ull : ~0ull << (p - lo));
+  const uint32_t c = ((uint32_t)__popcll(need & atOrPast) << 16) + (uint32_t)__popcll(need & ~atOrPast);
   uint32_t incl = c;
 #pragma unroll
   for(int off = 1; off < 64; off <<= 1) {
@@ -3328,18 +3335,36 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
   const uint32_t excl = wpre[w] + incl - c, all = wpre[16];
   const int totalHi = (int)(all >> 16), total = totalHi + (int)(all & 0xFFFFu), cap = d.nnCap;
   int oh = (int)(excl >> 16), ol = totalHi + (int)(excl & 0xFFFFu);
-  for(int i = lo; i < hi; i++) {
-    if(!d.nnNeed[i]) {
-      d.nnDefer[i] = 0;
-      continue;
-    }
+  auto place = [&](int i, uint32_t bid) {
     const int pos = i >= p ? oh++ : ol++;
     const bool in = pos < cap;
-    if(in)
+    if(in) {
       d.nnIdx[pos] = i;
+      // the evaluation's bid for its NN-cache slot (kBackup: the highest game stores it)
+      if(bid != ~0u)
+        atomicMax(&d.cTag[bid], (uint32_t)i + 1u);
+    }
     d.nnDefer[i] = in ? 0 : 1;
     if(total > cap && pos == cap - 1)
       *d.nnRR = i + 1 < d.G ? i + 1 : 0;
+  };
+  if(vec) {
+#pragma unroll
+    for(int k = 0; k < CP_VEC; k++) {
+      if(k < per && lo + k < d.G) {
+        if((need >> k) & 1u)
+          place(lo + k, bids[k]);
+        else
+          d.nnDefer[lo + k] = 0;
+      }
+    }
+  } else {
+    for(int i = lo; i < hi; i++) {
+      if((need >> (i - lo)) & 1u)
+        place(i, d.nnBid[i]);
+      else
+        d.nnDefer[i] = 0;
+    }
   }
   if(t == 1023) {
     const int count = min(total, cap);
@@ -3464,14 +3489,6 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate) {
   (void)d;
   hipLaunchKernelGGL(kCompact, dim3(1), dim3(1024), 0, st, dd, accumulate ? 1 : 0);
-  KC_HIP(hipGetLastError());
-}
-
-void launchCacheWrite(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
-  if(!d.cacheOn)
-    return;
-  const int per = CW_GAMES_PER_WAVE * CW_WAVES;
-  hipLaunchKernelGGL(kCacheWrite, dim3((d.G + per - 1) / per), dim3(64 * CW_WAVES), 0, st, dd);
   KC_HIP(hipGetLastError());
 }
 

@@ -202,6 +202,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.rDropped = devAlloc<unsigned long long>(owned_, 1);
   d.nnNeed = devAlloc<int32_t>(owned_, G);
   d.nnDefer = devAlloc<int32_t>(owned_, G);
+  d.nnBid = devAlloc<uint32_t>(owned_, G);
   d.nnRR = devAlloc<int32_t>(owned_, 1);
   if(c.nn_batch_cap < 0)
     throw std::invalid_argument("nn_batch_cap must be >= 0");
@@ -226,8 +227,6 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     d.cPol = devAlloc<float>(owned_, entries * P, false);
     d.cVal = devAlloc<float>(owned_, entries * 2, false);
     d.cTag = devAlloc<uint32_t>(owned_, entries);
-    d.cStage = devAlloc<float>(owned_, (size_t)G * (P + 2), false);
-    d.cStageKey = devAlloc<uint64_t>(owned_, (size_t)G * 2, false);
   }
   d.gCap = 2 * G;
   d.gRec = devAlloc<GameRec>(owned_, (size_t)d.gCap, false);
@@ -330,7 +329,6 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
       }
     });
     timedKernel(2, t2, [&](hipEvent_t a, hipEvent_t b) { launchBackup(d, dd_, st, a, b); });
-    launchCacheWrite(d, dd_, st);
     rounds_++;
     if(rounds_ % (uint64_t)commitInterval_ == 0 || r == rounds - 1) {
       const bool t3 = sampleNow(3);
