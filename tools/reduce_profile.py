@@ -22,13 +22,25 @@ def main():
     if kind == "trace":
         path = os.path.join(d, prefix + "_kernel_trace.csv")
         dur = collections.defaultdict(list)
+        seq = []
         for r in csv.DictReader(open(path)):
-            dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            dur[short(r["Kernel_Name"])].append(b - a)
+            seq.append((a, b, short(r["Kernel_Name"])))
+        # idle time between consecutive dispatches, per (previous -> next) kernel pair
+        seq.sort()
+        gaps = collections.defaultdict(list)
+        for (a0, b0, k0), (a1, b1, k1) in zip(seq, seq[1:]):
+            if 0 <= a1 - b0 < 1000000:
+                gaps[k0 + "->" + k1].append(a1 - b0)
         out = {}
         for k, v in dur.items():
             v.sort()
             out[k] = {"calls": len(v), "avg_ns": sum(v) / len(v), "p10_ns": v[len(v) // 10], "p50_ns": v[len(v) // 2],
                       "p90_ns": v[(9 * len(v)) // 10], "max_ns": v[-1]}
+        for k, v in gaps.items():
+            v.sort()
+            out["gap " + k] = {"calls": len(v), "avg_ns": sum(v) / len(v), "p50_ns": v[len(v) // 2]}
         json.dump(out, open(os.path.join(d, prefix + "_durations.json"), "w"), indent=1)
         os.remove(path)
     else:
