@@ -123,9 +123,14 @@ class NNEngine {
   void* wHalf_ = nullptr;  // device
   float* wF32_ = nullptr;  // device
   NNLayout* layoutDev_ = nullptr;
-  uint16_t* tabDev_ = nullptr;  // device row tables (nn.hip rowTables)
-  float* trunk_ = nullptr;      // f32 residual trunk scratch, [workgroup][fragment] (nn.hip)
-  int trunkCap_ = 0;            // workgroups it covers
+  uint16_t* tabDev_ = nullptr;   // device row tables (nn.hip rowTables), 8 boards per workgroup
+  uint16_t* tabDev4_ = nullptr;  // the same for 4 boards per workgroup
+  float* trunk_ = nullptr;       // f32 residual trunk scratch, [workgroup][fragment] (nn.hip)
+  size_t trunkBytes_ = 0;        // its size
+  int cus_ = 1;                  // compute units of the engine's device
+  template <class G>
+  void launch(int n, int inWords, const uint16_t* tab, const uint64_t* in, float* out, hipStream_t st,
+              const int* countDev, const int* rowIdx, hipEvent_t e0, hipEvent_t e1);
   std::unique_ptr<NNLayered> layered_;
 };
 

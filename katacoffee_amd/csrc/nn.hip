@@ -40,10 +40,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int NN_WAVES = 8;  // waves per workgroup (4 per SIMD)
 constexpr int NN_NT = NN_WAVES * 64;
 
-template <int X_, int Y_, int C_>
+template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
-  static constexpr int NB = NN_BOARDS_PER_WG;
+  static constexpr int NB = NB_;  // boards per workgroup (8, or 4 for batches of at most 4 per CU)
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
   // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): output
@@ -66,7 +66,8 @@ struct NNGeo {
   static constexpr int ACT_BYTES = (PROWS * ROWB + 15) / 16 * 16;
   // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
-  static constexpr int OFF_SCR = MROWS * SCR * 4;
+  // (at least the gpool linear weights' [96][64] f32, staged below it, for 4 boards)
+  static constexpr int OFF_SCR = MROWS * SCR * 4 > 96 * 64 * 4 ? MROWS * SCR * 4 : 96 * 64 * 4;
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
@@ -80,8 +81,8 @@ struct NNGeo {
   static constexpr int OFF_W = OFF_PRM + 2 * NPRM * 4;
   static constexpr int LDS = OFF_W + 3 * WBUF * 16;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
-  static_assert(2 * MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
-  static_assert(96 * 64 * 4 <= MROWS * SCR * 4, "gpool linear weights must fit below scr");
+  static_assert(OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
+  static_assert(96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
   static_assert(2 * PA * ROWB + 2 * 64 < 65536, "A-read offsets must fit the ds_read immediate");
   static_assert(LDS <= 163840, "LDS budget");
 };
@@ -460,13 +461,13 @@ KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ W
   return src >= 0 ? WF[src] : 0.0f;
 }
 
-template <int X, int Y, int C>
+template <int X, int Y, int C, int NB>
 __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
                const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
                const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
                float* __restrict__ out, float* __restrict__ trunk) {
-  using G = NNGeo<X, Y, C>;
+  using G = NNGeo<X, Y, C, NB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
   const int count = countDev ? min(*countDev, n) : n;
@@ -508,7 +509,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   {
     // wave w unpacks board w: its row index and all its packed words are loaded up
     // front (two round trips), then lane l sets bits l, l+64, ... (plane-major bits)
-    static_assert(G::NB == NN_WAVES, "one wave per board");
+    static_assert(G::NB <= NN_WAVES, "one wave per board");
     constexpr int NBITS = G::A * NUM_SPATIAL, NW = (NBITS + 63) / 64;
     const int b = __builtin_amdgcn_readfirstlane(wave);
     if(b < nb) {
@@ -746,12 +747,13 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   {
     // value (2) and misc (2) outputs: a 16-lane group per (board, output), each lane
     // summing every 16th term, reduced across the group
-    static_assert(G::NB * 4 * 16 == NN_NT, "one 16-lane group per (board, output)");
+    static_assert(G::NB * 4 * 16 <= NN_NT, "one 16-lane group per (board, output)");
     const int k = tid & 15, o = (tid >> 4) & 3, b = tid >> 6;
     const int v2 = L->v2;
+    const int bv = b < G::NB ? b : 0;  // waves past the boards compute a discarded copy
     float s = 0.0f;
     for(int i = k; i < v2; i += 16)
-      s += w3[o * v2 + i] * vh[b * 64 + i];
+      s += w3[o * v2 + i] * vh[bv * 64 + i];
     // lanes ^8, ^4, ^2, ^1 of the 16-lane group (DPP; after ^8 a partial depends only
     // on lane mod 8, so the row rotation by 4 reaches the ^4 partner's value)
     s += asF(partner<2>(bitsF(s)));
@@ -976,12 +978,19 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipMemcpy(wF32_, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&layoutDev_, sizeof(NNLayout)));
   KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
-  using G = NNGeo<5, 5, 96>;
-  const std::vector<uint16_t> tab = rowTables<G>();
-  KC_HIP(hipMalloc(&tabDev_, tab.size() * 2));
-  KC_HIP(hipMemcpy(tabDev_, tab.data(), tab.size() * 2, hipMemcpyHostToDevice));
+  using G8 = NNGeo<5, 5, 96, 8>;
+  using G4 = NNGeo<5, 5, 96, 4>;
+  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>();
+  KC_HIP(hipMalloc(&tabDev_, tab8.size() * 2));
+  KC_HIP(hipMemcpy(tabDev_, tab8.data(), tab8.size() * 2, hipMemcpyHostToDevice));
+  KC_HIP(hipMalloc(&tabDev4_, tab4.size() * 2));
+  KC_HIP(hipMemcpy(tabDev4_, tab4.data(), tab4.size() * 2, hipMemcpyHostToDevice));
   // function attributes are per device: every engine sets it on its own device
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, G8::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, G4::LDS));
+  int dev = 0;
+  KC_HIP(hipGetDevice(&dev));
+  KC_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev));
 }
 
 NNEngine::~NNEngine() {
@@ -990,6 +999,7 @@ NNEngine::~NNEngine() {
   (void)hipFree(wF32_);
   (void)hipFree(layoutDev_);
   (void)hipFree(tabDev_);
+  (void)hipFree(tabDev4_);
 }
 
 void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev,
@@ -1004,25 +1014,37 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
       KC_HIP(hipEventRecord(e1, st));
     return;
   }
-  using G = NNGeo<5, 5, 96>;
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
-  int grid = (n + G::NB - 1) / G::NB;
-  if(grid > trunkCap_) {
+  // A launch costs one workgroup's latency per wave of workgroups (one per CU): a
+  // batch bound that fits 4 boards per CU (e.g. each of two game groups' batches)
+  // runs 4 boards per workgroup, half the MFMA work on each workgroup's path.
+  if(n <= 4 * cus_)
+    launch<NNGeo<5, 5, 96, 4>>(n, inWords, tabDev4_, in, out, st, countDev, rowIdx, e0, e1);
+  else
+    launch<NNGeo<5, 5, 96, 8>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
+}
+
+template <class G>
+void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* in, float* out, hipStream_t st,
+                      const int* countDev, const int* rowIdx, hipEvent_t e0, hipEvent_t e1) {
+  const int grid = (n + G::NB - 1) / G::NB;
+  const size_t bytes = (size_t)grid * NN_WAVES * G::MAXT * G::NCT * 64 * 16;
+  if(bytes > trunkBytes_) {
     // stream-ordered: a launch still using the old scratch finishes before the free
     if(trunk_)
       KC_HIP(hipStreamSynchronize(st));
     (void)hipFree(trunk_);
     trunk_ = nullptr;
-    KC_HIP(hipMalloc(&trunk_, (size_t)grid * NN_WAVES * G::MAXT * G::NCT * 64 * 16));
-    trunkCap_ = grid;
+    KC_HIP(hipMalloc(&trunk_, bytes));
+    trunkBytes_ = bytes;
   }
+  auto kern = kNNForward<G::X, G::Y, G::C, G::NB>;
   if(e0)
-    hipExtLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, e0, e1, 0, layoutDev_,
-                          (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out,
-                          trunk_);
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(NN_NT), G::LDS, st, e0, e1, 0, layoutDev_, (const h16x8*)wHalf_,
+                          wF32_, tab, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
   else
-    hipLaunchKernelGGL((kNNForward<5, 5, 96>), dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_,
-                       (const h16x8*)wHalf_, wF32_, tabDev_, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_, (const h16x8*)wHalf_, wF32_, tab, n,
+                       countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
   KC_HIP(hipGetLastError());
 }
 
