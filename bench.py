@@ -336,11 +336,13 @@ def main():
     # benchmark mode clears the tree before every move: a search holds at
     # most visits + 1 nodes; production's cheap searches reuse the tree
     node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
+    fused = args.precision == "fast" and cfg["arch"] == "b6c96"
     if args.groups == 0:
-        args.groups = 2 if args.precision == "fast" and cfg["arch"] == "b6c96" and games % 2 == 0 else 1
+        args.groups = 2 if fused and games % 2 == 0 else 1
     cap = args.nn_batch_cap
-    if cap == 0 and args.groups > 1:
-        # the groups' network launches share one wave of workgroups
+    if cap == 0 and args.groups > 1 and fused:
+        # the groups' fused network launches share one wave of workgroups (the layered
+        # network has no batch cap: its cost grows with the batch)
         cap = torch.cuda.get_device_properties(local).multi_processor_count * 8
     sp = Groups(kc, args.groups, games, rank * games, X=X, Y=Y, W=W, max_visits=visits, seed=args.seed,
                 model_path=model_path, commit_interval=args.commit_interval, nn_cache_log2=args.nn_cache_log2,

@@ -3273,9 +3273,9 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
 // are deferred (nnDefer): their games keep their leaf and skip the next select.  The
 // oracle applies the same rule (ora_search.cpp selfplayRound).
 // accumulate != 0: the count is also added to *d.nnTimedEvals (sampled kernel timing).
-// The thread's need flags and cache bids are loaded once, before the scan (16-byte
-// loads when its G / 1024 games are a multiple of 4, up to CP_VEC), so the kernel
-// waits for one round of loads instead of one per game.
+// The thread's need flags and cache bids are loaded once, before the scan (all in
+// flight together when it has at most CP_VEC games), so the kernel waits for one
+// round of loads instead of one per game.
 constexpr int CP_VEC = 16;
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
@@ -3283,22 +3283,18 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = (d.G + 1023) / 1024;
   const int lo = t * per, hi = min(d.G, lo + per);
   const int p = *d.nnRR;
-  const bool vec = per <= CP_VEC && (per & 3) == 0 && (d.G & 3) == 0;
+  const bool vec = per <= CP_VEC;
   uint64_t need = 0;  // bit k: game lo + k needs the network (per <= 64)
   uint32_t bids[CP_VEC];
   if(vec) {
+    // unconditional loads from clamped indices (one basic block: all in flight at once)
 #pragma unroll
-    for(int q = 0; q < CP_VEC / 4; q++) {
-      bids[4 * q] = bids[4 * q + 1] = bids[4 * q + 2] = bids[4 * q + 3] = ~0u;
-      if(4 * q < per && lo + 4 * q < d.G) {
-        const int4 a = *reinterpret_cast<const int4*>(&d.nnNeed[lo + 4 * q]);
-        const uint4 b = *reinterpret_cast<const uint4*>(&d.nnBid[lo + 4 * q]);
-        need |= (uint64_t)((a.x ? 1u : 0u) | (a.y ? 2u : 0u) | (a.z ? 4u : 0u) | (a.w ? 8u : 0u)) << (4 * q);
-        bids[4 * q] = b.x;
-        bids[4 * q + 1] = b.y;
-        bids[4 * q + 2] = b.z;
-        bids[4 * q + 3] = b.w;
-      }
+    for(int k = 0; k < CP_VEC; k++) {
+      const bool valid = k < per && lo + k < d.G;
+      const int i = valid ? lo + k : 0;
+      const int nd = d.nnNeed[i];
+      bids[k] = d.nnBid[i];
+      need |= (uint64_t)(valid && nd ? 1u : 0u) << k;
     }
   } else {
     for(int i = lo; i < hi; i++)
