@@ -92,7 +92,7 @@ def parse():
     ap.add_argument("--groups", type=int, default=0,
                     help="independent game groups per GPU, each on its own stream (overlaps one group's network "
                          "with another's search kernels; the reference's numNNServerThreadsPerModel); "
-                         "0 = 2 with the fused network (measured +7%% rows/s at C2), else 1")
+                         "0 = 2 except for b18c384nbt (C5), whose forward is throughput-bound")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
@@ -338,7 +338,9 @@ def main():
     node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
     fused = args.precision == "fast" and cfg["arch"] == "b6c96"
     if args.groups == 0:
-        args.groups = 2 if fused and games % 2 == 0 else 1
+        # latency-bound rounds gain from two overlapped chains (measured: C2 +8 %, C3 +12 %,
+        # C4 +10 % rows/s); b18c384nbt's forward is throughput-bound (C5: -12 % playouts/s)
+        args.groups = 2 if cfg["arch"] != "b18c384nbt" and games % 2 == 0 else 1
     cap = args.nn_batch_cap
     if cap == 0 and args.groups > 1 and fused:
         # the groups' fused network launches share one wave of workgroups (the layered

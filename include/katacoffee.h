@@ -43,6 +43,10 @@ int coffee_abi_version(void);
 /* ---- device memory helpers (so callers need no HIP headers) ---- */
 int coffee_device_count(int* count);
 int coffee_set_device(int device);
+/* Compute units of `device` (the fused network runs one workgroup per CU: a host that
+   runs several self-play engines on one device splits cus x 8 rows of batch cap
+   between them, as the CLI does for numNNServerThreadsPerModel). */
+int coffee_device_compute_units(int device, int* cus);
 int coffee_malloc(void** dev_ptr, uint64_t bytes);
 int coffee_free(void* dev_ptr);
 /* kind: 0 host->device, 1 device->host, 2 device->device */

@@ -99,7 +99,7 @@ class SelfplayStats(ctypes.Structure):
 
 # Every symbol include/katacoffee.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "coffee_last_error", "coffee_abi_version", "coffee_device_count", "coffee_set_device", "coffee_malloc",
+    "coffee_last_error", "coffee_abi_version", "coffee_device_count", "coffee_set_device", "coffee_device_compute_units", "coffee_malloc",
     "coffee_free", "coffee_memcpy", "coffee_synchronize", "coffee_rules_batch", "coffee_play_batch",
     "coffee_encode_batch", "coffee_model_write_random", "coffee_model_flops", "coffee_nn_create",
     "coffee_nn_forward", "coffee_nn_destroy", "coffee_nn_create2", "coffee_nn_is_fused", "coffee_fake_net", "coffee_search_params_default",

@@ -97,6 +97,12 @@ int coffee_device_count(int* count) {
 int coffee_set_device(int device) {
   return guarded([&] { KC_HIP(hipSetDevice(device)); });
 }
+int coffee_device_compute_units(int device, int* cus) {
+  return guarded([&] {
+    need(cus != nullptr, "cus is NULL");
+    KC_HIP(hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, device));
+  });
+}
 int coffee_malloc(void** p, uint64_t bytes) {
   return guarded([&] {
     need(p != nullptr, "pointer is NULL");

@@ -14,9 +14,11 @@
 // layout), <output-dir>/<modelName>/sgfs/<hex>.sgfs (one SGF per finished game per
 // line, sgf.cpp:1526-1700 with Coffee's 3-letter moves, selfplaymanager.cpp:350-354)
 // and <output-dir>/log<time>.log.  Rows and games drained after a switch go to the new
-// model's directories.  One engine per GPU, each GPU on its own thread with games
-// [gpu*numGameThreads, (gpu+1)*numGameThreads); each writes its own files (SURVEY §8e
-// fallback, no collective).  SIGINT/SIGTERM: flush rows and exit.
+// model's directories.  Each GPU plays games [gpu*numGameThreads, (gpu+1)*numGameThreads)
+// on ceil(numNNServerThreadsPerModel / numGpus) engines (default 1; 2 overlaps one
+// engine's network with the other's search, +8 % rows/s at C2), each on its own thread
+// writing its own files (SURVEY §8e fallback, no collective).  SIGINT/SIGTERM: flush
+// rows and exit.
 #include <dirent.h>
 #include <sys/stat.h>
 
@@ -177,6 +179,7 @@ static void mkdirs(const std::string& path) {
 
 struct Settings {
   int x = 5, y = 5, winLen = 4, games = 4096, gpus = 1, maxRowsPerFile = 10000;
+  int servers = 1;  // numNNServerThreadsPerModel: self-play engines (own stream, batch, cache) over all GPUs
   float modelPollSeconds = 10.0f;
   int nnCacheLog2 = 21;  // selfplay1.cfg:121 nnCacheSizePowerOfTwo
   int nnPrecision = COFFEE_NN_FAST;  // nnPrecision = fast | accurate | fastLayered (the reference's useFP16)
@@ -211,6 +214,7 @@ static void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   geti("numGameThreads", s.games);
   geti("numGamesPerGpu", s.games);
   geti("numGpus", s.gpus);
+  geti("numNNServerThreadsPerModel", s.servers);
   geti("maxRowsPerTrainFile", s.maxRowsPerFile);
   getf("modelPollSeconds", s.modelPollSeconds);
   geti("nnCacheSizePowerOfTwo", s.nnCacheLog2);  // setup.cpp:268; <= 0 disables the cache
@@ -382,7 +386,12 @@ struct SgfSink {
 
 static std::atomic<int64_t> gGamesDone(0);
 
-static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
+// One self-play engine: `share` of GPU `gpu`'s games from slot `slot` on (the
+// reference's NN server thread with its game threads).  Engines on one device run
+// on their own streams, so one's network overlaps another's search kernels; they
+// split the device's batch cap (one wave of fused-network workgroups).
+static void runGpu(int gpu, int server, int perGpu, int slot, int share, const Settings& s,
+                   const std::string& outDir) {
   check(coffee_set_device(gpu), "set device");
   std::string model;
   int version = 0;
@@ -392,9 +401,14 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
   c.x = s.x;
   c.y = s.y;
   c.win_len = s.winLen;
-  c.num_games = s.games;
+  c.num_games = share;
   c.seed = s.seed;
-  c.slot_base = gpu * s.games;
+  c.slot_base = slot;
+  if(perGpu > 1) {
+    int cus = 0;
+    check(coffee_device_compute_units(gpu, &cus), "compute units");
+    c.nn_batch_cap = std::max(1, cus * 8 / perGpu);
+  }
   c.use_fake_net = 0;
   c.commit_interval = 8;
   c.model_path = model.c_str();
@@ -403,7 +417,7 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
   c.nn_precision = s.nnPrecision;
   coffee_selfplay* h = nullptr;
   check(coffee_selfplay_create(&c, &h), "create engine");
-  std::mt19937_64 fileRng(s.seed ^ (0x9E3779B97F4A7C15ULL * (gpu + 1)));
+  std::mt19937_64 fileRng(s.seed ^ (0x9E3779B97F4A7C15ULL * (gpu + 1)) ^ ((uint64_t)server << 48));
   auto dirsFor = [&](const std::string& m, std::string& tdata, std::string& sgfs) {
     tdata = outDir + "/" + modelNameOf(m) + "/tdata";
     sgfs = outDir + "/" + modelNameOf(m) + "/sgfs";
@@ -451,7 +465,7 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
       sink.flush(true);
       games.close();
       if(coffee_selfplay_set_model(h, latest.c_str()) == COFFEE_OK) {
-        logf("gpu %d: switched to model %s", gpu, latest.c_str());
+        logf("gpu %d.%d: switched to model %s", gpu, server, latest.c_str());
         model = latest;
         filesBefore += sink.filesWritten;
         rowsBefore += sink.rowsWritten;
@@ -462,7 +476,7 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
         games.modelName = modelNameOf(model);
         games.fileId = fileRng();
       } else {
-        logf("gpu %d: cannot load %s (%s); keeping %s", gpu, latest.c_str(), coffee_last_error(), model.c_str());
+        logf("gpu %d.%d: cannot load %s (%s); keeping %s", gpu, server, latest.c_str(), coffee_last_error(), model.c_str());
       }
       version = v;
     }
@@ -471,7 +485,7 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
     gGamesDone += (int64_t)(st.games_finished - lastGames);
     lastGames = st.games_finished;
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    logf("gpu %d: %llu games, %llu moves, %.1f rows/s, %.3g playouts/s, %llu rows dropped", gpu,
+    logf("gpu %d.%d: %llu games, %llu moves, %.1f rows/s, %.3g playouts/s, %llu rows dropped", gpu, server,
          (unsigned long long)st.games_finished, (unsigned long long)st.moves, st.moves / secs, st.playouts / secs,
          (unsigned long long)st.rows_dropped);
     if(s.maxGamesTotal >= 0 && gGamesDone >= s.maxGamesTotal)
@@ -481,7 +495,7 @@ static void runGpu(int gpu, const Settings& s, const std::string& outDir) {
   sink.flush(true);
   games.close();
   coffee_selfplay_destroy(h);
-  logf("gpu %d done: %lld files, %lld rows, %lld games", gpu, (long long)(filesBefore + sink.filesWritten),
+  logf("gpu %d.%d done: %lld files, %lld rows, %lld games", gpu, server, (long long)(filesBefore + sink.filesWritten),
        (long long)(rowsBefore + sink.rowsWritten), (long long)games.games);
 }
 
@@ -546,9 +560,18 @@ int main(int argc, char** argv) {
     die("numGpus must be in 1.." + std::to_string(ndev));
   logf("selfplay: model %s, %dx%d win %d, %d games/GPU x %d GPUs, %d visits", model.c_str(), s.x, s.y, s.winLen,
        s.games, s.gpus, s.sp.max_visits);
+  // numNNServerThreadsPerModel engines spread over the GPUs (at least one each); a
+  // GPU's games split evenly between its engines
+  const int perGpu = std::max(1, (s.servers + s.gpus - 1) / s.gpus);
+  if(perGpu > s.games)
+    die("numNNServerThreadsPerModel exceeds the games per GPU");
   std::vector<std::thread> th;
   for(int g = 0; g < s.gpus; g++)
-    th.emplace_back(runGpu, g, std::cref(s), std::cref(outDir));
+    for(int k = 0, off = 0; k < perGpu; k++) {
+      const int share = s.games / perGpu + (k < s.games % perGpu ? 1 : 0);
+      th.emplace_back(runGpu, g, k, perGpu, g * s.games + off, share, std::cref(s), std::cref(outDir));
+      off += share;
+    }
   for(auto& t : th)
     t.join();
   if(gLog)

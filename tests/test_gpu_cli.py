@@ -41,6 +41,33 @@ def test_cli_selfplay_writes_training_npz(tmp_path):
     assert total >= 40 * 5  # every finished game has at least five moves
 
 
+def test_cli_two_engines_per_gpu(tmp_path):
+    """numNNServerThreadsPerModel = 2 on one GPU: two engines (own streams, batches and
+    caches) split the GPU's games and both write rows and records."""
+    models = tmp_path / "models"
+    models.mkdir()
+    kc.write_random_model("b6c96", 5, str(models / "b6c96-s0.cfnn"))
+    out = tmp_path / "out"
+    cmd = [os.path.join(REPO, "katacoffee_amd", "katago"), "selfplay", "-config",
+           os.path.join(REPO, "configs", "selfplay_coffee5.cfg"), "-models-dir", str(models), "-output-dir", str(out),
+           "-max-games-total", "40", "-override-config",
+           "numGameThreads=64,maxVisits=16,maxRowsPerTrainFile=100,numNNServerThreadsPerModel=2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    log = r.stdout + r.stderr
+    assert "gpu 0.0 done" in log and "gpu 0.1 done" in log, log
+    files = glob.glob(str(out / "b6c96-s0" / "tdata" / "*.npz"))
+    assert files, log
+    total = 0
+    for f in files:
+        with np.load(f) as z:
+            total += z["globalTargetsNC"].shape[0]
+    assert total >= 40 * 5
+    games = _sgf_games(glob.glob(str(out / "b6c96-s0" / "sgfs" / "*.sgfs")))
+    ids = {g.split("gameId=")[1].split(":")[0] for g in games}
+    assert any(int(i) < 32 for i in ids) and any(int(i) >= 32 for i in ids), ids
+
+
 def _sgf_games(paths):
     games = []
     for p in paths:
