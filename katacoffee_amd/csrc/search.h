@@ -302,8 +302,9 @@ struct SearchDev {
 void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 // e0/e1 (optional): events recorded at the kernel's start and end (hipExtLaunchKernel),
 // so the bench times the kernel itself, not the stream gaps around it
+// resetCommit: zero the commit count first (the previous commit consumed its list)
 void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
-                  hipEvent_t e1 = nullptr);
+                  hipEvent_t e1 = nullptr, bool resetCommit = false);
 // accumulate: add the batch size to *d.nnTimedEvals (rounds whose network launch is timed)
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate);
 void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,

@@ -1016,9 +1016,14 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
 // ---------------------------------------------------------------------------
 // kSelect: root evaluation or one descent; NN leaves are encoded into the batch.
 template <int NI>
-__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
+__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp,
+                                                                int resetCommit) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
+  // the previous commit's list is consumed (kCommit/kRows ran before this kernel);
+  // this round's kBackup appends to an empty one
+  if(resetCommit && g == 0 && threadIdx.x == 0)
+    *d.commitCount = 0;
   if(g >= d.G)
     return;
   __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
@@ -3498,12 +3503,14 @@ static void launchEv(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t 
     hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
 }
 
-void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0, hipEvent_t e1,
+                  bool resetCommit) {
   const DTables* T = d.T;
+  const int rc = resetCommit ? 1 : 0;
   switch(laneItems(d.P)) {
-    case 2: launchEv(kSelect<2>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
-    case 4: launchEv(kSelect<4>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
-    default: launchEv(kSelect<7>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+    case 2: launchEv(kSelect<2>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T, rc); break;
+    case 4: launchEv(kSelect<4>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T, rc); break;
+    default: launchEv(kSelect<7>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T, rc); break;
   }
   KC_HIP(hipGetLastError());
 }

@@ -314,7 +314,8 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
     const bool t0 = sampleNow(0), t1 = sampleNow(1), t2 = sampleNow(2);
     // select, network and backup are timed by their own dispatches (kernel start to
     // end, like rocprofv3); compact and cache write run untimed between them
-    timedKernel(0, t0, [&](hipEvent_t a, hipEvent_t b) { launchSelect(d, dd_, st, a, b); });
+    timedKernel(0, t0, [&](hipEvent_t a, hipEvent_t b) { launchSelect(d, dd_, st, a, b, commitReset_); });
+    commitReset_ = false;
     launchCompact(d, dd_, st, t1);
     timedKernel(1, t1, [&](hipEvent_t a, hipEvent_t b) {
       const int rows = std::min(d.G, d.nnCap);  // grid bound; the batch is *d.nnCount rows
@@ -333,7 +334,7 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
     if(rounds_ % (uint64_t)commitInterval_ == 0 || r == rounds - 1) {
       const bool t3 = sampleNow(3);
       timed(3, st, [&] { launchCommit(d, dd_, st); }, t3);
-      KC_HIP(hipMemsetAsync(d.commitCount, 0, sizeof(int32_t), st));
+      commitReset_ = true;  // the next kSelect zeroes the count (no separate memset)
     }
   }
 }

@@ -58,6 +58,7 @@ class SelfplayEngine {
   int nnPath_ = 0;  // NNPath of the network (kept across hot reloads)
   int32_t modelGen_ = 0;  // hot reloads so far
   uint64_t rounds_ = 0;
+  bool commitReset_ = false;  // a commit ran: the next kSelect zeroes the commit count
   uint64_t rowsDrained_ = 0;
   int timingEvery_ = 0;
   uint64_t groupLaunches_[4] = {0, 0, 0, 0};
