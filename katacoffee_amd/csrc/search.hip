@@ -3292,15 +3292,22 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
   uint64_t need = 0;  // bit k: game lo + k needs the network (per <= 64)
   uint32_t bids[CP_VEC];
   if(vec) {
-    // unconditional loads from clamped indices (one basic block: all in flight at once)
+    // loads under the block-uniform bound `per` (clamped indices), all issued before
+    // the first use
+    int nd[CP_VEC];
 #pragma unroll
     for(int k = 0; k < CP_VEC; k++) {
-      const bool valid = k < per && lo + k < d.G;
-      const int i = valid ? lo + k : 0;
-      const int nd = d.nnNeed[i];
-      bids[k] = d.nnBid[i];
-      need |= (uint64_t)(valid && nd ? 1u : 0u) << k;
+      nd[k] = 0;
+      bids[k] = ~0u;
+      if(k < per) {
+        const int i = lo + k < d.G ? lo + k : 0;
+        nd[k] = d.nnNeed[i];
+        bids[k] = d.nnBid[i];
+      }
     }
+#pragma unroll
+    for(int k = 0; k < CP_VEC; k++)
+      need |= (uint64_t)(k < per && lo + k < d.G && nd[k] ? 1u : 0u) << k;
   } else {
     for(int i = lo; i < hi; i++)
       need |= (uint64_t)(d.nnNeed[i] ? 1u : 0u) << (i - lo);
