@@ -260,6 +260,12 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
   return s;
 }
 void ora_sp_free(void* h) { delete(Selfplay*)h; }
+// Composition tests: every later round's network batch goes to fn (nnMode 3).
+void ora_sp_set_netfn(void* h, void (*fn)(int, const uint64_t*, float*)) {
+  Selfplay* s = (Selfplay*)h;
+  s->cfg.netFn = fn;
+  s->cfg.nnMode = fn ? 3 : 0;
+}
 // CPU baseline: threads over games in select / backup (numGameThreads, selfplay.cpp:90)
 void ora_sp_set_parallel(void* h, int threads) { ((Selfplay*)h)->cfg.parallelGames = threads; }
 

@@ -34,7 +34,15 @@ inline real rmax(A a, B b) {
   return std::max<real>((real)a, (real)b);
 }
 
-static const int SVB_CAP = 4096;
+// Transposition and SVB tables: nextPow2(2 * nodeCap) entries each, as the device
+// (selfplay.cpp ttCap / svbCap).  Both hold at most one entry per live node, so a
+// power-of-two size above 2 x nodeCap keeps every linear probe short and terminating.
+static int tableCapFor(int nodeCap) {
+  int c = 1;
+  while(c < 2 * nodeCap)
+    c <<= 1;
+  return c;
+}
 
 // SPEC B27: subtree-value-bias sums are kept in 64-bit fixed point (2^-32 units)
 // so that concurrent/unordered updates are exact and order independent.
@@ -123,7 +131,7 @@ struct Ctx {
   // --- subtree value bias table (subtreevaluebiastable.cpp:61-78) ---
   int svbFindOrInsert(std::vector<uint64_t>& key, std::vector<int64_t>& d, std::vector<int64_t>& w,
                       std::vector<uint8_t>& used, uint64_t k) {
-    int mask = SVB_CAP - 1;
+    int mask = (int)key.size() - 1;
     for(int i = (int)(k & (uint64_t)mask);; i = (i + 1) & mask) {
       if(!used[i]) {
         used[i] = 1;
@@ -898,15 +906,16 @@ struct Ctx {
     for(int i = 0; i < gm.nodeCount; i++)
       if(i != gm.rootIdx)
         ttInsert(N(i).key0, N(i).key1, i);
-    std::vector<uint64_t> k2(SVB_CAP, 0);
-    std::vector<int64_t> d2(SVB_CAP, 0), w2(SVB_CAP, 0);
-    std::vector<uint8_t> u2(SVB_CAP, 0);
+    const size_t svbCap = gm.svbKey.size();
+    std::vector<uint64_t> k2(svbCap, 0);
+    std::vector<int64_t> d2(svbCap, 0), w2(svbCap, 0);
+    std::vector<uint8_t> u2(svbCap, 0);
     for(int i = 0; i < gm.nodeCount; i++) {
       Node& n = N(i);
       if(n.svbEntry < 0)
         continue;
       int oe = n.svbEntry;
-      int mask = SVB_CAP - 1;
+      int mask = (int)svbCap - 1;
       int slot = (int)(gm.svbKey[oe] & (uint64_t)mask);
       while(u2[slot] && k2[slot] != gm.svbKey[oe])
         slot = (slot + 1) & mask;
@@ -1734,13 +1743,14 @@ void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames) {
     gm.rootNoised.assign(g.P, 0.0f);
     gm.accPolicy.assign(g.P, 0.0f);
     gm.rawPolicy.assign(g.P, 0.0f);
-    gm.ttKey0.assign(2 * cfg.nodeCap, 0);
-    gm.ttKey1.assign(2 * cfg.nodeCap, 0);
-    gm.ttNode.assign(2 * cfg.nodeCap, -1);
-    gm.svbKey.assign(SVB_CAP, 0);
-    gm.svbDelta.assign(SVB_CAP, 0);
-    gm.svbWeight.assign(SVB_CAP, 0);
-    gm.svbUsed.assign(SVB_CAP, 0);
+    const int tcap = tableCapFor(cfg.nodeCap);
+    gm.ttKey0.assign(tcap, 0);
+    gm.ttKey1.assign(tcap, 0);
+    gm.ttNode.assign(tcap, -1);
+    gm.svbKey.assign(tcap, 0);
+    gm.svbDelta.assign(tcap, 0);
+    gm.svbWeight.assign(tcap, 0);
+    gm.svbUsed.assign(tcap, 0);
     Ctx(s, gm).startGame();
   }
 }
@@ -1841,6 +1851,17 @@ void selfplayRound(Selfplay& s) {
     for(int i : idx)
       fakeNet(g, &bin[(size_t)i * NUM_SPATIAL * A], &out[(size_t)i * (g.P + 4)], &out[(size_t)i * (g.P + 4) + g.P],
               &out[(size_t)i * (g.P + 4) + g.P + 2]);
+  } else if(s.cfg.nnMode == 3) {
+    if(!idx.empty()) {
+      const int n = (int)idx.size(), nw = (NUM_SPATIAL * A + 63) / 64;
+      std::vector<uint64_t> words((size_t)n * nw);
+      std::vector<float> res((size_t)n * (g.P + 4));
+      for(int j = 0; j < n; j++)
+        packPlanes(g, &bin[(size_t)idx[j] * NUM_SPATIAL * A], &words[(size_t)j * nw]);
+      s.cfg.netFn(n, words.data(), res.data());
+      for(int j = 0; j < n; j++)
+        memcpy(&out[(size_t)idx[j] * (g.P + 4)], &res[(size_t)j * (g.P + 4)], sizeof(float) * (g.P + 4));
+    }
   } else if(!idx.empty()) {
     int n = (int)idx.size();
     std::vector<float> cb((size_t)n * NUM_SPATIAL * A), cg(n), pol((size_t)n * 4 * A), val((size_t)n * 2), misc((size_t)n * 2);

@@ -125,8 +125,14 @@ struct SelfplayCfg {
   int nodeCap = 2048;
   uint64_t seed = 1;
   int slotBase = 0;        // global index of this engine's first game slot (rank * games)
-  int nnMode = 0;          // 0 fake deterministic net, 1 model fp32, 2 model bf16-emulation
+  int nnMode = 0;          // 0 fake deterministic net, 1 model fp32, 2 model bf16-emulation,
+                           // 3 external network (netFn; composition tests)
   const Model* model = nullptr;
+  // nnMode 3: called once per round with the batch's packed V1 rows [n][ceil(15A/64)]
+  // (coffee_encode_batch layout, batch order) and fills out [n][P+4] (coffee_nn_forward
+  // layout).  Tests plug the device network in here, so the oracle's search consumes the
+  // very outputs the device engine's network produces for the same rows.
+  void (*netFn)(int n, const uint64_t* packed, float* out) = nullptr;
   int nnThreads = 1;
   int cacheLog2 = 0;       // NN evaluation cache of 2^cacheLog2 entries, 0 = off (SPEC a7)
   int nnCap = 1 << 30;     // rows per network batch; the rest wait for the next round (device kCompact)

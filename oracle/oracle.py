@@ -61,6 +61,7 @@ def _setup(L):
         L.ora_block_apply_blob.argtypes = [ctypes.c_int] * 4 + [P, ctypes.c_longlong] + [ctypes.c_int] * 3 + [P,
                                                                                                             ctypes.c_int]
         L.ora_sp_set_parallel.argtypes = [P, ctypes.c_int]
+        L.ora_sp_set_netfn.argtypes = [P, P]
         L.ora_model_free.argtypes = [P]
         _load_tables(L)
     return L
@@ -234,6 +235,9 @@ PLAY_SETTINGS = {
 }
 
 
+_NETFN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+
+
 class Selfplay:
     """Round-synchronous self-play engine (select -> batched NN -> backup per round)."""
 
@@ -259,6 +263,29 @@ class Selfplay:
 
     def rounds(self, n):
         self.L.ora_sp_rounds(self.h, n)
+        if getattr(self, "_net_error", None) is not None:
+            raise RuntimeError("network callback failed") from self._net_error
+
+    def set_net(self, fn):
+        """Composition tests: every later round's network batch is evaluated by
+        fn(packed [n][ceil(15A/64)] u64) -> [n][P+4] f32 (coffee_nn_forward's layout),
+        e.g. the device network, instead of the oracle's own forward.  None restores
+        the stand-in network."""
+        words = (15 * self.A + 63) // 64
+        width = self.P + 4
+        self._net_error = None
+
+        def cb(n, pin, pout):
+            try:
+                packed = np.ctypeslib.as_array(ctypes.cast(pin, ctypes.POINTER(ctypes.c_uint64)), shape=(n, words))
+                res = np.asarray(fn(packed.copy()), np.float32)
+                assert res.shape == (n, width), res.shape
+                np.ctypeslib.as_array(ctypes.cast(pout, ctypes.POINTER(ctypes.c_float)), shape=(n, width))[:] = res
+            except BaseException as e:  # ctypes drops callback exceptions: re-raised by rounds()
+                self._net_error = e
+
+        self._cb = _NETFN(cb) if fn is not None else None
+        self.L.ora_sp_set_netfn(self.h, ctypes.cast(self._cb, P) if fn is not None else None)
 
     def set_parallel(self, threads):
         """CPU baseline only: threads over games in select/backup (row order then

@@ -1,0 +1,161 @@
+"""Self-play with the REAL network, composed: the oracle's search (oracle/ora_search.cpp)
+is fed the device network's outputs for its own batches (oracle.Selfplay.set_net ->
+kc.Network.forward on the GPU), and the device engine runs the same games with the same
+network end to end.  Game state, canonical trees, root priors and training rows must be
+bit-identical.  This pins the hand-off the stand-in-network parity tests cannot see:
+the batch's row indirection into the network (kCompact -> forward with rowIdx), real
+logits through post-processing (nneval.cpp:702-844: legal mask, softmax, the inverse
+symmetry of the row's random orientation), NN-cache payloads of real outputs, and
+batch-cap deferral, on the fused b6c96 kernel (4- and 8-board instances, one and two
+game groups) and on the layered kernels (b10c128 @ 5x5, b18c384nbt @ 9x9, the split
+"accurate" precision).  Reference: cpp/neuralnet/nneval.cpp:588-844 feeding
+cpp/search/searchnnhelpers.cpp:39-129.
+
+It relies on the network being a pure function of each row's input: the same row gives
+the same logits at any batch position, batch size and workgroup variant -- asserted
+first (test_network_row_independence)."""
+import numpy as np
+import pytest
+
+import katacoffee_amd as kc
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+INFO_KEYS = [("phase", "phase"), ("rootK", "rootK"), ("liveCount", "nodeCount"), ("gameNum", "gameNum"),
+             ("turn", "turn"), ("pla", "pla"), ("playouts", "playouts"), ("nnEvals", "nnEvals"),
+             ("moves", "movesMade"), ("gamesFinished", "gamesFinished"), ("rngCtr", "rngCtr"),
+             ("lastCell", "lastCell"), ("lastDir", "lastDir")]
+
+
+def _sorted_rows(r):
+    order = np.lexsort((r["meta"][:, 2], r["meta"][:, 1], r["meta"][:, 0]))
+    return {k: v[order] for k, v in r.items()}
+
+
+def _compare_game(gpu, ora, g, og, done):
+    gi, oi = gpu.game_info(g), ora.info(og)
+    for a, b in INFO_KEYS:
+        assert gi[a] == oi[b], (done, g, a, gi[a], oi[b])
+    gn, ge = gpu.game_tree(g)
+    on, oe = ora.game_tree(og)
+    np.testing.assert_array_equal(gn, on, err_msg="round %d game %d nodes" % (done, g))
+    np.testing.assert_array_equal(ge, oe, err_msg="round %d game %d edges" % (done, g))
+    if gi["phase"] == 1:
+        np.testing.assert_array_equal(gpu.root_policy(g), ora.root_noised(og))
+
+
+@pytest.fixture(scope="module")
+def nets(tmp_path_factory):
+    d = tmp_path_factory.mktemp("nets")
+    out = {}
+    for arch in ["b6c96", "b10c128", "b18c384nbt"]:
+        p = str(d / ("%s.cfnn" % arch))
+        kc.write_random_model(arch, 0xC0FFEE, p)
+        out[arch] = p
+    return out
+
+
+def _rows_of_game_positions(X, Y, W, n, seed):
+    """n encoded positions from oracle self-play-like random boards (device encoder)."""
+    rng = np.random.default_rng(seed)
+    A = X * Y
+    cells = np.zeros((n, A), np.uint8)
+    for i in range(n):
+        k = int(rng.integers(0, A // 2))
+        idx = rng.choice(A, size=k, replace=False)
+        cells[i, idx] = rng.integers(1, 3, size=k)
+    hc = np.full((n, 5), -1, np.int8)
+    hd = np.full((n, 5), 4, np.int8)
+    hc[:, 0] = rng.integers(0, A, n)
+    hd[:, 0] = rng.integers(0, 4, n)
+    pla = rng.integers(1, 3, n).astype(np.uint8)
+    sym = rng.integers(0, 8, n).astype(np.int32)
+    packed, _ = kc.encode_batch(X, Y, W, cells, hc, hd, pla, sym, want_planes=False)
+    return packed
+
+
+@pytest.mark.parametrize("arch,X,Y,W,precision", [("b6c96", 5, 5, 4, "fast"), ("b6c96", 5, 5, 4, "accurate"),
+                                                  ("b10c128", 5, 5, 4, "fast"),
+                                                  ("b18c384nbt", 9, 9, 5, "fast")],
+                         ids=["b6c96-fused", "b6c96-accurate", "b10c128-layered", "b18c384nbt-layered"])
+def test_network_row_independence(nets, arch, X, Y, W, precision):
+    """A row's logits do not depend on its batch position, the batch size or (fused)
+    the 4- / 8-board workgroup variant: a permuted batch gives the permuted outputs."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    # fused: n > 4 x CUs selects the 8-board instance, the prefix the 4-board one
+    n = 4 * cus + 37 if precision == "fast" and arch == "b6c96" else 203
+    packed = _rows_of_game_positions(X, Y, W, n, seed=n)
+    net = kc.Network(nets[arch], X, Y, W, precision=precision)
+    full = net.forward(packed)
+    perm = np.random.default_rng(1).permutation(n)
+    np.testing.assert_array_equal(net.forward(packed[perm]), full[perm])
+    np.testing.assert_array_equal(net.forward(packed[perm[:203]]), full[perm[:203]])
+    np.testing.assert_array_equal(net.forward(packed[5:6]), full[5:6])
+    net.close()
+
+
+# name: arch, geometry, precision, games per group, groups, visits, cache, batch cap, rounds, extra play settings
+PRODUCTION = dict(cheap_search_prob=0.75, cheap_search_visits=8, cheap_search_target_weight=0.0, reduce_visits=1,
+                  reduce_visits_threshold=0.9, reduce_visits_threshold_lookback=3, reduced_visits_min=8,
+                  reduced_visits_weight=0.1, policy_surprise_data_weight=0.5, value_surprise_data_weight=0.1)
+CASES = {
+    # C2 settings: fused fast b6c96, NN cache, binding batch cap above 4 x CUs (8-board kernel)
+    "c2-fused-nb8": ("b6c96", (5, 5, 4), "fast", 1536, 1, 24, 14, 1100, 420, {}),
+    # two game groups on their own streams, each capped (4-board kernel), selfplay1.cfg play
+    "c2-fused-two-groups": ("b6c96", (5, 5, 4), "fast", 384, 2, 24, 14, 300, 700, PRODUCTION),
+    # split-precision network (the 1e-3 path) in self-play
+    "c2-accurate": ("b6c96", (5, 5, 4), "accurate", 128, 1, 24, 12, 0, 900, {}),
+    # C3 network on the layered kernels
+    "c3-layered": ("b10c128", (5, 5, 4), "fast", 256, 1, 24, 12, 200, 900, {}),
+    # C5 network (nested bottlenecks) at 9x9 / 5 on the layered kernels
+    "c5-layered": ("b18c384nbt", (9, 9, 5), "fast", 24, 1, 12, 12, 0, 1500, {}),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
+    arch, (X, Y, W), precision, G, groups, visits, cache, cap, rounds, play = CASES[name]
+    path = nets[arch]
+    net = kc.Network(path, X, Y, W, precision=precision)
+    calls = []
+
+    def device_net(packed):
+        calls.append(packed.shape[0])
+        return net.forward(packed)
+
+    cap_node = 4 * visits + 32
+    gpus, oras = [], []
+    for k in range(groups):
+        gpus.append(kc.Selfplay(X, Y, W, num_games=G, max_visits=visits, seed=777, slot_base=k * G, model_path=path,
+                                node_cap=cap_node, commit_interval=1, nn_cache_log2=cache, nn_batch_cap=cap,
+                                nn_precision=precision, row_capacity=1 << 16, **play))
+        ora = oracle.Selfplay(X, Y, W, games=G, max_visits=visits, node_cap=cap_node, seed=777, slot_base=k * G,
+                              nn_cache_log2=cache, nn_batch_cap=cap, **play)
+        ora.set_net(device_net)
+        oras.append(ora)
+    sample = sorted(set(list(range(min(G, 8))) + list(np.random.default_rng(3).integers(0, G, 24))))
+    done = 0
+    for chunk in [1, 30, rounds]:
+        for gpu in gpus:  # the groups' rounds overlap on their streams
+            gpu.step(chunk - done)
+        for ora in oras:
+            ora.rounds(chunk - done)
+        done = chunk
+        for gpu, ora in zip(gpus, oras):
+            gpu.sync()
+            for g in sample:
+                _compare_game(gpu, ora, g, g, done)
+    if cap:
+        assert max(calls) == cap  # the cap binds
+    for gpu, ora in zip(gpus, oras):
+        st = gpu.stats()
+        assert st["errors"] == 0 and st["rows_dropped"] == 0 and st["games_finished"] > 0
+        gr = _sorted_rows(gpu.drain_rows())
+        orr = _sorted_rows(ora.rows())
+        assert len(gr["meta"]) == len(orr["meta"]) > 0
+        for k in orr:
+            np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
+        gpu.close()
+    net.close()

@@ -380,6 +380,29 @@ def test_selfplay_full_scale_sampled_slots_bit_exact():
     gpu.close()
 
 
+# Deep trees at the full C4 and C5 scales (stand-in network, benchmark play, the bench's
+# benchmark-mode node cap visits + 64): every game of the device engine runs, a sample of
+# slots is replayed one by one in the oracle from the same per-slot streams.  NN cache off
+# and a batch cap of G keep the games independent.  >= 3 committed moves per sampled slot.
+@pytest.mark.parametrize("X,Y,W,G,visits,rounds,slots",
+                         [(7, 7, 5, 8192, 800, 2600, [0, 1, 999, 4095, 4096, 6000, 8191]),
+                          (9, 9, 5, 4096, 1600, 5000, [0, 7, 2048, 3001, 4095])],
+                         ids=["C4-7x7-8192x800", "C5-9x9-4096x1600"])
+def test_selfplay_deep_trees_full_scale_sampled_slots(X, Y, W, G, visits, rounds, slots):
+    cap = visits + 64
+    gpu = kc.Selfplay(X, Y, W, num_games=G, max_visits=visits, seed=4242, node_cap=cap, commit_interval=1,
+                      nn_cache_log2=0, nn_batch_cap=G)
+    gpu.step(rounds)
+    st = gpu.stats()
+    assert st["errors"] == 0 and st["moves"] >= 3 * G
+    for s in slots:
+        ora = oracle.Selfplay(X, Y, W, games=1, max_visits=visits, node_cap=cap, seed=4242, slot_base=s)
+        ora.rounds(rounds)
+        assert ora.info(0)["movesMade"] >= 3
+        _compare_game(gpu, ora, s, 0, rounds)
+    gpu.close()
+
+
 def test_rows_record_network_switch(model_path):
     """Hot reload mid-game (switchNetsMidGame, play.cpp:1210-1226): rows of games that
     span the switch carry globalTargets[49] = 1 and [50] = reloads after the row's turn

@@ -226,3 +226,35 @@ def test_tree_positions():
     half.rounds(1500)
     n_half = int((half.rows()["globalTargetsNC"][:, 27] == 0.0).sum())
     assert 0 < n_half < tree.sum()
+
+
+def test_external_network_hook_matches_builtin():
+    """The composition tests' hook (nnMode 3): an external network fed the batch's
+    packed V1 rows.  Plugging in the stand-in network through it (unpack -> oracle
+    fake_net) must reproduce the built-in stand-in run exactly, with NN cache and a
+    binding batch cap, so the hook itself adds nothing to the search."""
+    A = 25
+    calls = []
+
+    def net(packed):
+        n = packed.shape[0]
+        calls.append(n)
+        bits = np.unpackbits(packed.view(np.uint8), axis=1, bitorder="little")[:, :15 * A]
+        return oracle.fake_net(5, 5, 4, bits.reshape(n, 15, A).astype(np.float32))
+
+    kw = dict(games=6, max_visits=24, node_cap=128, seed=21, nn_cache_log2=6, nn_batch_cap=4)
+    a = oracle.Selfplay(5, 5, 4, **kw)
+    b = oracle.Selfplay(5, 5, 4, **kw)
+    b.set_net(net)
+    a.rounds(2000)
+    b.rounds(2000)
+    assert calls and max(calls) <= 4
+    for g in range(6):
+        na, ea = a.game_tree(g)
+        nb, eb = b.game_tree(g)
+        np.testing.assert_array_equal(na, nb)
+        np.testing.assert_array_equal(ea, eb)
+    ra, rb = a.rows(), b.rows()
+    assert len(ra["meta"]) > 0
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k])

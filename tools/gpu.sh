@@ -1,0 +1,40 @@
+# The one GPU-box driver script: `gpurun -- bash tools/gpu.sh STEP [STEP ...]`.
+# Steps run in order, each under its own time limit; the first failing step ends the
+# call (no further GPU work after a fault, abort or timeout).  Logs go to gpurun_out/.
+#   test[=PATTERN]   pytest -m gpu (optionally -k PATTERN)
+#   file=PATH        pytest of one test file (gpu-marked tests in it)
+#   bench[=ARGS]     python bench.py ARGS (comma-separated: bench=--config,C3,--steps,10)
+#   smoke            __graft_entry__.smoke()
+#   prof             tools/profile_r03.sh (rocprofv3 trace + PMC passes)
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  name=${step%%=*}
+  arg=""
+  [ "$name" != "$step" ] && arg=${step#*=}
+  log=gpurun_out/step${n}_${name}.log
+  case $name in
+    test)
+      k=()
+      [ -n "$arg" ] && k=(-k "$arg")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1 ;;
+    file)
+      timeout -k 10 900 python -u -m pytest "$arg" -m gpu -x -v --timeout 300 --timeout-method thread > $log 2>&1 ;;
+    bench)
+      timeout -k 10 600 python -u bench.py ${arg//,/ } > $log 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
+    prof)
+      timeout -k 10 1100 bash tools/profile_r03.sh > $log 2>&1 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  echo "== step $n $step rc=$rc"
+  grep -E "PASSED|FAILED|ERROR|passed|failed|smoke ok|Error|error" $log | tail -40
+  tail -c 1500 $log | tail -3
+  [ $rc -eq 0 ] || exit $rc
+done
