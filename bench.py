@@ -18,12 +18,16 @@ each step's finished rows are drained from the device and, for N > 1, gathered t
 rank 0 over RCCL (the only collective); a writer thread on rank 0 writes them to
 .npz files (the reference's trainingwrite row format) inside the timed region.
 
-value = training rows produced per second in the timed window, whole job: in the
-benchmark play settings (one row per move at full visits) every committed
-move is exactly one row, fixed at commit; its game's rows are written when the game
-ends.  rows_written_npz counts the rows the writer actually wrote in the window.
-Game starts are staggered over the warm-up (a seeded per-slot idle delay), so game
-ends and row bursts are spread over the run rather than arriving in phase.
+value = training rows written per second in the timed window, whole job (the rows a
+step drains from the device -- those of games that ended -- gathered to rank 0 and
+written to .npz by the writer thread before the clock stops).  In the benchmark play
+settings (one row per move at full visits) every committed move becomes
+exactly one row when its game ends, so in steady state rows/s = moves/s.  Steady state
+(--window steady, the default for C2-C4): game starts are staggered over one game length
+(a seeded per-slot idle delay) and the warm-up covers 1.5 game lengths (rounds per step
+are raised to fit the --warmup steps), so game ends arrive at their steady rate through
+the whole window.  --window short (C5 default, whose games last ~65k rounds): value is
+committed moves/s and says so in value_kind.
 
 --gpus N without a torch.distributed launcher starts N ranks itself (one process per
 GPU, RCCL world size N); under torchrun the environment's WORLD_SIZE is used.
@@ -77,7 +81,11 @@ def parse():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="C2")
     ap.add_argument("--games", type=int, default=0, help="games per GPU (0 = the config's)")
     ap.add_argument("--visits", type=int, default=0, help="visits per move (0 = the config's)")
-    ap.add_argument("--rounds-per-step", type=int, default=0, help="0 = the config's")
+    ap.add_argument("--rounds-per-step", type=int, default=0,
+                    help="0 = the config's, raised so the warm-up covers 1.5 game lengths (--window steady)")
+    ap.add_argument("--window", choices=["steady", "short"], default=None,
+                    help="steady: warm-up past the first game ends, value = rows written/s; short: value = moves/s "
+                         "(default: steady except C5)")
     ap.add_argument("--precision", choices=["fast", "accurate", "fast-layered"], default="fast")
     ap.add_argument("--commit-interval", type=int, default=8)
     ap.add_argument("--nn-cache-log2", type=int, default=21,
@@ -93,6 +101,9 @@ def parse():
                     help="independent game groups per GPU, each on its own stream (overlaps one group's network "
                          "with another's search kernels; the reference's numNNServerThreadsPerModel); "
                          "0 = 2 except for b18c384nbt (C5), whose forward is throughput-bound")
+    ap.add_argument("--reload-every", type=int, default=0,
+                    help="hot reload every K timed steps: rank 0 writes a new random model and broadcasts its "
+                         "bytes over RCCL; every engine switches (the reference's model hot reload)")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
@@ -132,9 +143,12 @@ def launch_ranks(n, script=None, argv=None):
 
 
 def cpu_info():
+    """Threads the CPU baseline uses: OMP_NUM_THREADS (the GPU box sets 16, its CPU share
+    per GPU), else the affinity mask; the machine's totals are reported beside it."""
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if cores <= 0:
-        cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+        cores = affinity
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -143,7 +157,8 @@ def cpu_info():
                 break
     except OSError:
         pass
-    return cores, model
+    return cores, model, {"nproc": os.cpu_count(), "affinity": affinity,
+                          "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_run(oracle, model, X, Y, W, games, visits, threads, warm_s, timed_s, cache_log2):
@@ -173,7 +188,7 @@ def cpu_baseline(args, cfg, model_path):
     SGEMM) on this host: C1 (1 game, 200 visits) and the GPU's workload saturated
     (4 x cores games, threads over games and inside the forward, NN cache on)."""
     from oracle import oracle
-    cores, model_name = cpu_info()
+    cores, model_name, machine = cpu_info()
     model = oracle.Model(model_path)
     c1 = None
     if cfg["arch"] == "b6c96" and (cfg["X"], cfg["Y"]) == (5, 5):
@@ -184,7 +199,7 @@ def cpu_baseline(args, cfg, model_path):
     out = {
         "value": sat["rows_per_sec"], "unit": "rows/s", "cores": cores, "kind": "port",
         "playouts_per_sec": sat["playouts_per_sec"], "nn_evals_per_sec": sat["nn_evals_per_sec"],
-        "cpu_model": model_name,
+        "cpu_model": model_name, "host_cpus": machine,
         "sample": "oracle C++ self-play (fp32 im2col+SGEMM forward), %s workload on %d threads: %d games x %d visits, "
                   "%.0f s warm-up then %d rounds in %.1f s (%d moves, %d playouts)"
                   % (cfg["label"].split(":")[0], cores, 4 * cores, args.visits or cfg["visits"],
@@ -246,8 +261,10 @@ class Groups:
     chain select -> compact -> network -> backup; two groups overlap those chains."""
 
     def __init__(self, kc, k, games, slot_base, **kw):
-        assert games % k == 0
-        self.g = [kc.Selfplay(num_games=games // k, slot_base=slot_base + i * (games // k), **kw) for i in range(k)]
+        # floor / ceil shares over contiguous slot ranges (any k <= games)
+        sizes = [games // k + (1 if i < games % k else 0) for i in range(k)]
+        starts = [slot_base + sum(sizes[:i]) for i in range(k)]
+        self.g = [kc.Selfplay(num_games=n, slot_base=s0, **kw) for n, s0 in zip(sizes, starts)]
 
     def step(self, rounds, chunk=8):
         done = 0
@@ -287,6 +304,10 @@ class Groups:
     def timed_nn_evals(self):
         return sum(e.timed_nn_evals() for e in self.g)
 
+    def set_model_bytes(self, data):
+        for e in self.g:
+            e.set_model_bytes(data)
+
     def close(self):
         for e in self.g:
             e.close()
@@ -308,6 +329,11 @@ def main():
     games = args.games or cfg["games"]
     visits = args.visits or cfg["visits"]
     rps = args.rounds_per_step or cfg["rounds"]
+    window = args.window or ("short" if args.config == "C5" else "steady")
+    # rounds per game: (visits + root evaluations) per move x ~A/2 moves
+    game_rounds = (visits + 4) * X * Y // 2
+    if window == "steady" and not args.rounds_per_step:
+        rps = max(rps, -(-3 * game_rounds // (2 * max(1, args.warmup))))
     import numpy as np  # noqa: F401
     import torch
 
@@ -330,26 +356,24 @@ def main():
     flops_per_eval = kc.model_flops(model_path, X * Y)
 
     warm_rounds = args.warmup * rps
-    game_rounds = visits * X * Y // 2
-    stagger = args.stagger if args.stagger >= 0 else min(game_rounds, int(0.9 * warm_rounds))
+    if args.stagger >= 0:
+        stagger = args.stagger
+    else:
+        stagger = game_rounds if window == "steady" else min(game_rounds, int(0.9 * warm_rounds))
     play = PRODUCTION if args.play == "production" else {}
     # benchmark mode clears the tree before every move: a search holds at
     # most visits + 1 nodes; production's cheap searches reuse the tree
     node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
-    fused = args.precision == "fast" and cfg["arch"] == "b6c96"
     if args.groups == 0:
         # latency-bound rounds gain from two overlapped chains (measured: C2 +8 %, C3 +12 %,
         # C4 +10 % rows/s); b18c384nbt's forward is throughput-bound (C5: -12 % playouts/s)
-        args.groups = 2 if cfg["arch"] != "b18c384nbt" and games % 2 == 0 else 1
-    cap = args.nn_batch_cap
-    if cap == 0 and args.groups > 1 and fused:
-        # the groups' fused network launches share one wave of workgroups (the layered
-        # network has no batch cap: its cost grows with the batch)
-        cap = torch.cuda.get_device_properties(local).multi_processor_count * 8
+        args.groups = 2 if cfg["arch"] != "b18c384nbt" else 1
+    # nn_batch_cap 0: the engines split the fused network's one wave of workgroups
+    # (engines_per_device); the layered network has no batch cap (its cost grows with the batch)
     sp = Groups(kc, args.groups, games, rank * games, X=X, Y=Y, W=W, max_visits=visits, seed=args.seed,
                 model_path=model_path, commit_interval=args.commit_interval, nn_cache_log2=args.nn_cache_log2,
-                nn_batch_cap=cap // args.groups, nn_precision=args.precision, start_stagger=stagger,
-                node_cap=node_cap, **play)
+                nn_batch_cap=args.nn_batch_cap // args.groups, nn_precision=args.precision, start_stagger=stagger,
+                node_cap=node_cap, engines_per_device=args.groups, **play)
     for _ in range(args.warmup):
         sp.step(rps)
         sp.sync()  # bounded launch queue (a profiler's per-dispatch state stays small)
@@ -370,11 +394,26 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    from katacoffee_amd import weights as kcweights
+
+    def reload(k):
+        # rank 0 "trains" a new network; its bytes reach every rank over RCCL
+        path = os.path.join(tmpdir, "reload%d.cfnn" % k)
+        if rank == 0:
+            kc.write_random_model(cfg["arch"], 0xC0FFEE + k, path)
+        data = open(path, "rb").read() if dist is None else \
+            kcweights.broadcast_model(path, dist, torch.device("cuda", local))
+        sp.set_model_bytes(data)
+
     rows_gathered = 0
     per_rank_rows = 0
+    reloads = 0
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for step in range(args.steps):
+        if args.reload_every and step and step % args.reload_every == 0:
+            reloads += 1
+            reload(reloads)
         sp.step(rps)
         rows = sp.drain_rows()
         sp.drain_games()
@@ -458,11 +497,14 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, cfg, model_path)
-        rows_per_sec = d["moves"] / elapsed
+        # whole-job rows written (gathered to rank 0, on disk before the clock stopped)
+        rows_per_sec = rows_gathered / elapsed if window == "steady" else d["moves"] / elapsed
         out = {
             "metric": "self-play training rows/sec + MCTS playouts/sec, 5x5 Coffee b6c96 @600 visits",
             "value": rows_per_sec,
             "unit": "rows/s",
+            "value_kind": "rows written per second (steady state)" if window == "steady" else
+                          "committed moves per second (window shorter than one game: rows/s in steady state)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -477,7 +519,8 @@ def main():
                        "config": args.config, "games_per_gpu": games, "visits": visits, "arch": cfg["arch"],
                        "board": "%dx%d win %d" % (X, Y, W), "precision": args.precision,
                        "network_path": "fused" if args.precision == "fast" and cfg["arch"] == "b6c96" else "layered",
-                       "rounds_per_step": rps, "commit_interval": args.commit_interval,
+                       "rounds_per_step": rps, "window": window, "game_rounds_estimate": game_rounds,
+                       "warmup_rounds": warm_rounds, "commit_interval": args.commit_interval,
                        "nn_cache_log2": args.nn_cache_log2, "nn_batch_cap": args.nn_batch_cap or "engine default",
                        "play_settings": args.play, "start_stagger_rounds": stagger, "groups": args.groups, "node_cap": node_cap or "default",
                        "parallelism": "game-sharded x%d (RCCL row gather)" % world if world > 1 else "1 GPU"},
@@ -488,6 +531,7 @@ def main():
             "nn_evals_per_sec": d["nn_evals"] / elapsed,
             "rows_drained": rows_gathered,
             "rows_written_npz": writer.rows if writer else None,
+            "model_reloads": reloads,
             "rows_written_npz_per_sec": (writer.rows / elapsed) if writer else None,
             "npz_files": writer.files if writer else None,
             "kernels": kernels,

@@ -118,6 +118,15 @@ int coffee_nn_is_fused(coffee_nn* h, int* fused);
  * (win, loss) from the side to move, misc[2].  fp16 MFMA operands (see precision),
  * f32 accumulation. */
 int coffee_nn_forward(coffee_nn* h, int n, const uint64_t* in, float* out, void* stream);
+/* NeuralNet::getOutput's contract (eigenbackend.cpp:1776-1796): as coffee_nn_forward, with
+ * sym [n] i32 (device) = the symmetry each row was encoded with (coffee_encode_batch's
+ * sym); the policy logits come back in the CANONICAL frame, the inverse symmetry applied
+ * per SPEC B12 (cells un-flipped / un-transposed and the directions mapped back: a one-axis
+ * flip swaps NW<->NE, a transpose swaps N<->W), as copyOutputsWithSymmetry does.  Value
+ * logits (win, loss; side to move) and misc[2] are symmetry-free and unchanged.  The
+ * NNEvaluator-side post-processing (legal mask, softmax, white perspective;
+ * nneval.cpp:702-844) stays with the caller, as in the reference. */
+int coffee_nn_forward2(coffee_nn* h, int n, const uint64_t* in, const int32_t* sym, float* out, void* stream);
 int coffee_nn_destroy(coffee_nn* h);
 
 /* The deterministic stand-in network (oracle fakeNet), same I/O as coffee_nn_forward. */
@@ -207,12 +216,16 @@ typedef struct coffee_selfplay_config {
                             nnCacheSizePowerOfTwo = 21); 0 disables (SPEC a7) */
   int32_t nn_batch_cap;  /* rows per network launch; leaves past it wait for the next round,
                             ahead of new ones.  0 = one full wave of network workgroups
-                            (compute units x 8 boards: 2048 on MI355X) for the fused
-                            kernel, unbounded for the layered kernels */
+                            (compute units x 8 boards: 2048 on MI355X, / engines_per_device)
+                            for the fused kernel, unbounded for the layered kernels */
   int32_t nn_precision;  /* COFFEE_NN_FAST / _ACCURATE / _FAST_LAYERED (0 = fast) */
   int32_t start_stagger; /* > 0: each slot idles a seeded number of rounds in [0, start_stagger)
                             before its first game (benchmarks: spreads game ends over the
                             run); 0 = all games start in round 0 */
+  int32_t engines_per_device; /* engines sharing this device (the CLI's numNNServerThreadsPerModel
+                            engines on one GPU); with nn_batch_cap 0 a fused network's default
+                            cap (one wave of network workgroups) is split between them, also
+                            after a hot reload that changes the network path; 0 or 1 = alone */
 } coffee_selfplay_config;
 
 typedef struct coffee_selfplay coffee_selfplay;
@@ -262,6 +275,10 @@ int coffee_selfplay_drain_games(coffee_selfplay* h, int max_games, int32_t* head
  * model hot reload with switchNetsMidGame, selfplay.cpp:135-260, play.cpp:1210-1226).
  * On error (unreadable / mismatched model) the current network stays in use. */
 int coffee_selfplay_set_model(coffee_selfplay* h, const char* model_path);
+/* The same from a CFNN file image in HOST memory (bytes long): a multi-rank host
+ * broadcasts the new weights from rank 0 (RCCL) and every rank switches from the
+ * received image, instead of each rank re-reading the file. */
+int coffee_selfplay_set_model_bytes(coffee_selfplay* h, const void* data, uint64_t bytes);
 int coffee_selfplay_destroy(coffee_selfplay* h);
 
 /* Writes n rows (HOST arrays, drain_rows layout) as a training .npz in the reference's

@@ -88,6 +88,7 @@ class SelfplayConfig(ctypes.Structure):
         ("nn_batch_cap", ctypes.c_int32),
         ("nn_precision", ctypes.c_int32),
         ("start_stagger", ctypes.c_int32),
+        ("engines_per_device", ctypes.c_int32),
     ]
 
 
@@ -102,9 +103,10 @@ EXPORTS = [
     "coffee_last_error", "coffee_abi_version", "coffee_device_count", "coffee_set_device", "coffee_device_compute_units", "coffee_malloc",
     "coffee_free", "coffee_memcpy", "coffee_synchronize", "coffee_rules_batch", "coffee_play_batch",
     "coffee_encode_batch", "coffee_model_write_random", "coffee_model_flops", "coffee_nn_create",
-    "coffee_nn_forward", "coffee_nn_destroy", "coffee_nn_create2", "coffee_nn_is_fused", "coffee_fake_net", "coffee_search_params_default",
+    "coffee_nn_forward", "coffee_nn_forward2", "coffee_nn_destroy", "coffee_nn_create2", "coffee_nn_is_fused", "coffee_fake_net", "coffee_search_params_default",
     "coffee_selfplay_create", "coffee_selfplay_step", "coffee_selfplay_sync", "coffee_selfplay_stats_get",
     "coffee_selfplay_drain_rows", "coffee_selfplay_drain_games", "coffee_selfplay_set_model",
+    "coffee_selfplay_set_model_bytes",
     "coffee_selfplay_destroy", "coffee_selfplay_game_info",
     "coffee_selfplay_game_tree", "coffee_selfplay_root_policy", "coffee_debug_cdf_table", "coffee_debug_zobrist",
     "coffee_selfplay_enable_timing", "coffee_selfplay_kernel_time", "coffee_selfplay_timed_nn_evals",
@@ -140,6 +142,7 @@ def lib():
         L.coffee_nn_create2.argtypes = [ctypes.c_char_p, c_i, c_i, c_i, c_i, c_p]
         L.coffee_nn_is_fused.argtypes = [c_p, c_p]
         L.coffee_nn_forward.argtypes = [c_p, c_i, c_p, c_p, c_p]
+        L.coffee_nn_forward2.argtypes = [c_p, c_i, c_p, c_p, c_p, c_p]
         L.coffee_nn_destroy.argtypes = [c_p]
         L.coffee_fake_net.argtypes = [c_i, c_i, c_i, c_i, c_p, c_p, c_p]
         L.coffee_rules_batch.argtypes = [c_i, c_i, c_i, c_i] + [c_p] * 7
@@ -154,6 +157,7 @@ def lib():
         L.coffee_selfplay_drain_rows.argtypes = [c_p, c_i] + [c_p] * 7
         L.coffee_selfplay_drain_games.argtypes = [c_p, c_i, c_p, c_p, c_p]
         L.coffee_selfplay_set_model.argtypes = [c_p, ctypes.c_char_p]
+        L.coffee_selfplay_set_model_bytes.argtypes = [c_p, c_p, c_u64]
         L.coffee_selfplay_destroy.argtypes = [c_p]
         L.coffee_selfplay_game_info.argtypes = [c_p, c_i, c_p]
         L.coffee_selfplay_game_tree.argtypes = [c_p, c_i, c_i, c_p, c_p, c_p]
@@ -305,6 +309,21 @@ class Network:
         _sync(torch)
         return out.cpu().numpy()
 
+    def forward_canonical(self, packed, sym):
+        """NeuralNet::getOutput (eigenbackend.cpp:1776-1796): packed [n][words] u64 rows
+        encoded with symmetries sym [n] -> [n][P+4] f32 with the policy logits in the
+        canonical frame (coffee_nn_forward2)."""
+        torch = _torch_cuda()
+        n = packed.shape[0]
+        P = 4 * self.X * self.Y
+        din = _dev(torch, np.ascontiguousarray(packed).view(np.int64))
+        dsym = _dev(torch, sym, np.int32)
+        out = torch.zeros((n, P + 4), dtype=torch.float32, device="cuda")
+        _sync(torch)
+        check(lib().coffee_nn_forward2(self.h, n, _dp(din), _dp(dsym), _dp(out), None))
+        _sync(torch)
+        return out.cpu().numpy()
+
     def close(self):
         if self.h:
             lib().coffee_nn_destroy(self.h)
@@ -358,7 +377,7 @@ class Selfplay:
 
     def __init__(self, X=5, Y=5, W=4, num_games=4096, max_visits=600, seed=1, slot_base=0, model_path=None,
                  node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, nn_batch_cap=0, nn_precision="fast",
-                 start_stagger=0, **search_over):
+                 start_stagger=0, engines_per_device=0, **search_over):
         _torch_cuda()
         self.X, self.Y, self.W = X, Y, W
         self.A, self.P = X * Y, 4 * X * Y
@@ -376,6 +395,7 @@ class Selfplay:
         cfg.nn_batch_cap = nn_batch_cap
         cfg.nn_precision = PRECISIONS[nn_precision]
         cfg.start_stagger = start_stagger
+        cfg.engines_per_device = engines_per_device
         self._model = model_path.encode() if model_path else None
         cfg.model_path = self._model
         cfg.search = default_search_params(max_visits=max_visits, **search_over)
@@ -427,6 +447,12 @@ class Selfplay:
         """Hot reload: every later round of every game uses this network."""
         self._model = model_path.encode()
         check(lib().coffee_selfplay_set_model(self.h, self._model))
+
+    def set_model_bytes(self, data):
+        """Hot reload from a CFNN image in memory (bytes / uint8 array), e.g. weights
+        broadcast from rank 0 (katacoffee_amd.weights.broadcast_model)."""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        check(lib().coffee_selfplay_set_model_bytes(self.h, _ptr(buf), buf.size))
 
     def game_info(self, slot):
         info = np.zeros(16, np.int64)

@@ -86,7 +86,7 @@ static void checkGeom(int x, int y, int w) {
 extern "C" {
 
 const char* coffee_last_error(void) { return gLastError.c_str(); }
-int coffee_abi_version(void) { return 104; }
+int coffee_abi_version(void) { return 105; }
 
 int coffee_device_count(int* count) {
   return guarded([&] {
@@ -178,6 +178,7 @@ int coffee_model_flops(const char* path, int area, double* flops) {
 
 struct coffee_nn {
   NNEngine* eng;
+  int x, y, w;
 };
 
 int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_nn** out) {
@@ -192,7 +193,7 @@ int coffee_nn_create2(const char* model_path, int x, int y, int win_len, int pre
     checkGeom(x, y, win_len);
     ModelHost m = loadModel(model_path);
     (void)deviceTables(x, y, win_len);
-    coffee_nn* h = new coffee_nn{nullptr};
+    coffee_nn* h = new coffee_nn{nullptr, x, y, win_len};
     try {
       h->eng = new NNEngine(m, x, y, win_len, precision);
     } catch(...) {
@@ -209,6 +210,16 @@ int coffee_nn_forward(coffee_nn* h, int n, const uint64_t* in, float* out, void*
     need(n >= 0, "n must be >= 0");
     need(n == 0 || (in && out), "NULL buffer");
     h->eng->forward(n, in, out, (hipStream_t)stream);
+  });
+}
+
+int coffee_nn_forward2(coffee_nn* h, int n, const uint64_t* in, const int32_t* sym, float* out, void* stream) {
+  return guarded([&] {
+    need(h && h->eng, "NULL handle");
+    need(n >= 0, "n must be >= 0");
+    need(n == 0 || (in && sym && out), "NULL buffer");
+    h->eng->forward(n, in, out, (hipStream_t)stream);
+    launchCanonicalRows(deviceTables(h->x, h->y, h->w), n, sym, out, (hipStream_t)stream);
   });
 }
 
@@ -358,6 +369,13 @@ int coffee_selfplay_set_model(coffee_selfplay* h, const char* model_path) {
   return guarded([&] {
     need(h && h->eng && model_path, "NULL argument");
     h->eng->setModel(model_path);
+  });
+}
+
+int coffee_selfplay_set_model_bytes(coffee_selfplay* h, const void* data, uint64_t bytes) {
+  return guarded([&] {
+    need(h && h->eng && data, "NULL argument");
+    h->eng->setModelBytes(data, (size_t)bytes);
   });
 }
 

@@ -40,6 +40,9 @@
 #include <vector>
 
 #include "../../include/katacoffee.h"
+#include "cli_config.h"
+
+using namespace kccli;
 
 static std::atomic<bool> gStop(false);
 static void onSignal(int) { gStop = true; }
@@ -62,30 +65,6 @@ static void logf(const char* fmt, ...) {
     fprintf(gLog, "%s: %s\n", ts, buf);
     fflush(gLog);
   }
-}
-
-static std::string trim(const std::string& s) {
-  size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
-  return a == std::string::npos ? "" : s.substr(a, b - a + 1);
-}
-
-static bool readConfig(const std::string& path, std::map<std::string, std::string>& kv) {
-  std::ifstream in(path);
-  if(!in)
-    return false;
-  std::string line;
-  while(std::getline(in, line)) {
-    size_t h = line.find('#');
-    if(h != std::string::npos)
-      line = line.substr(0, h);
-    size_t eq = line.find('=');
-    if(eq == std::string::npos)
-      continue;
-    std::string k = trim(line.substr(0, eq)), v = trim(line.substr(eq + 1));
-    if(!k.empty())
-      kv[k] = v;
-  }
-  return true;
 }
 
 static void die(const std::string& msg) {
@@ -175,118 +154,6 @@ static void mkdirs(const std::string& path) {
     cur += part + "/";
     mkdir(cur.c_str(), 0755);
   }
-}
-
-struct Settings {
-  int x = 5, y = 5, winLen = 4, games = 4096, gpus = 1, maxRowsPerFile = 10000;
-  int servers = 1;  // numNNServerThreadsPerModel: self-play engines (own stream, batch, cache) over all GPUs
-  float modelPollSeconds = 10.0f;
-  int nnCacheLog2 = 21;  // selfplay1.cfg:121 nnCacheSizePowerOfTwo
-  int nnPrecision = COFFEE_NN_FAST;  // nnPrecision = fast | accurate | fastLayered (the reference's useFP16)
-  int64_t maxGamesTotal = -1;
-  uint64_t seed = 0;
-  coffee_search_params sp;
-};
-
-static void applyConfig(const std::map<std::string, std::string>& kv, Settings& s) {
-  auto geti = [&](const char* k, int& v) {
-    auto it = kv.find(k);
-    if(it != kv.end())
-      v = std::stoi(it->second);
-  };
-  auto getf = [&](const char* k, float& v) {
-    auto it = kv.find(k);
-    if(it != kv.end())
-      v = std::stof(it->second);
-  };
-  auto getb = [&](const char* k, int32_t& v) {
-    auto it = kv.find(k);
-    if(it != kv.end())
-      v = (it->second == "true" || it->second == "True" || it->second == "1") ? 1 : 0;
-  };
-  auto it = kv.find("bSizes");
-  if(it != kv.end()) {
-    s.x = s.y = std::stoi(it->second.substr(0, it->second.find(',')));
-  }
-  geti("boardXLen", s.x);
-  geti("boardYLen", s.y);
-  geti("winLen", s.winLen);
-  geti("numGameThreads", s.games);
-  geti("numGamesPerGpu", s.games);
-  geti("numGpus", s.gpus);
-  geti("numNNServerThreadsPerModel", s.servers);
-  geti("maxRowsPerTrainFile", s.maxRowsPerFile);
-  getf("modelPollSeconds", s.modelPollSeconds);
-  geti("nnCacheSizePowerOfTwo", s.nnCacheLog2);  // setup.cpp:268; <= 0 disables the cache
-  s.nnCacheLog2 = std::max(0, s.nnCacheLog2);
-  it = kv.find("nnPrecision");
-  if(it != kv.end()) {
-    if(it->second == "fast")
-      s.nnPrecision = COFFEE_NN_FAST;
-    else if(it->second == "accurate")
-      s.nnPrecision = COFFEE_NN_ACCURATE;
-    else if(it->second == "fastLayered")
-      s.nnPrecision = COFFEE_NN_FAST_LAYERED;
-    else
-      throw std::runtime_error("nnPrecision must be fast, accurate or fastLayered");
-  }
-  coffee_search_params& p = s.sp;
-  geti("maxVisits", p.max_visits);
-  getf("cpuctExploration", p.cpuct_exploration);
-  getf("cpuctExplorationLog", p.cpuct_exploration_log);
-  getf("cpuctExplorationBase", p.cpuct_exploration_base);
-  getf("fpuReductionMax", p.fpu_reduction_max);
-  getf("rootFpuReductionMax", p.root_fpu_reduction_max);
-  getf("fpuLossProp", p.fpu_loss_prop);
-  getf("rootFpuLossProp", p.root_fpu_loss_prop);
-  getb("fpuParentWeightByVisitedPolicy", p.fpu_parent_weight_by_visited_policy);
-  getf("fpuParentWeightByVisitedPolicyPow", p.fpu_parent_weight_by_visited_policy_pow);
-  getf("valueWeightExponent", p.value_weight_exponent);
-  getb("rootNoiseEnabled", p.root_noise_enabled);
-  getf("rootDirichletNoiseTotalConcentration", p.root_dirichlet_noise_total_concentration);
-  getf("rootDirichletNoiseWeight", p.root_dirichlet_noise_weight);
-  getf("rootPolicyTemperature", p.root_policy_temperature);
-  getf("rootPolicyTemperatureEarly", p.root_policy_temperature_early);
-  getf("rootDesiredPerChildVisitsCoeff", p.root_desired_per_child_visits_coeff);
-  geti("rootNumSymmetriesToSample", p.root_num_symmetries_to_sample);
-  getf("chosenMoveTemperature", p.chosen_move_temperature);
-  getf("chosenMoveTemperatureEarly", p.chosen_move_temperature_early);
-  getf("chosenMoveTemperatureHalflife", p.chosen_move_temperature_halflife);
-  getf("chosenMoveSubtract", p.chosen_move_subtract);
-  getf("chosenMovePrune", p.chosen_move_prune);
-  getb("useLcbForSelection", p.use_lcb_for_selection);
-  getf("lcbStdevs", p.lcb_stdevs);
-  getf("minVisitPropForLCB", p.min_visit_prop_for_lcb);
-  getf("subtreeValueBiasFactor", p.subtree_value_bias_factor);
-  getf("subtreeValueBiasWeightExponent", p.subtree_value_bias_weight_exponent);
-  getf("subtreeValueBiasFreeProp", p.subtree_value_bias_free_prop);
-  getb("useGraphSearch", p.use_graph_search);
-  // PlaySettings (playsettings.cpp:80-99)
-  getf("cheapSearchProb", p.cheap_search_prob);
-  geti("cheapSearchVisits", p.cheap_search_visits);
-  getf("cheapSearchTargetWeight", p.cheap_search_target_weight);
-  getb("reduceVisits", p.reduce_visits);
-  getf("reduceVisitsThreshold", p.reduce_visits_threshold);
-  geti("reduceVisitsThresholdLookback", p.reduce_visits_threshold_lookback);
-  geti("reducedVisitsMin", p.reduced_visits_min);
-  getf("reducedVisitsWeight", p.reduced_visits_weight);
-  getf("policySurpriseDataWeight", p.policy_surprise_data_weight);
-  getf("valueSurpriseDataWeight", p.value_surprise_data_weight);
-  getb("initGamesWithPolicy", p.init_games_with_policy);
-  getf("policyInitAreaProp", p.policy_init_area_prop);
-  getf("policyInitAreaTemperature", p.policy_init_area_temperature);
-  getf("earlyForkGameProb", p.early_fork_game_prob);
-  getf("earlyForkGameExpectedMoveProp", p.early_fork_game_expected_move_prop);
-  getf("forkGameProb", p.fork_game_prob);
-  geti("forkGameMinChoices", p.fork_game_min_choices);
-  geti("earlyForkGameMaxChoices", p.early_fork_game_max_choices);
-  geti("forkGameMaxChoices", p.fork_game_max_choices);
-  getf("sidePositionProb", p.side_position_prob);
-  // PlaySettings fields the reference's loader never reads (playsettings.cpp:14): accepted
-  // here so the recording can be switched on from a config
-  getb("recordTreePositions", p.record_tree_positions);
-  geti("recordTreeThreshold", p.record_tree_threshold);
-  getf("recordTreeTargetWeight", p.record_tree_target_weight);
 }
 
 struct RowSink {
@@ -404,11 +271,11 @@ static void runGpu(int gpu, int server, int perGpu, int slot, int share, const S
   c.num_games = share;
   c.seed = s.seed;
   c.slot_base = slot;
-  if(perGpu > 1) {
-    int cus = 0;
-    check(coffee_device_compute_units(gpu, &cus), "compute units");
-    c.nn_batch_cap = std::max(1, cus * 8 / perGpu);
-  }
+  // engines sharing this GPU split the default batch cap of a fused network (one wave
+  // of network workgroups); layered networks stay uncapped (the engine decides, also
+  // after a hot reload that changes the network path)
+  c.nn_batch_cap = 0;
+  c.engines_per_device = perGpu;
   c.use_fake_net = 0;
   c.commit_interval = 8;
   c.model_path = model.c_str();
@@ -539,7 +406,11 @@ int main(int argc, char** argv) {
   }
   Settings s;
   coffee_search_params_default(&s.sp);
-  applyConfig(kv, s);
+  try {
+    applyConfig(kv, s);
+  } catch(const std::exception& e) {
+    die(e.what());
+  }
   s.maxGamesTotal = maxGames;
   s.seed = std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32);
   mkdirs(outDir);
@@ -560,18 +431,27 @@ int main(int argc, char** argv) {
     die("numGpus must be in 1.." + std::to_string(ndev));
   logf("selfplay: model %s, %dx%d win %d, %d games/GPU x %d GPUs, %d visits", model.c_str(), s.x, s.y, s.winLen,
        s.games, s.gpus, s.sp.max_visits);
-  // numNNServerThreadsPerModel engines spread over the GPUs (at least one each); a
-  // GPU's games split evenly between its engines
-  const int perGpu = std::max(1, (s.servers + s.gpus - 1) / s.gpus);
-  if(perGpu > s.games)
-    die("numNNServerThreadsPerModel exceeds the games per GPU");
-  std::vector<std::thread> th;
+  // numNNServerThreadsPerModel engines spread over the GPUs: floor / ceil per GPU so the
+  // total is exactly the configured count (the reference gives each server thread its
+  // GPU, gpuToUseThreadN); every GPU runs at least one.  A GPU's games split evenly
+  // between its engines.
+  int engines = 0;
   for(int g = 0; g < s.gpus; g++)
+    engines += std::max(1, s.servers / s.gpus + (g < s.servers % s.gpus ? 1 : 0));
+  if(engines != s.servers)
+    logf("selfplay: numNNServerThreadsPerModel %d < numGpus %d: running %d engines (one per GPU)", s.servers,
+         s.gpus, engines);
+  std::vector<std::thread> th;
+  for(int g = 0; g < s.gpus; g++) {
+    const int perGpu = std::max(1, s.servers / s.gpus + (g < s.servers % s.gpus ? 1 : 0));
+    if(perGpu > s.games)
+      die("numNNServerThreadsPerModel exceeds the games per GPU");
     for(int k = 0, off = 0; k < perGpu; k++) {
       const int share = s.games / perGpu + (k < s.games % perGpu ? 1 : 0);
       th.emplace_back(runGpu, g, k, perGpu, g * s.games + off, share, std::cref(s), std::cref(outDir));
       off += share;
     }
+  }
   for(auto& t : th)
     t.join();
   if(gLog)

@@ -17,6 +17,9 @@ void launchPlayBatch(const DTables* T, int n, const uint8_t* cells, const int8_t
                      int32_t* maxRunOut, uint64_t* posHash, uint64_t* stHash, hipStream_t st);
 void launchEncodeBatch(const DTables* T, int n, const uint8_t* cells, const int8_t* histCell, const int8_t* histDir,
                        const uint8_t* pla, const int32_t* sym, uint64_t* packed, float* planes, hipStream_t st);
+// Policy logits of n network rows [n][P+4] from each row's symmetric frame sym[n] to
+// the canonical frame, in place (coffee_nn_forward2).
+void launchCanonicalRows(const DTables* T, int n, const int32_t* sym, float* out, hipStream_t st);
 
 // Device copy of the geometry tables, cached per (X, Y, W).
 const DTables* deviceTables(int X, int Y, int W);
@@ -125,6 +128,8 @@ class NNEngine {
   NNLayout* layoutDev_ = nullptr;
   uint16_t* tabDev_ = nullptr;   // device row tables (nn.hip rowTables), 8 boards per workgroup
   uint16_t* tabDev4_ = nullptr;  // the same for 4 boards per workgroup
+  uint16_t* tabDev2_ = nullptr;  // the same for 2 boards per (4-wave) workgroup
+  bool small4_ = false;          // small batches on the 4-board instance (A/B runs)
   float* trunk_ = nullptr;       // f32 residual trunk scratch, [workgroup][fragment] (nn.hip)
   size_t trunkBytes_ = 0;        // its size
   int cus_ = 1;                  // compute units of the engine's device

@@ -174,13 +174,28 @@ void saveModel(const std::string& path, const ModelHost& m) {
 }
 
 namespace {
+// Reads a CFNN image in memory (a file's bytes, or weights broadcast from another rank).
 struct FileReader {
-  FILE* f;
+  const unsigned char* p;
+  size_t left;  // bytes left in the image: no tensor is sized past its end
   bool ok = true;
-  void r(std::vector<float>& v, size_t n) {
-    v.resize(n);
-    if(fread(v.data(), 4, n, f) != n)
+  bool raw(void* dst, size_t bytes) {
+    if(!ok || bytes > left) {
       ok = false;
+      return false;
+    }
+    memcpy(dst, p, bytes);
+    p += bytes;
+    left -= bytes;
+    return true;
+  }
+  void r(std::vector<float>& v, size_t n) {
+    if(!ok || n > left / 4) {
+      ok = false;
+      return;
+    }
+    v.resize(n);
+    raw(v.data(), n * 4);
   }
   void block(ModelBlock& b, int k, int W, int Cg, int mid) {
     b.kind = k;
@@ -205,33 +220,32 @@ struct FileReader {
 };
 }  // namespace
 
-ModelHost loadModel(const std::string& path) {
-  FILE* f = fopen(path.c_str(), "rb");
-  if(!f)
-    throw std::runtime_error("cannot open model " + path);
+ModelHost loadModelBytes(const void* data, size_t bytes, const std::string& name) {
+  FileReader rd{static_cast<const unsigned char*>(data), data ? bytes : 0};
   char magic[4];
   int32_t ver = 0, hdr[10] = {0};
-  if(fread(magic, 1, 4, f) != 4 || memcmp(magic, "CFNN", 4) != 0 || fread(&ver, 4, 1, f) != 1 ||
-     (ver != 1 && ver != 2) || fread(hdr, 4, ver == 1 ? 9 : 10, f) != (size_t)(ver == 1 ? 9 : 10) || hdr[8] < 1 ||
-     hdr[8] > 64) {
-    fclose(f);
-    throw std::runtime_error("not a CFNN v1/v2 model: " + path);
-  }
+  if(!rd.raw(magic, 4) || memcmp(magic, "CFNN", 4) != 0 || !rd.raw(&ver, 4) || (ver != 1 && ver != 2) ||
+     !rd.raw(hdr, 4 * (ver == 1 ? 9 : 10)) || hdr[8] < 1 || hdr[8] > 64)
+    throw std::runtime_error("not a CFNN v1/v2 model: " + name);
+  // header sizes: positive and bounded (a corrupted field must not size a tensor)
+  bool sane = true;
+  for(int i = 0; i < 8; i++)
+    sane = sane && hdr[i] >= 1 && hdr[i] <= 4096;
+  sane = sane && hdr[3] < hdr[2] && (ver == 1 || (hdr[9] >= 1 && hdr[9] <= hdr[2]));
+  if(!sane)
+    throw std::runtime_error("bad header sizes in model " + name);
   ModelHost m;
   ModelCfg& c = m.cfg;
   c.cin = hdr[0]; c.gin = hdr[1]; c.C = hdr[2]; c.Cg = hdr[3]; c.p1 = hdr[4]; c.g1 = hdr[5]; c.v1 = hdr[6];
   c.v2 = hdr[7];
   c.mid = ver == 2 ? hdr[9] : 0;
   c.kinds.resize(hdr[8]);
-  FileReader rd{f};
-  rd.ok = fread(c.kinds.data(), 4, hdr[8], f) == (size_t)hdr[8];
+  rd.raw(c.kinds.data(), 4 * (size_t)hdr[8]);
   for(int k : c.kinds)
     if(k < 0 || k > 3 || (k >= 2 && c.mid <= 0))
       rd.ok = false;
-  if(!rd.ok) {
-    fclose(f);
-    throw std::runtime_error("bad block kinds in model " + path);
-  }
+  if(!rd.ok)
+    throw std::runtime_error("bad block kinds in model " + name);
   const int C = c.C;
   rd.r(m.convInit, (size_t)C * c.cin * 9);
   rd.r(m.globInit, (size_t)C * c.gin);
@@ -245,11 +259,25 @@ ModelHost loadModel(const std::string& path) {
   rd.r(m.pLinG, (size_t)c.p1 * 3 * c.g1); rd.r(m.pBias2, c.p1); rd.r(m.pConv2, (size_t)4 * c.p1);
   rd.r(m.vConv1, (size_t)c.v1 * C); rd.r(m.vBias1, c.v1); rd.r(m.vLin2, (size_t)c.v2 * 3 * c.v1); rd.r(m.vB2, c.v2);
   rd.r(m.vLin3, (size_t)2 * c.v2); rd.r(m.vB3, 2); rd.r(m.vLinM, (size_t)2 * c.v2); rd.r(m.vBM, 2);
-  const bool trailing = fgetc(f) != EOF;
-  fclose(f);
-  if(!rd.ok || trailing)
-    throw std::runtime_error("truncated or oversized model file " + path);
+  if(!rd.ok || rd.left != 0)
+    throw std::runtime_error("truncated or oversized model " + name);
   return m;
+}
+
+ModelHost loadModel(const std::string& path) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if(!f)
+    throw std::runtime_error("cannot open model " + path);
+  std::vector<unsigned char> img;
+  unsigned char buf[1 << 16];
+  size_t got;
+  while((got = fread(buf, 1, sizeof(buf), f)) > 0)
+    img.insert(img.end(), buf, buf + got);
+  const bool err = ferror(f) != 0;
+  fclose(f);
+  if(err)
+    throw std::runtime_error("cannot read model " + path);
+  return loadModelBytes(img.data(), img.size(), path);
 }
 
 static double blockMacs(int k, double A, double W, double Cg, double mid) {

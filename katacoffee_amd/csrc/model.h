@@ -58,6 +58,8 @@ ModelCfg modelCfgByName(const std::string& name);
 ModelHost randomModel(const ModelCfg& cfg, uint64_t seed);
 void saveModel(const std::string& path, const ModelHost& m);
 ModelHost loadModel(const std::string& path);
+// The same from a CFNN image in memory (e.g. weights broadcast from rank 0); name labels errors.
+ModelHost loadModelBytes(const void* data, size_t bytes, const std::string& name);
 // FLOPs per evaluation at area A (2 x MACs of every conv / matmul).
 double modelFlopsPerEval(const ModelCfg& cfg, int A);
 

@@ -37,18 +37,23 @@ namespace kc {
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int NN_WAVES = 8;  // waves per workgroup (4 per SIMD)
-constexpr int NN_NT = NN_WAVES * 64;
-
-template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG>
+template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int NW_ = 8>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
-  static constexpr int NB = NB_;  // boards per workgroup (8, or 4 for batches of at most 4 per CU)
+  // boards per workgroup: 8 on 8 waves (one workgroup per CU, 2 waves per SIMD), or 2 on
+  // 4 waves for batches of at most 4 per CU (two workgroups per CU, one wave per SIMD
+  // each: one workgroup's epilogues, pooling and barrier waits overlap the other's MFMAs)
+  static constexpr int NB = NB_;
+  static constexpr int NW = NW_, NT = NW_ * 64;  // waves / threads per workgroup
+  // weight ring slots: 3 (tap k+2 requested at the start of tap k) for 8 waves; 2 (tap
+  // k+1) for 4 waves, whose LDS must fit twice per CU -- the partner workgroup covers
+  // the shorter prefetch
+  static constexpr int RING = NW_ == 8 ? 3 : 2;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
   // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): output
   // rows [ROWS, 64*MAXT) are padding (computed from arbitrary data, never stored).
-  static constexpr int RGROUPS = NN_WAVES / 2;  // row groups (x 2 column halves)
+  static constexpr int RGROUPS = NW / 2;  // row groups (x 2 column halves)
   static constexpr int MAXT = (RT + RGROUPS - 1) / RGROUPS;
   static constexpr int MROWS = RGROUPS * MAXT * 16;  // computed output rows
   // Activations in LDS are stored per board with a one-cell zero border
@@ -66,8 +71,11 @@ struct NNGeo {
   static constexpr int ACT_BYTES = (PROWS * ROWB + 15) / 16 * 16;
   // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
-  // (at least the gpool linear weights' [96][64] f32, staged below it, for 4 boards)
-  static constexpr int OFF_SCR = MROWS * SCR * 4 > 96 * 64 * 4 ? MROWS * SCR * 4 : 96 * 64 * 4;
+  // (at least the gpool linear weights' [96][64] f32, staged below it when LIN_LDS; the
+  // 2-board instance's act is too small for them: its gpool linear reads them from L2)
+  static constexpr bool LIN_LDS = NW == 8;
+  static constexpr int OFF_SCR =
+      MROWS * SCR * 4 > 96 * 64 * 4 || !LIN_LDS ? MROWS * SCR * 4 : 96 * 64 * 4;
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
@@ -79,12 +87,13 @@ struct NNGeo {
   static constexpr int NPRM = 448;
   static constexpr int OFF_PRM = (OFF_TAB + NTAB * 2 + 15) / 16 * 16;
   static constexpr int OFF_W = OFF_PRM + 2 * NPRM * 4;
-  static constexpr int LDS = OFF_W + 3 * WBUF * 16;
+  static constexpr int LDS = OFF_W + RING * WBUF * 16;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
   static_assert(OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
-  static_assert(96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
+  static_assert(!LIN_LDS || 96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
+  static_assert(RING * WBUF * 16 >= (32 + 64) * 96 * 4, "head linear weights must fit in the ring");
   static_assert(2 * PA * ROWB + 2 * 64 < 65536, "A-read offsets must fit the ds_read immediate");
-  static_assert(LDS <= 163840, "LDS budget");
+  static_assert(LDS <= (NW == 8 ? 163840 : 163840 / 2), "LDS budget (two 4-wave workgroups per CU)");
 };
 
 #ifdef KC_NN_PROFILE
@@ -144,9 +153,10 @@ KC_D void glds16(const void* src, uint32_t lds) {
                : "memory");
 }
 
-// A tap's weights (CH pieces of 64 fragments) into its ring slot; piece c by wave c % 8.
+// A tap's weights (CH pieces of 64 fragments) into its ring slot; piece c by wave c % nw.
+template <int NW>
 KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, int wave, int lane) {
-  for(int c = wave; c < ch; c += NN_WAVES)
+  for(int c = wave; c < ch; c += NW)
     glds16(src + c * 64 + lane, slotAddr + c * 1024);
 }
 
@@ -162,21 +172,25 @@ KC_D void barrierKeepDma() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 // acc[t][ct] += W(ct, K) * act(K, t), so each lane's accumulator holds 4
 // consecutive output channels of one position (16-byte-friendly epilogues).
 //
-// Weights stream through a 3-slot LDS ring shared by the workgroup's 8 waves by
-// LDS-DMA: tap k lives in slot k%3, and tap k+2 is requested at the start of tap
-// k, two taps ahead of its use.  The stream runs across convolutions: taps 7 and
-// 8 request the NEXT convolution's taps 0 and 1 (wNext, chNext pieces per tap,
-// nextTaps), so only the first convolution pays an L2 round trip up front.  One
+// Weights stream through an LDS ring shared by the workgroup's waves by LDS-DMA.
+// 3 slots (8 waves): tap k lives in slot k%3, and tap k+2 is requested at the start of
+// tap k, two taps ahead of its use; taps 7 and 8 request the NEXT convolution's taps 0
+// and 1 (wNext, chNext pieces per tap, nextTaps).  2 slots (4 waves): tap k lives in
+// slot (PAR+k)%2 -- PAR, the parity of the convolution's first tap in the kernel's tap
+// sequence, is fixed per call site (stem 0, every block's conv1 1, conv2 0, head 1) --
+// and tap k+1 is requested at the start of tap k; tap 8 requests the next convolution's
+// tap 0.  Either way only the first convolution pays an L2 round trip up front.  One
 // barrier per tap, before its last K-step: it publishes tap k+1 (each wave first
-// retires its own pieces of it) and frees slot k%3 for the request of tap k+3.
+// retires its own pieces of it) and frees the slot of tap k for a later request.
 // Within a wave the A/B fragments of the next K-step are read from LDS while the
 // current step's MFMAs issue.  Fully unrolled: slot and fragment-buffer indices
 // are compile-time constants and every LDS read a per-lane base plus an immediate.
-// The caller keeps ring slots 0/1 untouched between convolutions and separates
-// them with __syncthreads() (which also retires the requests for taps 0/1).
+// The caller keeps the ring slots of the next convolution's first taps untouched
+// between convolutions and separates them with __syncthreads() (which also retires
+// the requests for those taps).
 // DBG (tools/conv_bench.hip ablations only): bit 0 skips the weight requests, bit 1
 // the per-tap barriers, bit 3 the vmcnt waits, bit 8 the entry wait + barrier.
-template <class G, int NTAPS, int NCB, bool FIRST, int DBG = 0>
+template <class G, int NTAPS, int NCB, int PAR, int DBG = 0>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                     f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid,
                     const h16x8* __restrict__ wNext, int chNext, int nextTaps) {
@@ -185,11 +199,7 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   constexpr int STEPS = NTAPS * NCB;
   const int wave = tid >> 6;
   const uint32_t ring = ldsAddr(wl);
-  if(FIRST) {
-#pragma unroll
-    for(int tap = 0; tap < (NTAPS < 2 ? NTAPS : 2); tap++)
-      stageTapDma(w + (size_t)tap * UNITS, ring + tap * G::WBUF * 16, CH, wave, lane);
-  }
+  auto slotOf = [](int tap) { return G::RING == 3 ? tap % 3 : (PAR + tap) & 1; };
   if(!(DBG & 256)) {
     waitVm<0>();
     __syncthreads();
@@ -201,7 +211,7 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
     const int tap = st / NCB, cb = st - tap * NCB;
     const int tb = NTAPS == 9 ? tap : 4;  // 1x1: the centre tap
     const int aoff = ((tb / 3) * G::PX + tb % 3) * G::ROWB + cb * 64;
-    const h16x8* wb = wlane + (tap % 3) * G::WBUF + cb * G::NCT_ALL * 64;
+    const h16x8* wb = wlane + slotOf(tap) * G::WBUF + cb * G::NCT_ALL * 64;
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++)
       bf[buf][ct] = wb[ct * 64];
@@ -212,25 +222,35 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   loadStep(0, 0);
 #pragma unroll
   for(int tap = 0; tap < NTAPS; tap++) {
-    // request stream tap tap+2 (this conv's, or the next conv's tap 0 / 1)
     if(DBG & 1) {
-    } else if(tap + 2 < NTAPS)
-      stageTapDma(w + (size_t)(tap + 2) * UNITS, ring + ((tap + 2) % 3) * G::WBUF * 16, CH, wave, lane);
-    else if(NTAPS == 9 && tap == 7)
-      stageTapDma(wNext, ring, chNext, wave, lane);
-    else if(NTAPS == 9 && tap == 8 && nextTaps > 1)
-      stageTapDma(wNext + chNext * 64, ring + G::WBUF * 16, chNext, wave, lane);
+    } else if(G::RING == 3) {
+      // request stream tap tap+2 (this conv's, or the next conv's tap 0 / 1)
+      if(tap + 2 < NTAPS)
+        stageTapDma<G::NW>(w + (size_t)(tap + 2) * UNITS, ring + slotOf(tap + 2) * G::WBUF * 16, CH, wave, lane);
+      else if(NTAPS == 9 && tap == 7)
+        stageTapDma<G::NW>(wNext, ring, chNext, wave, lane);
+      else if(NTAPS == 9 && tap == 8 && nextTaps > 1)
+        stageTapDma<G::NW>(wNext + chNext * 64, ring + G::WBUF * 16, chNext, wave, lane);
+    } else {
+      // request stream tap tap+1 (this conv's, or the next conv's tap 0)
+      if(tap + 1 < NTAPS)
+        stageTapDma<G::NW>(w + (size_t)(tap + 1) * UNITS, ring + slotOf(tap + 1) * G::WBUF * 16, CH, wave, lane);
+      else if(nextTaps > 0)
+        stageTapDma<G::NW>(wNext, ring + slotOf(NTAPS) * G::WBUF * 16, chNext, wave, lane);
+    }
 #pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
       const int st = tap * NCB + cb;
       if(cb == NCB - 1 && tap + 1 < NTAPS) {
-        // retire this wave's pieces of tap+1 (only the tap+2 request, >= N pieces
-        // per wave, may stay in flight), then publish them / free slot tap%3
+        // retire this wave's pieces of tap+1 (with 3 slots only the tap+2 request, >= N
+        // pieces per wave, may stay in flight), then publish them / free slot of tap
         if(DBG & 8) {
-        } else if(tap + 2 < NTAPS)
-          waitVm<CH / NN_WAVES>();
+        } else if(G::RING == 2)
+          waitVm<0>();
+        else if(tap + 2 < NTAPS)
+          waitVm<CH / G::NW>();
         else
-          waitVm<(2 * G::NCT_ALL) / NN_WAVES>();  // next conv's tap 0: at least 12 pieces
+          waitVm<(2 * G::NCT_ALL) / G::NW>();  // next conv's tap 0: at least 12 pieces
         if(!(DBG & 2))
           barrierKeepDma();
       }
@@ -254,9 +274,10 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 // Copies a [96][rows] f32 matrix (a [rows][96] linear layer the host stored
 // transposed; global, 16-B aligned) into LDS: consecutive output rows of one wave
 // read consecutive banks in the dot-product loops.  16-byte stores, no conflicts.
+template <int NT>
 KC_D void stage96(float* __restrict__ dst, const float* __restrict__ src, int rows, int tid) {
   const int n4 = rows * 24;
-  for(int q = tid; q < n4; q += NN_NT)
+  for(int q = tid; q < n4; q += NT)
     reinterpret_cast<float4*>(dst)[q] = reinterpret_cast<const float4*>(src)[q];
 }
 
@@ -267,10 +288,25 @@ KC_D void stage96(float* __restrict__ dst, const float* __restrict__ src, int ro
 // without the 24 VGPRs a register copy would cost.
 template <class G>
 KC_D f32x4* trunkBase(float* trunk, int wave, int lane) {
-  return reinterpret_cast<f32x4*>(trunk) + ((size_t)blockIdx.x * NN_WAVES + wave) * (G::MAXT * G::NCT * 64) + lane;
+  return reinterpret_cast<f32x4*>(trunk) + ((size_t)blockIdx.x * G::NW + wave) * (G::MAXT * G::NCT * 64) + lane;
+}
+// With at most 2 x 3 accumulator tiles per wave (the 4-board instance: 184 VGPRs) the
+// parked trunk fits in 24 more registers (< 256, no spill): kept in `reg`, no scratch.
+template <class G>
+constexpr bool regTrunk() {
+  return G::MAXT * G::NCT <= 6;
 }
 template <class G>
-KC_D void storeTrunk(float* trunk, const f32x4 (&a)[G::MAXT][G::NCT], int wave, int lane) {
+KC_D void storeTrunk(float* trunk, f32x4 (&reg)[G::MAXT][G::NCT], const f32x4 (&a)[G::MAXT][G::NCT], int wave,
+                     int lane) {
+  if(regTrunk<G>()) {
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++)
+        reg[t][ct] = a[t][ct];
+    return;
+  }
   f32x4* p = trunkBase<G>(trunk, wave, lane);
 #pragma unroll
   for(int t = 0; t < G::MAXT; t++)
@@ -279,7 +315,16 @@ KC_D void storeTrunk(float* trunk, const f32x4 (&a)[G::MAXT][G::NCT], int wave, 
       p[(t * G::NCT + ct) * 64] = a[t][ct];
 }
 template <class G>
-KC_D void loadTrunk(f32x4 (&a)[G::MAXT][G::NCT], float* trunk, int wave, int lane) {
+KC_D void loadTrunk(f32x4 (&a)[G::MAXT][G::NCT], const f32x4 (&reg)[G::MAXT][G::NCT], float* trunk, int wave,
+                    int lane) {
+  if(regTrunk<G>()) {
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++)
+        a[t][ct] = reg[t][ct];
+    return;
+  }
   const f32x4* p = trunkBase<G>(trunk, wave, lane);
 #pragma unroll
   for(int t = 0; t < G::MAXT; t++)
@@ -341,7 +386,7 @@ template <class G>
 KC_D void zeroBorders(uint16_t* act, int tid) {
   constexpr int CH = G::ASTR / 8;  // 16-B chunks per row
   constexpr int NBORD = G::PA - G::A;
-  for(int idx = tid; idx < G::NB * NBORD * CH; idx += NN_NT) {
+  for(int idx = tid; idx < G::NB * NBORD * CH; idx += G::NT) {
     const int q = idx / CH, c = idx - q * CH;
     const int b = q / NBORD, k = q - b * NBORD;
     // k-th border cell: top row, bottom row, then left/right columns
@@ -364,7 +409,7 @@ KC_D void zeroBorders(uint16_t* act, int tid) {
 // A lane pair per (board, channel), each summing half of the board's cells.
 template <class G>
 KC_D void poolBoards(const float* scr, const float* vsrc, float* poolP, float* poolV, float sqOff, int tid) {
-  for(int idx = tid; idx < G::NB * 64; idx += NN_NT) {
+  for(int idx = tid; idx < G::NB * 64; idx += G::NT) {
     const int pr = idx >> 1, half = idx & 1;
     const int b = pr >> 5, c = pr & 31;
     const int p0 = half ? (G::A + 1) / 2 : 0, p1 = half ? G::A : (G::A + 1) / 2;
@@ -404,7 +449,7 @@ template <class G>
 KC_D void linear96(const float* wT, int O, const float* in, float* out, int ostr, const float* bias, bool relu,
                    int tid) {
   const int quads = O >> 2;
-  for(int idx = tid; idx < G::NB * quads * 4; idx += NN_NT) {
+  for(int idx = tid; idx < G::NB * quads * 4; idx += G::NT) {
     const int ks = idx & 3, q = (idx >> 2) % quads, b = (idx >> 2) / quads;
     float4 s = float4{0.0f, 0.0f, 0.0f, 0.0f};
     const float* xi = in + b * 96 + ks * 24;
@@ -461,13 +506,13 @@ KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ W
   return src >= 0 ? WF[src] : 0.0f;
 }
 
-template <int X, int Y, int C, int NB>
-__global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
+template <int X, int Y, int C, int NB, int NW>
+__global__ void __launch_bounds__(NW * 64, 2)
     kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
                const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
                const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
                float* __restrict__ out, float* __restrict__ trunk) {
-  using G = NNGeo<X, Y, C, NB>;
+  using G = NNGeo<X, Y, C, NB, NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
   const int count = countDev ? min(*countDev, n) : n;
@@ -491,35 +536,40 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   h16x8* wl = reinterpret_cast<h16x8*>(smem + G::OFF_W);
   const float sqOff = sqrtf((float)G::A) - 14.0f;
 
-  // the stem's first two weight taps stream into the ring while the input is unpacked
+  // the stem's first weight taps (as many as the ring prefetches) stream into the ring
+  // while the input is unpacked
   {
     constexpr int CH0 = G::NCT_ALL;  // 1-KiB pieces per stem tap (one 32-channel block)
     const uint32_t ring = ldsAddr(wl);
 #pragma unroll
-    for(int tap = 0; tap < 2; tap++)
-      stageTapDma(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WBUF * 16, CH0, wave, lane);
+    for(int tap = 0; tap < G::RING - 1; tap++)
+      stageTapDma<G::NW>(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WBUF * 16, CH0, wave, lane);
   }
   // ---- row tables; unpack the packed V1 planes into the zero-bordered act ----
-  float pre = loadParam(L, WF, 0, tid);  // block 0's slab, stored after the stem conv
-  for(int i = tid; i < G::NTAB; i += NN_NT)
+  constexpr int NPK = (G::NPRM + G::NT - 1) / G::NT;  // parameter-slab elements per thread
+  float pre[NPK];
+#pragma unroll
+  for(int j = 0; j < NPK; j++)
+    pre[j] = loadParam(L, WF, 0, tid + j * G::NT);  // block 0's slab, stored after the stem conv
+  for(int i = tid; i < G::NTAB; i += G::NT)
     rowPa[i] = tabs[i];
-  for(int idx = tid; idx < G::ACT_BYTES / 16; idx += NN_NT)
+  for(int idx = tid; idx < G::ACT_BYTES / 16; idx += G::NT)
     reinterpret_cast<uint4*>(smem)[idx] = uint4{0u, 0u, 0u, 0u};
   __syncthreads();
   {
     // wave w unpacks board w: its row index and all its packed words are loaded up
     // front (two round trips), then lane l sets bits l, l+64, ... (plane-major bits)
-    static_assert(G::NB <= NN_WAVES, "one wave per board");
-    constexpr int NBITS = G::A * NUM_SPATIAL, NW = (NBITS + 63) / 64;
+    static_assert(G::NB <= G::NW, "one wave per board");
+    constexpr int NBITS = G::A * NUM_SPATIAL, NWD = (NBITS + 63) / 64;
     const int b = __builtin_amdgcn_readfirstlane(wave);
     if(b < nb) {
       const int src = rowIdx ? rowIdx[base + b] : base + b;
-      uint64_t words[NW];
+      uint64_t words[NWD];
 #pragma unroll
-      for(int k = 0; k < NW; k++)
+      for(int k = 0; k < NWD; k++)
         words[k] = in[(size_t)src * inWords + k];
 #pragma unroll
-      for(int k = 0; k < NW; k++) {
+      for(int k = 0; k < NWD; k++) {
         const int i = k * 64 + lane;
         if(i < NBITS && ((words[k] >> lane) & 1ULL)) {
           const int c = i / G::A, p = i - c * G::A;
@@ -534,8 +584,9 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   int ab[G::MAXT];
   aBases<G>(ab, rowPa, tstart, lane);
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
+  f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
+  convTiles<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                            L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL, L->nblocks > 0 ? 9 : 1);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
@@ -552,9 +603,11 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     }
   }
   if(L->nblocks > 0)
-    storeTrunk<G>(trunk, acc, wave, lane);
-  if(tid < G::NPRM)
-    prm[tid] = pre;
+    storeTrunk<G>(trunk, park, acc, wave, lane);
+#pragma unroll
+  for(int j = 0; j < NPK; j++)
+    if(tid + j * G::NT < G::NPRM)
+      prm[tid + j * G::NT] = pre[j];
   const int Cr = G::C - L->Cg;
   NN_PHASE(2);
   for(int blk = 0; blk < L->nblocks; blk++) {
@@ -566,12 +619,16 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     storeBnRelu<G>(act, rowPa, acc, P, P + 96, tstart, cg, lane);
     __syncthreads();
     zeroAcc<G>(acc);
-    pre = loadParam(L, WF, blk + 1, tid);  // next slab: its latency hides behind conv1
+#pragma unroll
+    for(int j = 0; j < NPK; j++)
+      pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
-    convTiles<G, 9, G::C / 32, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
-                                      (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL, 9);
-    if(tid < G::NPRM)
-      prm[((blk + 1) & 1) * G::NPRM + tid] = pre;
+    convTiles<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
+                                  (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL, 9);
+#pragma unroll
+    for(int j = 0; j < NPK; j++)
+      if(tid + j * G::NT < G::NPRM)
+        prm[((blk + 1) & 1) * G::NPRM + tid + j * G::NT] = pre[j];
     __syncthreads();
     NN_PHASE(5 + 4 * blk);
     const bool lastBlk = blk + 1 == L->nblocks;
@@ -580,7 +637,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
     if(L->kinds[blk] == 0) {
       // the parked trunk is requested before the epilogue, whose LDS work hides its latency
       f32x4 tr[G::MAXT][G::NCT];
-      loadTrunk<G>(tr, trunk, wave, lane);
+      loadTrunk<G>(tr, park, trunk, wave, lane);
       storeBnRelu<G>(act, rowPa, acc, P + 192, P + 288, tstart, cg, lane);
 #pragma unroll
       for(int t = 0; t < G::MAXT; t++)
@@ -589,10 +646,10 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
           acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, G::C / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                        3 * G::NCT_ALL, nextTaps);
+      convTiles<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                    3 * G::NCT_ALL, nextTaps);
       if(!lastBlk)
-        storeTrunk<G>(trunk, acc, wave, lane);
+        storeTrunk<G>(trunk, park, acc, wave, lane);
     } else {
       // g branch: BN-ReLU into scr (f32, aliases the dead conv input), then
       // KataGPool per board (model_pytorch.py:326-352)
@@ -600,13 +657,13 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       const float* gbias = P + 416;
       // the gpool linear weights ([96][Cr] f32) are requested now and land in LDS
       // after the epilogue's barrier
-      constexpr int LW = (96 * 64 / 4 + NN_NT - 1) / NN_NT;  // float4 per thread (Cr <= 64)
+      constexpr int LW = G::LIN_LDS ? (96 * 64 / 4 + G::NT - 1) / G::NT : 1;  // float4 per thread (Cr <= 64)
       float4 lw[LW];
-      {
+      if(G::LIN_LDS) {
         const float4* src = reinterpret_cast<const float4*>(WF + L->linG[blk]);
 #pragma unroll
         for(int k = 0; k < LW; k++) {
-          const int q = tid + k * NN_NT;
+          const int q = tid + k * G::NT;
           lw[k] = q < Cr * 24 ? src[q] : float4{0.0f, 0.0f, 0.0f, 0.0f};
         }
       }
@@ -631,19 +688,24 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
       __syncthreads();
       NN_PHASE(50);
       float* lgT = actF;  // transposed linear weights in the idle front of act
+      if(G::LIN_LDS) {
 #pragma unroll
-      for(int k = 0; k < LW; k++) {
-        const int q = tid + k * NN_NT;
-        if(q < Cr * 24)
-          reinterpret_cast<float4*>(lgT)[q] = lw[k];
+        for(int k = 0; k < LW; k++) {
+          const int q = tid + k * G::NT;
+          if(q < Cr * 24)
+            reinterpret_cast<float4*>(lgT)[q] = lw[k];
+        }
       }
       poolBoards<G>(scr, nullptr, poolP, poolV, sqOff, tid);
       __syncthreads();
       NN_PHASE(51);
-      linear96<G>(lgT, Cr, poolP, biasS, Cr, nullptr, false, tid);
+      if(G::LIN_LDS)
+        linear96<G>(lgT, Cr, poolP, biasS, Cr, nullptr, false, tid);
+      else
+        linear96<G>(WF + L->linG[blk], Cr, poolP, biasS, Cr, nullptr, false, tid);
       __syncthreads();
       f32x4 tr[G::MAXT][G::NCT];  // the parked trunk, in flight during the epilogue
-      loadTrunk<G>(tr, trunk, wave, lane);
+      loadTrunk<G>(tr, park, trunk, wave, lane);
       zeroBorders<G>(act, tid);  // the f32 scratch overwrote border cells (disjoint from r-epi cells)
       NN_PHASE(52);
       {
@@ -678,10 +740,10 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
           acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, (G::C - 32) / 32, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                               3 * G::NCT_ALL, nextTaps);
+      convTiles<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                           3 * G::NCT_ALL, nextTaps);
       if(!lastBlk)
-        storeTrunk<G>(trunk, acc, wave, lane);
+        storeTrunk<G>(trunk, park, acc, wave, lane);
     }
   }
   // ---- trunk tip ----
@@ -692,7 +754,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0);
+  convTiles<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0);
   __syncthreads();  // act dead from here: f32 [MROWS][SCR] value branch at actF, g branch at scr
   NN_PHASE(41);
   {
@@ -722,12 +784,14 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   NN_PHASE(53);
   float* plgT = reinterpret_cast<float*>(wl);
   float* l2T = plgT + 32 * 96;
-  float* w3 = l2T + 96 * L->v2;  // value / misc output weights [4][v2], then their 4 biases
-  stage96(plgT, WF + L->pLinG, 32, tid);
-  stage96(l2T, WF + L->vLin2, L->v2, tid);
+  // value / misc output weights [4][v2], then their 4 biases: in the idle parameter slab
+  float* w3 = prm + ((L->nblocks + 1) & 1) * G::NPRM;
+  static_assert(4 * 64 + 4 <= G::NPRM, "value weights fit a parameter slab");
+  stage96<G::NT>(plgT, WF + L->pLinG, 32, tid);
+  stage96<G::NT>(l2T, WF + L->vLin2, L->v2, tid);
   {
     const int v2 = L->v2;
-    for(int i = tid; i < 4 * v2 + 4; i += NN_NT) {
+    for(int i = tid; i < 4 * v2 + 4; i += G::NT) {
       float w;
       if(i < 2 * v2)
         w = WF[L->vLin3 + i];
@@ -747,7 +811,7 @@ __global__ void __launch_bounds__(NN_NT, NN_WAVES / 4)
   {
     // value (2) and misc (2) outputs: a 16-lane group per (board, output), each lane
     // summing every 16th term, reduced across the group
-    static_assert(G::NB * 4 * 16 <= NN_NT, "one 16-lane group per (board, output)");
+    static_assert(G::NB * 4 * 16 <= G::NT, "one 16-lane group per (board, output)");
     const int k = tid & 15, o = (tid >> 4) & 3, b = tid >> 6;
     const int v2 = L->v2;
     const int bv = b < G::NB ? b : 0;  // waves past the boards compute a discarded copy
@@ -978,16 +1042,27 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipMemcpy(wF32_, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&layoutDev_, sizeof(NNLayout)));
   KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
-  using G8 = NNGeo<5, 5, 96, 8>;
-  using G4 = NNGeo<5, 5, 96, 4>;
-  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>();
+  using G8 = NNGeo<5, 5, 96, 8, 8>;
+  using G4 = NNGeo<5, 5, 96, 4, 8>;
+  using G2 = NNGeo<5, 5, 96, 2, 4>;
+  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>(), tab2 = rowTables<G2>();
   KC_HIP(hipMalloc(&tabDev_, tab8.size() * 2));
   KC_HIP(hipMemcpy(tabDev_, tab8.data(), tab8.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&tabDev4_, tab4.size() * 2));
   KC_HIP(hipMemcpy(tabDev4_, tab4.data(), tab4.size() * 2, hipMemcpyHostToDevice));
+  KC_HIP(hipMalloc(&tabDev2_, tab2.size() * 2));
+  KC_HIP(hipMemcpy(tabDev2_, tab2.data(), tab2.size() * 2, hipMemcpyHostToDevice));
   // function attributes are per device: every engine sets it on its own device
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, G8::LDS));
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, G4::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             G8::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             G4::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             G2::LDS));
+  // small-batch instance (tools / A-B runs only): KATACOFFEE_NN_SMALL=4 selects 4 boards on
+  // 8 waves (one workgroup per CU) instead of 2 boards on 4 waves (two per CU)
+  const char* small = getenv("KATACOFFEE_NN_SMALL");
+  small4_ = small && atoi(small) == 4;
   int dev = 0;
   KC_HIP(hipGetDevice(&dev));
   KC_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev));
@@ -1000,6 +1075,7 @@ NNEngine::~NNEngine() {
   (void)hipFree(layoutDev_);
   (void)hipFree(tabDev_);
   (void)hipFree(tabDev4_);
+  (void)hipFree(tabDev2_);
 }
 
 void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev,
@@ -1015,20 +1091,22 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
     return;
   }
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
-  // A launch costs one workgroup's latency per wave of workgroups (one per CU): a
-  // batch bound that fits 4 boards per CU (e.g. each of two game groups' batches)
-  // runs 4 boards per workgroup, half the MFMA work on each workgroup's path.
-  if(n <= 4 * cus_)
-    launch<NNGeo<5, 5, 96, 4>>(n, inWords, tabDev4_, in, out, st, countDev, rowIdx, e0, e1);
+  // A launch costs about one workgroup's latency per wave of workgroups: a batch bound
+  // that fits 4 boards per CU (e.g. each of two game groups' batches) runs as two
+  // 2-board workgroups per CU, whose phases interleave on the CU's matrix pipes.
+  if(n <= 4 * cus_ && small4_)
+    launch<NNGeo<5, 5, 96, 4, 8>>(n, inWords, tabDev4_, in, out, st, countDev, rowIdx, e0, e1);
+  else if(n <= 4 * cus_)
+    launch<NNGeo<5, 5, 96, 2, 4>>(n, inWords, tabDev2_, in, out, st, countDev, rowIdx, e0, e1);
   else
-    launch<NNGeo<5, 5, 96, 8>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
+    launch<NNGeo<5, 5, 96, 8, 8>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
 }
 
 template <class G>
 void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* in, float* out, hipStream_t st,
                       const int* countDev, const int* rowIdx, hipEvent_t e0, hipEvent_t e1) {
   const int grid = (n + G::NB - 1) / G::NB;
-  const size_t bytes = (size_t)grid * NN_WAVES * G::MAXT * G::NCT * 64 * 16;
+  const size_t bytes = regTrunk<G>() ? 0 : (size_t)grid * G::NW * G::MAXT * G::NCT * 64 * 16;
   if(bytes > trunkBytes_) {
     // stream-ordered: a launch still using the old scratch finishes before the free
     if(trunk_)
@@ -1038,12 +1116,12 @@ void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* i
     KC_HIP(hipMalloc(&trunk_, bytes));
     trunkBytes_ = bytes;
   }
-  auto kern = kNNForward<G::X, G::Y, G::C, G::NB>;
+  auto kern = kNNForward<G::X, G::Y, G::C, G::NB, G::NW>;
   if(e0)
-    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(NN_NT), G::LDS, st, e0, e1, 0, layoutDev_, (const h16x8*)wHalf_,
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, e0, e1, 0, layoutDev_, (const h16x8*)wHalf_,
                           wF32_, tab, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
   else
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NN_NT), G::LDS, st, layoutDev_, (const h16x8*)wHalf_, wF32_, tab, n,
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, layoutDev_, (const h16x8*)wHalf_, wF32_, tab, n,
                        countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
   KC_HIP(hipGetLastError());
 }

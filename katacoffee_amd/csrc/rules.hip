@@ -106,6 +106,38 @@ __global__ void __launch_bounds__(64) kEncodeBatch(const DTables* __restrict__ T
   }
 }
 
+// Network rows back to the canonical frame (coffee_nn_forward2; the reference backend's
+// SymmetryHelpers::copyOutputsWithSymmetry in NeuralNet::getOutput, eigenbackend.cpp:
+// 1776-1796): canonical[d][cell] = symmetric[symDir[s][d]][symCell[s][cell]], in place,
+// one 64-lane workgroup per row staged through LDS; value / misc logits unchanged.
+__global__ void __launch_bounds__(64) kCanonicalRows(const DTables* __restrict__ Tp, int n, const int32_t* sym,
+                                                     float* out) {
+  const DTables& T = *Tp;
+  __shared__ float row[4 * MAX_AREA + 4];
+  const int i = blockIdx.x;
+  if(i >= n)
+    return;
+  const int P = T.P, A = T.A;
+  int s = sym[i] & 7;
+  if(T.X != T.Y)
+    s &= 3;
+  float* o = out + (size_t)i * (P + 4);
+  for(int j = laneId(); j < P; j += 64)
+    row[j] = o[j];
+  __syncthreads();
+  for(int pos = laneId(); pos < P; pos += 64) {
+    const int d = pos / A, cell = pos - d * A;
+    o[pos] = row[T.symDir[s][d] * A + T.symCell[s][cell]];
+  }
+}
+
+void launchCanonicalRows(const DTables* T, int n, const int32_t* sym, float* out, hipStream_t st) {
+  if(n <= 0)
+    return;
+  hipLaunchKernelGGL(kCanonicalRows, dim3(n), dim3(64), 0, st, T, n, sym, out);
+  KC_HIP(hipGetLastError());
+}
+
 void launchRulesBatch(const DTables* T, int n, const uint8_t* cells, const int8_t* lastCell, const int8_t* lastDir,
                       const uint8_t* pla, uint8_t* legal, uint8_t* hasLegal, hipStream_t st) {
   if(n <= 0)

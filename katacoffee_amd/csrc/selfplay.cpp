@@ -206,14 +206,17 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.nnRR = devAlloc<int32_t>(owned_, 1);
   if(c.nn_batch_cap < 0)
     throw std::invalid_argument("nn_batch_cap must be >= 0");
-  if(c.nn_batch_cap > 0) {
-    d.nnCap = c.nn_batch_cap;
-  } else {
-    int dev = 0, cus = 0;
+  if(c.engines_per_device < 0)
+    throw std::invalid_argument("engines_per_device must be >= 0");
+  userCap_ = c.nn_batch_cap;
+  enginesPerDevice_ = std::max(1, c.engines_per_device);
+  {
+    int dev = 0;
     KC_HIP(hipGetDevice(&dev));
-    KC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    d.nnCap = nn_ ? std::min(G, nn_->batchCap(std::max(1, cus))) : std::max(1, cus) * NN_BOARDS_PER_WG;
+    KC_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev));
+    cus_ = std::max(1, cus_);
   }
+  d.nnCap = nnCapFor(G);
   d.nnIdx = devAlloc<int32_t>(owned_, G);
   d.modelGen = devAlloc<int32_t>(owned_, 1);
   d.nnCount = devAlloc<int32_t>(owned_, 1);
@@ -448,13 +451,41 @@ int SelfplayEngine::drainGames(int maxGames, int32_t* header, uint8_t* moves) {
   return n;
 }
 
+// Rows per network launch: the configured cap, else the network's own (one wave of
+// fused workgroups, split between the engines sharing the device; the layered path is
+// uncapped), never more than the games.
+int SelfplayEngine::nnCapFor(int G) const {
+  if(userCap_ > 0)
+    return userCap_;
+  if(!nn_)
+    return std::min(G, cus_ * NN_BOARDS_PER_WG);
+  if(!nn_->fused())
+    return G;
+  return std::min(G, std::max(1, nn_->batchCap(cus_) / enginesPerDevice_));
+}
+
 void SelfplayEngine::setModel(const char* path) {
   if(!nn_)
     throw std::invalid_argument("engine runs the stand-in network (use_fake_net)");
-  ModelHost m = loadModel(path);  // throws on a bad file; the current network stays
+  switchModel(loadModel(path));  // throws on a bad file; the current network stays
+}
+
+void SelfplayEngine::setModelBytes(const void* data, size_t bytes) {
+  if(!nn_)
+    throw std::invalid_argument("engine runs the stand-in network (use_fake_net)");
+  switchModel(loadModelBytes(data, bytes, "<model bytes>"));
+}
+
+void SelfplayEngine::switchModel(const ModelHost& m) {
   std::unique_ptr<NNEngine> next(new NNEngine(m, xLen_, yLen_, winLen_, nnPath_));
   sync();
   nn_ = std::move(next);
+  // a reload may change the network path (fused <-> layered) and with it the default cap
+  const int cap = nnCapFor(hd_.G);
+  if(cap != hd_.nnCap) {
+    hd_.nnCap = cap;
+    KC_HIP(hipMemcpy(&dd_->nnCap, &cap, sizeof(int), hipMemcpyHostToDevice));
+  }
   // network generation: rows of games that span the switch carry it in [49] / [50]
   // (ChangedNeuralNet, play.cpp:1210-1226; trainingwrite.cpp:459-461)
   modelGen_++;

@@ -23,6 +23,8 @@ class SelfplayEngine {
   int drainGames(int maxGames, int32_t* header, uint8_t* moves);
   // Replaces the network for all subsequent rounds (all games: switchNetsMidGame).
   void setModel(const char* path);
+  // The same from a CFNN image in host memory (weights broadcast from another rank).
+  void setModelBytes(const void* data, size_t bytes);
   void gameInfo(int slot, int64_t* info);
   int gameTree(int slot, int maxNodes, uint32_t* nodes, uint32_t* edges);
   void rootPolicy(int slot, float* out);
@@ -40,6 +42,7 @@ class SelfplayEngine {
     int which;
     hipEvent_t a, b;
   };
+  void switchModel(const ModelHost& m);
   void timed(int which, hipStream_t st, const std::function<void()>& f, bool on);
   void timedKernel(int which, bool on, const std::function<void(hipEvent_t, hipEvent_t)>& f);
   bool sampleNow(int which) { return timingEvery_ > 0 && groupLaunches_[which]++ % (uint64_t)timingEvery_ == 0; }
@@ -56,6 +59,10 @@ class SelfplayEngine {
   int commitInterval_ = 8;
   int xLen_ = 0, yLen_ = 0, winLen_ = 0;
   int nnPath_ = 0;  // NNPath of the network (kept across hot reloads)
+  int userCap_ = 0;          // coffee_selfplay_config.nn_batch_cap (0 = the network's default)
+  int enginesPerDevice_ = 1; // engines sharing the device's default fused batch cap
+  int cus_ = 1;              // compute units of the device
+  int nnCapFor(int G) const;
   int32_t modelGen_ = 0;  // hot reloads so far
   uint64_t rounds_ = 0;
   bool commitReset_ = false;  // a commit ran: the next kSelect zeroes the commit count

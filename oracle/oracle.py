@@ -36,9 +36,11 @@ def lib(f64=False):
             _lib64 = _setup(ctypes.CDLL(LIB_F64_PATH))
         return _lib64
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        # ORACLE_LIB: an alternative build of the same library (tests/san sanitizer build)
+        path = os.environ.get("ORACLE_LIB", LIB_PATH)
+        if path == LIB_PATH and not os.path.exists(LIB_PATH):
             build()
-        _lib = _setup(ctypes.CDLL(LIB_PATH))
+        _lib = _setup(ctypes.CDLL(path))
     return _lib
 
 

@@ -74,3 +74,37 @@ def test_pack_roundtrip():
     for f, _ in R.FIELDS:
         np.testing.assert_array_equal(back[f], rows[f])
     assert R.row_bytes(5, 5) == 15 * 4 + 4 + 400 + 256 + 125 + 16
+
+
+def _bcast_worker(rank, world, port, path, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from katacoffee_amd import weights
+    data = weights.broadcast_model(path if rank == 0 else None, dist, "cpu")
+    q.put((rank, data))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_model_broadcast_world2(tmp_path):
+    """Hot reload across ranks: rank 0 broadcasts the new CFNN image and
+    every rank receives the file's exact bytes, which load as the same network."""
+    import katacoffee_amd as kc
+    path = str(tmp_path / "new.cfnn")
+    kc.write_random_model("b6c96", 99, path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = open(path, "rb").read()
+    assert got[0] == ref and got[1] == ref
+    back = str(tmp_path / "received.cfnn")
+    open(back, "wb").write(got[1])
+    assert kc.model_flops(back, 25) == kc.model_flops(path, 25)

@@ -135,3 +135,76 @@ def test_selfplay_runs_on_layered_network(models, arch, X, Y, W):
     sp.close()
     assert st["errors"] == 0
     assert st["moves"] > 0 and st["nn_evals"] > 0
+
+
+def _symmetry_maps(X, Y, W):
+    """symCell[s][c], symDir[s][d] derived from the oracle's (reference-pinned) V1
+    encoder, independently of the device tables: a lone own stone at c lights plane 1
+    at symCell[s][c]; a last move in direction d lights plane 3 + symDir[s][d]."""
+    A = X * Y
+    cells = np.zeros((8 * A, A), np.uint8)
+    cells[np.arange(8 * A), np.tile(np.arange(A), 8)] = 1
+    hc = np.full((8 * A, 5), -1, np.int8)
+    hd = np.full((8 * A, 5), 4, np.int8)
+    sym = np.repeat(np.arange(8), A).astype(np.int32)
+    binp, _ = oracle.encode_batch(X, Y, W, cells, hc, hd, np.ones(8 * A, np.uint8), sym)
+    sym_cell = binp[:, 1, :].argmax(axis=1).reshape(8, A)
+    cells = np.zeros((32, A), np.uint8)
+    cells[:, A // 2] = 2
+    hc = np.full((32, 5), -1, np.int8)
+    hd = np.full((32, 5), 4, np.int8)
+    hc[:, 0] = A // 2
+    hd[:, 0] = np.tile(np.arange(4), 8)
+    sym = np.repeat(np.arange(8), 4).astype(np.int32)
+    binp, _ = oracle.encode_batch(X, Y, W, cells, hc, hd, np.ones(32, np.uint8), sym)
+    sym_dir = binp[:, 3:7, :].sum(axis=2).argmax(axis=1).reshape(8, 4)
+    return sym_cell, sym_dir
+
+
+@pytest.mark.parametrize("arch,X,Y,W,precision", [("b6c96", 5, 5, 4, "accurate"), ("b6c96", 5, 5, 4, "fast"),
+                                                  ("b10c128", 7, 7, 5, "accurate")])
+def test_forward_canonical_frame_vs_oracle(models, arch, X, Y, W, precision):
+    """coffee_nn_forward2 = NeuralNet::getOutput (eigenbackend.cpp:1776-1796): rows
+    encoded under symmetry s come back with policy logits in the canonical frame.
+    Reference: the oracle's fp32 forward of the same (symmetric-frame) planes, mapped
+    back with maps taken from the oracle encoder; value/misc unchanged."""
+    A, P = X * Y, 4 * X * Y
+    n = 96
+    rng = np.random.default_rng(11)
+    sym = rng.integers(0, 8, n).astype(np.int32)
+    sym[:8] = np.arange(8)
+    # re-encode the same positions under the chosen symmetries through the oracle encoder
+    colors = np.zeros((n, A), np.uint8)
+    hc = np.full((n, 5), -1, np.int8)
+    hd = np.full((n, 5), 4, np.int8)
+    for i in range(n):
+        k = int(rng.integers(1, A // 2))
+        idx = rng.choice(A, size=k, replace=False)
+        colors[i, idx] = rng.integers(1, 3, size=k)
+        hc[i, 0] = idx[0]
+        hd[i, 0] = int(rng.integers(0, 4))
+    pla = rng.integers(1, 3, n).astype(np.uint8)
+    binp, glob = oracle.encode_batch(X, Y, W, colors, hc, hd, pla, sym)
+    glob = glob.reshape(n, 1).astype(np.float32)
+    packed = _pack_u64(binp)
+    net = kc.Network(models[arch], X, Y, W, precision=precision)
+    canon = net.forward_canonical(packed, sym)
+    raw = net.forward(packed)
+    np.testing.assert_array_equal(net.forward_canonical(packed, np.zeros(n, np.int32)), raw)
+    net.close()
+    sym_cell, sym_dir = _symmetry_maps(X, Y, W)
+    src = np.zeros((8, P), np.int64)
+    for s in range(8):
+        for d in range(4):
+            src[s, d * A:(d + 1) * A] = sym_dir[s, d] * A + sym_cell[s]
+    # the device's own symmetric-frame output, mapped back: exact
+    expect = raw.copy()
+    expect[:, :P] = np.take_along_axis(raw[:, :P], src[sym], axis=1)
+    np.testing.assert_array_equal(canon, expect)
+    # and against the oracle's fp32 forward mapped back the same way
+    ref = _ref(models[arch], X, Y, binp, glob, 0)
+    ref[:, :P] = np.take_along_axis(ref[:, :P], src[sym], axis=1)
+    err = float(np.abs(canon - ref).max())
+    print(arch, precision, "canonical-frame max |diff| vs fp32 oracle", err)
+    assert err <= (1e-3 if precision == "accurate" else 2e-3 * max(1.0, float(np.abs(ref).max())))
+    assert not np.array_equal(src[sym[1]], np.arange(P))  # a non-identity symmetry is exercised

@@ -430,3 +430,26 @@ def test_rows_record_network_switch(model_path):
             spanning += int(f50[0] == 1.0 and f50[-1] == 0.0)
     assert spanning > 0
     sp.close()
+
+
+def test_set_model_bytes_matches_file_reload(model_path):
+    """coffee_selfplay_set_model_bytes (weights broadcast from rank 0) switches the
+    network exactly like coffee_selfplay_set_model on the same file."""
+    other = model_path.replace(".cfnn", "-bytes.cfnn")
+    kc.write_random_model("b6c96", 91, other)
+    a = kc.Selfplay(5, 5, 4, num_games=16, max_visits=12, seed=8, model_path=model_path, commit_interval=1)
+    b = kc.Selfplay(5, 5, 4, num_games=16, max_visits=12, seed=8, model_path=model_path, commit_interval=1)
+    for e in (a, b):
+        e.step(120)
+    a.set_model(other)
+    b.set_model_bytes(open(other, "rb").read())
+    with pytest.raises(kc.CoffeeError):
+        b.set_model_bytes(open(other, "rb").read()[:-4])  # truncated image: rejected, network kept
+    for e in (a, b):
+        e.step(900)
+    ra, rb = _sorted_rows(a.drain_rows()), _sorted_rows(b.drain_rows())
+    assert len(ra["meta"]) > 0
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k])
+    a.close()
+    b.close()

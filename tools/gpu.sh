@@ -6,6 +6,7 @@
 #   bench[=ARGS]     python bench.py ARGS (comma-separated: bench=--config,C3,--steps,10)
 #   smoke            __graft_entry__.smoke()
 #   prof             tools/profile_r03.sh (rocprofv3 trace + PMC passes)
+#   run=CMD          any other command (comma-separated words), e.g. run=tools/_build/nn_phase,960
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -27,6 +28,8 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py ${arg//,/ } > $log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
+    run)
+      timeout -k 10 300 ${arg//,/ } > $log 2>&1 ;;
     prof)
       timeout -k 10 1100 bash tools/profile_r03.sh > $log 2>&1 ;;
     *)

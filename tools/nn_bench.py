@@ -28,7 +28,7 @@ def main():
     kc.write_random_model(a.arch, 1, path)
     net = kc.Network(path, X, Y, W, precision=a.precision)
     flops1 = kc.model_flops(path, A)
-    for n in [int(v) for v in a.n.split(",")]:
+    for n in [int(v) for v in a.n.replace("/", ",").split(",")]:
         rng = np.random.default_rng(0)
         cells = rng.integers(0, 3, size=(n, A)).astype(np.uint8)
         hc = np.full((n, 5), -1, np.int8)

@@ -1,5 +1,6 @@
 // Phase timing of the fused network kernel (shader-clock stamps from the first
-// workgroups).  Build: make -C tools nn_phase ; run on the GPU box.
+// workgroups).  Build: make -C tools nn_phase ; run on the GPU box:
+// tools/_build/nn_phase [boards]
 #define KC_NN_PROFILE
 #include "../katacoffee_amd/csrc/nn.hip"
 
@@ -8,8 +9,8 @@
 
 using namespace kc;
 
-int main() {
-  const int n = 4096;
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 4096;  // <= 4 x CUs: the 4-board instance
   ModelHost m = randomModel(modelCfgByName("b6c96"), 1);
   NNEngine eng(m, 5, 5, 4);
   const int words = (15 * 25 + 63) / 64;
