@@ -128,8 +128,7 @@ class NNEngine {
   NNLayout* layoutDev_ = nullptr;
   uint16_t* tabDev_ = nullptr;   // device row tables (nn.hip rowTables), 8 boards per workgroup
   uint16_t* tabDev4_ = nullptr;  // the same for 4 boards per workgroup
-  uint16_t* tabDev2_ = nullptr;  // the same for 2 boards per (4-wave) workgroup
-  bool small4_ = false;          // small batches on the 4-board instance (A/B runs)
+  int small_ = 0;                // KATACOFFEE_NN_SMALL=8: small batches on the 8-board instance (A/B runs)
   float* trunk_ = nullptr;       // f32 residual trunk scratch, [workgroup][fragment] (nn.hip)
   size_t trunkBytes_ = 0;        // its size
   int cus_ = 1;                  // compute units of the engine's device

@@ -40,15 +40,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int NW_ = 8>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
-  // boards per workgroup: 8 on 8 waves (one workgroup per CU, 2 waves per SIMD), or 2 on
-  // 4 waves for batches of at most 4 per CU (two workgroups per CU, one wave per SIMD
-  // each: one workgroup's epilogues, pooling and barrier waits overlap the other's MFMAs)
+  // boards per workgroup: 8, or 4 for batches of at most 4 per CU; one 8-wave
+  // workgroup per CU, 2 waves per SIMD (tools/conv_bench.hip measured the alternatives:
+  // 2 boards on 4 waves at two workgroups per CU streams every weight twice per CU, and
+  // 4 boards on 4 waves with one wave per SIMD cuts the LDS reads per MFMA by 30 % but
+  // exposes every LDS and barrier latency: both slower)
   static constexpr int NB = NB_;
   static constexpr int NW = NW_, NT = NW_ * 64;  // waves / threads per workgroup
-  // weight ring slots: 3 (tap k+2 requested at the start of tap k) for 8 waves; 2 (tap
-  // k+1) for 4 waves, whose LDS must fit twice per CU -- the partner workgroup covers
-  // the shorter prefetch
-  static constexpr int RING = NW_ == 8 ? 3 : 2;
+  static_assert(NW_ == 8, "8-wave workgroups");
+  // weight ring slots: tap k+2 is requested at the start of tap k
+  static constexpr int RING = 3;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
   // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): output
@@ -71,11 +72,8 @@ struct NNGeo {
   static constexpr int ACT_BYTES = (PROWS * ROWB + 15) / 16 * 16;
   // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
-  // (at least the gpool linear weights' [96][64] f32, staged below it when LIN_LDS; the
-  // 2-board instance's act is too small for them: its gpool linear reads them from L2)
-  static constexpr bool LIN_LDS = NW == 8;
-  static constexpr int OFF_SCR =
-      MROWS * SCR * 4 > 96 * 64 * 4 || !LIN_LDS ? MROWS * SCR * 4 : 96 * 64 * 4;
+  // (at least the gpool linear weights' [96][64] f32, staged below it, for 4 boards)
+  static constexpr int OFF_SCR = MROWS * SCR * 4 > 96 * 64 * 4 ? MROWS * SCR * 4 : 96 * 64 * 4;
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
@@ -90,10 +88,10 @@ struct NNGeo {
   static constexpr int LDS = OFF_W + RING * WBUF * 16;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
   static_assert(OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
-  static_assert(!LIN_LDS || 96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
+  static_assert(96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
   static_assert(RING * WBUF * 16 >= (32 + 64) * 96 * 4, "head linear weights must fit in the ring");
   static_assert(2 * PA * ROWB + 2 * 64 < 65536, "A-read offsets must fit the ds_read immediate");
-  static_assert(LDS <= (NW == 8 ? 163840 : 163840 / 2), "LDS budget (two 4-wave workgroups per CU)");
+  static_assert(LDS <= 163840, "LDS budget");
 };
 
 #ifdef KC_NN_PROFILE
@@ -160,6 +158,16 @@ KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, 
     glds16(src + c * 64 + lane, slotAddr + c * 1024);
 }
 
+// Pieces [q0, q1) of this wave's share of a tap (piece c = wave + q * NW).
+template <int NW>
+KC_D void stageTapPieces(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, int wave, int lane, int q0, int q1) {
+  for(int q = q0; q < q1; q++) {
+    const int c = wave + q * NW;
+    if(c < ch)
+      glds16(src + c * 64 + lane, slotAddr + c * 1024);
+  }
+}
+
 template <int N>
 KC_D void waitVm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -172,16 +180,13 @@ KC_D void barrierKeepDma() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 // acc[t][ct] += W(ct, K) * act(K, t), so each lane's accumulator holds 4
 // consecutive output channels of one position (16-byte-friendly epilogues).
 //
-// Weights stream through an LDS ring shared by the workgroup's waves by LDS-DMA.
-// 3 slots (8 waves): tap k lives in slot k%3, and tap k+2 is requested at the start of
-// tap k, two taps ahead of its use; taps 7 and 8 request the NEXT convolution's taps 0
-// and 1 (wNext, chNext pieces per tap, nextTaps).  2 slots (4 waves): tap k lives in
-// slot (PAR+k)%2 -- PAR, the parity of the convolution's first tap in the kernel's tap
-// sequence, is fixed per call site (stem 0, every block's conv1 1, conv2 0, head 1) --
-// and tap k+1 is requested at the start of tap k; tap 8 requests the next convolution's
-// tap 0.  Either way only the first convolution pays an L2 round trip up front.  One
+// Weights stream through a 3-slot LDS ring shared by the workgroup's 8 waves by
+// LDS-DMA: tap k lives in slot k%3, and tap k+2 is requested at the start of tap k,
+// two taps ahead of its use.  The stream runs across convolutions: taps 7 and 8
+// request the NEXT convolution's taps 0 and 1 (wNext, chNext pieces per tap,
+// nextTaps), so only the first convolution pays an L2 round trip up front.  One
 // barrier per tap, before its last K-step: it publishes tap k+1 (each wave first
-// retires its own pieces of it) and frees the slot of tap k for a later request.
+// retires its own pieces of it) and frees slot k%3 for the request of tap k+3.
 // Within a wave the A/B fragments of the next K-step are read from LDS while the
 // current step's MFMAs issue.  Fully unrolled: slot and fragment-buffer indices
 // are compile-time constants and every LDS read a per-lane base plus an immediate.
@@ -190,16 +195,21 @@ KC_D void barrierKeepDma() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 // the requests for those taps).
 // DBG (tools/conv_bench.hip ablations only): bit 0 skips the weight requests, bit 1
 // the per-tap barriers, bit 3 the vmcnt waits, bit 8 the entry wait + barrier.
-template <class G, int NTAPS, int NCB, int PAR, int DBG = 0>
+template <class G, int NTAPS, int NCB, int DBG = 0>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                     f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid,
                     const h16x8* __restrict__ wNext, int chNext, int nextTaps) {
   constexpr int CH = NCB * G::NCT_ALL;  // 1-KiB pieces per tap
   constexpr int UNITS = CH * 64;        // 16-B fragments per tap
   constexpr int STEPS = NTAPS * NCB;
+#ifdef KC_NN_NOSPREAD
+  constexpr bool SPREAD = false;  // A/B builds only (Makefile `alt`)
+#else
+  constexpr bool SPREAD = G::MAXT * G::NCT <= 6;
+#endif
   const int wave = tid >> 6;
   const uint32_t ring = ldsAddr(wl);
-  auto slotOf = [](int tap) { return G::RING == 3 ? tap % 3 : (PAR + tap) & 1; };
+  auto slotOf = [](int tap) { return tap % 3; };
   if(!(DBG & 256)) {
     waitVm<0>();
     __syncthreads();
@@ -222,38 +232,60 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   loadStep(0, 0);
 #pragma unroll
   for(int tap = 0; tap < NTAPS; tap++) {
-    if(DBG & 1) {
-    } else if(G::RING == 3) {
-      // request stream tap tap+2 (this conv's, or the next conv's tap 0 / 1)
-      if(tap + 2 < NTAPS)
+    // the stream's request at this tap: tap+2 of this conv, or the next conv's tap 0 / 1
+    if(!SPREAD) {
+      if(DBG & 1) {
+      } else if(tap + 2 < NTAPS)
         stageTapDma<G::NW>(w + (size_t)(tap + 2) * UNITS, ring + slotOf(tap + 2) * G::WBUF * 16, CH, wave, lane);
       else if(NTAPS == 9 && tap == 7)
         stageTapDma<G::NW>(wNext, ring, chNext, wave, lane);
       else if(NTAPS == 9 && tap == 8 && nextTaps > 1)
         stageTapDma<G::NW>(wNext + chNext * 64, ring + G::WBUF * 16, chNext, wave, lane);
-    } else {
-      // request stream tap tap+1 (this conv's, or the next conv's tap 0)
-      if(tap + 1 < NTAPS)
-        stageTapDma<G::NW>(w + (size_t)(tap + 1) * UNITS, ring + slotOf(tap + 1) * G::WBUF * 16, CH, wave, lane);
-      else if(nextTaps > 0)
-        stageTapDma<G::NW>(wNext, ring + slotOf(NTAPS) * G::WBUF * 16, chNext, wave, lane);
     }
+    const h16x8* rq = nullptr;
+    uint32_t rqSlot = 0;
+    int rqCh = 0;
+    if(!SPREAD || (DBG & 1)) {
+    } else if(tap + 2 < NTAPS) {
+      rq = w + (size_t)(tap + 2) * UNITS;
+      rqSlot = ring + slotOf(tap + 2) * G::WBUF * 16;
+      rqCh = CH;
+    } else if(NTAPS == 9 && tap == 7) {
+      rq = wNext;
+      rqSlot = ring;
+      rqCh = chNext;
+    } else if(NTAPS == 9 && tap == 8 && nextTaps > 1) {
+      rq = wNext + chNext * 64;
+      rqSlot = ring + G::WBUF * 16;
+      rqCh = chNext;
+    }
+    // 4-board instance: a wave's (at most 3) pieces of it spread one per K-step, the
+    // rest at the last, so the 8 waves' LDS-DMA issue does not bunch up behind the
+    // barrier (conv 9.3 k -> 8.0 k cycles); the 8-board instance, at its register
+    // budget, issues them at once (spreading keeps the request live across the
+    // K-steps: more spills)
+    const int rqPer = (rqCh + G::NW - 1) / G::NW;
 #pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
       const int st = tap * NCB + cb;
+      if(SPREAD && rq && cb < NCB - 1)
+        stageTapPieces<G::NW>(rq, rqSlot, rqCh, wave, lane, cb, cb + 1);
       if(cb == NCB - 1 && tap + 1 < NTAPS) {
-        // retire this wave's pieces of tap+1 (with 3 slots only the tap+2 request, >= N
-        // pieces per wave, may stay in flight), then publish them / free slot of tap
+        // retire this wave's pieces of tap+1: only the pieces of this tap's request
+        // issued before this point may stay in flight (every wave has issued at least
+        // min(pieces per wave, NCB - 1) of them when spread, all of them otherwise),
+        // then publish them / free slot tap%3
+        constexpr int INF_TAP = CH / G::NW, INF_NEXT = (2 * G::NCT_ALL) / G::NW;  // next conv: >= 12 pieces
         if(DBG & 8) {
-        } else if(G::RING == 2)
-          waitVm<0>();
-        else if(tap + 2 < NTAPS)
-          waitVm<CH / G::NW>();
+        } else if(tap + 2 < NTAPS)
+          waitVm<(SPREAD && INF_TAP > NCB - 1 ? NCB - 1 : INF_TAP)>();
         else
-          waitVm<(2 * G::NCT_ALL) / G::NW>();  // next conv's tap 0: at least 12 pieces
+          waitVm<(SPREAD && INF_NEXT > NCB - 1 ? NCB - 1 : INF_NEXT)>();
         if(!(DBG & 2))
           barrierKeepDma();
       }
+      if(SPREAD && rq && cb == NCB - 1)
+        stageTapPieces<G::NW>(rq, rqSlot, rqCh, wave, lane, NCB - 1, rqPer);
       if(st + 1 < STEPS)
         loadStep(st + 1, (st + 1) & 1);
       // keep the next step's LDS reads ahead of this step's MFMAs (the scheduler
@@ -586,7 +618,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
+  convTiles<G, 9, 1>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                            L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL, L->nblocks > 0 ? 9 : 1);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
@@ -623,7 +655,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
     for(int j = 0; j < NPK; j++)
       pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
-    convTiles<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
+    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
                                   (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL, 9);
 #pragma unroll
     for(int j = 0; j < NPK; j++)
@@ -646,7 +678,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
           acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                     3 * G::NCT_ALL, nextTaps);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
@@ -657,9 +689,9 @@ __global__ void __launch_bounds__(NW * 64, 2)
       const float* gbias = P + 416;
       // the gpool linear weights ([96][Cr] f32) are requested now and land in LDS
       // after the epilogue's barrier
-      constexpr int LW = G::LIN_LDS ? (96 * 64 / 4 + G::NT - 1) / G::NT : 1;  // float4 per thread (Cr <= 64)
+      constexpr int LW = (96 * 64 / 4 + G::NT - 1) / G::NT;  // float4 per thread (Cr <= 64)
       float4 lw[LW];
-      if(G::LIN_LDS) {
+      {
         const float4* src = reinterpret_cast<const float4*>(WF + L->linG[blk]);
 #pragma unroll
         for(int k = 0; k < LW; k++) {
@@ -688,21 +720,16 @@ __global__ void __launch_bounds__(NW * 64, 2)
       __syncthreads();
       NN_PHASE(50);
       float* lgT = actF;  // transposed linear weights in the idle front of act
-      if(G::LIN_LDS) {
 #pragma unroll
-        for(int k = 0; k < LW; k++) {
-          const int q = tid + k * G::NT;
-          if(q < Cr * 24)
-            reinterpret_cast<float4*>(lgT)[q] = lw[k];
-        }
+      for(int k = 0; k < LW; k++) {
+        const int q = tid + k * G::NT;
+        if(q < Cr * 24)
+          reinterpret_cast<float4*>(lgT)[q] = lw[k];
       }
       poolBoards<G>(scr, nullptr, poolP, poolV, sqOff, tid);
       __syncthreads();
       NN_PHASE(51);
-      if(G::LIN_LDS)
-        linear96<G>(lgT, Cr, poolP, biasS, Cr, nullptr, false, tid);
-      else
-        linear96<G>(WF + L->linG[blk], Cr, poolP, biasS, Cr, nullptr, false, tid);
+      linear96<G>(lgT, Cr, poolP, biasS, Cr, nullptr, false, tid);
       __syncthreads();
       f32x4 tr[G::MAXT][G::NCT];  // the parked trunk, in flight during the epilogue
       loadTrunk<G>(tr, park, trunk, wave, lane);
@@ -740,7 +767,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
           acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                            3 * G::NCT_ALL, nextTaps);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
@@ -754,7 +781,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0);
+  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0);
   __syncthreads();  // act dead from here: f32 [MROWS][SCR] value branch at actF, g branch at scr
   NN_PHASE(41);
   {
@@ -1044,25 +1071,20 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
   using G8 = NNGeo<5, 5, 96, 8, 8>;
   using G4 = NNGeo<5, 5, 96, 4, 8>;
-  using G2 = NNGeo<5, 5, 96, 2, 4>;
-  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>(), tab2 = rowTables<G2>();
+  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>();
   KC_HIP(hipMalloc(&tabDev_, tab8.size() * 2));
   KC_HIP(hipMemcpy(tabDev_, tab8.data(), tab8.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&tabDev4_, tab4.size() * 2));
   KC_HIP(hipMemcpy(tabDev4_, tab4.data(), tab4.size() * 2, hipMemcpyHostToDevice));
-  KC_HIP(hipMalloc(&tabDev2_, tab2.size() * 2));
-  KC_HIP(hipMemcpy(tabDev2_, tab2.data(), tab2.size() * 2, hipMemcpyHostToDevice));
+
   // function attributes are per device: every engine sets it on its own device
   KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G8::LDS));
   KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G4::LDS));
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             G2::LDS));
-  // small-batch instance (tools / A-B runs only): KATACOFFEE_NN_SMALL=4 selects 4 boards on
-  // 8 waves (one workgroup per CU) instead of 2 boards on 4 waves (two per CU)
+  // A/B runs only: KATACOFFEE_NN_SMALL=8 runs small batches on the 8-board instance too
   const char* small = getenv("KATACOFFEE_NN_SMALL");
-  small4_ = small && atoi(small) == 4;
+  small_ = small ? atoi(small) : 0;
   int dev = 0;
   KC_HIP(hipGetDevice(&dev));
   KC_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev));
@@ -1075,7 +1097,7 @@ NNEngine::~NNEngine() {
   (void)hipFree(layoutDev_);
   (void)hipFree(tabDev_);
   (void)hipFree(tabDev4_);
-  (void)hipFree(tabDev2_);
+
 }
 
 void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev,
@@ -1091,13 +1113,11 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
     return;
   }
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
-  // A launch costs about one workgroup's latency per wave of workgroups: a batch bound
-  // that fits 4 boards per CU (e.g. each of two game groups' batches) runs as two
-  // 2-board workgroups per CU, whose phases interleave on the CU's matrix pipes.
-  if(n <= 4 * cus_ && small4_)
+  // A launch costs about one workgroup's latency per wave of workgroups (one per CU):
+  // a batch bound that fits 4 boards per CU (e.g. each of two game groups' batches)
+  // runs 4 boards per workgroup, half the MFMA work on each workgroup's path.
+  if(n <= 4 * cus_ && small_ != 8)
     launch<NNGeo<5, 5, 96, 4, 8>>(n, inWords, tabDev4_, in, out, st, countDev, rowIdx, e0, e1);
-  else if(n <= 4 * cus_)
-    launch<NNGeo<5, 5, 96, 2, 4>>(n, inWords, tabDev2_, in, out, st, countDev, rowIdx, e0, e1);
   else
     launch<NNGeo<5, 5, 96, 8, 8>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
 }

@@ -3,9 +3,12 @@
 // Layout in HBM (DESIGN.md "Data layout"), every array indexed by game slot g:
 //   GameDev   games[G]                         per-game scalars (boards, RNG, phase, counters)
 //   Node      nodes[G][cap]                    64-B statistics record per search node
-//   Edge      edges[G][cap][P]                 (child, edgeVisits, prior, move) per child slot,
+//   Edge      edges[G][cap][16]                (child, edgeVisits, prior, move) of child slots 0..15,
 //                                              slots in expansion order (SearchChildPointer, searchnode.h)
-//   OrderEnt  order[G][cap][P]                 legal moves by descending prior (next expansion = order[k])
+//   Edge      edgePool[G][2][edgePoolCap]      slots 16.. of the nodes with more children: one block per
+//                                              node at Node::edgeBase, grown 48 -> P-16 like the reference's
+//                                              child arrays (8 -> 64 -> P, searchnode.h:172-174), double
+//                                              buffered so tree reuse compacts the live blocks
 //   uint64_t  nodeKey[G][cap][2]               transposition key per node (TT rebuild after tree reuse)
 //   float     policy[G][cap][P]                NN policy of the node (NNOutput::policyProbs)
 //   uint32_t  freeList[G][cap], allocBits[G][cap/32]   node allocator
@@ -22,6 +25,21 @@
 namespace kc {
 
 constexpr int MAX_DEPTH = MAX_AREA + 2;
+// Child slots stored with the node (the selection's speculative first read); more
+// children go to a block in the game's edge pool
+constexpr int INLINE_EDGES = 16;
+// Capacity of a node's pool block once it has k > INLINE_EDGES children: 48 (to 64
+// slots in all) then P - 16 (reference growth 8 -> 64 -> P, searchnode.cpp:160-235).
+KC_HD int edgeBlockCap(int k, int P) {
+  return (P > 64 && k <= 64) ? 64 - INLINE_EDGES : P - INLINE_EDGES;
+}
+// Pool entries per buffer for node cap `cap`.  A node with k > 16 children holds 48
+// entries, or 48 + P - 16 once k > 64 (the abandoned 48-block included); only nodes
+// with more than 16 visits have more than 16 children, so a search of V <= cap visits
+// has few of them (C5, 1600 visits at 9x9: the root's block and tens of 48-blocks,
+// a few thousand entries against 4 cap).  Exhaustion is counted as a device error
+// (coffee_selfplay_stats.errors), like node-pool exhaustion; it never writes out of bounds.
+inline int edgePoolCapFor(int cap, int P) { return 4 * cap + 2 * P; }
 constexpr int MAX_LANE_ITEMS = (MAX_P + 63) / 64;  // 7
 
 enum LeafKind {
@@ -104,21 +122,16 @@ struct Node {
   uint16_t numChildren;
   uint8_t nextPla;
   uint8_t flags;                  // 1 expanded (NN output stored), 2 terminal
-  // next expansion of a non-root node (order[numChildren]), cached here so the
-  // selection reads it with the node record: prior and policy position
-  // (0xFFFF: every legal move expanded)
+  // next expansion of a non-root node: the legal move with the highest prior among
+  // the unexpanded ones (ties: lower position), cached here so the selection reads it
+  // with the node record: prior and policy position (0xFFFF: every legal move expanded)
   float nextPrior;
   uint16_t nextPos;
   uint16_t pad0;
-  uint32_t pad1[2];
+  uint32_t edgeBase;              // the node's block of child slots >= INLINE_EDGES in the edge pool
+  uint32_t pad1;
 };
 static_assert(sizeof(Node) == 64, "Node layout");
-
-// One entry of a node's expansion order: the move and its prior (pos 0xFFFF ends the list).
-struct OrderEnt {
-  float prior;
-  uint32_t pos;
-};
 
 struct Edge {
   uint32_t child, visits;
@@ -200,6 +213,7 @@ struct GameDev {
   int32_t leafKind, leafNode, leafSym, nnSlot;
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
+  int32_t edgeSel, edgeTop;       // current edge-pool buffer, its first free slot
   float accWin, accLoss, rawWin, rawLoss;
 };
 
@@ -239,8 +253,9 @@ struct SearchDev {
   uint64_t seed;
   DPtr<GameDev> games;
   DPtr<Node> nodes;
-  DPtr<Edge> edges;
-  DPtr<OrderEnt> order;
+  DPtr<Edge> edges;           // [G][cap][INLINE_EDGES]
+  DPtr<Edge> edgePool;        // [G][2][edgePoolCap]
+  int edgePoolCap;
   DPtr<uint64_t> nodeKey;     // [G][cap][2] transposition key of each node (TT rebuild after reuse)
   DPtr<float> policy;
   DPtr<uint32_t> freeList;

@@ -120,18 +120,31 @@ KC_D unsigned long long* sprofLds() {
   } while(0)
 #endif
 
+// A node's child slots: 0..INLINE_EDGES-1 stored with the node, the rest in its block
+// of the game's edge pool (search.h).
+struct NodeEdges {
+  Edge* inl;
+  Edge* pool;  // slot INLINE_EDGES of the node's pool block
+  KC_D Edge& operator[](int i) const { return i < INLINE_EDGES ? inl[i] : pool[i - INLINE_EDGES]; }
+};
+
 // Per-game view of the SoA arrays.
 struct GV {
   const SearchDev& d;
   const DTables& T;
   int g, lane;
   const SP* sp;  // this move's search parameters (moveParams after loadGame)
+  mutable int esel = 0;  // the game's current edge-pool buffer (GameDev::edgeSel; setEdgeSel)
   KC_D GV(const SearchDev& d_, int g_) : d(d_), T(*d_.T), g(g_), lane(laneId()), sp(&d_.sp) {}
   // tables through a readonly noalias kernel argument: uniform reads become scalar loads
   KC_D GV(const SearchDev& d_, const DTables& t_, int g_) : d(d_), T(t_), g(g_), lane(laneId()), sp(&d_.sp) {}
   KC_D Node* nodes() const { return d.nodes + (size_t)g * d.cap; }
-  KC_D Edge* edges(int n) const { return d.edges + ((size_t)g * d.cap + n) * d.P; }
-  KC_D OrderEnt* order(int n) const { return d.order + ((size_t)g * d.cap + n) * d.P; }
+  KC_D Edge* inlineEdges(int n) const { return d.edges + ((size_t)g * d.cap + n) * INLINE_EDGES; }
+  KC_D Edge* edgePool() const { return d.edgePool + ((size_t)g * 2 + esel) * d.edgePoolCap; }
+  KC_D void setEdgeSel(int sel) const { esel = __builtin_amdgcn_readfirstlane(sel); }
+  // child slots of node n whose pool block starts at ebase (Node::edgeBase)
+  KC_D NodeEdges edges(int n, uint32_t ebase) const { return NodeEdges{inlineEdges(n), edgePool() + ebase}; }
+  KC_D NodeEdges edges(int n) const { return edges(n, nodes()[n].edgeBase); }
   KC_D uint64_t* nodeKey(int n) const { return d.nodeKey + ((size_t)g * d.cap + n) * 2; }
   KC_D float* pol(int n) const { return d.policy + ((size_t)g * d.cap + n) * d.P; }
   KC_D uint32_t* freeList() const { return d.freeList + (size_t)g * d.cap; }
@@ -170,6 +183,7 @@ KC_D void loadGame(GV& v, GameDev& s) {
   // a cheap search without recorded rows runs without root noise and root-specific
   // settings (runBotWithLimits play.cpp:1024-1037); the flag is uniform
   v.sp = __builtin_amdgcn_readfirstlane(s.noNoise) ? &v.d.spCheap : &v.d.sp;
+  v.setEdgeSel(s.edgeSel);
 }
 
 template <int NI>
@@ -187,7 +201,7 @@ KC_D float tsum(const float (&x)[NI], int n, int lane) {
 KC_D int bcastI(int v, int srcLane) { return bcastLane(v, srcLane); }
 
 // Child slots read speculatively with their node record (2 x 128-B lines of Edge).
-constexpr int SPEC_EDGES = 16;
+constexpr int SPEC_EDGES = INLINE_EDGES;
 KC_D int firstLane(uint64_t m) { return __builtin_ctzll(m); }
 
 KC_D float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeight) {
@@ -293,7 +307,8 @@ KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k
     n.nextPrior = -1.0f;
     n.nextPos = 0xFFFF;
     n.pad0 = 0;
-    n.pad1[0] = n.pad1[1] = 0;
+    n.edgeBase = 0;
+    n.pad1 = 0;
     v.nodes()[idx] = n;
     v.nodeKey(idx)[0] = k0;
     v.nodeKey(idx)[1] = k1;
@@ -379,6 +394,7 @@ KC_D float cdfT(const DTables& T, float z) {
 template <int NI>
 struct PathLevel {
   int ni, slot, k, nextPla, svbEntry;
+  uint32_t ebase;
   float nnWin, nnLoss, lastSvbDelta, lastSvbWeight;
   uint32_t visits0;
   uint32_t ech[NI], evis[NI];  // edge child and visits
@@ -396,10 +412,11 @@ struct LevelOut {
 template <int NI>
 KC_D void loadLevel(const GV& v, int ni, int slot, PathLevel<NI>& L) {
   const Node nd = v.nodes()[ni];
-  const Edge* E = v.edges(ni);
+  const Edge* E = v.inlineEdges(ni);
   // the first SPEC_EDGES slots speculatively with the record (slots past numChildren
   // are ignored); the rest once the record says how many there are
   const Edge e0 = v.lane < SPEC_EDGES && v.lane < v.d.P ? E[v.lane] : Edge{0u, 0u, 0.0f, 0u};
+  L.ebase = nd.edgeBase;
   L.ech[0] = e0.child;
   L.evis[0] = e0.visits;
   L.ni = ni;
@@ -417,7 +434,7 @@ KC_D void loadLevel(const GV& v, int ni, int slot, PathLevel<NI>& L) {
 template <int NI>
 KC_D void loadKids(const GV& v, const GameDev& s, PathLevel<NI>& L) {
   const SP& sp = *v.sp;
-  const Edge* E = v.edges(L.ni);
+  const NodeEdges E = v.edges(L.ni, L.ebase);
   const Node* NS = v.nodes();
 #pragma unroll
   for(int j = 0; j < NI; j++) {
@@ -459,7 +476,7 @@ KC_D LevelOut computeLevel(const GV& v, const GameDev& s, PathLevel<NI>& L, cons
   const int k = L.k, slot = L.slot;
   const int nextPla = L.nextPla;
   const int svbEntry = L.svbEntry;
-  Edge* E = v.edges(L.ni);
+  const NodeEdges E = v.edges(L.ni, L.ebase);
   const bool svbOn = sp.svbFactor != 0.0f && svbEntry >= 0;
   int64_t svbD0 = L.svbD0, svbW0 = L.svbW0;
   if(svbOn && haveBelow && below.svbEntry == svbEntry) {
@@ -748,7 +765,7 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
       hasBits[w] = 0;
     waveSync();
   }
-  const Edge* E = v.edges(ni);
+  const NodeEdges E = v.edges(ni, n.edgeBase);
   const Node* NS = v.nodes();
   float probs[NI], cw[NI], pv[NI], cu[NI];
   uint32_t cvis[NI], cfl[NI];
@@ -859,6 +876,33 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
   return bestSlot;
 }
 
+// A non-root node's expansion order is its legal moves by descending prior, ties by
+// ascending position -- the order selectBest's new-child scan yields
+// (selectBestChildToDescend searchexplorehelpers.cpp:304-451: "first strictly
+// greater" over positions).  The node caches only its next entry (Node::nextPrior /
+// nextPos); the entry after (curPrior, curPos) is found when that one is expanded by
+// one scan of the node's policy: the highest prior below curPrior, or equal to it at a
+// higher position.  pv: the node's policy, lane-strided (illegal = -1).  No entry:
+// (-1, 0xFFFF).
+template <int NI>
+KC_D void nextExpansion(const GV& v, const float (&pv)[NI], float curPrior, int curPos, float& nPrior, int& nPos) {
+  const int P = v.d.P;
+  float best = -1.0f;
+  int bi = BIG;
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    const int p = v.lane + 64 * j;
+    const float x = pv[j];
+    if(p < P && x >= 0.0f && (x < curPrior || (x == curPrior && p > curPos)) && x > best) {
+      best = x;
+      bi = p;
+    }
+  }
+  waveArgmax(best, bi);
+  nPrior = bi != BIG ? best : -1.0f;
+  nPos = bi != BIG ? bi : 0xFFFF;
+}
+
 // oracle descend (playoutDescend search.cpp:936-1165, allocateOrFindNode :704-759,
 // maybeCatchUpEdgeVisits :1169-1207)
 template <int NI>
@@ -874,7 +918,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
   // a dependent round trip; wider speculation would touch cold lines.  Each
   // level's loads are issued before anything waits on the previous level.
   auto loadE0 = [&](int node) {
-    return v.lane < SPEC_EDGES && v.lane < v.d.P ? v.edges(node)[v.lane] : Edge{0u, 0u, 0.0f, 0u};
+    return v.lane < SPEC_EDGES && v.lane < v.d.P ? v.inlineEdges(node)[v.lane] : Edge{0u, 0u, 0.0f, 0u};
   };
   Edge e0 = loadE0(ni);
   Node n = v.nodes()[ni];
@@ -923,10 +967,40 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
     if(slot == n.numChildren) {
       const unsigned long long tExp = SPROF_NOW();
       (void)tExp;
-      // the node's following expansion candidate (non-root), loaded up front
-      OrderEnt nxt{-1.0f, 0xFFFFu};
-      if(!isRoot && slot + 1 < v.d.P)
-        nxt = v.order(ni)[slot + 1];
+      // the node's following expansion candidate (non-root): one scan of its policy
+      float nxtPrior = -1.0f;
+      int nxtPos = 0xFFFF;
+      if(!isRoot) {
+        const float* pp = v.pol(ni);
+        float pvn[NI];
+#pragma unroll
+        for(int j = 0; j < NI; j++) {
+          const int p = v.lane + 64 * j;
+          pvn[j] = p < v.d.P ? pp[p] : -1.0f;
+        }
+        nextExpansion<NI>(v, pvn, n.nextPrior, n.nextPos, nxtPrior, nxtPos);
+      }
+      // child slot `slot` past the inline ones lives in the node's edge-pool block,
+      // allocated (16 -> 64 slots) or grown (-> P) here; pool exhaustion ends the
+      // descent like node-pool exhaustion (a counted device error)
+      uint32_t ebase = n.edgeBase;
+      if(slot == INLINE_EDGES || (slot == 64 && v.d.P > 64)) {
+        const int need = edgeBlockCap(slot + 1, v.d.P);
+        if(s.edgeTop + need > v.d.edgePoolCap) {
+          s.err = 1;
+          s.leafKind = LEAF_NOCHILD;
+          s.leafNode = ni;
+          break;
+        }
+        const uint32_t nb = (uint32_t)s.edgeTop;
+        s.edgeTop += need;
+        if(slot > INLINE_EDGES) {
+          Edge* pool = v.edgePool();
+          for(int i = v.lane; i < slot - INLINE_EDGES; i += 64)
+            pool[nb + i] = pool[ebase + i];
+        }
+        ebase = nb;
+      }
       const float prior = isRoot ? v.pol(ni)[newPos] : n.nextPrior;
       const int cell = newPos % T.A, dir = newPos / T.A;
       // SVB key of the expansion (needs the board before the move); computed
@@ -961,11 +1035,12 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
       }
       waveSync();
       if(v.lane == 0) {
-        v.edges(ni)[slot] = Edge{(uint32_t)child, 0u, prior, (uint32_t)newPos};
+        v.edges(ni, ebase)[slot] = Edge{(uint32_t)child, 0u, prior, (uint32_t)newPos};
         v.nodes()[ni].numChildren = (uint16_t)(slot + 1);
+        v.nodes()[ni].edgeBase = ebase;
         if(!isRoot) {
-          v.nodes()[ni].nextPos = (uint16_t)nxt.pos;
-          v.nodes()[ni].nextPrior = nxt.prior;
+          v.nodes()[ni].nextPos = (uint16_t)nxtPos;
+          v.nodes()[ni].nextPrior = nxtPrior;
         }
         v.pathNode()[s.pathLen] = ni;
         v.pathSlot()[s.pathLen] = slot;
@@ -1027,8 +1102,8 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   if(g >= d.G)
     return;
   __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
-  GV v(d, *Tp, g);
   __shared__ GameDev s;
+  GV v(d, *Tp, g);
   SPROF_INIT();
   const unsigned long long t0 = SPROF_NOW();
   if(d.nnDefer[g]) {
@@ -1327,62 +1402,15 @@ KC_D void noiseAndTemp(const GV& v, GameDev& s, DRng& rng, const float* raw, flo
   }
 }
 
-// Expansion order of a freshly evaluated node: legal moves by descending prior,
-// ties by ascending position (the order selectBest's new-child scan yields),
-// 0xFFFF after the last legal move. Rank by counting; priors staged in LDS.
+// A freshly evaluated node's first expansion candidate.
 template <int NI>
-KC_D void buildOrder(const GV& v, int ni, const float (&pv)[NI], float* lds) {
-  const int P = v.d.P;
-  // one 64-bit key per entry ordering "higher prior first, then lower position":
-  // the prior's bits in an order-preserving form above the complemented position
-  // (priors are >= +0 or exactly -1, so float order is the key order)
-  uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
-  auto keyOf = [](float x, int p) {
-    const uint32_t b = __builtin_bit_cast(uint32_t, x);
-    const uint32_t o = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-    return ((uint64_t)o << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)p);
-  };
-  uint64_t myKey[NI];
-  waveSync();
-#pragma unroll
-  for(int j = 0; j < NI; j++) {
-    const int p = v.lane + 64 * j;
-    myKey[j] = keyOf(pv[j], p);
-    if(p < P)
-      keys[p] = myKey[j];
-  }
-  waveSync();
-  OrderEnt* ord = v.order(ni);
-  int nLegal = 0;
-  // rank of each of the lane's entries = entries ordered before it (larger keys)
-  int rank[NI];
-#pragma unroll
-  for(int j = 0; j < NI; j++)
-    rank[j] = 0;
-  for(int q = 0; q < P; q += 2) {
-    const uint64_t k0 = keys[q], k1 = keys[q + 1];
-#pragma unroll
-    for(int j = 0; j < NI; j++) {
-      rank[j] += k0 > myKey[j] ? 1 : 0;
-      rank[j] += k1 > myKey[j] ? 1 : 0;
-    }
-  }
-#pragma unroll
-  for(int j = 0; j < NI; j++) {
-    const int p = v.lane + 64 * j;
-    if(p < P && pv[j] >= 0.0f)
-      ord[rank[j]] = OrderEnt{pv[j], (uint32_t)p};
-  }
-#pragma unroll
-  for(int j = 0; j < NI; j++)
-    nLegal += __builtin_popcountll(ballot(v.lane + 64 * j < P && pv[j] >= 0.0f));
-  for(int r = nLegal + v.lane; r < P; r += 64)
-    ord[r] = OrderEnt{-1.0f, 0xFFFFu};
-  waveSync();
+KC_D void firstExpansion(const GV& v, int ni, const float (&pv)[NI]) {
+  float pr;
+  int pos;
+  nextExpansion<NI>(v, pv, __builtin_inff(), -1, pr, pos);
   if(v.lane == 0) {
-    const OrderEnt first = ord[0];
-    v.nodes()[ni].nextPos = (uint16_t)first.pos;
-    v.nodes()[ni].nextPrior = first.prior;
+    v.nodes()[ni].nextPos = (uint16_t)pos;
+    v.nodes()[ni].nextPrior = pr;
   }
   waveSync();
 }
@@ -1484,8 +1512,8 @@ __global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* 
   if(g >= d.G || d.nnDefer[g])  // a deferred leaf is backed up in a later round
     return;
   __shared__ __attribute__((aligned(16))) float scratch[3 * MAX_P];
-  GV v(d, *Tp, g);
   __shared__ GameDev s;
+  GV v(d, *Tp, g);
   SPROF_INIT();
   const unsigned long long t0 = SPROF_NOW();
   (void)t0;
@@ -1604,7 +1632,7 @@ __global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* 
           }
         }
       }
-      buildOrder<NI>(v, s.leafNode, pv, scratch);
+      firstExpansion<NI>(v, s.leafNode, pv);
       if(v.lane == 0) {
         Node* n = &v.nodes()[s.leafNode];
         n->nnWin = w;
@@ -1724,7 +1752,7 @@ KC_D int playSelectionValuesAt(const GV& v, const SP& sp, const GameDev& s, int 
   const Node& n = v.nodes()[ri];
   const int k = n.numChildren;
   const int pla = n.nextPla;
-  const Edge* E = v.edges(ri);
+  const NodeEdges E = v.edges(ri, n.edgeBase);
   float cw[NI], val[NI];
   uint32_t ev[NI];
   int posv[NI];
@@ -2008,6 +2036,7 @@ KC_D void clearTables(const GV& v, GameDev& s) {
   const size_t sb = v.svbBase(s.svbSel);
   fillWords(reinterpret_cast<uint32_t*>(&v.d.svbKey[sb]), 2 * v.d.svbCap, 0u, v.lane);
   s.freeTop = cap;
+  s.edgeTop = 0;
   s.liveCount = 0;
   s.rootIdx = -1;
   waveSync();
@@ -2023,7 +2052,7 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
   int child = -1;
   if(ri >= 0) {
     const Node& r = v.nodes()[ri];
-    const Edge* E = v.edges(ri);
+    const NodeEdges E = v.edges(ri, r.edgeBase);
     for(int base = 0; base < r.numChildren; base += 64) {
       int i = base + v.lane;
       bool hit = i < r.numChildren && (int)E[i].move == chosenPos;
@@ -2057,14 +2086,16 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
     const int cnt = min(64, tail - head);
     if(v.lane < cnt) {
       const int nd = queue[head + v.lane];
-      const int kc = v.nodes()[nd].numChildren;
-      const Edge* E = v.edges(nd);
+      const Node& nr = v.nodes()[nd];
+      const int kc = nr.numChildren;
+      const Edge* inl = v.inlineEdges(nd);
+      const Edge* pool = v.edgePool() + nr.edgeBase - INLINE_EDGES;  // indexed by child slot
       // four child loads in flight before the LDS atomics that consume them
       for(int i = 0; i < kc; i += 4) {
         int ch[4];
 #pragma unroll
         for(int u = 0; u < 4; u++)
-          ch[u] = i + u < kc ? (int)E[i + u].child : -1;
+          ch[u] = i + u < kc ? (int)(i + u < INLINE_EDGES ? inl : pool)[i + u].child : -1;
 #pragma unroll
         for(int u = 0; u < 4; u++) {
           const int c = ch[u];
@@ -2208,6 +2239,41 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
     }
   }
   s.svbSel = nsel;
+  // edge pool: the live nodes' blocks into the other buffer (queue order, prefix sums
+  // of the block sizes), so the dead nodes' blocks are reclaimed
+  {
+    const int P = v.d.P;
+    Edge* src = v.edgePool();
+    Edge* dst = v.d.edgePool + ((size_t)v.g * 2 + (s.edgeSel ^ 1)) * v.d.edgePoolCap;
+    int top = 0;
+    for(int base = 0; base < liveCount; base += 64) {
+      const int i = base + v.lane;
+      const int nd = i < liveCount ? (int)queue[i] : -1;
+      const Node* np = nd >= 0 ? &v.nodes()[nd] : nullptr;
+      const int k = np ? (int)np->numChildren : 0;
+      const int need = k > INLINE_EDGES ? edgeBlockCap(k, P) : 0;
+      int incl = need;
+#pragma unroll
+      for(int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if(v.lane >= off)
+          incl += y;
+      }
+      const int mine = top + incl - need;
+      if(need) {
+        const uint32_t ob = np->edgeBase;
+        for(int e = 0; e < k - INLINE_EDGES; e++)
+          dst[mine + e] = src[ob + e];
+        v.nodes()[nd].edgeBase = (uint32_t)mine;
+      }
+      top += __shfl(incl, 63, 64);
+    }
+    const int nsel2 = s.edgeSel ^ 1;
+    waveSync();
+    s.edgeSel = nsel2;
+    s.edgeTop = top;
+    v.setEdgeSel(nsel2);
+  }
   waveSync();
 }
 
@@ -2702,7 +2768,7 @@ KC_D void recordTreePositions(const GV& v, const SP& sp, const GameDev& s, DRng&
   while(depth >= 0) {
     const int ni = fNode[depth];
     const int k = v.nodes()[ni].numChildren;
-    const Edge* E = v.edges(ni);
+    const NodeEdges E = v.edges(ni);
     if(enter) {
       enter = false;
       if(k <= 0) {
@@ -3132,8 +3198,8 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   int* qtail = reinterpret_cast<int*>(tmp2 + MAX_P);
   uint32_t* liveBits = reinterpret_cast<uint32_t*>(qtail + 4);  // [cap/32]
   uint16_t* queue = reinterpret_cast<uint16_t*>(liveBits + d.cap / 32);     // [cap]
-  GV v(d, *Tp, g);
   __shared__ GameDev s;
+  GV v(d, *Tp, g);
   SPROF_INIT();
   [[maybe_unused]] const unsigned long long t0 = SPROF_NOW();
   loadGame(v, s);
@@ -3387,8 +3453,8 @@ __global__ void __launch_bounds__(64) kInit(const SearchDev* __restrict__ dp, co
   const int g = blockIdx.x;
   if(g >= d.G)
     return;
-  GV v(d, *Tp, g);
   __shared__ GameDev s;
+  GV v(d, *Tp, g);
   for(int i = v.lane; i < (int)(sizeof(GameDev) / 4); i += 64)
     reinterpret_cast<uint32_t*>(&s)[i] = 0;
   waveSync();
@@ -3460,7 +3526,8 @@ __global__ void kGameTree(const SearchDev* __restrict__ dp, int g, int maxNodes,
     o[20] = (uint32_t)((uint64_t)sw >> 32);
     o[21] = 0;
     o[22] = 0;
-    const Edge* E = d.edges + ((size_t)g * d.cap + idx) * d.P;
+    const NodeEdges E{d.edges + ((size_t)g * d.cap + idx) * INLINE_EDGES,
+                      d.edgePool + ((size_t)g * 2 + d.games[g].edgeSel) * d.edgePoolCap + x.edgeBase};
     for(int i = 0; i < x.numChildren; i++) {
       const int c = (int)E[i].child;
       int ci = -1;

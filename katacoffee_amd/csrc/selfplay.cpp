@@ -164,8 +164,9 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.seed = c.seed;
   d.games = devAlloc<GameDev>(owned_, G);
   d.nodes = devAlloc<Node>(owned_, (size_t)G * cap, false);
-  d.edges = devAlloc<Edge>(owned_, (size_t)G * cap * P, false);
-  d.order = devAlloc<OrderEnt>(owned_, (size_t)G * cap * P, false);
+  d.edges = devAlloc<Edge>(owned_, (size_t)G * cap * INLINE_EDGES, false);
+  d.edgePoolCap = edgePoolCapFor(cap, P);
+  d.edgePool = devAlloc<Edge>(owned_, (size_t)G * 2 * d.edgePoolCap, false);
   d.policy = devAlloc<float>(owned_, (size_t)G * cap * P, false);
   d.nodeKey = devAlloc<uint64_t>(owned_, (size_t)G * cap * 2, false);
   d.freeList = devAlloc<uint32_t>(owned_, (size_t)G * cap, false);

@@ -211,7 +211,8 @@ int ora_block_apply_blob(int kind, int W, int mid, int Cg, const float* blob, lo
 // policy_init_area_prop, policy_init_area_temperature, early_fork_game_prob,
 // early_fork_game_expected_move_prop, fork_game_prob, fork_game_min_choices,
 // early_fork_game_max_choices, fork_game_max_choices, side_position_prob,
-// record_tree_positions, record_tree_threshold, record_tree_target_weight).
+// record_tree_positions, record_tree_threshold, record_tree_target_weight) and the
+// search's cpuct_exploration.
 void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, uint64_t seed, int slotBase,
                     int nnMode, void* model, int nnThreads, int cacheLog2, const float* play, int nnCap) {
   if(!T.loaded)
@@ -244,6 +245,7 @@ void* ora_sp_create(int X, int Y, int W, int games, int maxVisits, int nodeCap, 
     cfg.sp.recordTreePositions = (int)play[20];
     cfg.sp.recordTreeThreshold = (int)play[21];
     cfg.sp.recordTreeTargetWeight = play[22];
+    cfg.sp.cpuctExploration = play[23];
   }
   cfg.nodeCap = nodeCap;
   cfg.seed = seed;

@@ -234,6 +234,7 @@ PLAY_SETTINGS = {
     "fork_game_min_choices": 3, "early_fork_game_max_choices": 12, "fork_game_max_choices": 36,
     "side_position_prob": 0.0,
     "record_tree_positions": 0, "record_tree_threshold": 0, "record_tree_target_weight": 0.0,
+    "cpuct_exploration": 1.1,
 }
 
 

@@ -156,6 +156,9 @@ def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
         orr = _sorted_rows(ora.rows())
         assert len(gr["meta"]) == len(orr["meta"]) > 0
         for k in orr:
+            bad = np.argwhere(gr[k].reshape(len(gr[k]), -1) != orr[k].reshape(len(orr[k]), -1))
+            if len(bad):  # which rows (slot, game, turn) and which columns differ
+                print(k, "mismatches (meta, column):", [(gr["meta"][r].tolist(), int(c)) for r, c in bad[:20]])
             np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
         gpu.close()
     net.close()

@@ -403,6 +403,42 @@ def test_selfplay_deep_trees_full_scale_sampled_slots(X, Y, W, G, visits, rounds
     gpu.close()
 
 
+# Edge pool (search.h): child slots past 16 live in per-node blocks of the game's pool,
+# grown 48 -> P-16 and compacted into the other buffer when a cheap search keeps the
+# subtree (reuseTree).  Wide 9x9 roots (P = 324) at 600 visits grow blocks past 64 slots;
+# selfplay1.cfg's cheap searches reuse trees.  Bit-exact vs the oracle (which has no pool).
+# (cpuct 8 spreads the visits so the root passes 64 children)
+@pytest.mark.parametrize("play", [dict(cpuct_exploration=8.0),
+                                  dict(PRODUCTION, cheap_search_visits=60, reduced_visits_min=60,
+                                       cpuct_exploration=8.0)],
+                         ids=["9x9-wide-bench", "9x9-wide-reuse"])
+def test_selfplay_edge_pool_growth_and_compaction(play):
+    X, Y, W, G, visits, cap, rounds = 9, 9, 5, 4, 600, 700, 2600
+    gpu = kc.Selfplay(X, Y, W, num_games=G, max_visits=visits, seed=515, node_cap=cap, commit_interval=1,
+                      nn_cache_log2=0, **play)
+    ora = oracle.Selfplay(X, Y, W, games=G, max_visits=visits, node_cap=cap, seed=515, **play)
+    done = 0
+    wide = 0
+    # round 590: still the first (empty-board, 324 legal moves) search, the widest roots
+    for chunk in [400, 590, 1000, rounds]:
+        gpu.step(chunk - done)
+        ora.rounds(chunk - done)
+        done = chunk
+        for g in range(G):
+            _compare_game(gpu, ora, g, g, done)
+            gn, _ = gpu.game_tree(g)
+            wide = max(wide, int((gn[:, 10] & 0xFFFF).max()))
+    st = gpu.stats()
+    assert st["errors"] == 0 and st["moves"] > 0
+    assert wide > 64  # some node used a grown (P - 16) pool block
+    gr = _sorted_rows(gpu.drain_rows())
+    orr = _sorted_rows(ora.rows())
+    assert len(gr["meta"]) == len(orr["meta"])
+    for k in orr:
+        np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
+    gpu.close()
+
+
 def test_rows_record_network_switch(model_path):
     """Hot reload mid-game (switchNetsMidGame, play.cpp:1210-1226): rows of games that
     span the switch carry globalTargets[49] = 1 and [50] = reloads after the row's turn

@@ -1,26 +1,25 @@
 // Steady-state cycles of the network's 96->96 3x3 convolution (convTiles) and of
-// stripped variants, one 512-thread workgroup per CU, 256 workgroups.
+// stripped variants for each fused-kernel instance (8 / 4 boards on 8 waves, one
+// workgroup per CU).
 //   real      : convTiles as shipped (LDS weight ring + barriers + fragment loads)
 //   nobar     : same loads, weights read from a fixed LDS slot, no ring stores/barriers
 //   noload    : MFMAs on register-resident fragments only (no LDS reads)
 //   nodma / dma-nowait-nobar / dma-neverwait: convTiles with parts of the weight
 //               stream removed (convTiles' DBG ablation flags)
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I katacoffee_amd/csrc tools/conv_bench.hip
-//        katacoffee_amd/csrc/model.cpp -o tools/_build/conv_bench
+// Build: make -C tools conv_bench ; run: tools/_build/conv_bench
 #include "../katacoffee_amd/csrc/nn.hip"
 
 #include <cstdio>
 #include <vector>
 
 using namespace kc;
-using G = NNGeo<5, 5, 96>;
 constexpr int REPS = 16;
 
 // convTiles DBG flags per mode (modes 1 and 2 are hand-written loops)
 constexpr int kDbg[6] = {0, 0, 0, 1, 10, 256 + 10};
 
-template <int MODE>
-__global__ void __launch_bounds__(NN_NT, 2) kConv(const h16x8* __restrict__ w, const uint16_t* __restrict__ tabs,
+template <class G, int MODE>
+__global__ void __launch_bounds__(G::NT, 2) kConv(const h16x8* __restrict__ w, const uint16_t* __restrict__ tabs,
                                                   float* out, unsigned long long* cyc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -29,11 +28,11 @@ __global__ void __launch_bounds__(NN_NT, 2) kConv(const h16x8* __restrict__ w, c
   uint16_t* act = reinterpret_cast<uint16_t*>(smem);
   uint16_t* rowPa = reinterpret_cast<uint16_t*>(smem + G::OFF_TAB);
   h16x8* wl = reinterpret_cast<h16x8*>(smem + G::OFF_W);
-  for(int i = tid; i < G::NTAB; i += NN_NT)
+  for(int i = tid; i < G::NTAB; i += G::NT)
     rowPa[i] = tabs[i];
-  for(int i = tid; i < G::ACT_BYTES / 2; i += NN_NT)
+  for(int i = tid; i < G::ACT_BYTES / 2; i += G::NT)
     act[i] = (uint16_t)(0x3000 + (i * 7 & 0x3ff));
-  for(int i = tid; i < 3 * G::WBUF; i += NN_NT)
+  for(int i = tid; i < G::RING * G::WBUF; i += G::NT)
     wl[i] = w[i % (9 * G::WBUF)];
   __syncthreads();
   int ab[G::MAXT];
@@ -45,7 +44,7 @@ __global__ void __launch_bounds__(NN_NT, 2) kConv(const h16x8* __restrict__ w, c
     if(MODE == 0 || MODE >= 3) {
       // the stream's taps 7/8 re-request this conv's taps 0/1 for the next rep
       constexpr int DBG = kDbg[MODE];
-      convTiles<G, 9, 3, false, DBG>(act, w, wl, acc, ab, cg, lane, tid, w, 3 * G::NCT_ALL, 9);
+      convTiles<G, 9, 3, DBG>(act, w, wl, acc, ab, cg, lane, tid, w, 3 * G::NCT_ALL, 9);
       if(!(DBG & 256))
         __syncthreads();
     } else if(MODE == 1) {
@@ -55,7 +54,7 @@ __global__ void __launch_bounds__(NN_NT, 2) kConv(const h16x8* __restrict__ w, c
       auto loadStep = [&](int st, int buf) {
         const int tap = st / 3, cb = st - tap * 3;
         const int aoff = ((tap / 3) * G::PX + tap % 3) * G::ROWB + cb * 64;
-        const h16x8* wb = wlane + (tap % 3) * G::WBUF + cb * G::NCT_ALL * 64;
+        const h16x8* wb = wlane + (tap % G::RING) * G::WBUF + cb * G::NCT_ALL * 64;
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++)
           bf[buf][ct] = wb[ct * 64];
@@ -99,47 +98,58 @@ __global__ void __launch_bounds__(NN_NT, 2) kConv(const h16x8* __restrict__ w, c
   for(int t = 0; t < G::MAXT; t++)
     for(int ct = 0; ct < G::NCT; ct++)
       s += acc[t][ct][0] + acc[t][ct][3];
-  out[blockIdx.x * NN_NT + tid] = s;
+  out[blockIdx.x * G::NT + tid] = s;
   if(tid == 0)
     cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int MODE>
-void run(const char* name, const h16x8* w, const uint16_t* tabs, float* out, unsigned long long* cyc) {
-  KC_HIP(hipFuncSetAttribute((const void*)kConv<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+template <class G, int MODE>
+void run(const char* name, int wgPerCu, const h16x8* w, const uint16_t* tabs, float* out, unsigned long long* cyc) {
+  const int grid = 256 * wgPerCu;
+  KC_HIP(hipFuncSetAttribute((const void*)kConv<G, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
   for(int it = 0; it < 3; it++)
-    hipLaunchKernelGGL(kConv<MODE>, dim3(256), dim3(NN_NT), G::LDS, 0, w, tabs, out, cyc);
+    hipLaunchKernelGGL((kConv<G, MODE>), dim3(grid), dim3(G::NT), G::LDS, 0, w, tabs, out, cyc);
   KC_HIP(hipDeviceSynchronize());
-  std::vector<unsigned long long> c(256);
-  KC_HIP(hipMemcpy(c.data(), cyc, 256 * 8, hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> c(grid);
+  KC_HIP(hipMemcpy(c.data(), cyc, grid * 8, hipMemcpyDeviceToHost));
   double avg = 0;
   for(auto v : c)
     avg += v;
-  avg /= 256.0;
-  printf("%-8s %8.0f cycles per conv (%.1f per K-step; ideal 2-wave MFMA %.0f)\n", name, avg / REPS,
-         avg / REPS / 27, 27 * 24 * 8.7);
+  avg /= grid;
+  // MFMA issue floor per SIMD per conv: 27 K-steps x MAXT x NCT MFMAs x 16 cycles x waves per SIMD
+  const double floor = 27.0 * G::MAXT * G::NCT * 16.0 * (G::NW * wgPerCu / 4);
+  printf("NB%d/NW%d %-17s %8.0f cycles per conv (%.1f per K-step; MFMA floor %.0f)\n", G::NB, G::NW, name,
+         avg / REPS, avg / REPS / 27, floor);
 }
 
-int main() {
-  std::vector<uint16_t> hw((size_t)9 * G::WBUF * 8);
-  for(size_t i = 0; i < hw.size(); i++)
-    hw[i] = (uint16_t)(0x2000 + (i * 13 & 0x7ff));
-  h16x8* w;
-  KC_HIP(hipMalloc(&w, hw.size() * 2));
-  KC_HIP(hipMemcpy(w, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+template <class G>
+void runAll(int wgPerCu, const h16x8* w) {
   std::vector<uint16_t> tab = rowTables<G>();
   uint16_t* tabs;
   KC_HIP(hipMalloc(&tabs, tab.size() * 2));
   KC_HIP(hipMemcpy(tabs, tab.data(), tab.size() * 2, hipMemcpyHostToDevice));
   float* out;
   unsigned long long* cyc;
-  KC_HIP(hipMalloc(&out, 256 * NN_NT * 4));
-  KC_HIP(hipMalloc(&cyc, 256 * 8));
-  run<0>("real", w, tabs, out, cyc);
-  run<1>("nobar", w, tabs, out, cyc);
-  run<2>("noload", w, tabs, out, cyc);
-  run<3>("nodma", w, tabs, out, cyc);
-  run<4>("dma-nowait-nobar", w, tabs, out, cyc);
-  run<5>("dma-neverwait", w, tabs, out, cyc);
+  KC_HIP(hipMalloc(&out, (size_t)512 * G::NT * 4));
+  KC_HIP(hipMalloc(&cyc, 512 * 8));
+  run<G, 0>("real", wgPerCu, w, tabs, out, cyc);
+  run<G, 1>("nobar", wgPerCu, w, tabs, out, cyc);
+  run<G, 2>("noload", wgPerCu, w, tabs, out, cyc);
+  run<G, 3>("nodma", wgPerCu, w, tabs, out, cyc);
+  run<G, 4>("dma-nowait-nobar", wgPerCu, w, tabs, out, cyc);
+  run<G, 5>("dma-neverwait", wgPerCu, w, tabs, out, cyc);
+}
+
+int main() {
+  using G8 = NNGeo<5, 5, 96, 8, 8>;
+  std::vector<uint16_t> hw((size_t)9 * G8::WBUF * 8);
+  for(size_t i = 0; i < hw.size(); i++)
+    hw[i] = (uint16_t)(0x2000 + (i * 13 & 0x7ff));
+  h16x8* w;
+  KC_HIP(hipMalloc(&w, hw.size() * 2));
+  KC_HIP(hipMemcpy(w, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+  runAll<G8>(1, w);
+  runAll<NNGeo<5, 5, 96, 4, 8>>(1, w);
+
   return 0;
 }

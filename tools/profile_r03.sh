@@ -1,4 +1,4 @@
-# round-2 profiles: C2 bench + rocprofv3 kernel trace/stats of the same command, FETCH/WRITE
+# round-3 profiles: C2 bench + rocprofv3 kernel trace/stats of the same command, FETCH/WRITE
 # PMC passes on a shorter window; a C3 (layered network) trace.  Each GPU step time-limited.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
