@@ -462,7 +462,7 @@ def main():
         if net["launches_timed"]:
             per_launch = timed_evals / net["launches_timed"]
             achieved = per_launch * flops_per_eval / (net["avg_us"] * 1e-6) / 1e12
-            fused = args.precision == "fast" and cfg["arch"] == "b6c96"
+            fused = args.precision in ("fast", "accurate") and cfg["arch"] == "b6c96"
             mfma_factor = 3 if args.precision == "accurate" else 1
             roof_all["network"] = {
                 "kernel": "kNNForward (fused %s forward)" % cfg["arch"] if fused else
@@ -518,7 +518,8 @@ def main():
                                                    if (games, visits) != (cfg["games"], cfg["visits"]) else ""),
                        "config": args.config, "games_per_gpu": games, "visits": visits, "arch": cfg["arch"],
                        "board": "%dx%d win %d" % (X, Y, W), "precision": args.precision,
-                       "network_path": "fused" if args.precision == "fast" and cfg["arch"] == "b6c96" else "layered",
+                       "network_path": "fused" if args.precision in ("fast", "accurate") and cfg["arch"] == "b6c96"
+                       else "layered",
                        "rounds_per_step": rps, "window": window, "game_rounds_estimate": game_rounds,
                        "warmup_rounds": warm_rounds, "commit_interval": args.commit_interval,
                        "nn_cache_log2": args.nn_cache_log2, "nn_batch_cap": args.nn_batch_cap or "engine default",

@@ -104,8 +104,9 @@ int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_n
  *   COFFEE_NN_FAST          fp16 MFMA operands, f32 accumulation and residual trunk
  *                           (the fused single-launch kernel where it covers the net,
  *                           b6c96 @ 5x5; the layered kernels otherwise)
- *   COFFEE_NN_ACCURATE      fp16 hi/lo operand pairs on three MFMAs (layered kernels):
- *                           logits within 1e-3 of the fp32 (Eigen-semantics) forward
+ *   COFFEE_NN_ACCURATE      fp16 hi/lo operand pairs on three MFMAs (the fused kernel's
+ *                           split instance where it covers the net, the layered kernels
+ *                           otherwise): logits within 1e-3 of the fp32 (Eigen-semantics) forward
  *   COFFEE_NN_FAST_LAYERED  fp16 operands on the layered kernels (any architecture) */
 #define COFFEE_NN_FAST 0
 #define COFFEE_NN_ACCURATE 1

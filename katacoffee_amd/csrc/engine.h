@@ -93,7 +93,8 @@ class NNLayered {
 // Network precision / path (coffee_nn_create2, coffee_selfplay_config.nn_precision)
 enum NNPath : int {
   NN_FAST = 0,          // fp16 operands, f32 accumulation and trunk: fused kernel when it covers the net
-  NN_ACCURATE = 1,      // fp16 hi/lo operand pairs (layered path): logits within 1e-3 of fp32 for any net
+  NN_ACCURATE = 1,      // fp16 hi/lo operand pairs (fused kernel when it covers the net, else layered):
+                        // logits within 1e-3 of fp32 for any net
   NN_FAST_LAYERED = 2,  // fp16 operands on the layered path (comparison / any architecture)
 };
 
@@ -128,6 +129,8 @@ class NNEngine {
   NNLayout* layoutDev_ = nullptr;
   uint16_t* tabDev_ = nullptr;   // device row tables (nn.hip rowTables), 8 boards per workgroup
   uint16_t* tabDev4_ = nullptr;  // the same for 4 boards per workgroup
+  uint16_t* tabDevS_ = nullptr;  // the same for the split-precision instance (2 boards per workgroup)
+  bool split_ = false;           // NN_ACCURATE on the fused kernel: fp16 hi/lo operand pairs
   int small_ = 0;                // KATACOFFEE_NN_SMALL=8: small batches on the 8-board instance (A/B runs)
   float* trunk_ = nullptr;       // f32 residual trunk scratch, [workgroup][fragment] (nn.hip)
   size_t trunkBytes_ = 0;        // its size

@@ -37,7 +37,7 @@ namespace kc {
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int NW_ = 8>
+template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int SPLIT_ = 0>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
   // boards per workgroup: 8, or 4 for batches of at most 4 per CU; one 8-wave
@@ -46,8 +46,13 @@ struct NNGeo {
   // 4 boards on 4 waves with one wave per SIMD cuts the LDS reads per MFMA by 30 % but
   // exposes every LDS and barrier latency: both slower)
   static constexpr int NB = NB_;
-  static constexpr int NW = NW_, NT = NW_ * 64;  // waves / threads per workgroup
-  static_assert(NW_ == 8, "8-wave workgroups");
+  static constexpr int NW = 8, NT = NW * 64;  // waves / threads per workgroup
+  // SPLIT ("accurate" precision, as the layered kernels): every conv operand is an fp16
+  // pair hi + lo (lo = fp16(x - hi)) and each product hi*hi + lo*hi + hi*lo on three
+  // MFMAs; activations carry a second (lo) LDS plane, weight taps a lo block after the
+  // hi one.  2 boards per workgroup so the planes and the ring fit the 160 KiB.
+  static constexpr bool SPLIT = SPLIT_ != 0;
+  static constexpr int PLANES = SPLIT ? 2 : 1;
   // weight ring slots: tap k+2 is requested at the start of tap k
   static constexpr int RING = 3;
   static constexpr int ROWS = NB * A;
@@ -69,7 +74,8 @@ struct NNGeo {
   static constexpr int NCT = C / 32;     // 16-col tiles per wave
   static constexpr int NCT_ALL = C / 16;
   static constexpr int P = 4 * A;
-  static constexpr int ACT_BYTES = (PROWS * ROWB + 15) / 16 * 16;
+  static constexpr int PLANE_BYTES = (PROWS * ROWB + 15) / 16 * 16;  // one fp16 plane (hi or lo)
+  static constexpr int ACT_BYTES = PLANES * PLANE_BYTES;
   // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
   // (at least the gpool linear weights' [96][64] f32, staged below it, for 4 boards)
@@ -77,7 +83,8 @@ struct NNGeo {
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
-  static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap (one slot)
+  static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap and plane
+  static constexpr int WSLOT = PLANES * WBUF;           // one ring slot
   // row tables (u16): rowPa[MROWS], rowBP[MROWS], bpRow[ROWS] -- built on the host
   static constexpr int NTAB = 2 * MROWS + ROWS;
   static constexpr int OFF_TAB = OFF_VH + NB * 64 * 4;
@@ -85,12 +92,13 @@ struct NNGeo {
   static constexpr int NPRM = 448;
   static constexpr int OFF_PRM = (OFF_TAB + NTAB * 2 + 15) / 16 * 16;
   static constexpr int OFF_W = OFF_PRM + 2 * NPRM * 4;
-  static constexpr int LDS = OFF_W + RING * WBUF * 16;
+  static constexpr int LDS = OFF_W + RING * WSLOT * 16;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
   static_assert(OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
   static_assert(96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
-  static_assert(RING * WBUF * 16 >= (32 + 64) * 96 * 4, "head linear weights must fit in the ring");
-  static_assert(2 * PA * ROWB + 2 * 64 < 65536, "A-read offsets must fit the ds_read immediate");
+  static_assert(RING * WSLOT * 16 >= (32 + 64) * 96 * 4, "head linear weights must fit in the ring");
+  static_assert((PLANES - 1) * PLANE_BYTES + 2 * PA * ROWB + 2 * 64 < 65536,
+                "A-read offsets must fit the ds_read immediate");
   static_assert(LDS <= 163840, "LDS budget");
 };
 
@@ -158,16 +166,6 @@ KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, 
     glds16(src + c * 64 + lane, slotAddr + c * 1024);
 }
 
-// Pieces [q0, q1) of this wave's share of a tap (piece c = wave + q * NW).
-template <int NW>
-KC_D void stageTapPieces(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, int wave, int lane, int q0, int q1) {
-  for(int q = q0; q < q1; q++) {
-    const int c = wave + q * NW;
-    if(c < ch)
-      glds16(src + c * 64 + lane, slotAddr + c * 1024);
-  }
-}
-
 template <int N>
 KC_D void waitVm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -199,14 +197,10 @@ template <class G, int NTAPS, int NCB, int DBG = 0>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                     f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid,
                     const h16x8* __restrict__ wNext, int chNext, int nextTaps) {
-  constexpr int CH = NCB * G::NCT_ALL;  // 1-KiB pieces per tap
-  constexpr int UNITS = CH * 64;        // 16-B fragments per tap
+  constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap and plane
+  constexpr int CH = CHP * G::PLANES;    // 1-KiB pieces per tap (the lo block after the hi one)
+  constexpr int UNITS = CH * 64;         // 16-B fragments per tap
   constexpr int STEPS = NTAPS * NCB;
-#ifdef KC_NN_NOSPREAD
-  constexpr bool SPREAD = false;  // A/B builds only (Makefile `alt`)
-#else
-  constexpr bool SPREAD = G::MAXT * G::NCT <= 6;
-#endif
   const int wave = tid >> 6;
   const uint32_t ring = ldsAddr(wl);
   auto slotOf = [](int tap) { return tap % 3; };
@@ -217,75 +211,50 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   const char* actB = reinterpret_cast<const char*>(act);
   const h16x8* wlane = wl + (cg * G::NCT) * 64 + lane;
   h16x8 af[2][G::MAXT], bf[2][G::NCT];
+  h16x8 afl[G::SPLIT ? 2 : 1][G::MAXT], bfl[G::SPLIT ? 2 : 1][G::NCT];  // lo planes (SPLIT)
   auto loadStep = [&](int st, int buf) {
     const int tap = st / NCB, cb = st - tap * NCB;
     const int tb = NTAPS == 9 ? tap : 4;  // 1x1: the centre tap
     const int aoff = ((tb / 3) * G::PX + tb % 3) * G::ROWB + cb * 64;
-    const h16x8* wb = wlane + slotOf(tap) * G::WBUF + cb * G::NCT_ALL * 64;
+    const h16x8* wb = wlane + slotOf(tap) * G::WSLOT + cb * G::NCT_ALL * 64;
 #pragma unroll
-    for(int ct = 0; ct < G::NCT; ct++)
+    for(int ct = 0; ct < G::NCT; ct++) {
       bf[buf][ct] = wb[ct * 64];
+      if constexpr(G::SPLIT)
+        bfl[buf][ct] = wb[CHP * 64 + ct * 64];
+    }
 #pragma unroll
-    for(int t = 0; t < G::MAXT; t++)
+    for(int t = 0; t < G::MAXT; t++) {
       af[buf][t] = *reinterpret_cast<const h16x8*>(actB + ab[t] + aoff);
+      if constexpr(G::SPLIT)
+        afl[buf][t] = *reinterpret_cast<const h16x8*>(actB + G::PLANE_BYTES + ab[t] + aoff);
+    }
   };
   loadStep(0, 0);
 #pragma unroll
   for(int tap = 0; tap < NTAPS; tap++) {
-    // the stream's request at this tap: tap+2 of this conv, or the next conv's tap 0 / 1
-    if(!SPREAD) {
-      if(DBG & 1) {
-      } else if(tap + 2 < NTAPS)
-        stageTapDma<G::NW>(w + (size_t)(tap + 2) * UNITS, ring + slotOf(tap + 2) * G::WBUF * 16, CH, wave, lane);
-      else if(NTAPS == 9 && tap == 7)
-        stageTapDma<G::NW>(wNext, ring, chNext, wave, lane);
-      else if(NTAPS == 9 && tap == 8 && nextTaps > 1)
-        stageTapDma<G::NW>(wNext + chNext * 64, ring + G::WBUF * 16, chNext, wave, lane);
-    }
-    const h16x8* rq = nullptr;
-    uint32_t rqSlot = 0;
-    int rqCh = 0;
-    if(!SPREAD || (DBG & 1)) {
-    } else if(tap + 2 < NTAPS) {
-      rq = w + (size_t)(tap + 2) * UNITS;
-      rqSlot = ring + slotOf(tap + 2) * G::WBUF * 16;
-      rqCh = CH;
-    } else if(NTAPS == 9 && tap == 7) {
-      rq = wNext;
-      rqSlot = ring;
-      rqCh = chNext;
-    } else if(NTAPS == 9 && tap == 8 && nextTaps > 1) {
-      rq = wNext + chNext * 64;
-      rqSlot = ring + G::WBUF * 16;
-      rqCh = chNext;
-    }
-    // 4-board instance: a wave's (at most 3) pieces of it spread one per K-step, the
-    // rest at the last, so the 8 waves' LDS-DMA issue does not bunch up behind the
-    // barrier (conv 9.3 k -> 8.0 k cycles); the 8-board instance, at its register
-    // budget, issues them at once (spreading keeps the request live across the
-    // K-steps: more spills)
-    const int rqPer = (rqCh + G::NW - 1) / G::NW;
+    // request stream tap tap+2 (this conv's, or the next conv's tap 0 / 1)
+    if(DBG & 1) {
+    } else if(tap + 2 < NTAPS)
+      stageTapDma<G::NW>(w + (size_t)(tap + 2) * UNITS, ring + slotOf(tap + 2) * G::WSLOT * 16, CH, wave, lane);
+    else if(NTAPS == 9 && tap == 7)
+      stageTapDma<G::NW>(wNext, ring, chNext, wave, lane);
+    else if(NTAPS == 9 && tap == 8 && nextTaps > 1)
+      stageTapDma<G::NW>(wNext + chNext * 64, ring + G::WSLOT * 16, chNext, wave, lane);
 #pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
       const int st = tap * NCB + cb;
-      if(SPREAD && rq && cb < NCB - 1)
-        stageTapPieces<G::NW>(rq, rqSlot, rqCh, wave, lane, cb, cb + 1);
       if(cb == NCB - 1 && tap + 1 < NTAPS) {
-        // retire this wave's pieces of tap+1: only the pieces of this tap's request
-        // issued before this point may stay in flight (every wave has issued at least
-        // min(pieces per wave, NCB - 1) of them when spread, all of them otherwise),
-        // then publish them / free slot tap%3
-        constexpr int INF_TAP = CH / G::NW, INF_NEXT = (2 * G::NCT_ALL) / G::NW;  // next conv: >= 12 pieces
+        // retire this wave's pieces of tap+1 (only the tap+2 request, >= N pieces per
+        // wave, may stay in flight), then publish them / free slot tap%3
         if(DBG & 8) {
         } else if(tap + 2 < NTAPS)
-          waitVm<(SPREAD && INF_TAP > NCB - 1 ? NCB - 1 : INF_TAP)>();
+          waitVm<CH / G::NW>();
         else
-          waitVm<(SPREAD && INF_NEXT > NCB - 1 ? NCB - 1 : INF_NEXT)>();
+          waitVm<(2 * G::NCT_ALL * G::PLANES) / G::NW>();  // next conv's tap 0: at least 12 pieces per plane
         if(!(DBG & 2))
           barrierKeepDma();
       }
-      if(SPREAD && rq && cb == NCB - 1)
-        stageTapPieces<G::NW>(rq, rqSlot, rqCh, wave, lane, NCB - 1, rqPer);
       if(st + 1 < STEPS)
         loadStep(st + 1, (st + 1) & 1);
       // keep the next step's LDS reads ahead of this step's MFMAs (the scheduler
@@ -296,6 +265,19 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++)
           acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[st & 1][ct], af[st & 1][t], acc[t][ct], 0, 0, 0);
+      if constexpr(G::SPLIT) {
+        // + lo(w) * hi(x), then + hi(w) * lo(x) (the layered kernels' order)
+#pragma unroll
+        for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+          for(int ct = 0; ct < G::NCT; ct++)
+            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfl[st & 1][ct], af[st & 1][t], acc[t][ct], 0, 0, 0);
+#pragma unroll
+        for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+          for(int ct = 0; ct < G::NCT; ct++)
+            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[st & 1][ct], afl[st & 1][t], acc[t][ct], 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -383,6 +365,18 @@ KC_D int chOf(int cg, int ct, int lane) {
 KC_D uint2 packH4(float a, float b, float c, float d) {
   return uint2{(uint32_t)f16bits(a) | ((uint32_t)f16bits(b) << 16), (uint32_t)f16bits(c) | ((uint32_t)f16bits(d) << 16)};
 }
+// lo = fp16(x - f32(fp16(x))) of four values (SPLIT activations' second plane)
+KC_D uint2 packH4lo(float a, float b, float c, float d) {
+  auto lo = [](float x) { return x - (float)(_Float16)x; };
+  return packH4(lo(a), lo(b), lo(c), lo(d));
+}
+// Four activated channels of one row into act: the hi plane, and the lo plane (SPLIT).
+template <class G>
+KC_D void storeAct4(uint16_t* act, int row, int ch, float y0, float y1, float y2, float y3) {
+  *reinterpret_cast<uint2*>(act + row * G::ASTR + ch) = packH4(y0, y1, y2, y3);
+  if constexpr(G::SPLIT)
+    *reinterpret_cast<uint2*>(act + G::PLANE_BYTES / 2 + row * G::ASTR + ch) = packH4lo(y0, y1, y2, y3);
+}
 
 // act[pad(row)][ch..ch+3] = f16(relu(v * s[ch] + b[ch])) for on-board rows, all channels.
 template <class G, class V>
@@ -400,14 +394,13 @@ KC_D void storeBnRelu(uint16_t* act, const uint16_t* rowPa, const V (&v)[G::MAXT
     const int row = (tstart + t) * 16 + (lane & 15);
     if(row >= G::ROWS)
       continue;
-    uint16_t* dst = act + (int)rowPa[row] * G::ASTR;
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++) {
       const float y0 = fmaxf((float)v[t][ct][0] * sc[ct].x + bi[ct].x, 0.0f);
       const float y1 = fmaxf((float)v[t][ct][1] * sc[ct].y + bi[ct].y, 0.0f);
       const float y2 = fmaxf((float)v[t][ct][2] * sc[ct].z + bi[ct].z, 0.0f);
       const float y3 = fmaxf((float)v[t][ct][3] * sc[ct].w + bi[ct].w, 0.0f);
-      *reinterpret_cast<uint2*>(dst + chOf<G>(cg, ct, lane)) = packH4(y0, y1, y2, y3);
+      storeAct4<G>(act, (int)rowPa[row], chOf<G>(cg, ct, lane), y0, y1, y2, y3);
     }
   }
 }
@@ -431,7 +424,9 @@ KC_D void zeroBorders(uint16_t* act, int tid) {
       const int m = k - 2 * G::PX;
       cell = (1 + (m >> 1)) * G::PX + ((m & 1) ? G::PX - 1 : 0);
     }
-    reinterpret_cast<uint4*>(act + (b * G::PA + cell) * G::ASTR)[c] = uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for(int pl = 0; pl < G::PLANES; pl++)
+      reinterpret_cast<uint4*>(act + pl * (G::PLANE_BYTES / 2) + (b * G::PA + cell) * G::ASTR)[c] = uint4{0u, 0u, 0u, 0u};
   }
 }
 
@@ -538,13 +533,13 @@ KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ W
   return src >= 0 ? WF[src] : 0.0f;
 }
 
-template <int X, int Y, int C, int NB, int NW>
-__global__ void __launch_bounds__(NW * 64, 2)
+template <int X, int Y, int C, int NB, int SPLIT>
+__global__ void __launch_bounds__(512, 2)
     kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
                const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
                const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
                float* __restrict__ out, float* __restrict__ trunk) {
-  using G = NNGeo<X, Y, C, NB, NW>;
+  using G = NNGeo<X, Y, C, NB, SPLIT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
   const int count = countDev ? min(*countDev, n) : n;
@@ -571,11 +566,11 @@ __global__ void __launch_bounds__(NW * 64, 2)
   // the stem's first weight taps (as many as the ring prefetches) stream into the ring
   // while the input is unpacked
   {
-    constexpr int CH0 = G::NCT_ALL;  // 1-KiB pieces per stem tap (one 32-channel block)
+    constexpr int CH0 = G::NCT_ALL * G::PLANES;  // 1-KiB pieces per stem tap (one 32-channel block)
     const uint32_t ring = ldsAddr(wl);
 #pragma unroll
     for(int tap = 0; tap < G::RING - 1; tap++)
-      stageTapDma<G::NW>(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WBUF * 16, CH0, wave, lane);
+      stageTapDma<G::NW>(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WSLOT * 16, CH0, wave, lane);
   }
   // ---- row tables; unpack the packed V1 planes into the zero-bordered act ----
   constexpr int NPK = (G::NPRM + G::NT - 1) / G::NT;  // parameter-slab elements per thread
@@ -619,7 +614,8 @@ __global__ void __launch_bounds__(NW * 64, 2)
   f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
   convTiles<G, 9, 1>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
-                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL, L->nblocks > 0 ? 9 : 1);
+                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
+                        L->nblocks > 0 ? 9 : 1);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
 #pragma unroll
@@ -656,7 +652,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
       pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
     convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
-                                  (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL, 9);
+                                  (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, 9);
 #pragma unroll
     for(int j = 0; j < NPK; j++)
       if(tid + j * G::NT < G::NPRM)
@@ -679,7 +675,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
       convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                    3 * G::NCT_ALL, nextTaps);
+                                    3 * G::NCT_ALL * G::PLANES, nextTaps);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
     } else {
@@ -752,11 +748,10 @@ __global__ void __launch_bounds__(NW * 64, 2)
             if(row >= G::ROWS)
               continue;
             const float4 gb = *reinterpret_cast<const float4*>(biasS + ((int)rowBP[row] / G::A) * Cr + ch);
-            *reinterpret_cast<uint2*>(act + (int)rowPa[row] * G::ASTR + ch) =
-                packH4(fmaxf((acc[t][ct][0] + gb.x) * sc.x + bi.x, 0.0f),
-                       fmaxf((acc[t][ct][1] + gb.y) * sc.y + bi.y, 0.0f),
-                       fmaxf((acc[t][ct][2] + gb.z) * sc.z + bi.z, 0.0f),
-                       fmaxf((acc[t][ct][3] + gb.w) * sc.w + bi.w, 0.0f));
+            storeAct4<G>(act, (int)rowPa[row], ch, fmaxf((acc[t][ct][0] + gb.x) * sc.x + bi.x, 0.0f),
+                         fmaxf((acc[t][ct][1] + gb.y) * sc.y + bi.y, 0.0f),
+                         fmaxf((acc[t][ct][2] + gb.z) * sc.z + bi.z, 0.0f),
+                         fmaxf((acc[t][ct][3] + gb.w) * sc.w + bi.w, 0.0f));
           }
         }
       }
@@ -768,7 +763,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
       convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                           3 * G::NCT_ALL, nextTaps);
+                                           3 * G::NCT_ALL * G::PLANES, nextTaps);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
     }
@@ -925,17 +920,42 @@ static uint16_t f2h(float f) {
 
 // B fragment order for one conv: [kstep = tap*NCB + cb][coltile][lane][8],
 // element = W(co = ct*16 + (lane&15), cin = cb*32 + 8*(lane>>4) + j, tap).
+// IEEE binary16 bits -> float (exact).
+static float h2f(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  float f;
+  if(e == 0) {
+    f = ldexpf((float)m, -24);
+  } else if(e == 31) {
+    const uint32_t u = 0x7f800000u | (m << 13);
+    memcpy(&f, &u, 4);
+  } else {
+    const uint32_t u = ((e + 112u) << 23) | (m << 13);
+    memcpy(&f, &u, 4);
+  }
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  u |= sign;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// split: after each tap's hi fragments the same fragments of lo = fp16(w - hi)
+// (convTiles' SPLIT ring slot layout).
 static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout,
-                     const std::function<float(int, int, int)>& W) {
+                     const std::function<float(int, int, int)>& W, bool split = false) {
   const int ncb = cinPad / 32, nct = cout / 16;
   for(int tap = 0; tap < ntaps; tap++)
-    for(int cb = 0; cb < ncb; cb++)
-      for(int ct = 0; ct < nct; ct++)
-        for(int l = 0; l < 64; l++)
-          for(int j = 0; j < 8; j++) {
-            int co = ct * 16 + (l & 15), ci = cb * 32 + 8 * (l >> 4) + j;
-            dst.push_back(f2h(W(co, ci, tap)));
-          }
+    for(int part = 0; part < (split ? 2 : 1); part++)
+      for(int cb = 0; cb < ncb; cb++)
+        for(int ct = 0; ct < nct; ct++)
+          for(int l = 0; l < 64; l++)
+            for(int j = 0; j < 8; j++) {
+              const int co = ct * 16 + (l & 15), ci = cb * 32 + 8 * (l >> 4) + j;
+              const float w = W(co, ci, tap);
+              const uint16_t hi = f2h(w);
+              dst.push_back(part == 0 ? hi : f2h(w - h2f(hi)));
+            }
 }
 
 // Output-row order of a workgroup's NB boards: row r takes a cell whose padded
@@ -984,10 +1004,11 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   flops_ = modelFlopsPerEval(cfg_, X * Y);
   if(path != NN_FAST && path != NN_ACCURATE && path != NN_FAST_LAYERED)
     throw std::invalid_argument("NNEngine: unknown precision/path");
-  if(path != NN_FAST || !fusedSupported(m.cfg, X, Y)) {
+  if(path == NN_FAST_LAYERED || !fusedSupported(m.cfg, X, Y)) {
     layered_.reset(new NNLayered(m, X, Y, W, path == NN_ACCURATE));
     return;
   }
+  split_ = path == NN_ACCURATE;  // the fused kernel's SPLIT instance (2 boards per workgroup)
   const int C = cfg_.C, Cr = C - cfg_.Cg;
   std::vector<uint16_t> wb;
   std::vector<float> wf;
@@ -1015,7 +1036,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   L.wInit = bfOff();
   packConv(wb, 9, 32, C, [&](int co, int ci, int tap) {
     return ci < cfg_.cin ? m.convInit[((size_t)co * cfg_.cin + ci) * 9 + tap] : 0.0f;
-  });
+  }, split_);
   L.globInit = f32(m.globInit);
   for(int i = 0; i < L.nblocks; i++) {
     const ModelBlock& b = m.blocks[i];
@@ -1024,22 +1045,23 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
     L.bn1b[i] = f32(b.bn1b);
     L.wConv1[i] = bfOff();
     if(b.kind == 0) {
-      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv1[((size_t)co * C + ci) * 9 + tap]; });
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv1[((size_t)co * C + ci) * 9 + tap]; }, split_);
       L.bn2s[i] = f32(b.bn2s);
       L.bn2b[i] = f32(b.bn2b);
       L.wConv2[i] = bfOff();
-      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * C + ci) * 9 + tap]; });
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * C + ci) * 9 + tap]; }, split_);
     } else {
       packConv(wb, 9, C, C, [&](int co, int ci, int tap) {
         return co < Cr ? b.conv1[((size_t)co * C + ci) * 9 + tap] : b.conv1g[((size_t)(co - Cr) * C + ci) * 9 + tap];
-      });
+      }, split_);
       L.bngs[i] = f32(b.bngs);
       L.bngb[i] = f32(b.bngb);
       L.linG[i] = f32T(b.linG, Cr);
       L.bn2s[i] = f32(b.bn2s);
       L.bn2b[i] = f32(b.bn2b);
       L.wConv2[i] = bfOff();
-      packConv(wb, 9, Cr, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * Cr + ci) * 9 + tap]; });
+      packConv(wb, 9, Cr, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * Cr + ci) * 9 + tap]; },
+               split_);
     }
   }
   L.tips = f32(m.tips);
@@ -1051,7 +1073,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
     if(co < 64)
       return m.pConvG[(size_t)(co - 32) * C + ci];
     return m.vConv1[(size_t)(co - 64) * C + ci];
-  });
+  }, split_);
   L.pBiasG = f32(m.pBiasG);
   L.pLinG = f32T(m.pLinG, 32);
   L.pBias2 = f32(m.pBias2);
@@ -1069,19 +1091,24 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipMemcpy(wF32_, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&layoutDev_, sizeof(NNLayout)));
   KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
-  using G8 = NNGeo<5, 5, 96, 8, 8>;
-  using G4 = NNGeo<5, 5, 96, 4, 8>;
-  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>();
+  using G8 = NNGeo<5, 5, 96, 8, 0>;
+  using G4 = NNGeo<5, 5, 96, 4, 0>;
+  using GS = NNGeo<5, 5, 96, 2, 1>;
+  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>(), tabS = rowTables<GS>();
   KC_HIP(hipMalloc(&tabDev_, tab8.size() * 2));
   KC_HIP(hipMemcpy(tabDev_, tab8.data(), tab8.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&tabDev4_, tab4.size() * 2));
   KC_HIP(hipMemcpy(tabDev4_, tab4.data(), tab4.size() * 2, hipMemcpyHostToDevice));
+  KC_HIP(hipMalloc(&tabDevS_, tabS.size() * 2));
+  KC_HIP(hipMemcpy(tabDevS_, tabS.data(), tabS.size() * 2, hipMemcpyHostToDevice));
 
   // function attributes are per device: every engine sets it on its own device
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G8::LDS));
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 4, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G4::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             GS::LDS));
   // A/B runs only: KATACOFFEE_NN_SMALL=8 runs small batches on the 8-board instance too
   const char* small = getenv("KATACOFFEE_NN_SMALL");
   small_ = small ? atoi(small) : 0;
@@ -1097,6 +1124,7 @@ NNEngine::~NNEngine() {
   (void)hipFree(layoutDev_);
   (void)hipFree(tabDev_);
   (void)hipFree(tabDev4_);
+  (void)hipFree(tabDevS_);
 
 }
 
@@ -1116,10 +1144,12 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   // A launch costs about one workgroup's latency per wave of workgroups (one per CU):
   // a batch bound that fits 4 boards per CU (e.g. each of two game groups' batches)
   // runs 4 boards per workgroup, half the MFMA work on each workgroup's path.
-  if(n <= 4 * cus_ && small_ != 8)
-    launch<NNGeo<5, 5, 96, 4, 8>>(n, inWords, tabDev4_, in, out, st, countDev, rowIdx, e0, e1);
+  if(split_)  // "accurate": one instance for every batch size (its results never depend on n)
+    launch<NNGeo<5, 5, 96, 2, 1>>(n, inWords, tabDevS_, in, out, st, countDev, rowIdx, e0, e1);
+  else if(n <= 4 * cus_ && small_ != 8)
+    launch<NNGeo<5, 5, 96, 4, 0>>(n, inWords, tabDev4_, in, out, st, countDev, rowIdx, e0, e1);
   else
-    launch<NNGeo<5, 5, 96, 8, 8>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
+    launch<NNGeo<5, 5, 96, 8, 0>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
 }
 
 template <class G>
@@ -1136,7 +1166,7 @@ void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* i
     KC_HIP(hipMalloc(&trunk_, bytes));
     trunkBytes_ = bytes;
   }
-  auto kern = kNNForward<G::X, G::Y, G::C, G::NB, G::NW>;
+  auto kern = kNNForward<G::X, G::Y, G::C, G::NB, G::SPLIT ? 1 : 0>;
   if(e0)
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, e0, e1, 0, layoutDev_, (const h16x8*)wHalf_,
                           wF32_, tab, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);

@@ -2,7 +2,7 @@
 against the CPU oracle (eigenbackend.cpp semantics, oracle/ora_nn.cpp) for every
 BASELINE architecture and board geometry:
 
-  C2  b6c96 @ 5x5        fused kernel and layered kernels
+  C2  b6c96 @ 5x5        fused kernel (fast and split "accurate" instances) and layered kernels
   C3  b10c128 @ 5x5      layered kernels
   C4  b10c128 @ 7x7      layered kernels
   C5  b18c384nbt @ 9x9   layered kernels (nested bottleneck blocks)
@@ -92,7 +92,7 @@ def test_network_vs_oracle(models, arch, X, Y, W, n, precision):
     path = models[arch]
     binp, glob = _boards(n, X, Y, W, seed=n)
     net = kc.Network(path, X, Y, W, precision=precision)
-    assert net.fused == (precision == "fast" and arch == "b6c96")
+    assert net.fused == (precision in ("fast", "accurate") and arch == "b6c96")
     out = net.forward(_pack_u64(binp))
     net.close()
     ref32 = _ref(path, X, Y, binp, glob, 0)

@@ -51,6 +51,7 @@ def test_trained_net_runs_on_device_kernel():
     planes = batch["binp"].numpy().reshape(len(ref), 15, 25)
     packed = _pack_u64(planes)
     acc = kc.Network(path, 5, 5, 4, precision="accurate")
+    assert acc.fused  # the split-precision instance of the fused kernel
     out_acc = acc.forward(packed)
     acc.close()
     fast = kc.Network(path, 5, 5, 4)
