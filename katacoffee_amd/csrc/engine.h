@@ -54,7 +54,7 @@ class NNLayered {
 
  private:
   struct Conv {
-    int kt = 3, cin = 0, cinReal = 0, cout = 0, tn = 3, coutTiles = 0;
+    int kt = 3, cin = 0, cinReal = 0, cout = 0, tn = 3, wn = 2, coutTiles = 0;
     long wOff = 0;  // 16-byte fragments into wHi_/wLo_
   };
   struct Block {

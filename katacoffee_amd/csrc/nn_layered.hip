@@ -44,7 +44,6 @@ typedef _Float16 lh16x4 __attribute__((ext_vector_type(4)));
 typedef float lf32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int L_WAVES = 8, L_NT = L_WAVES * 64;
-constexpr int L_WM = 4, L_WN = 2;  // wave grid: 4 row groups x 2 column groups
 constexpr int L_STRIDE = 40;       // fp16 per staged row: 32 channels + 8 pad (80 B rows)
 
 enum LPro : int { PRO_BITS = 0, PRO_F16 = 1, PRO_BN = 2, PRO_BN_GB = 3 };
@@ -56,7 +55,6 @@ struct LGeo {
   static constexpr int BPW = 256 / A < 1 ? 1 : 256 / A;  // boards per workgroup
   static constexpr int ROWS = BPW * A;
   static constexpr int RT = (ROWS + 15) / 16;
-  static constexpr int TM = (RT + L_WM - 1) / L_WM;  // row tiles per wave
   static constexpr int PX = X + 2, PY = Y + 2, PA = PX * PY;
   static constexpr int PROWS = BPW * PA;
   static constexpr int STAGE = PROWS * L_STRIDE * 2;  // bytes per staged 32-channel slice
@@ -201,13 +199,13 @@ KC_D void stageStore(const LConvArgs& a, const StageRegs<G>& R, char* stHi, char
 
 // Epilogue shared by the conv kernels: lane holds channels ch..ch+3 of row
 // (lane & 15) of each of its tiles.
-template <class G, int TN>
-KC_D void convEpilogue(const LConvArgs& a, const lf32x4 (&acc)[G::TM][TN], int base, int nb, int wm, int ctBase,
+template <class G, int TM, int TN>
+KC_D void convEpilogue(const LConvArgs& a, const lf32x4 (&acc)[TM][TN], int base, int nb, int wm, int ctBase,
                        int lane) {
   const int rowsValid = nb * G::A;
 #pragma unroll
-  for(int t = 0; t < G::TM; t++) {
-    const int r = (wm * G::TM + t) * 16 + (lane & 15);
+  for(int t = 0; t < TM; t++) {
+    const int r = (wm * TM + t) * 16 + (lane & 15);
     if(r >= rowsValid)
       continue;
     const size_t g = (size_t)base * G::A + r;
@@ -240,11 +238,12 @@ KC_D void convEpilogue(const LConvArgs& a, const lf32x4 (&acc)[G::TM][TN], int b
   }
 }
 
-template <int X, int Y, int KT, int TN, bool SPLIT>
+template <int X, int Y, int KT, int TN, bool SPLIT, int WN>
 __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   using G = LGeo<X, Y>;
   constexpr int T = KT * KT;
-  constexpr int NCT = TN * L_WN;  // column tiles per workgroup
+  constexpr int WM = L_WAVES / WN, TM = (G::RT + WM - 1) / WM;  // wave grid WM x WN, row tiles per wave
+  constexpr int NCT = TN * WN;                                   // column tiles per workgroup
   constexpr int PLANES = SPLIT ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int count = a.countDev ? min(*a.countDev, a.n) : a.n;
@@ -253,7 +252,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     return;
   const int nb = min(G::BPW, count - base);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int ctBase = blockIdx.y * NCT + wn * TN;  // this wave's first global column tile
   char* stage = smem;                                        // [2][PLANES][STAGE]
   float* sS = reinterpret_cast<float*>(smem + 2 * PLANES * G::STAGE);  // [cin]
@@ -277,10 +276,10 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   stageStore<G, SPLIT>(a, sr, stage, stage + G::STAGE, 0, base, nb, sS, sB, sG, tid);
 
   // per-lane A row bases (bytes, shifted to the (-r,-r) neighbour), padding rows -> row 0
-  int ab[G::TM];
+  int ab[TM];
 #pragma unroll
-  for(int t = 0; t < G::TM; t++) {
-    int r = (wm * G::TM + t) * 16 + (lane & 15);
+  for(int t = 0; t < TM; t++) {
+    int r = (wm * TM + t) * 16 + (lane & 15);
     if(r >= G::ROWS)
       r = 0;
     const int brd = r / G::A, p = r - brd * G::A;
@@ -288,9 +287,9 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     const int shift = KT == 3 ? G::PX + 1 : 0;
     ab[t] = ((pr - shift) * L_STRIDE) * 2 + 16 * (lane >> 4);
   }
-  lf32x4 acc[G::TM][TN];
+  lf32x4 acc[TM][TN];
 #pragma unroll
-  for(int t = 0; t < G::TM; t++)
+  for(int t = 0; t < TM; t++)
 #pragma unroll
     for(int c = 0; c < TN; c++)
       acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -324,15 +323,15 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
       loadB(s + R - 1, (slot + R - 1) % R);
     const int dy = KT == 3 ? tap / 3 : 0, dx = KT == 3 ? tap % 3 : 0;
     const int aoff = (dy * G::PX + dx) * L_STRIDE * 2;
-    lh16x8 ah[G::TM], al[SPLIT ? G::TM : 1];
+    lh16x8 ah[TM], al[SPLIT ? TM : 1];
 #pragma unroll
-    for(int t = 0; t < G::TM; t++) {
+    for(int t = 0; t < TM; t++) {
       ah[t] = *reinterpret_cast<const lh16x8*>(stHi + ab[t] + aoff);
       if constexpr(SPLIT)
         al[t] = *reinterpret_cast<const lh16x8*>(stLo + ab[t] + aoff);
     }
 #pragma unroll
-    for(int t = 0; t < G::TM; t++)
+    for(int t = 0; t < TM; t++)
 #pragma unroll
       for(int c = 0; c < TN; c++) {
         acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[slot][c], ah[t], acc[t][c], 0, 0, 0);
@@ -370,7 +369,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   if(cb < NCB)
     slice(cb, 0);
 
-  convEpilogue<G, TN>(a, acc, base, nb, wm, ctBase, lane);
+  convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
 }
 
 // 1x1 convolutions (bottleneck in / out, heads): no halo, so a stage holds 128
@@ -386,10 +385,11 @@ constexpr int l1StageBytes() {
   return G::ROWS * L1_STRIDE * 2;
 }
 
-template <int X, int Y, int TN, bool SPLIT>
+template <int X, int Y, int TN, bool SPLIT, int WN>
 __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
   using G = LGeo<X, Y>;
-  constexpr int NCT = TN * L_WN;
+  constexpr int WM = L_WAVES / WN, TM = (G::RT + WM - 1) / WM;
+  constexpr int NCT = TN * WN;
   constexpr int SB = l1StageBytes<G>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int count = a.countDev ? min(*a.countDev, a.n) : a.n;
@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
     return;
   const int nb = min(G::BPW, count - base);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int ctBase = blockIdx.y * NCT + wn * TN;
   char* stHi = smem;
   char* stLo = smem + SB;
@@ -408,17 +408,17 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
     sS[i] = i < a.cinReal ? a.ps[i] : 0.0f;
     sB[i] = i < a.cinReal ? a.pb[i] : 0.0f;
   }
-  int ab[G::TM];
+  int ab[TM];
 #pragma unroll
-  for(int t = 0; t < G::TM; t++) {
-    int r = (wm * G::TM + t) * 16 + (lane & 15);
+  for(int t = 0; t < TM; t++) {
+    int r = (wm * TM + t) * 16 + (lane & 15);
     if(r >= G::ROWS)
       r = 0;
     ab[t] = r * L1_STRIDE * 2 + 16 * (lane >> 4);
   }
-  lf32x4 acc[G::TM][TN];
+  lf32x4 acc[TM][TN];
 #pragma unroll
-  for(int t = 0; t < G::TM; t++)
+  for(int t = 0; t < TM; t++)
 #pragma unroll
     for(int c = 0; c < TN; c++)
       acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -495,15 +495,15 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
         break;
       if(s + 1 < NCB)
         loadB(s + 1, (j + 1) & 1);
-      lh16x8 ah[G::TM], al[SPLIT ? G::TM : 1];
+      lh16x8 ah[TM], al[SPLIT ? TM : 1];
 #pragma unroll
-      for(int t = 0; t < G::TM; t++) {
+      for(int t = 0; t < TM; t++) {
         ah[t] = *reinterpret_cast<const lh16x8*>(stHi + ab[t] + 64 * j);
         if constexpr(SPLIT)
           al[t] = *reinterpret_cast<const lh16x8*>(stLo + ab[t] + 64 * j);
       }
 #pragma unroll
-      for(int t = 0; t < G::TM; t++)
+      for(int t = 0; t < TM; t++)
 #pragma unroll
         for(int c = 0; c < TN; c++) {
           acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j & 1][c], ah[t], acc[t][c], 0, 0, 0);
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
         }
     }
   }
-  convEpilogue<G, TN>(a, acc, base, nb, wm, ctBase, lane);
+  convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
 }
 
 // Gpool branch of a gpool block: g = relu(T[:, Cr:Cr+Cg] * s + b), KataGPool
@@ -666,7 +666,7 @@ uint16_t lf2h(float f) {
   return u;
 }
 
-template <int X, int Y, int KT, int TN, bool SPLIT>
+template <int X, int Y, int KT, int TN, bool SPLIT, int WN>
 void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
   using G = LGeo<X, Y>;
   size_t lds;
@@ -675,10 +675,10 @@ void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
     if(a.pro != PRO_BN)
       throw std::invalid_argument("1x1 convolutions take a BN-ReLU prologue");
     lds = (SPLIT ? 2 : 1) * l1StageBytes<G>() + 2 * (size_t)a.cin * 4;
-    fnp = (const void*)kConv1L<X, Y, TN, SPLIT>;
+    fnp = (const void*)kConv1L<X, Y, TN, SPLIT, WN>;
   } else {
     lds = 2 * (SPLIT ? 2 : 1) * G::STAGE + (2 * a.cin + G::BPW * (a.gbLd > 0 ? a.gbLd : 0)) * 4;
-    fnp = (const void*)kConvL<X, Y, KT, TN, SPLIT>;
+    fnp = (const void*)kConvL<X, Y, KT, TN, SPLIT, WN>;
   }
   if(lds > 160 * 1024)
     throw std::invalid_argument("layered conv: LDS budget exceeded");
@@ -693,24 +693,34 @@ void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
       done.insert(dev);
     }
   }
-  const int gy = (a.coutTiles + TN * L_WN - 1) / (TN * L_WN);
+  const int gy = (a.coutTiles + TN * WN - 1) / (TN * WN);
   if constexpr(KT == 1)
-    hipLaunchKernelGGL((kConv1L<X, Y, TN, SPLIT>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+    hipLaunchKernelGGL((kConv1L<X, Y, TN, SPLIT, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
   else
-    hipLaunchKernelGGL((kConvL<X, Y, KT, TN, SPLIT>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+    hipLaunchKernelGGL((kConvL<X, Y, KT, TN, SPLIT, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
   KC_HIP(hipGetLastError());
 }
 
+// (kt, tn, wn) of a conv -> its instance (chooseGrid).
 template <int X, int Y, bool SPLIT>
-void launchConvG(const LConvArgs& a, int kt, int tn, int grid, hipStream_t st) {
+void launchConvG(const LConvArgs& a, int kt, int tn, int wn, int grid, hipStream_t st) {
+  if constexpr(!SPLIT) {
+    if(wn == 4) {
+      if(kt == 3)
+        tn == 2 ? launchConvT<X, Y, 3, 2, false, 4>(a, grid, st) : launchConvT<X, Y, 3, 3, false, 4>(a, grid, st);
+      else
+        tn == 2 ? launchConvT<X, Y, 1, 2, false, 4>(a, grid, st) : launchConvT<X, Y, 1, 3, false, 4>(a, grid, st);
+      return;
+    }
+  }
   if(kt == 3) {
-    if(tn == 2) launchConvT<X, Y, 3, 2, SPLIT>(a, grid, st);
-    else if(tn == 3) launchConvT<X, Y, 3, 3, SPLIT>(a, grid, st);
-    else launchConvT<X, Y, 3, 4, SPLIT>(a, grid, st);
+    if(tn == 2) launchConvT<X, Y, 3, 2, SPLIT, 2>(a, grid, st);
+    else if(tn == 3) launchConvT<X, Y, 3, 3, SPLIT, 2>(a, grid, st);
+    else launchConvT<X, Y, 3, 4, SPLIT, 2>(a, grid, st);
   } else {
-    if(tn == 2) launchConvT<X, Y, 1, 2, SPLIT>(a, grid, st);
-    else if(tn == 3) launchConvT<X, Y, 1, 3, SPLIT>(a, grid, st);
-    else launchConvT<X, Y, 1, 4, SPLIT>(a, grid, st);
+    if(tn == 2) launchConvT<X, Y, 1, 2, SPLIT, 2>(a, grid, st);
+    else if(tn == 3) launchConvT<X, Y, 1, 3, SPLIT, 2>(a, grid, st);
+    else launchConvT<X, Y, 1, 4, SPLIT, 2>(a, grid, st);
   }
 }
 
@@ -724,12 +734,32 @@ int lBoardsPerWG(int X, int Y) {
 
 bool NNLayered::supportedGeometry(int X, int Y) { return (X == 5 && Y == 5) || (X == 7 && Y == 7) || (X == 9 && Y == 9); }
 
-// Column tiles per wave for a conv with `cout` outputs: the widest of 4/3/2 that
-// tiles the (padded) output channels in 32*TN-wide workgroup columns.
-static int chooseTN(int cout) {
-  if(cout % 128 == 0) return 4;
-  if(cout % 96 == 0) return 3;
-  return 2;
+// Wave grid and column tiles per wave for a conv with `cout` outputs.  Default: the
+// 4 x 2 grid (4 row groups x 2 column groups) with the widest TN of 4/3/2 that tiles
+// the (padded) outputs in 32*TN-wide workgroup columns.  A fast conv whose output
+// tiles then need more column groups (blockIdx.y, each re-staging the whole input)
+// than a 2 x 4 grid with TN 3 or 2 takes that grid instead: 8 row tiles per wave,
+// each B fragment shared by 2 waves instead of 4 -- b18c384nbt's 192-wide convs run
+// in one column group instead of two and its 384-wide 1x1 in two instead of three
+// (9x9 forward 25 % faster); at equal column groups (b10c128) the 4 x 2 grid is faster.
+static void chooseGrid(int cout, bool split, int& tn, int& wn) {
+  const int tiles = (cout + 15) / 16;
+  wn = 2;
+  tn = cout % 128 == 0 ? 4 : cout % 96 == 0 ? 3 : 2;
+  const int gy2 = (tiles + 2 * tn - 1) / (2 * tn);
+#ifndef KC_LAYERED_WN2  // (A/B builds: csrc/Makefile `alt` target, ALT_FLAGS=-DKC_LAYERED_WN2)
+  if(split)
+    return;
+  for(int t : {3, 2})
+    if(tiles % (4 * t) == 0 && tiles / (4 * t) < gy2) {
+      tn = t;
+      wn = 4;
+      return;
+    }
+#else
+  (void)split;
+  (void)gy2;
+#endif
 }
 
 NNLayered::NNLayered(const ModelHost& m, int X, int Y, int W, bool split)
@@ -763,8 +793,8 @@ NNLayered::NNLayered(const ModelHost& m, int X, int Y, int W, bool split)
     c.cinReal = cin;
     c.cin = (cin + 31) / 32 * 32;
     c.cout = cout;
-    c.tn = chooseTN(cout);
-    const int ncw = 32 * c.tn;
+    chooseGrid(cout, split_, c.tn, c.wn);
+    const int ncw = 16 * c.tn * c.wn;
     c.coutTiles = (cout + ncw - 1) / ncw * ncw / 16;
     c.wOff = (long)(wh.size() / 8);
     const int taps = kt * kt;
@@ -941,11 +971,14 @@ void NNLayered::conv(const Conv& c, int pro, const void* src, int srcLd, int src
   const int grid = (n + bpw - 1) / bpw;
   const bool sp = split_;
   if(X_ == 5)
-    sp ? launchConvG<5, 5, true>(a, c.kt, c.tn, grid, st) : launchConvG<5, 5, false>(a, c.kt, c.tn, grid, st);
+    sp ? launchConvG<5, 5, true>(a, c.kt, c.tn, c.wn, grid, st)
+       : launchConvG<5, 5, false>(a, c.kt, c.tn, c.wn, grid, st);
   else if(X_ == 7)
-    sp ? launchConvG<7, 7, true>(a, c.kt, c.tn, grid, st) : launchConvG<7, 7, false>(a, c.kt, c.tn, grid, st);
+    sp ? launchConvG<7, 7, true>(a, c.kt, c.tn, c.wn, grid, st)
+       : launchConvG<7, 7, false>(a, c.kt, c.tn, c.wn, grid, st);
   else
-    sp ? launchConvG<9, 9, true>(a, c.kt, c.tn, grid, st) : launchConvG<9, 9, false>(a, c.kt, c.tn, grid, st);
+    sp ? launchConvG<9, 9, true>(a, c.kt, c.tn, c.wn, grid, st)
+       : launchConvG<9, 9, false>(a, c.kt, c.tn, c.wn, grid, st);
 }
 
 // x: trunk (f32, width = block width) updated in place.
