@@ -374,9 +374,17 @@ def main():
                 model_path=model_path, commit_interval=args.commit_interval, nn_cache_log2=args.nn_cache_log2,
                 nn_batch_cap=args.nn_batch_cap // args.groups, nn_precision=args.precision, start_stagger=stagger,
                 node_cap=node_cap, engines_per_device=args.groups, **play)
-    for _ in range(args.warmup):
+    tw = time.perf_counter()
+
+    def progress(what, i, n, t):  # stderr, rank 0: a long window keeps printing
+        if rank == 0:
+            print("bench: %s step %d/%d  %.1f s" % (what, i + 1, n, time.perf_counter() - t), file=sys.stderr,
+                  flush=True)
+
+    for i in range(args.warmup):
         sp.step(rps)
         sp.sync()  # bounded launch queue (a profiler's per-dispatch state stays small)
+        progress("warm-up", i, args.warmup, tw)
     sp.drain_rows()
     sp.drain_games()
     if not args.no_timing:
@@ -425,6 +433,7 @@ def main():
             rows_gathered += len(rows["meta"])
             if writer:
                 writer.put(rows)
+        progress("timed", step, args.steps, t0)
     sp.sync()
     if writer:
         writer.close()  # every drained row is on disk before the clock stops
