@@ -1,6 +1,6 @@
-"""Committed summaries of a tools/profile_r02.sh session (gpurun_out/ -> profiles/):
+"""Committed summaries of a tools/profile_r0N.sh session (gpurun_out/ -> profiles/):
   profiles/<round>_c2_kernel_stats.csv / _kernel_durations.json   rocprofv3 --kernel-trace --stats of the C2 bench
-  profiles/<round>_c3_kernel_stats.csv / _kernel_durations.json   the same for C3 (layered network)
+  profiles/<round>_c3|c5_kernel_stats.csv / _kernel_durations.json   the same for C3 / C5 (layered network)
   profiles/<round>_pmc.json, profiles/traffic_latest.json         per-dispatch FETCH_SIZE / WRITE_SIZE bytes
 FETCH_SIZE is doubled (gfx950: it reports half the bytes of 16-B/lane streaming reads,
 MI355X_MICROARCH.md HBM section); WRITE_SIZE is in KB.
@@ -17,7 +17,7 @@ PROF = os.path.join(REPO, "profiles")
 
 def main():
     rnd = sys.argv[1]
-    for tag, d, prefix in [("c2", "prof_trace", "trace"), ("c3", "prof_c3", "c3")]:
+    for tag, d, prefix in [("c2", "prof_trace", "trace"), ("c3", "prof_c3", "c3"), ("c5", "prof_c5", "c5")]:
         src = os.path.join(OUT, d)
         if os.path.exists(os.path.join(src, prefix + "_kernel_stats.csv")):
             shutil.copy(os.path.join(src, prefix + "_kernel_stats.csv"),
