@@ -31,6 +31,7 @@
 
 #include "detmath.h"
 #include "engine.h"
+#include "lds_dma.h"
 
 namespace kc {
 
@@ -141,38 +142,12 @@ KC_D void aBases(int (&ab)[G::MAXT], const uint16_t* rowPa, int tstart, int lane
   }
 }
 
-// LDS byte address of a pointer into dynamic shared memory.
-KC_D uint32_t ldsAddr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// One 1-KiB LDS-DMA piece: each lane's 16 bytes at src land at lds + 16 * lane
-// (global_load_lds_dwordx4, no VGPR destination).  Issued from inline asm so the
-// compiler neither waits on it nor reorders LDS accesses around it; completion is
-// counted by hand (s_waitcnt vmcnt) before the barrier that publishes the slot.
-KC_D void glds16(const void* src, uint32_t lds) {
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds);
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(dst)
-               : "memory");
-}
-
 // A tap's weights (CH pieces of 64 fragments) into its ring slot; piece c by wave c % nw.
 template <int NW>
 KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, int wave, int lane) {
   for(int c = wave; c < ch; c += NW)
     glds16(src + c * 64 + lane, slotAddr + c * 1024);
 }
-
-template <int N>
-KC_D void waitVm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// Workgroup barrier that leaves LDS-DMA loads in flight (a __syncthreads()
-// would drain them with vmcnt(0)); LDS reads and writes issued before it complete.
-KC_D void barrierKeepDma() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Implicit-GEMM convolution over the wave's tiles, computed transposed:
 // acc[t][ct] += W(ct, K) * act(K, t), so each lane's accumulator holds 4

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "lds_dma.h"
 
 namespace kc {
 
@@ -44,7 +45,11 @@ typedef _Float16 lh16x4 __attribute__((ext_vector_type(4)));
 typedef float lf32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int L_WAVES = 8, L_NT = L_WAVES * 64;
-constexpr int L_STRIDE = 40;       // fp16 per staged row: 32 channels + 8 pad (80 B rows)
+// fp16 per staged row: 32 channels + pad.  Fast: 48 (24 dwords: a 16-row tile's
+// A-fragment ds_read_b128 lane groups hit distinct banks for contiguous rows, and the
+// padded-board rows average 2 LDS cycles per group instead of 2.66 at 40).  Split: 40
+// (two planes x two stages must fit the LDS).
+constexpr int lStride(bool split) { return split ? 40 : 48; }
 
 enum LPro : int { PRO_BITS = 0, PRO_F16 = 1, PRO_BN = 2, PRO_BN_GB = 3 };
 enum LEpi : int { EPI_STORE = 0, EPI_ADD = 1, EPI_BNRELU16 = 2, EPI_STEM = 3 };
@@ -57,7 +62,7 @@ struct LGeo {
   static constexpr int RT = (ROWS + 15) / 16;
   static constexpr int PX = X + 2, PY = Y + 2, PA = PX * PY;
   static constexpr int PROWS = BPW * PA;
-  static constexpr int STAGE = PROWS * L_STRIDE * 2;  // bytes per staged 32-channel slice
+  static constexpr int stage(bool split) { return PROWS * lStride(split) * 2; }  // bytes per staged slice
 };
 
 struct LConvArgs {
@@ -141,7 +146,7 @@ KC_D void stageStore(const LConvArgs& a, const StageRegs<G>& R, char* stHi, char
     const int brd = r / G::A, p = r - brd * G::A;
     const int pr = brd * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1;
     const int c0 = cb * 32 + q * 8;
-    char* dHi = stHi + (pr * L_STRIDE + q * 8) * 2;
+    char* dHi = stHi + (pr * lStride(SPLIT) + q * 8) * 2;
     if(a.pro == PRO_F16) {
       *reinterpret_cast<float4*>(dHi) = R.x0[k];  // already fp16 (zeros past the batch)
       continue;
@@ -192,7 +197,7 @@ KC_D void stageStore(const LConvArgs& a, const StageRegs<G>& R, char* stHi, char
       l4.y = packHalf2(lo[2], lo[3]);
       l4.z = packHalf2(lo[4], lo[5]);
       l4.w = packHalf2(lo[6], lo[7]);
-      *reinterpret_cast<uint4*>(stLo + (pr * L_STRIDE + q * 8) * 2) = l4;
+      *reinterpret_cast<uint4*>(stLo + (pr * lStride(SPLIT) + q * 8) * 2) = l4;
     }
   }
 }
@@ -255,11 +260,11 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int ctBase = blockIdx.y * NCT + wn * TN;  // this wave's first global column tile
   char* stage = smem;                                        // [2][PLANES][STAGE]
-  float* sS = reinterpret_cast<float*>(smem + 2 * PLANES * G::STAGE);  // [cin]
+  float* sS = reinterpret_cast<float*>(smem + 2 * PLANES * G::stage(SPLIT));  // [cin]
   float* sB = sS + a.cin;
   float* sG = sB + a.cin;  // [BPW][gbLd]
   // zero both stages (borders and boards past the batch stay zero), parameters to LDS
-  for(int i = tid; i < 2 * PLANES * G::STAGE / 16; i += L_NT)
+  for(int i = tid; i < 2 * PLANES * G::stage(SPLIT) / 16; i += L_NT)
     reinterpret_cast<uint4*>(smem)[i] = uint4{0u, 0u, 0u, 0u};
   if(a.pro == PRO_BN || a.pro == PRO_BN_GB)
     for(int i = tid; i < a.cin; i += L_NT) {
@@ -273,7 +278,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   const int NCB = a.cin / 32;
   StageRegs<G> sr;
   stageLoad<G>(a, sr, 0, base, nb, tid);
-  stageStore<G, SPLIT>(a, sr, stage, stage + G::STAGE, 0, base, nb, sS, sB, sG, tid);
+  stageStore<G, SPLIT>(a, sr, stage, stage + G::stage(SPLIT), 0, base, nb, sS, sB, sG, tid);
 
   // per-lane A row bases (bytes, shifted to the (-r,-r) neighbour), padding rows -> row 0
   int ab[TM];
@@ -285,7 +290,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     const int brd = r / G::A, p = r - brd * G::A;
     const int pr = brd * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1;
     const int shift = KT == 3 ? G::PX + 1 : 0;
-    ab[t] = ((pr - shift) * L_STRIDE) * 2 + 16 * (lane >> 4);
+    ab[t] = ((pr - shift) * lStride(SPLIT)) * 2 + 16 * (lane >> 4);
   }
   lf32x4 acc[TM][TN];
 #pragma unroll
@@ -322,7 +327,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     if(s + R - 1 < S)
       loadB(s + R - 1, (slot + R - 1) % R);
     const int dy = KT == 3 ? tap / 3 : 0, dx = KT == 3 ? tap % 3 : 0;
-    const int aoff = (dy * G::PX + dx) * L_STRIDE * 2;
+    const int aoff = (dy * G::PX + dx) * lStride(SPLIT) * 2;
     lh16x8 ah[TM], al[SPLIT ? TM : 1];
 #pragma unroll
     for(int t = 0; t < TM; t++) {
@@ -344,8 +349,8 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   // one slice: the next slice's global loads, its taps, then the next slice's
   // prologue into the other stage buffer
   auto slice = [&](int cb, int parity) {
-    const char* stHi = stage + (cb & 1) * PLANES * G::STAGE;
-    const char* stLo = stHi + G::STAGE;
+    const char* stHi = stage + (cb & 1) * PLANES * G::stage(SPLIT);
+    const char* stLo = stHi + G::stage(SPLIT);
     if(cb + 1 < NCB)
       stageLoad<G>(a, sr, cb + 1, base, nb, tid);
     if constexpr(T % 3 == 0) {
@@ -356,8 +361,8 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
       step(cb, 0, parity, stHi, stLo);
     }
     if(cb + 1 < NCB) {
-      char* nHi = stage + ((cb + 1) & 1) * PLANES * G::STAGE;
-      stageStore<G, SPLIT>(a, sr, nHi, nHi + G::STAGE, cb + 1, base, nb, sS, sB, sG, tid);
+      char* nHi = stage + ((cb + 1) & 1) * PLANES * G::stage(SPLIT);
+      stageStore<G, SPLIT>(a, sr, nHi, nHi + G::stage(SPLIT), cb + 1, base, nb, sS, sB, sG, tid);
     }
     __syncthreads();
   };
@@ -372,17 +377,145 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
 }
 
-// 1x1 convolutions (bottleneck in / out, heads): no halo, so a stage holds 128
+// 3x3 fast convolutions with the weights in LDS: the workgroup's B fragments of three
+// taps (3 x NCT pieces of 1 KiB) stream by LDS-DMA into one of two ring slots, so
+// each fragment crosses the L1 once per workgroup instead of once per wave that uses
+// it (kConvL's register ring: 4 or 2 waves per fragment).  Group q (slice cb, taps
+// 3g..3g+2, q = 3cb + g) lives in slot q & 1; group q+1 is requested at the start of
+// group q and published by the barrier before group q's last K-step, which also
+// frees slot q & 1's previous group and, at a slice's end, publishes the next
+// slice's stage.  Fragments of the next K-step (A from the stage, B from the ring)
+// are read before the current step's MFMAs.  Same staging, tiles and epilogues as
+// kConvL.
+template <int X, int Y, int TN, int WN>
+__global__ void __launch_bounds__(L_NT, 2) kConvLB(LConvArgs a) {
+  using G = LGeo<X, Y>;
+  constexpr int WM = L_WAVES / WN, TM = (G::RT + WM - 1) / WM;
+  constexpr int NCT = TN * WN;
+  constexpr int GPIECES = 3 * NCT;            // 1-KiB pieces per tap group
+  constexpr int GBYTES = GPIECES * 1024;      // one ring slot
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int count = a.countDev ? min(*a.countDev, a.n) : a.n;
+  const int base = blockIdx.x * G::BPW;
+  if(base >= count)
+    return;
+  const int nb = min(G::BPW, count - base);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int ctBase = blockIdx.y * NCT + wn * TN;
+  char* stage = smem;                          // [2][STAGE]
+  char* ring = smem + 2 * G::stage(false);            // [2][GBYTES]
+  float* sS = reinterpret_cast<float*>(ring + 2 * GBYTES);
+  float* sB = sS + a.cin;
+  float* sG = sB + a.cin;
+  const int NCB = a.cin / 32;
+  // group q's pieces: tap 3g + j, column tile blockIdx.y * NCT + ct -> slot offset (j * NCT + ct) KiB
+  const lh16x8* wg = a.w + (size_t)blockIdx.y * NCT * 64 + lane;
+  const uint32_t ringAddr = ldsAddr(ring);
+  auto request = [&](int q) {
+    const int cb = q / 3, g = q - 3 * cb;
+    for(int pc = wave; pc < GPIECES; pc += L_WAVES) {
+      const int j = pc / NCT, ct = pc - j * NCT;
+      glds16(wg + ((size_t)(cb * 9 + 3 * g + j) * a.coutTiles + ct) * 64, ringAddr + (q & 1) * GBYTES + pc * 1024);
+    }
+  };
+  request(0);
+  for(int i = tid; i < 2 * G::stage(false) / 16; i += L_NT)
+    reinterpret_cast<uint4*>(smem)[i] = uint4{0u, 0u, 0u, 0u};
+  if(a.pro == PRO_BN || a.pro == PRO_BN_GB)
+    for(int i = tid; i < a.cin; i += L_NT) {
+      sS[i] = i < a.cinReal ? a.ps[i] : 0.0f;
+      sB[i] = i < a.cinReal ? a.pb[i] : 0.0f;
+    }
+  if(a.pro == PRO_BN_GB)
+    for(int i = tid; i < nb * a.gbLd; i += L_NT)
+      sG[i] = a.gb[(size_t)base * a.gbLd + i];
+  __syncthreads();  // (drains group 0's DMA too)
+  StageRegs<G> sr;
+  stageLoad<G>(a, sr, 0, base, nb, tid);
+  stageStore<G, false>(a, sr, stage, nullptr, 0, base, nb, sS, sB, sG, tid);
+  int ab[TM];
+#pragma unroll
+  for(int t = 0; t < TM; t++) {
+    int r = (wm * TM + t) * 16 + (lane & 15);
+    if(r >= G::ROWS)
+      r = 0;
+    const int brd = r / G::A, p = r - brd * G::A;
+    const int pr = brd * G::PA + (p / G::X + 1) * G::PX + p % G::X + 1;
+    ab[t] = ((pr - G::PX - 1) * lStride(false)) * 2 + 16 * (lane >> 4);
+  }
+  lf32x4 acc[TM][TN];
+#pragma unroll
+  for(int t = 0; t < TM; t++)
+#pragma unroll
+    for(int c = 0; c < TN; c++)
+      acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int Q = NCB * 3;  // tap groups
+  __syncthreads();        // stage 0 published
+  lh16x8 af[2][TM], bf[2][TN];
+  // fragments of K-step (slice parity par, tap) into buffer buf
+  auto loadFr = [&](int par, int tap, int buf) {
+    const char* st = stage + par * G::stage(false);
+    const int aoff = ((tap / 3) * G::PX + tap % 3) * lStride(false) * 2;
+    const char* rb = ring + ((par + tap / 3) & 1) * GBYTES + ((tap % 3) * NCT + wn * TN) * 1024 + lane * 16;
+#pragma unroll
+    for(int c = 0; c < TN; c++)
+      bf[buf][c] = *reinterpret_cast<const lh16x8*>(rb + c * 1024);
+#pragma unroll
+    for(int t = 0; t < TM; t++)
+      af[buf][t] = *reinterpret_cast<const lh16x8*>(st + ab[t] + aoff);
+  };
+  loadFr(0, 0, 0);
+  // one slice; par = cb & 1 (compile-time: slices run in pairs)
+  auto slice = [&](int cb, int par) {
+    const bool more = cb + 1 < NCB;
+    if(more)
+      stageLoad<G>(a, sr, cb + 1, base, nb, tid);
+#pragma unroll
+    for(int tap = 0; tap < 9; tap++) {
+      const int q = 3 * cb + tap / 3;
+      if(tap % 3 == 0 && q + 1 < Q)
+        request(q + 1);
+      const int buf = (par + tap) & 1;  // K-step s = 9 cb + tap alternates buffers
+      if(tap == 8 && more)
+        stageStore<G, false>(a, sr, stage + (par ^ 1) * G::stage(false), nullptr, cb + 1, base, nb, sS, sB, sG, tid);
+      if(tap % 3 == 2 && q + 1 < Q) {
+        waitVm<0>();
+        barrierKeepDma();
+      }
+      if(tap < 8)
+        loadFr(par, tap + 1, buf ^ 1);
+      else if(more)
+        loadFr(par ^ 1, 0, buf ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for(int t = 0; t < TM; t++)
+#pragma unroll
+        for(int c = 0; c < TN; c++)
+          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[buf][c], af[buf][t], acc[t][c], 0, 0, 0);
+    }
+  };
+  int cb = 0;
+  for(; cb + 1 < NCB; cb += 2) {
+    slice(cb, 0);
+    slice(cb + 1, 1);
+  }
+  if(cb < NCB)
+    slice(cb, 0);
+  convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
+}
+
+// 1x1 convolutions, split precision (fast: kConv1LP below): no halo, so a stage holds 128
 // channels of the workgroup's rows unpadded (four 32-channel K steps per stage,
 // staged synchronously with all of a thread's loads in flight), the stage count is
 // a quarter of the 32-channel slices and a stage's load latency is paid once per
 // four K steps.  Same wave grid, fragments, prologues and epilogues as kConvL.
 constexpr int L1_SW = 4;                  // 32-channel slices per stage
-constexpr int L1_STRIDE = 32 * L1_SW + 8;  // fp16 per staged row (272 B)
+constexpr int l1Stride(bool) { return 32 * L1_SW + 8; }  // fp16 per staged row (272 B)
 
-template <class G>
+template <class G, bool SPLIT>
 constexpr int l1StageBytes() {
-  return G::ROWS * L1_STRIDE * 2;
+  return G::ROWS * l1Stride(SPLIT) * 2;
 }
 
 template <int X, int Y, int TN, bool SPLIT, int WN>
@@ -390,7 +523,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
   using G = LGeo<X, Y>;
   constexpr int WM = L_WAVES / WN, TM = (G::RT + WM - 1) / WM;
   constexpr int NCT = TN * WN;
-  constexpr int SB = l1StageBytes<G>();
+  constexpr int SB = l1StageBytes<G, SPLIT>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int count = a.countDev ? min(*a.countDev, a.n) : a.n;
   const int base = blockIdx.x * G::BPW;
@@ -414,7 +547,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
     int r = (wm * TM + t) * 16 + (lane & 15);
     if(r >= G::ROWS)
       r = 0;
-    ab[t] = r * L1_STRIDE * 2 + 16 * (lane >> 4);
+    ab[t] = r * l1Stride(SPLIT) * 2 + 16 * (lane >> 4);
   }
   lf32x4 acc[TM][TN];
 #pragma unroll
@@ -473,7 +606,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
       hi.y = packHalf2(v[2], v[3]);
       hi.z = packHalf2(v[4], v[5]);
       hi.w = packHalf2(v[6], v[7]);
-      *reinterpret_cast<uint4*>(stHi + (r * L1_STRIDE + q * 8) * 2) = hi;
+      *reinterpret_cast<uint4*>(stHi + (r * l1Stride(SPLIT) + q * 8) * 2) = hi;
       if constexpr(SPLIT) {
         float lo[8];
 #pragma unroll
@@ -484,7 +617,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
         l4.y = packHalf2(lo[2], lo[3]);
         l4.z = packHalf2(lo[4], lo[5]);
         l4.w = packHalf2(lo[6], lo[7]);
-        *reinterpret_cast<uint4*>(stLo + (r * L1_STRIDE + q * 8) * 2) = l4;
+        *reinterpret_cast<uint4*>(stLo + (r * l1Stride(SPLIT) + q * 8) * 2) = l4;
       }
     }
     __syncthreads();
@@ -513,6 +646,132 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
           }
         }
     }
+  }
+  convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
+}
+
+// Fast 1x1 convolutions, pipelined: 64-channel stages, double-buffered in LDS; the
+// next stage's global loads are issued before the current stage's MFMAs and converted
+// (BN-ReLU -> fp16) into the other buffer after them, so the HBM latency of the f32
+// input overlaps the MFMAs (kConv1L waits for each stage before any MFMA: 5 % MFMA
+// busy on b18c384nbt's bottleneck convs).  Rows are 40 dwords (64 channels + 16 pad:
+// 10 mod 16 chunks, conflict-free A-fragment reads for contiguous rows).
+constexpr int L1P_SW = 2;                  // 32-channel slices per stage
+constexpr int L1P_STRIDE = 32 * L1P_SW + 16;  // fp16 per staged row
+
+template <int X, int Y, int TN, int WN>
+__global__ void __launch_bounds__(L_NT, 2) kConv1LP(LConvArgs a) {
+  using G = LGeo<X, Y>;
+  constexpr int WM = L_WAVES / WN, TM = (G::RT + WM - 1) / WM;
+  constexpr int NCT = TN * WN;
+  constexpr int SB = G::ROWS * L1P_STRIDE * 2;
+  constexpr int CPR = 4 * L1P_SW;           // 8-channel chunks per staged row
+  constexpr int TASKS = G::ROWS * CPR;
+  constexpr int TPT = (TASKS + L_NT - 1) / L_NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int count = a.countDev ? min(*a.countDev, a.n) : a.n;
+  const int base = blockIdx.x * G::BPW;
+  if(base >= count)
+    return;
+  const int nb = min(G::BPW, count - base);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int ctBase = blockIdx.y * NCT + wn * TN;
+  float* sS = reinterpret_cast<float*>(smem + 2 * SB);
+  float* sB = sS + a.cin;
+  for(int i = tid; i < a.cin; i += L_NT) {
+    sS[i] = i < a.cinReal ? a.ps[i] : 0.0f;
+    sB[i] = i < a.cinReal ? a.pb[i] : 0.0f;
+  }
+  const int NCB = a.cin / 32, NST = (NCB + L1P_SW - 1) / L1P_SW;
+  float4 x0[TPT], x1[TPT];
+  auto load = [&](int st) {
+#pragma unroll
+    for(int k = 0; k < TPT; k++) {
+      const int t = tid + k * L_NT;
+      const int r = t / CPR, q = t - r * CPR;
+      const int c0 = st * 32 * L1P_SW + q * 8;
+      x0[k] = x1[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+      if(t < TASKS && r / G::A < nb && c0 < a.cin) {
+        const float* sp = reinterpret_cast<const float*>(a.src) + ((size_t)base * G::A + r) * a.srcLd + a.srcOff + c0;
+        x0[k] = *reinterpret_cast<const float4*>(sp);
+        x1[k] = *reinterpret_cast<const float4*>(sp + 4);
+      }
+    }
+  };
+  auto store = [&](int st, char* buf) {
+#pragma unroll
+    for(int k = 0; k < TPT; k++) {
+      const int t = tid + k * L_NT;
+      if(t >= TASKS)
+        continue;
+      const int r = t / CPR, q = t - r * CPR;
+      const int brd = r / G::A;
+      const int c0 = st * 32 * L1P_SW + q * 8;
+      const float xs[8] = {x0[k].x, x0[k].y, x0[k].z, x0[k].w, x1[k].x, x1[k].y, x1[k].z, x1[k].w};
+      float v[8];
+#pragma unroll
+      for(int j = 0; j < 8; j++)
+        v[j] = (brd < nb && c0 + j < a.cinReal) ? fmaxf(xs[j] * sS[c0 + j] + sB[c0 + j], 0.0f) : 0.0f;
+      uint4 hi;
+      hi.x = packHalf2(v[0], v[1]);
+      hi.y = packHalf2(v[2], v[3]);
+      hi.z = packHalf2(v[4], v[5]);
+      hi.w = packHalf2(v[6], v[7]);
+      *reinterpret_cast<uint4*>(buf + (r * L1P_STRIDE + q * 8) * 2) = hi;
+    }
+  };
+  int ab[TM];
+#pragma unroll
+  for(int t = 0; t < TM; t++) {
+    int r = (wm * TM + t) * 16 + (lane & 15);
+    if(r >= G::ROWS)
+      r = 0;
+    ab[t] = r * L1P_STRIDE * 2 + 16 * (lane >> 4);
+  }
+  lf32x4 acc[TM][TN];
+#pragma unroll
+  for(int t = 0; t < TM; t++)
+#pragma unroll
+    for(int c = 0; c < TN; c++)
+      acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const lh16x8* wl = a.w + (size_t)ctBase * 64 + lane;
+  const size_t stepStride = (size_t)a.coutTiles * 64;
+  lh16x8 bh[2][TN];
+  auto loadB = [&](int s, int slot) {
+#pragma unroll
+    for(int c = 0; c < TN; c++)
+      bh[slot][c] = wl[(size_t)s * stepStride + c * 64];
+  };
+  load(0);
+  loadB(0, 0);
+  __syncthreads();  // sS / sB
+  store(0, smem);
+  __syncthreads();
+  for(int st = 0; st < NST; st++) {
+    const char* cur = smem + (st & 1) * SB;
+    if(st + 1 < NST)
+      load(st + 1);
+#pragma unroll
+    for(int j = 0; j < L1P_SW; j++) {
+      const int s = st * L1P_SW + j;
+      if(s >= NCB)
+        break;
+      if(s + 1 < NCB)
+        loadB(s + 1, (j + 1) & 1);
+      lh16x8 ah[TM];
+#pragma unroll
+      for(int t = 0; t < TM; t++)
+        ah[t] = *reinterpret_cast<const lh16x8*>(cur + ab[t] + 64 * j);
+#pragma unroll
+      for(int t = 0; t < TM; t++)
+#pragma unroll
+        for(int c = 0; c < TN; c++)
+          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j & 1][c], ah[t], acc[t][c], 0, 0, 0);
+    }
+    if(st + 1 < NST)
+      store(st + 1, smem + ((st + 1) & 1) * SB);
+    __syncthreads();
   }
   convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
 }
@@ -666,6 +925,12 @@ uint16_t lf2h(float f) {
   return u;
 }
 
+#ifdef KC_NO_LDSB  // (A/B builds)
+constexpr bool kConvLdsB = false;
+#else
+constexpr bool kConvLdsB = true;
+#endif
+
 template <int X, int Y, int KT, int TN, bool SPLIT, int WN>
 void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
   using G = LGeo<X, Y>;
@@ -674,10 +939,18 @@ void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
   if constexpr(KT == 1) {
     if(a.pro != PRO_BN)
       throw std::invalid_argument("1x1 convolutions take a BN-ReLU prologue");
-    lds = (SPLIT ? 2 : 1) * l1StageBytes<G>() + 2 * (size_t)a.cin * 4;
-    fnp = (const void*)kConv1L<X, Y, TN, SPLIT, WN>;
+    if constexpr(!SPLIT) {
+      lds = 2 * (size_t)G::ROWS * L1P_STRIDE * 2 + 2 * (size_t)a.cin * 4;
+      fnp = (const void*)kConv1LP<X, Y, TN, WN>;
+    } else {
+      lds = 2 * l1StageBytes<G, SPLIT>() + 2 * (size_t)a.cin * 4;
+      fnp = (const void*)kConv1L<X, Y, TN, SPLIT, WN>;
+    }
+  } else if constexpr(kConvLdsB && !SPLIT && WN == 2) {
+    lds = 2 * G::stage(SPLIT) + 2 * 3 * TN * WN * 1024 + (2 * a.cin + G::BPW * (a.gbLd > 0 ? a.gbLd : 0)) * 4;
+    fnp = (const void*)kConvLB<X, Y, TN, WN>;
   } else {
-    lds = 2 * (SPLIT ? 2 : 1) * G::STAGE + (2 * a.cin + G::BPW * (a.gbLd > 0 ? a.gbLd : 0)) * 4;
+    lds = 2 * (SPLIT ? 2 : 1) * G::stage(SPLIT) + (2 * a.cin + G::BPW * (a.gbLd > 0 ? a.gbLd : 0)) * 4;
     fnp = (const void*)kConvL<X, Y, KT, TN, SPLIT, WN>;
   }
   if(lds > 160 * 1024)
@@ -694,8 +967,12 @@ void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
     }
   }
   const int gy = (a.coutTiles + TN * WN - 1) / (TN * WN);
-  if constexpr(KT == 1)
+  if constexpr(KT == 1 && !SPLIT)
+    hipLaunchKernelGGL((kConv1LP<X, Y, TN, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+  else if constexpr(KT == 1)
     hipLaunchKernelGGL((kConv1L<X, Y, TN, SPLIT, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+  else if constexpr(kConvLdsB && !SPLIT && WN == 2)
+    hipLaunchKernelGGL((kConvLB<X, Y, TN, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
   else
     hipLaunchKernelGGL((kConvL<X, Y, KT, TN, SPLIT, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
   KC_HIP(hipGetLastError());
