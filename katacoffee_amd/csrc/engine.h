@@ -28,6 +28,14 @@ const DTables& hostTables(int X, int Y, int W);
 // ---- nn.hip ----
 // Boards per network workgroup (one workgroup per compute unit at a time).
 constexpr int NN_BOARDS_PER_WG = 8;
+// Boards per workgroup of the small-batch instance (batches of at most that many per
+// CU): 5 boards = 125 positions fill the 128 rows its 8 waves compute as exactly as 4
+// (100 rows) do, so a launch takes one workgroup's latency on a fifth fewer CUs; the
+// other game group's search waves take the free CUs (nn.hip NNGeo).
+#ifndef NN_SMALL_BOARDS
+#define NN_SMALL_BOARDS 5
+#endif
+constexpr int NN_SMALL_NB = NN_SMALL_BOARDS;
 // Offsets (elements) into the packed weight buffers; see nn.hip.
 constexpr int NN_MAX_BLOCKS = 16;
 struct NNLayout {
@@ -128,7 +136,7 @@ class NNEngine {
   float* wF32_ = nullptr;  // device
   NNLayout* layoutDev_ = nullptr;
   uint16_t* tabDev_ = nullptr;   // device row tables (nn.hip rowTables), 8 boards per workgroup
-  uint16_t* tabDev4_ = nullptr;  // the same for 4 boards per workgroup
+  uint16_t* tabDevSm_ = nullptr; // the same for the small-batch instance (NN_SMALL_NB boards)
   uint16_t* tabDevS_ = nullptr;  // the same for the split-precision instance (2 boards per workgroup)
   bool split_ = false;           // NN_ACCURATE on the fused kernel: fp16 hi/lo operand pairs
   int small_ = 0;                // KATACOFFEE_NN_SMALL=8: small batches on the 8-board instance (A/B runs)

@@ -28,6 +28,23 @@ KC_D void glds16(const void* src, uint32_t lds) {
                : "memory");
 }
 
+// The same piece addressed as a wave-uniform base (SGPR pair, global_load's saddr form)
+// plus a 32-bit per-lane byte offset: a burst of pieces costs no VGPR per piece (the
+// per-lane 64-bit addresses of glds16 raise the network kernels' VGPR allocation,
+// which decides whether the other game group's search waves fit beside them on a CU).
+KC_D void glds16s(const void* base, uint32_t laneOff, uint32_t lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds);
+  // (readfirstlane returns int: widen through uint32_t, a sign extension of the low
+  // word would corrupt the high word of addresses with bit 31 set)
+  const uint64_t b = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)base) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)base >> 32)) << 32);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(laneOff), "s"(b), "s"(dst)
+               : "memory");
+}
+
 template <int N>
 KC_D void waitVm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

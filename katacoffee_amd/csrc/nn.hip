@@ -54,8 +54,14 @@ struct NNGeo {
   // hi one.  2 boards per workgroup so the planes and the ring fit the 160 KiB.
   static constexpr bool SPLIT = SPLIT_ != 0;
   static constexpr int PLANES = SPLIT ? 2 : 1;
-  // weight ring slots: tap k+2 is requested at the start of tap k
-  static constexpr int RING = 3;
+  // weight ring slots.  3 (8-board and SPLIT instances, whose LDS holds no more): tap
+  // k+2 is requested at the start of tap k, one barrier per tap.  4 (4-board
+  // instance): taps move in pairs (g, g+1), g even in the stream's global tap count;
+  // pair j+1 is requested at the start of pair j and published by one barrier per pair.
+  // (6 slots, one barrier per 3 taps, would fill all 160 KiB and keep the other game
+  // group's search kernels off the CU while the network runs.)
+  static constexpr int RING = (NB_ == NN_SMALL_NB && SPLIT_ == 0) ? 4 : 3;
+  static constexpr bool PAIRS = RING == 4;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
   // Every wave owns MAXT whole tiles (uniform, branch-free MFMA loops): output
@@ -83,12 +89,14 @@ struct NNGeo {
   static constexpr int OFF_SCR = MROWS * SCR * 4 > 96 * 64 * 4 ? MROWS * SCR * 4 : 96 * 64 * 4;
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
-  static constexpr int OFF_VH = OFF_BIAS + NB * 64 * 4;
   static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap and plane
   static constexpr int WSLOT = PLANES * WBUF;           // one ring slot
   // row tables (u16): rowPa[MROWS], rowBP[MROWS], bpRow[ROWS] -- built on the host
   static constexpr int NTAB = 2 * MROWS + ROWS;
-  static constexpr int OFF_TAB = OFF_VH + NB * 64 * 4;
+  static constexpr int OFF_TAB = OFF_BIAS + NB * 64 * 4;
+  // the value head's hidden layer [NB][64] f32 lives in the (idle) ring during the
+  // heads, after the policy-gpool and value linear weights staged there
+  static constexpr int RING_VH = (32 + 64) * 96 * 4;
   // per-block f32 parameter slabs (double buffered, filled one block ahead)
   static constexpr int NPRM = 448;
   static constexpr int OFF_PRM = (OFF_TAB + NTAB * 2 + 15) / 16 * 16;
@@ -97,7 +105,7 @@ struct NNGeo {
   static_assert(C % 32 == 0, "C must be a multiple of 32");
   static_assert(OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
   static_assert(96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
-  static_assert(RING * WSLOT * 16 >= (32 + 64) * 96 * 4, "head linear weights must fit in the ring");
+  static_assert(RING * WSLOT * 16 >= RING_VH + NB * 64 * 4, "head linear weights and vh must fit in the ring");
   static_assert((PLANES - 1) * PLANE_BYTES + 2 * PA * ROWB + 2 * 64 < 65536,
                 "A-read offsets must fit the ds_read immediate");
   static_assert(LDS <= 163840, "LDS budget");
@@ -142,11 +150,12 @@ KC_D void aBases(int (&ab)[G::MAXT], const uint16_t* rowPa, int tstart, int lane
   }
 }
 
-// A tap's weights (CH pieces of 64 fragments) into its ring slot; piece c by wave c % nw.
+// A tap's weights (CH pieces of 64 fragments) into its ring slot; piece c by wave
+// (c + rot) % nw (rot spreads two taps' remainders over different waves).
 template <int NW>
-KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, int wave, int lane) {
-  for(int c = wave; c < ch; c += NW)
-    glds16(src + c * 64 + lane, slotAddr + c * 1024);
+KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, int wave, int lane, int rot = 0) {
+  for(int c = (wave + NW - rot % NW) % NW; c < ch; c += NW)
+    glds16s(src + c * 64, (uint32_t)lane * 16u, slotAddr + c * 1024);
 }
 
 // Implicit-GEMM convolution over the wave's tiles, computed transposed:
@@ -168,17 +177,27 @@ KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, 
 // the requests for those taps).
 // DBG (tools/conv_bench.hip ablations only): bit 0 skips the weight requests, bit 1
 // the per-tap barriers, bit 3 the vmcnt waits, bit 8 the entry wait + barrier.
-template <class G, int NTAPS, int NCB, int DBG = 0>
+//
+// G::PAIRS (4-slot ring): the weight stream's taps are counted globally across the
+// convolutions (g0 = this conv's first tap: the stem 0, block b's conv1 9 + 18b and
+// conv2 18 + 18b, the head 9 + 18 nblocks; PAR = g0 & 1 fixes the pair boundaries at
+// compile time); tap g lives in slot g & 3.  At the start of each pair (g even) the
+// next pair (g+2, g+3: this conv's or the next conv's first taps) is requested into the
+// slots that the previous pair's barrier freed; the barrier before the pair's last
+// K-step retires every wave's pieces of the next pair (vmcnt 0: nothing newer is in
+// flight) and frees this pair's slots -- one barrier per two taps instead of one per tap.
+template <class G, int NTAPS, int NCB, int PAR = 0, int DBG = 0>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                     f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid,
-                    const h16x8* __restrict__ wNext, int chNext, int nextTaps) {
+                    const h16x8* __restrict__ wNext, int chNext, int nextTaps, int g0 = 0) {
   constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap and plane
   constexpr int CH = CHP * G::PLANES;    // 1-KiB pieces per tap (the lo block after the hi one)
   constexpr int UNITS = CH * 64;         // 16-B fragments per tap
   constexpr int STEPS = NTAPS * NCB;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t ring = ldsAddr(wl);
-  auto slotOf = [](int tap) { return tap % 3; };
+  // ring slot of local tap t (the 3-slot ring's taps start at slot 0 in every conv)
+  auto slotOf = [&](int tap) { return G::PAIRS ? (g0 + tap) & 3 : tap % 3; };
   if(!(DBG & 256)) {
     waitVm<0>();
     __syncthreads();
@@ -208,9 +227,23 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   loadStep(0, 0);
 #pragma unroll
   for(int tap = 0; tap < NTAPS; tap++) {
-    // request stream tap tap+2 (this conv's, or the next conv's tap 0 / 1)
+    const bool pairStart = ((PAR + tap) & 1) == 0;
     if(DBG & 1) {
+    } else if(G::PAIRS) {
+      if(pairStart) {
+        // request the next pair: stream taps tap+2, tap+3 (this conv's or the next's)
+#pragma unroll
+        for(int k = 2; k <= 3; k++) {
+          const int u = tap + k;
+          const uint32_t dst = ring + (uint32_t)(((g0 + u) & 3) * G::WSLOT * 16);
+          if(u < NTAPS)
+            stageTapDma<G::NW>(w + (size_t)u * UNITS, dst, CH, wave, lane, (k - 2) * CH);
+          else if(u - NTAPS < nextTaps)
+            stageTapDma<G::NW>(wNext + (size_t)(u - NTAPS) * chNext * 64, dst, chNext, wave, lane, (k - 2) * chNext);
+        }
+      }
     } else if(tap + 2 < NTAPS)
+      // request stream tap tap+2 (this conv's, or the next conv's tap 0 / 1)
       stageTapDma<G::NW>(w + (size_t)(tap + 2) * UNITS, ring + slotOf(tap + 2) * G::WSLOT * 16, CH, wave, lane);
     else if(NTAPS == 9 && tap == 7)
       stageTapDma<G::NW>(wNext, ring, chNext, wave, lane);
@@ -219,7 +252,14 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
 #pragma unroll
     for(int cb = 0; cb < NCB; cb++) {
       const int st = tap * NCB + cb;
-      if(cb == NCB - 1 && tap + 1 < NTAPS) {
+      if(G::PAIRS && cb == NCB - 1 && !pairStart && tap + 1 < NTAPS) {
+        // end of a pair: retire this wave's pieces of the next pair, publish them and
+        // free this pair's slots
+        if(!(DBG & 8))
+          waitVm<0>();
+        if(!(DBG & 2))
+          barrierKeepDma();
+      } else if(!G::PAIRS && cb == NCB - 1 && tap + 1 < NTAPS) {
         // retire this wave's pieces of tap+1 (only the tap+2 request, >= N pieces per
         // wave, may stay in flight), then publish them / free slot tap%3
         if(DBG & 8) {
@@ -531,7 +571,7 @@ __global__ void __launch_bounds__(512, 2)
   float* poolP = reinterpret_cast<float*>(smem + G::OFF_POOL);
   float* poolV = poolP + G::NB * 96;
   float* biasS = reinterpret_cast<float*>(smem + G::OFF_BIAS);
-  float* vh = reinterpret_cast<float*>(smem + G::OFF_VH);
+  float* vh = reinterpret_cast<float*>(smem + G::OFF_W + G::RING_VH);  // heads only (ring idle)
   uint16_t* rowPa = reinterpret_cast<uint16_t*>(smem + G::OFF_TAB);  // [MROWS] padded cell of row
   uint16_t* rowBP = rowPa + G::MROWS;                                 // [MROWS] b*A+p (0xFFFF: padding)
   float* prm = reinterpret_cast<float*>(smem + G::OFF_PRM);  // [2][NPRM] parameter slabs
@@ -544,7 +584,7 @@ __global__ void __launch_bounds__(512, 2)
     constexpr int CH0 = G::NCT_ALL * G::PLANES;  // 1-KiB pieces per stem tap (one 32-channel block)
     const uint32_t ring = ldsAddr(wl);
 #pragma unroll
-    for(int tap = 0; tap < G::RING - 1; tap++)
+    for(int tap = 0; tap < 2; tap++)
       stageTapDma<G::NW>(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WSLOT * 16, CH0, wave, lane);
   }
   // ---- row tables; unpack the packed V1 planes into the zero-bordered act ----
@@ -588,9 +628,9 @@ __global__ void __launch_bounds__(512, 2)
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
-                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
-                        L->nblocks > 0 ? 9 : 1);
+  convTiles<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
+                        L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
+                        L->nblocks > 0 ? 9 : 1, 0);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
 #pragma unroll
@@ -626,8 +666,8 @@ __global__ void __launch_bounds__(512, 2)
     for(int j = 0; j < NPK; j++)
       pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
-    convTiles<G, 9, G::C / 32>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
-                                  (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, 9);
+    convTiles<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
+                                  (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, 9, 9 + 18 * blk);
 #pragma unroll
     for(int j = 0; j < NPK; j++)
       if(tid + j * G::NT < G::NPRM)
@@ -649,8 +689,8 @@ __global__ void __launch_bounds__(512, 2)
           acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, G::C / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                    3 * G::NCT_ALL * G::PLANES, nextTaps);
+      convTiles<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                    3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
     } else {
@@ -737,8 +777,8 @@ __global__ void __launch_bounds__(512, 2)
           acc[t][ct] = tr[t][ct];
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, (G::C - 32) / 32>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                           3 * G::NCT_ALL * G::PLANES, nextTaps);
+      convTiles<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                           3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
     }
@@ -751,7 +791,7 @@ __global__ void __launch_bounds__(512, 2)
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0);
+  convTiles<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0, 9 + 18 * L->nblocks);
   __syncthreads();  // act dead from here: f32 [MROWS][SCR] value branch at actF, g branch at scr
   NN_PHASE(41);
   {
@@ -1067,20 +1107,20 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipMalloc(&layoutDev_, sizeof(NNLayout)));
   KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
   using G8 = NNGeo<5, 5, 96, 8, 0>;
-  using G4 = NNGeo<5, 5, 96, 4, 0>;
+  using G4 = NNGeo<5, 5, 96, NN_SMALL_NB, 0>;
   using GS = NNGeo<5, 5, 96, 2, 1>;
   const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>(), tabS = rowTables<GS>();
   KC_HIP(hipMalloc(&tabDev_, tab8.size() * 2));
   KC_HIP(hipMemcpy(tabDev_, tab8.data(), tab8.size() * 2, hipMemcpyHostToDevice));
-  KC_HIP(hipMalloc(&tabDev4_, tab4.size() * 2));
-  KC_HIP(hipMemcpy(tabDev4_, tab4.data(), tab4.size() * 2, hipMemcpyHostToDevice));
+  KC_HIP(hipMalloc(&tabDevSm_, tab4.size() * 2));
+  KC_HIP(hipMemcpy(tabDevSm_, tab4.data(), tab4.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&tabDevS_, tabS.size() * 2));
   KC_HIP(hipMemcpy(tabDevS_, tabS.data(), tabS.size() * 2, hipMemcpyHostToDevice));
 
   // function attributes are per device: every engine sets it on its own device
   KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G8::LDS));
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 4, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G4::LDS));
   KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GS::LDS));
@@ -1098,7 +1138,7 @@ NNEngine::~NNEngine() {
   (void)hipFree(wF32_);
   (void)hipFree(layoutDev_);
   (void)hipFree(tabDev_);
-  (void)hipFree(tabDev4_);
+  (void)hipFree(tabDevSm_);
   (void)hipFree(tabDevS_);
 
 }
@@ -1117,12 +1157,13 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   }
   const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
   // A launch costs about one workgroup's latency per wave of workgroups (one per CU):
-  // a batch bound that fits 4 boards per CU (e.g. each of two game groups' batches)
-  // runs 4 boards per workgroup, half the MFMA work on each workgroup's path.
+  // a batch bound that fits NN_SMALL_NB boards per CU (e.g. each of two game groups'
+  // batches) runs that many boards per workgroup, half the MFMA work on each
+  // workgroup's path.
   if(split_)  // "accurate": one instance for every batch size (its results never depend on n)
     launch<NNGeo<5, 5, 96, 2, 1>>(n, inWords, tabDevS_, in, out, st, countDev, rowIdx, e0, e1);
-  else if(n <= 4 * cus_ && small_ != 8)
-    launch<NNGeo<5, 5, 96, 4, 0>>(n, inWords, tabDev4_, in, out, st, countDev, rowIdx, e0, e1);
+  else if(n <= NN_SMALL_NB * cus_ && small_ != 8)
+    launch<NNGeo<5, 5, 96, NN_SMALL_NB, 0>>(n, inWords, tabDevSm_, in, out, st, countDev, rowIdx, e0, e1);
   else
     launch<NNGeo<5, 5, 96, 8, 0>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
 }

@@ -6,7 +6,7 @@ bit-identical.  This pins the hand-off the stand-in-network parity tests cannot 
 the batch's row indirection into the network (kCompact -> forward with rowIdx), real
 logits through post-processing (nneval.cpp:702-844: legal mask, softmax, the inverse
 symmetry of the row's random orientation), NN-cache payloads of real outputs, and
-batch-cap deferral, on the fused b6c96 kernel (4- and 8-board instances, one and two
+batch-cap deferral, on the fused b6c96 kernel (5- and 8-board instances, one and two
 game groups) and on the layered kernels (b10c128 @ 5x5, b18c384nbt @ 9x9, the split
 "accurate" precision).  Reference: cpp/neuralnet/nneval.cpp:588-844 feeding
 cpp/search/searchnnhelpers.cpp:39-129.
@@ -81,11 +81,11 @@ def _rows_of_game_positions(X, Y, W, n, seed):
                          ids=["b6c96-fused", "b6c96-accurate", "b10c128-layered", "b18c384nbt-layered"])
 def test_network_row_independence(nets, arch, X, Y, W, precision):
     """A row's logits do not depend on its batch position, the batch size or (fused)
-    the 4- / 8-board workgroup variant: a permuted batch gives the permuted outputs."""
+    the 5- / 8-board workgroup variant: a permuted batch gives the permuted outputs."""
     import torch
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    # fused: n > 4 x CUs selects the 8-board instance, the prefix the 4-board one
-    n = 4 * cus + 37 if precision == "fast" and arch == "b6c96" else 203
+    # fused: n > 5 x CUs selects the 8-board instance, the prefix the small (5-board) one
+    n = 5 * cus + 37 if precision == "fast" and arch == "b6c96" else 203
     packed = _rows_of_game_positions(X, Y, W, n, seed=n)
     net = kc.Network(nets[arch], X, Y, W, precision=precision)
     full = net.forward(packed)
@@ -101,9 +101,9 @@ PRODUCTION = dict(cheap_search_prob=0.75, cheap_search_visits=8, cheap_search_ta
                   reduce_visits_threshold=0.9, reduce_visits_threshold_lookback=3, reduced_visits_min=8,
                   reduced_visits_weight=0.1, policy_surprise_data_weight=0.5, value_surprise_data_weight=0.1)
 CASES = {
-    # C2 settings: fused fast b6c96, NN cache, binding batch cap above 4 x CUs (8-board kernel)
-    "c2-fused-nb8": ("b6c96", (5, 5, 4), "fast", 1536, 1, 24, 14, 1100, 420, {}),
-    # two game groups on their own streams, each capped (4-board kernel), selfplay1.cfg play
+    # C2 settings: fused fast b6c96, NN cache, binding batch cap above 5 x CUs (8-board kernel)
+    "c2-fused-nb8": ("b6c96", (5, 5, 4), "fast", 1536, 1, 24, 14, 1300, 420, {}),
+    # two game groups on their own streams, each capped (5-board kernel), selfplay1.cfg play
     "c2-fused-two-groups": ("b6c96", (5, 5, 4), "fast", 384, 2, 24, 14, 300, 700, PRODUCTION),
     # split-precision network (the 1e-3 path) in self-play
     "c2-accurate": ("b6c96", (5, 5, 4), "accurate", 128, 1, 24, 12, 0, 900, {}),

@@ -40,11 +40,16 @@ __global__ void __launch_bounds__(G::NT, 2) kConv(const h16x8* __restrict__ w, c
   f32x4 acc[G::MAXT][G::NCT];
   zeroAcc<G>(acc);
   unsigned long long t0 = clock64();
-  for(int r = 0; r < REPS; r++) {
+  for(int r = 0; r < REPS; r += 2) {
     if(MODE == 0 || MODE >= 3) {
-      // the stream's taps 7/8 re-request this conv's taps 0/1 for the next rep
+      // the stream's last taps re-request this conv's first taps for the next rep; two
+      // reps per iteration so the 4-board instance's tap pairs alternate as in the
+      // network (conv1 starts at an odd stream tap, conv2 at an even one)
       constexpr int DBG = kDbg[MODE];
-      convTiles<G, 9, 3, DBG>(act, w, wl, acc, ab, cg, lane, tid, w, 3 * G::NCT_ALL, 9);
+      convTiles<G, 9, 3, 1, DBG>(act, w, wl, acc, ab, cg, lane, tid, w, 3 * G::NCT_ALL, 9, 9 + 9 * r);
+      if(!(DBG & 256))
+        __syncthreads();
+      convTiles<G, 9, 3, 0, DBG>(act, w, wl, acc, ab, cg, lane, tid, w, 3 * G::NCT_ALL, 9, 18 + 9 * r);
       if(!(DBG & 256))
         __syncthreads();
     } else if(MODE == 1) {
@@ -64,9 +69,9 @@ __global__ void __launch_bounds__(G::NT, 2) kConv(const h16x8* __restrict__ w, c
       };
       loadStep(0, 0);
 #pragma unroll
-      for(int st = 0; st < 27; st++) {
-        if(st + 1 < 27)
-          loadStep(st + 1, (st + 1) & 1);
+      for(int st = 0; st < 54; st++) {  // two convs per iteration
+        if(st + 1 < 54)
+          loadStep((st + 1) % 27, (st + 1) & 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for(int t = 0; t < G::MAXT; t++)
@@ -84,7 +89,7 @@ __global__ void __launch_bounds__(G::NT, 2) kConv(const h16x8* __restrict__ w, c
       for(int ct = 0; ct < G::NCT; ct++)
         bf[ct] = wl[(cg * G::NCT + ct) * 64 + lane];
 #pragma unroll
-      for(int st = 0; st < 27; st++) {
+      for(int st = 0; st < 54; st++) {  // two convs per iteration
 #pragma unroll
         for(int t = 0; t < G::MAXT; t++)
 #pragma unroll
@@ -141,7 +146,7 @@ void runAll(int wgPerCu, const h16x8* w) {
 }
 
 int main() {
-  using G8 = NNGeo<5, 5, 96, 8, 8>;
+  using G8 = NNGeo<5, 5, 96, 8, 0>;
   std::vector<uint16_t> hw((size_t)9 * G8::WBUF * 8);
   for(size_t i = 0; i < hw.size(); i++)
     hw[i] = (uint16_t)(0x2000 + (i * 13 & 0x7ff));
@@ -149,7 +154,7 @@ int main() {
   KC_HIP(hipMalloc(&w, hw.size() * 2));
   KC_HIP(hipMemcpy(w, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
   runAll<G8>(1, w);
-  runAll<NNGeo<5, 5, 96, 4, 8>>(1, w);
+  runAll<NNGeo<5, 5, 96, 4, 0>>(1, w);
 
   return 0;
 }
