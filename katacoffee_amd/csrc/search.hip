@@ -3351,7 +3351,8 @@ constexpr int CP_VEC = 16;
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
   __shared__ uint32_t wsum[16], wpre[17];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = (d.G + 1023) / 1024;
+  const int nt = blockDim.x, nw = nt >> 6;  // 256 or 1024 threads (launchCompact)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = (d.G + nt - 1) / nt;
   const int lo = t * per, hi = min(d.G, lo + per);
   const int p = *d.nnRR;
   const bool vec = per <= CP_VEC;
@@ -3393,7 +3394,7 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
     wsum[w] = incl;
   __syncthreads();
   if(t < 64) {
-    uint32_t x = t < 16 ? wsum[t] : 0u, xi = x;
+    uint32_t x = t < nw ? wsum[t] : 0u, xi = x;
 #pragma unroll
     for(int off = 1; off < 16; off <<= 1) {
       const uint32_t v = (uint32_t)__shfl_up((int)xi, off, 64);
@@ -3440,7 +3441,7 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
         d.nnDefer[i] = 0;
     }
   }
-  if(t == 1023) {
+  if(t == nt - 1) {
     const int count = min(total, cap);
     *d.nnCount = count;
     if(accumulate)
@@ -3561,9 +3562,12 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
   KC_HIP(hipGetLastError());
 }
 
+// 256 threads (one wave per SIMD) while each keeps at most CP_VEC games: a workgroup
+// that small fits beside a network workgroup of the other game group on its CU (1024
+// threads need 4 waves per SIMD) and does not wait for a free one.
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate) {
-  (void)d;
-  hipLaunchKernelGGL(kCompact, dim3(1), dim3(1024), 0, st, dd, accumulate ? 1 : 0);
+  const int nt = d.G <= 256 * CP_VEC ? 256 : 1024;
+  hipLaunchKernelGGL(kCompact, dim3(1), dim3(nt), 0, st, dd, accumulate ? 1 : 0);
   KC_HIP(hipGetLastError());
 }
 
