@@ -67,3 +67,8 @@ def test_trained_net_runs_on_device_kernel():
           "| max |ref|", np.abs(ref).max())
     assert err_acc <= 1e-3
     assert err16 <= 2e-3 * max(1.0, float(np.abs(ref).max()))
+    # the fast (fp16-operand) path against fp32 on a trained net: fp16 rounding of the
+    # weights and activations moves the logits by ~1e-3 of the largest logit (DESIGN.md
+    # section 5: 7e-3 measured on logits up to 6.4); bound asserted at 3e-3 of it.  The
+    # absolute 1e-3 of north_star is met by the accurate path above.
+    assert err <= 3e-3 * max(1.0, float(np.abs(ref).max()))
