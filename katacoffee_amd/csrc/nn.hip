@@ -186,7 +186,10 @@ KC_D void stageTapDma(const h16x8* __restrict__ src, uint32_t slotAddr, int ch, 
 // slots that the previous pair's barrier freed; the barrier before the pair's last
 // K-step retires every wave's pieces of the next pair (vmcnt 0: nothing newer is in
 // flight) and frees this pair's slots -- one barrier per two taps instead of one per tap.
-template <class G, int NTAPS, int NCB, int PAR = 0, int DBG = 0>
+// ENTRY = false: the caller already retired its DMA (waitVm<0>) before the barrier that
+// published the conv's input, which then also publishes the first taps (one barrier
+// fewer per conv).
+template <class G, int NTAPS, int NCB, int PAR = 0, int DBG = 0, bool ENTRY = true>
 KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                     f32x4 (&acc)[G::MAXT][G::NCT], const int (&ab)[G::MAXT], int cg, int lane, int tid,
                     const h16x8* __restrict__ wNext, int chNext, int nextTaps, int g0 = 0) {
@@ -198,7 +201,7 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   const uint32_t ring = ldsAddr(wl);
   // ring slot of local tap t (the 3-slot ring's taps start at slot 0 in every conv)
   auto slotOf = [&](int tap) { return G::PAIRS ? (g0 + tap) & 3 : tap % 3; };
-  if(!(DBG & 256)) {
+  if(ENTRY && !(DBG & 256)) {
     waitVm<0>();
     __syncthreads();
   }
@@ -486,13 +489,17 @@ KC_D void poolBoards(const float* scr, const float* vsrc, float* poolP, float* p
 
 // out[b*ostr + o] = f(bias[o] + sum_i wT[i*O + o] * in[b*96 + i]) for every board,
 // O % 4 == 0, wT staged transposed in LDS.  A lane owns 4 consecutive outputs and
-// a quarter of the 96 inputs; the quarters are reduced across adjacent lanes.
+// a quarter of the 96 inputs; the quarters are reduced across lanes.
+// O = 32 or 64 (the gpool and value linears): lanes run over the outputs first, then
+// the quarter, then the board, so each 16-lane ds_read_b128 group reads 16 consecutive
+// float4 (conflict-free; quarter-major lanes put the 4 quarters of an output on one
+// bank: 4-way conflicts) and the quarters, O/4 lanes apart, are reduced by DPP /
+// permlane swaps -- in the same order, (q0 + q1) + (q2 + q3), as the fallback below.
 template <class G>
 KC_D void linear96(const float* wT, int O, const float* in, float* out, int ostr, const float* bias, bool relu,
                    int tid) {
   const int quads = O >> 2;
-  for(int idx = tid; idx < G::NB * quads * 4; idx += G::NT) {
-    const int ks = idx & 3, q = (idx >> 2) % quads, b = (idx >> 2) / quads;
+  auto dot = [&](int q, int ks, int b) {
     float4 s = float4{0.0f, 0.0f, 0.0f, 0.0f};
     const float* xi = in + b * 96 + ks * 24;
     const float* wi = wT + (ks * 24) * O + 4 * q;
@@ -505,6 +512,56 @@ KC_D void linear96(const float* wT, int O, const float* in, float* out, int ostr
       s.z += w4.z * xv;
       s.w += w4.w * xv;
     }
+    return s;
+  };
+  auto emit = [&](const float4& s, int q, int b) {
+    float r[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for(int j = 0; j < 4; j++) {
+      float v = bias ? bias[4 * q + j] + r[j] : r[j];
+      out[b * ostr + 4 * q + j] = relu ? fmaxf(v, 0.0f) : v;
+    }
+  };
+  auto add2 = [](float& x, int lvl) {  // x += x of the lane 16 (lvl 1) / 32 (lvl 0) apart
+    int a0, a1;
+    if(lvl == 0)
+      swapPair<0>(bitsF(x), a0, a1);
+    else
+      swapPair<1>(bitsF(x), a0, a1);
+    x = asF(a0) + asF(a1);
+  };
+  if(quads == 16 || quads == 8) {
+    const int per = 4 * quads;  // lanes per board: a whole wave (O 64) or half of one (O 32)
+    for(int idx = tid; idx < G::NB * per; idx += G::NT) {
+      const int q = idx & (quads - 1), ks = (idx / quads) & 3, b = idx / per;
+      float4 s = dot(q, ks, b);
+      if(quads == 16) {
+        add2(s.x, 1);
+        add2(s.y, 1);
+        add2(s.z, 1);
+        add2(s.w, 1);
+        add2(s.x, 0);
+        add2(s.y, 0);
+        add2(s.z, 0);
+        add2(s.w, 0);
+      } else {
+        s.x += asF(partner<2>(bitsF(s.x)));  // lane ^8 (row rotation by 8)
+        s.y += asF(partner<2>(bitsF(s.y)));
+        s.z += asF(partner<2>(bitsF(s.z)));
+        s.w += asF(partner<2>(bitsF(s.w)));
+        add2(s.x, 1);
+        add2(s.y, 1);
+        add2(s.z, 1);
+        add2(s.w, 1);
+      }
+      if(ks == 0)
+        emit(s, q, b);
+    }
+    return;
+  }
+  for(int idx = tid; idx < G::NB * quads * 4; idx += G::NT) {
+    const int ks = idx & 3, q = (idx >> 2) % quads, b = (idx >> 2) / quads;
+    float4 s = dot(q, ks, b);
     // quarters reduced over lanes ^1 then ^2 (DPP quad permutes)
     s.x += asF(partner<5>(bitsF(s.x)));
     s.y += asF(partner<5>(bitsF(s.y)));
@@ -514,14 +571,8 @@ KC_D void linear96(const float* wT, int O, const float* in, float* out, int ostr
     s.y += asF(partner<4>(bitsF(s.y)));
     s.z += asF(partner<4>(bitsF(s.z)));
     s.w += asF(partner<4>(bitsF(s.w)));
-    if(ks == 0) {
-      float r[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-      for(int j = 0; j < 4; j++) {
-        float v = bias ? bias[4 * q + j] + r[j] : r[j];
-        out[b * ostr + 4 * q + j] = relu ? fmaxf(v, 0.0f) : v;
-      }
-    }
+    if(ks == 0)
+      emit(s, q, b);
   }
 }
 
@@ -620,6 +671,7 @@ __global__ void __launch_bounds__(512, 2)
       }
     }
   }
+  waitVm<0>();  // the stem's first taps (convTiles skips its entry barrier)
   __syncthreads();
 
   NN_PHASE(1);
@@ -628,7 +680,7 @@ __global__ void __launch_bounds__(512, 2)
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
+  convTiles<G, 9, 1, 0, 0, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                         L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
                         L->nblocks > 0 ? 9 : 1, 0);
   {
@@ -660,13 +712,14 @@ __global__ void __launch_bounds__(512, 2)
     NN_PHASE(3 + 4 * blk);
     const float* P = prm + (blk & 1) * G::NPRM;
     storeBnRelu<G>(act, rowPa, acc, P, P + 96, tstart, cg, lane);
+    waitVm<0>();
     __syncthreads();
     zeroAcc<G>(acc);
 #pragma unroll
     for(int j = 0; j < NPK; j++)
       pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
-    convTiles<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
+    convTiles<G, 9, G::C / 32, 1, 0, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
                                   (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, 9, 9 + 18 * blk);
 #pragma unroll
     for(int j = 0; j < NPK; j++)
@@ -687,9 +740,10 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++)
           acc[t][ct] = tr[t][ct];
+      waitVm<0>();
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+      convTiles<G, 9, G::C / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                     3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
@@ -775,9 +829,10 @@ __global__ void __launch_bounds__(512, 2)
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++)
           acc[t][ct] = tr[t][ct];
+      waitVm<0>();
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+      convTiles<G, 9, (G::C - 32) / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                            3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
@@ -788,10 +843,11 @@ __global__ void __launch_bounds__(512, 2)
   NN_PHASE(40);
   const float* PT = prm + (L->nblocks & 1) * G::NPRM;  // tip slab
   storeBnRelu<G>(act, rowPa, acc, PT, PT + 96, tstart, cg, lane);
+  waitVm<0>();
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0, 9 + 18 * L->nblocks);
+  convTiles<G, 1, G::C / 32, 1, 0, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0, 9 + 18 * L->nblocks);
   __syncthreads();  // act dead from here: f32 [MROWS][SCR] value branch at actF, g branch at scr
   NN_PHASE(41);
   {
