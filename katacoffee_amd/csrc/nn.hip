@@ -5,18 +5,21 @@
 // GlobalPoolingResidualBlock :935-1015, Trunk :1169-1227, PolicyHead :1229-1299,
 // ValueHead :1301-1377), Coffee head contract nninputs.h:75-118.
 //
-// MI355X design (DESIGN.md "NN forward"):
-//  * one 512-thread workgroup (8 waves) per 8 boards = 200 rows (positions),
-//    204 VGPRs -> 2 waves/SIMD, one resident workgroup per CU (LDS ~80 KB);
+// MI355X design ("The fused network at C2 batch sizes"):
+//  * one 512-thread workgroup (8 waves, 2 per SIMD, one workgroup per CU) per 8
+//    boards, or per 5 boards when the batch fits 5 per CU (125 positions in the 128
+//    rows the waves compute; 185 VGPRs, so one search wave of the other game group
+//    still fits on each SIMD beside it);
 //  * 3x3 convolutions are implicit GEMMs on v_mfma_f32_16x16x32_f16 (fp16
 //    operands, f32 accumulation; same rate as bf16 on gfx950, 3 more mantissa
-//    bits, so logits stay within 1e-3 of the fp32 reference):
-//    A = activations gathered from LDS by neighbour offset (fp16, NHWC, padded
-//    rows -> conflict-free ds_read_b128), B = weights pre-swizzled on the host
-//    into per-lane 16-byte fragments streamed from L2 (one dwordx4 per lane);
-//  * the f32 residual trunk lives in the accumulators between blocks and is
-//    parked in a workgroup-private L2-resident scratch during each block's first
-//    conv; only the fp16 conv input is staged through LDS;
+//    bits), computed transposed (weights x activations):
+//    A = activations gathered from LDS by neighbour offset (fp16, NHWC, zero-bordered
+//    boards, conflict-free ds_read_b128), B = weights pre-swizzled on the host into
+//    per-lane 16-byte fragments streamed into an LDS ring by LDS-DMA across the
+//    convolution boundaries;
+//  * the f32 residual trunk lives in the accumulators between blocks; during each
+//    block's first conv it is parked in registers (5-board instance) or in a
+//    workgroup-private L2-resident scratch (8-board instance);
 //  * BN + ReLU, global pooling, the gpool bias and both heads are fused epilogues.
 // Waves: rg = wave>>1 owns a contiguous range of 16-row tiles, cg = wave&1 owns
 // half of the output channels.
@@ -41,8 +44,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int SPLIT_ = 0>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
-  // boards per workgroup: 8, or 4 for batches of at most 4 per CU; one 8-wave
-  // workgroup per CU, 2 waves per SIMD (tools/conv_bench.hip measured the alternatives:
+  // boards per workgroup: 8, or NN_SMALL_NB (5) for batches of at most 5 per CU; one
+  // 8-wave workgroup per CU, 2 waves per SIMD (tools/conv_bench.hip measured the alternatives:
   // 2 boards on 4 waves at two workgroups per CU streams every weight twice per CU, and
   // 4 boards on 4 waves with one wave per SIMD cuts the LDS reads per MFMA by 30 % but
   // exposes every LDS and barrier latency: both slower)
@@ -55,7 +58,7 @@ struct NNGeo {
   static constexpr bool SPLIT = SPLIT_ != 0;
   static constexpr int PLANES = SPLIT ? 2 : 1;
   // weight ring slots.  3 (8-board and SPLIT instances, whose LDS holds no more): tap
-  // k+2 is requested at the start of tap k, one barrier per tap.  4 (4-board
+  // k+2 is requested at the start of tap k, one barrier per tap.  4 (small-batch
   // instance): taps move in pairs (g, g+1), g even in the stream's global tap count;
   // pair j+1 is requested at the start of pair j and published by one barrier per pair.
   // (6 slots, one barrier per 3 taps, would fill all 160 KiB and keep the other game
@@ -85,7 +88,7 @@ struct NNGeo {
   static constexpr int ACT_BYTES = PLANES * PLANE_BYTES;
   // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
-  // (at least the gpool linear weights' [96][64] f32, staged below it, for 4 boards)
+  // (at least the gpool linear weights' [96][64] f32, staged below it)
   static constexpr int OFF_SCR = MROWS * SCR * 4 > 96 * 64 * 4 ? MROWS * SCR * 4 : 96 * 64 * 4;
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
@@ -322,7 +325,7 @@ template <class G>
 KC_D f32x4* trunkBase(float* trunk, int wave, int lane) {
   return reinterpret_cast<f32x4*>(trunk) + ((size_t)blockIdx.x * G::NW + wave) * (G::MAXT * G::NCT * 64) + lane;
 }
-// With at most 2 x 3 accumulator tiles per wave (the 4-board instance: 184 VGPRs) the
+// With at most 2 x 3 accumulator tiles per wave (the small-batch instance: 185 VGPRs) the
 // parked trunk fits in 24 more registers (< 256, no spill): kept in `reg`, no scratch.
 template <class G>
 constexpr bool regTrunk() {

@@ -1,5 +1,5 @@
 // Steady-state cycles of the network's 96->96 3x3 convolution (convTiles) and of
-// stripped variants for each fused-kernel instance (8 / 4 boards on 8 waves, one
+// stripped variants for each fused-kernel instance (8 / 5 boards on 8 waves, one
 // workgroup per CU).
 //   real      : convTiles as shipped (LDS weight ring + barriers + fragment loads)
 //   nobar     : same loads, weights read from a fixed LDS slot, no ring stores/barriers
@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(G::NT, 2) kConv(const h16x8* __restrict__ w, c
   for(int r = 0; r < REPS; r += 2) {
     if(MODE == 0 || MODE >= 3) {
       // the stream's last taps re-request this conv's first taps for the next rep; two
-      // reps per iteration so the 4-board instance's tap pairs alternate as in the
+      // reps per iteration so the small-batch instance's tap pairs alternate as in the
       // network (conv1 starts at an odd stream tap, conv2 at an even one)
       constexpr int DBG = kDbg[MODE];
       convTiles<G, 9, 3, 1, DBG>(act, w, wl, acc, ab, cg, lane, tid, w, 3 * G::NCT_ALL, 9, 9 + 9 * r);
@@ -154,7 +154,7 @@ int main() {
   KC_HIP(hipMalloc(&w, hw.size() * 2));
   KC_HIP(hipMemcpy(w, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
   runAll<G8>(1, w);
-  runAll<NNGeo<5, 5, 96, 4, 0>>(1, w);
+  runAll<NNGeo<5, 5, 96, NN_SMALL_NB, 0>>(1, w);
 
   return 0;
 }

@@ -10,7 +10,7 @@
 using namespace kc;
 
 int main(int argc, char** argv) {
-  const int n = argc > 1 ? atoi(argv[1]) : 4096;  // <= 4 x CUs: the 4-board instance
+  const int n = argc > 1 ? atoi(argv[1]) : 4096;  // <= 5 x CUs: the small-batch (5-board) instance
   ModelHost m = randomModel(modelCfgByName("b6c96"), 1);
   NNEngine eng(m, 5, 5, 4);
   const int words = (15 * 25 + 63) / 64;
