@@ -87,9 +87,7 @@ def parse():
                     help="steady: warm-up past the first game ends, value = rows written/s; short: value = moves/s "
                          "(default: steady except C5)")
     ap.add_argument("--precision", choices=["fast", "accurate", "fast-layered"], default="fast")
-    # 16: a game whose search is done waits at most 15 rounds for its move; half the
-    # commit / row launches of 8 on every group's round chain (+1.2 % rows/s at C2)
-    ap.add_argument("--commit-interval", type=int, default=16)
+    ap.add_argument("--commit-interval", type=int, default=8)
     ap.add_argument("--nn-cache-log2", type=int, default=21,
                     help="NN evaluation cache entries = 2^k (selfplay1.cfg nnCacheSizePowerOfTwo = 21); 0 = off")
     ap.add_argument("--nn-batch-cap", type=int, default=0,
@@ -262,16 +260,19 @@ class Groups:
     deterministic as a single engine.  Each group's round is still its own serial
     chain select -> compact -> network -> backup; two groups overlap those chains."""
 
-    def __init__(self, kc, k, games, slot_base, **kw):
+    def __init__(self, kc, k, games, slot_base, chunk=8, **kw):
+        self.chunk = chunk
         # floor / ceil shares over contiguous slot ranges (any k <= games)
         sizes = [games // k + (1 if i < games % k else 0) for i in range(k)]
         starts = [slot_base + sum(sizes[:i]) for i in range(k)]
         self.g = [kc.Selfplay(num_games=n, slot_base=s0, **kw) for n, s0 in zip(sizes, starts)]
 
-    def step(self, rounds, chunk=8):
+    def step(self, rounds):
+        # chunks of the commit interval: an engine's step() also commits on its last
+        # round, so shorter chunks would commit more often than the interval asks
         done = 0
         while done < rounds:
-            n = min(chunk, rounds - done)
+            n = min(self.chunk, rounds - done)
             for e in self.g:
                 e.step(n)
             done += n
@@ -372,7 +373,7 @@ def main():
         args.groups = 2 if cfg["arch"] != "b18c384nbt" else 1
     # nn_batch_cap 0: the engines split the fused network's one wave of workgroups
     # (engines_per_device); the layered network has no batch cap (its cost grows with the batch)
-    sp = Groups(kc, args.groups, games, rank * games, X=X, Y=Y, W=W, max_visits=visits, seed=args.seed,
+    sp = Groups(kc, args.groups, games, rank * games, chunk=args.commit_interval, X=X, Y=Y, W=W, max_visits=visits, seed=args.seed,
                 model_path=model_path, commit_interval=args.commit_interval, nn_cache_log2=args.nn_cache_log2,
                 nn_batch_cap=args.nn_batch_cap // args.groups, nn_precision=args.precision, start_stagger=stagger,
                 node_cap=node_cap, engines_per_device=args.groups, **play)
