@@ -277,7 +277,7 @@ static void runGpu(int gpu, int server, int perGpu, int slot, int share, const S
   c.nn_batch_cap = 0;
   c.engines_per_device = perGpu;
   c.use_fake_net = 0;
-  c.commit_interval = 8;
+  c.commit_interval = 16;  // moves committed every 16 rounds (bench.py's default)
   c.model_path = model.c_str();
   c.search = s.sp;
   c.nn_cache_log2 = s.nnCacheLog2;
