@@ -108,16 +108,25 @@ def parse():
                          "bytes over RCCL; every engine switches (the reference's model hot reload)")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
-    ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
-    ap.add_argument("--cpu-c1-seconds", type=float, default=30.0, help="timed CPU-baseline window (C1 run)")
-    ap.add_argument("--cpu-warmup-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=40.0, help="timed CPU-baseline window (saturated run)")
+    ap.add_argument("--cpu-c1-seconds", type=float, default=20.0,
+                    help="timed CPU-baseline window (C1 and single-thread runs)")
+    ap.add_argument("--cpu-warmup-seconds", type=float, default=5.0)
+    ap.add_argument("--cpu-whole-host", action="store_true",
+                    help="also time the CPU baseline on every CPU of the affinity mask (default: extrapolated, "
+                         "since the GPU box asks to stay within its CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP event timing")
     ap.add_argument("--timing-every", type=int, default=16,
                     help="time every N-th launch of each kernel group (an event pair costs a few us of stream gap)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from a PMC pass (see profiles/)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.commit_interval < 1:
+        ap.error("--commit-interval must be >= 1")
+    if args.groups < 0 or args.steps < 1 or args.warmup < 0:
+        ap.error("--groups >= 0, --steps >= 1, --warmup >= 0")
+    return args
 
 
 def free_port():
@@ -144,13 +153,26 @@ def launch_ranks(n, script=None, argv=None):
     return max(rcs, key=abs)
 
 
+def physical_cores(cpus):
+    """Physical cores behind a set of logical CPUs (SMT siblings counted once)."""
+    cores = set()
+    for c in cpus:
+        try:
+            sib = open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c).read().strip()
+        except OSError:
+            sib = str(c)
+        cores.add(sib)
+    return len(cores)
+
+
 def cpu_info():
     """Threads the CPU baseline uses: OMP_NUM_THREADS (the GPU box sets 16, its CPU share
-    per GPU), else the affinity mask; the machine's totals are reported beside it."""
-    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    per GPU, and asks that worker pools stay within it), else the affinity mask; the
+    machine's totals (logical CPUs, physical cores) are reported beside it."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if cores <= 0:
-        cores = affinity
+        cores = len(aff)
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -159,7 +181,9 @@ def cpu_info():
                 break
     except OSError:
         pass
-    return cores, model, {"nproc": os.cpu_count(), "affinity": affinity,
+    n = os.cpu_count()
+    return cores, model, {"nproc": n, "affinity": len(aff), "physical_cores": physical_cores(range(n)),
+                          "affinity_physical_cores": physical_cores(aff),
                           "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
@@ -192,21 +216,45 @@ def cpu_baseline(args, cfg, model_path):
     from oracle import oracle
     cores, model_name, machine = cpu_info()
     model = oracle.Model(model_path)
+    visits = args.visits or cfg["visits"]
+    run = lambda games, v, threads, secs: cpu_run(oracle, model, cfg["X"], cfg["Y"], cfg["W"], games, v, threads,
+                                                  args.cpu_warmup_seconds, secs, args.nn_cache_log2)
     c1 = None
     if cfg["arch"] == "b6c96" and (cfg["X"], cfg["Y"]) == (5, 5):
-        c1 = cpu_run(oracle, model, 5, 5, 4, 1, 200, 1, args.cpu_warmup_seconds, args.cpu_c1_seconds,
-                     args.nn_cache_log2)
-    sat = cpu_run(oracle, model, cfg["X"], cfg["Y"], cfg["W"], 4 * cores, args.visits or cfg["visits"], cores,
-                  args.cpu_warmup_seconds, args.cpu_seconds, args.nn_cache_log2)
+        c1 = run(1, 200, 1, args.cpu_c1_seconds)
+    sat = run(4 * cores, visits, cores, args.cpu_seconds)
+    one = run(4, visits, 1, args.cpu_c1_seconds) if cores > 1 else sat
+    eff = sat["rows_per_sec"] / (cores * one["rows_per_sec"]) if one["rows_per_sec"] > 0 else None
+    desc = lambda r, g, t: ("%d games x %d visits on %d threads, %.0f s warm-up then %d rounds in %.1f s "
+                            "(%d moves, %d playouts)" % (g, visits, t, args.cpu_warmup_seconds, r["rounds"],
+                                                         r["seconds"], r["moves"], r["playouts"]))
     out = {
         "value": sat["rows_per_sec"], "unit": "rows/s", "cores": cores, "kind": "port",
         "playouts_per_sec": sat["playouts_per_sec"], "nn_evals_per_sec": sat["nn_evals_per_sec"],
         "cpu_model": model_name, "host_cpus": machine,
-        "sample": "oracle C++ self-play (fp32 im2col+SGEMM forward), %s workload on %d threads: %d games x %d visits, "
-                  "%.0f s warm-up then %d rounds in %.1f s (%d moves, %d playouts)"
-                  % (cfg["label"].split(":")[0], cores, 4 * cores, args.visits or cfg["visits"],
-                     args.cpu_warmup_seconds, sat["rounds"], sat["seconds"], sat["moves"], sat["playouts"]),
+        "sample": "oracle C++ self-play (fp32 im2col+SGEMM forward), %s workload, %s"
+                  % (cfg["label"].split(":")[0], desc(sat, 4 * cores, cores)),
+        "single_thread": {"rows_per_sec": one["rows_per_sec"], "sample": desc(one, 4, 1),
+                          "scaling_efficiency_at_%d" % cores: eff},
     }
+    # Whole host (all physical cores, numGameThreads = 2 x cores).  The GPU box
+    # asks that worker pools stay within its CPU share (16 threads per GPU), so by default
+    # the whole-host figure is extrapolated from the share's measured rate, linearly over
+    # every logical CPU of the machine: SMT siblings counted as full cores and no loss of
+    # scaling, i.e. an upper bound on the CPU (a lower bound on the GPU/CPU ratio).
+    # --cpu-whole-host measures it instead (threads = the affinity mask, 2 x threads games).
+    nproc = machine["nproc"] or cores
+    if args.cpu_whole_host:
+        t = machine["affinity"]
+        wh = run(2 * t, visits, t, args.cpu_seconds)
+        out["whole_host"] = {"value": wh["rows_per_sec"], "unit": "rows/s", "threads": t, "kind": "measured",
+                             "physical_cores": machine["physical_cores"], "sample": desc(wh, 2 * t, t)}
+    else:
+        out["whole_host"] = {"value": sat["rows_per_sec"] * nproc / cores, "unit": "rows/s", "threads": nproc,
+                             "physical_cores": machine["physical_cores"], "kind": "extrapolated",
+                             "method": "measured %d-thread rate x %d logical CPUs / %d (linear, SMT counted as cores; "
+                                       "measured 1->%d thread efficiency %s)"
+                                       % (cores, nproc, cores, cores, "%.2f" % eff if eff else "n/a")}
     if c1:
         out["C1"] = {"rows_per_sec": c1["rows_per_sec"], "playouts_per_sec": c1["playouts_per_sec"], "threads": 1,
                      "sample": "1 game x 200 visits, b6c96 fp32, %.0f s warm-up then %.1f s (%d moves, %d playouts)"
@@ -287,7 +335,7 @@ class Groups:
         out = {}
         for e in self.g:
             for k, v in e.stats().items():
-                out[k] = out.get(k, 0) + v
+                out[k] = max(out.get(k, 0), v) if k in ("edge_pool_peak", "edge_pool_cap") else out.get(k, 0) + v
         return out
 
     def drain_rows(self):
@@ -555,7 +603,10 @@ def main():
             "cpu_baseline": cpu,
         }
         if cpu and cpu["value"] > 0:
-            out["speedup_vs_cpu"] = rows_per_sec / cpu["value"]
+            # against the whole host; the share's own ratio beside it
+            out["speedup_vs_cpu"] = rows_per_sec / cpu["whole_host"]["value"]
+            out["speedup_vs_cpu_basis"] = "whole host, %s" % cpu["whole_host"]["kind"]
+            out["speedup_vs_cpu_share"] = rows_per_sec / cpu["value"]
         print(json.dumps(out), flush=True)
     sp.close()
     shutil.rmtree(tmpdir, ignore_errors=True)

@@ -246,6 +246,10 @@ typedef struct coffee_selfplay_stats {
   uint64_t tree_levels;     /* tree levels descended by all playouts (path nodes) */
   uint64_t tree_children;   /* children scanned at those path nodes (select reads each
                                path node and its k children; backup re-aggregates them) */
+  uint64_t errors_node_pool; /* slots whose node pool ran out (part of errors) */
+  uint64_t errors_edge_pool; /* slots whose edge pool (children past 16 per node) ran out */
+  uint64_t edge_pool_peak;  /* largest edge-pool use of any slot so far (entries) */
+  uint64_t edge_pool_cap;   /* edge-pool entries per slot and buffer */
 } coffee_selfplay_stats;
 
 int coffee_selfplay_create(const coffee_selfplay_config* cfg, coffee_selfplay** out);

@@ -306,7 +306,7 @@ static void runGpu(int gpu, int server, int perGpu, int slot, int share, const S
   std::vector<int32_t> ghdr((size_t)gchunk * 4);
   std::vector<uint8_t> gmv((size_t)gchunk * A * 2);
   uint64_t lastGames = 0;
-  int64_t filesBefore = 0, rowsBefore = 0;
+  int64_t filesBefore = 0, rowsBefore = 0, rowsDrained = 0;
   auto t0 = std::chrono::steady_clock::now();
   auto drainAll = [&]() {
     int got = 0;
@@ -314,8 +314,10 @@ static void runGpu(int gpu, int server, int perGpu, int slot, int share, const S
       check(coffee_selfplay_drain_rows(h, chunk, bin.data(), glob.data(), pol.data(), gt.data(), val.data(),
                                        meta.data(), &got),
             "drain");
-      if(got > 0)
+      if(got > 0) {
         sink.append(got, bin.data(), glob.data(), pol.data(), gt.data(), val.data());
+        rowsDrained += got;
+      }
     } while(got == chunk);
     check(coffee_selfplay_drain_games(h, gchunk, ghdr.data(), gmv.data(), &got), "drain games");
     games.write(got, ghdr.data(), gmv.data());
@@ -352,9 +354,12 @@ static void runGpu(int gpu, int server, int perGpu, int slot, int share, const S
     gGamesDone += (int64_t)(st.games_finished - lastGames);
     lastGames = st.games_finished;
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    logf("gpu %d.%d: %llu games, %llu moves, %.1f rows/s, %.3g playouts/s, %llu rows dropped", gpu, server,
-         (unsigned long long)st.games_finished, (unsigned long long)st.moves, st.moves / secs, st.playouts / secs,
-         (unsigned long long)st.rows_dropped);
+    // rows/s counts the training rows drained for the .npz files (after weight
+    // resolution: cheap searches, surprise weighting and side positions make it differ
+    // from moves/s)
+    logf("gpu %d.%d: %llu games, %llu moves, %lld rows, %.1f rows/s, %.1f moves/s, %.3g playouts/s, %llu rows dropped",
+         gpu, server, (unsigned long long)st.games_finished, (unsigned long long)st.moves, (long long)rowsDrained,
+         rowsDrained / secs, st.moves / secs, st.playouts / secs, (unsigned long long)st.rows_dropped);
     if(s.maxGamesTotal >= 0 && gGamesDone >= s.maxGamesTotal)
       gStop = true;
   }

@@ -1183,9 +1183,12 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
                              G4::LDS));
   KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GS::LDS));
-  // A/B runs only: KATACOFFEE_NN_SMALL=8 runs small batches on the 8-board instance too
+#ifdef KC_AB_HOOKS
+  // A/B builds only (tools/Makefile alt, -DKC_AB_HOOKS): KATACOFFEE_NN_SMALL=8 runs small
+  // batches on the 8-board instance too; the product library never reads the variable
   const char* small = getenv("KATACOFFEE_NN_SMALL");
   small_ = small ? atoi(small) : 0;
+#endif
   int dev = 0;
   KC_HIP(hipGetDevice(&dev));
   KC_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev));

@@ -33,13 +33,22 @@ constexpr int INLINE_EDGES = 16;
 KC_HD int edgeBlockCap(int k, int P) {
   return (P > 64 && k <= 64) ? 64 - INLINE_EDGES : P - INLINE_EDGES;
 }
-// Pool entries per buffer for node cap `cap`.  A node with k > 16 children holds 48
-// entries, or 48 + P - 16 once k > 64 (the abandoned 48-block included); only nodes
-// with more than 16 visits have more than 16 children, so a search of V <= cap visits
-// has few of them (C5, 1600 visits at 9x9: the root's block and tens of 48-blocks,
-// a few thousand entries against 4 cap).  Exhaustion is counted as a device error
-// (coffee_selfplay_stats.errors), like node-pool exhaustion; it never writes out of bounds.
-inline int edgePoolCapFor(int cap, int P) { return 4 * cap + 2 * P; }
+// Pool entries per buffer for node cap `cap`, bounded through the edges: a node with
+// k > 16 children holds 48 entries (<= 48/17 per edge), or 48 + P - 16 once k > 64
+// (the abandoned 48-block included: <= (32 + P)/65 per edge, 5.5 at 9x9).  Every edge
+// is one expansion of a playout and leads to a node or, with graph search, to a
+// transposition of one, so a tree holds about as many edges as nodes; the pool takes
+// max(48/17, (32 + P)/65) entries for each of 1.5 x cap edges (half again for
+// transposition edges) plus two root-sized blocks.  Measured use is far below (only
+// nodes with more than 16 visits have more than 16 children): coffee_selfplay_stats
+// reports the high-water mark.  Exhaustion is counted as a device error of its own
+// (errors_edge_pool), like node-pool exhaustion; it never writes out of bounds.
+inline int edgePoolCapFor(int cap, int P) {
+  const double perEdge = (32.0 + P) / 65.0 > 48.0 / 17.0 ? (32.0 + P) / 65.0 : 48.0 / 17.0;
+  return (int)(perEdge * 1.5 * cap) + 2 * P;
+}
+// GameDev::err codes (coffee_selfplay_stats.errors counts slots with any of them)
+enum { ERR_NODE_POOL = 1, ERR_NO_CANDIDATE = 2, ERR_EDGE_POOL = 3 };
 constexpr int MAX_LANE_ITEMS = (MAX_P + 63) / 64;  // 7
 
 enum LeafKind {
@@ -214,6 +223,7 @@ struct GameDev {
   int32_t rootIdx, liveCount, freeTop, pathLen;
   int32_t gameNum, numTurns, svbSel, err;
   int32_t edgeSel, edgeTop;       // current edge-pool buffer, its first free slot
+  int32_t edgePeak, pad0;         // edge-pool high-water mark (stats)
   float accWin, accLoss, rawWin, rawLoss;
 };
 

@@ -290,7 +290,7 @@ KC_D uint64_t svbKeyOf(const GV& v, const DBoard& before, int parentPrevPos, int
 // freeIdx: freeList[freeTop - 1] when the caller loaded it ahead, else -1.
 KC_D int allocNode(const GV& v, GameDev& s, int nextPla, uint64_t k0, uint64_t k1, bool terminal, int freeIdx = -1) {
   if(s.freeTop <= 0) {
-    s.err = 1;
+    s.err = ERR_NODE_POOL;
     return -1;
   }
   s.freeTop--;
@@ -984,16 +984,19 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
       // allocated (16 -> 64 slots) or grown (-> P) here; pool exhaustion ends the
       // descent like node-pool exhaustion (a counted device error)
       uint32_t ebase = n.edgeBase;
+      int reserved = 0;  // pool entries taken for this expansion (returned if it fails)
       if(slot == INLINE_EDGES || (slot == 64 && v.d.P > 64)) {
         const int need = edgeBlockCap(slot + 1, v.d.P);
         if(s.edgeTop + need > v.d.edgePoolCap) {
-          s.err = 1;
+          s.err = ERR_EDGE_POOL;
           s.leafKind = LEAF_NOCHILD;
           s.leafNode = ni;
           break;
         }
         const uint32_t nb = (uint32_t)s.edgeTop;
         s.edgeTop += need;
+        s.edgePeak = max(s.edgePeak, s.edgeTop);
+        reserved = need;
         if(slot > INLINE_EDGES) {
           Edge* pool = v.edgePool();
           for(int i = v.lane; i < slot - INLINE_EDGES; i += 64)
@@ -1020,6 +1023,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
       if(fresh) {
         child = allocNode(v, s, b.pla, k0, k1, b.finished != 0, freeIdx);
         if(child < 0) {
+          s.edgeTop -= reserved;  // the block was never linked to the node
           s.leafKind = LEAF_NOCHILD;
           s.leafNode = ni;
           break;
@@ -2272,6 +2276,7 @@ KC_D void reuseTree(const GV& v, GameDev& s, int chosenPos, uint32_t* liveBits, 
     waveSync();
     s.edgeSel = nsel2;
     s.edgeTop = top;
+    s.edgePeak = max(s.edgePeak, top);
     v.setEdgeSel(nsel2);
   }
   waveSync();
@@ -3225,7 +3230,7 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
   // play.cpp:1040-1046), not for a side position's response (:1590)
   int n = playSelectionValues<NI>(v, *v.sp, s, 0.0f, true, posv, vals, side ? sp.useLcb != 0 : false);
   if(n <= 0) {
-    s.err = 2;
+    s.err = ERR_NO_CANDIDATE;
     n = 1;
     posv[0] = 0;
   }

@@ -360,6 +360,9 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
     out.moves += x.moves;
     out.games_finished += x.gamesFinished;
     out.errors += x.err != 0 ? 1 : 0;
+    out.errors_node_pool += x.err == ERR_NODE_POOL ? 1 : 0;
+    out.errors_edge_pool += x.err == ERR_EDGE_POOL ? 1 : 0;
+    out.edge_pool_peak = std::max<uint64_t>(out.edge_pool_peak, (uint64_t)x.edgePeak);
     out.tree_levels += x.treeLevels;
     out.tree_children += x.treeChildren;
   }
@@ -372,9 +375,13 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
   unsigned long long gdrop = 0;
   KC_HIP(hipMemcpy(&gdrop, hd_.gDropped, 8, hipMemcpyDeviceToHost));
   out.games_dropped = gdrop;
+  out.edge_pool_cap = (uint64_t)hd_.edgePoolCap;
   if(out.errors)
     throw InternalError("self-play device invariant violated in " + std::to_string(out.errors) +
-                        " game slot(s) (node pool exhausted or no move candidate; raise node_cap)");
+                        " game slot(s): " + std::to_string(out.errors_node_pool) + " node pool exhausted, " +
+                        std::to_string(out.errors_edge_pool) + " edge pool exhausted, " +
+                        std::to_string(out.errors - out.errors_node_pool - out.errors_edge_pool) +
+                        " without a move candidate (raise node_cap)");
 }
 
 int SelfplayEngine::drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, float* gt, int8_t* val,
