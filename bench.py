@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--window", choices=["steady", "short"], default=None,
                     help="steady: warm-up past the first game ends, value = rows written/s; short: value = moves/s "
                          "(default: steady except C5)")
-    ap.add_argument("--precision", choices=["fast", "accurate", "fast-layered"], default="fast")
+    ap.add_argument("--precision", choices=["fast", "accurate", "fast-layered", "corrected"], default="fast")
     # 16: a game whose search is done waits at most 15 rounds for its move, and every
     # group's round chain carries half the commit / row launches of 8 (C2: +2.4 %)
     ap.add_argument("--commit-interval", type=int, default=16)
@@ -524,8 +524,10 @@ def main():
         if net["launches_timed"]:
             per_launch = timed_evals / net["launches_timed"]
             achieved = per_launch * flops_per_eval / (net["avg_us"] * 1e-6) / 1e12
-            fused = args.precision in ("fast", "accurate") and cfg["arch"] == "b6c96"
-            mfma_factor = 3 if args.precision == "accurate" else 1
+            fused = args.precision in ("fast", "accurate", "corrected") and cfg["arch"] == "b6c96"
+            # MFMA work per model product, in fp16-MFMA equivalents: split pairs 3, corrected
+            # 1 fp16 + 2 cross terms on e4m3 MFMAs at twice the rate
+            mfma_factor = {"accurate": 3, "corrected": 2}.get(args.precision, 1)
             roof_all["network"] = {
                 "kernel": "kNNForward (fused %s forward)" % cfg["arch"] if fused else
                           "kConvL/kGpoolBias/kHeadsL (layered %s forward, one launch group)" % cfg["arch"],
@@ -574,13 +576,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp16" if args.precision != "accurate" else "fp16x2 (split hi/lo)",
+            "dtype": {"accurate": "fp16x2 (split hi/lo)",
+                      "corrected": "fp16 + e4m3 cross terms"}.get(args.precision, "fp16"),
             "data": "synthetic: self-play from empty %dx%d boards, random-init %s (seed 0xC0FFEE)" % (X, Y, cfg["arch"]),
             "config": {"workload": cfg["label"] + (" (%d games, %d visits)" % (games, visits)
                                                    if (games, visits) != (cfg["games"], cfg["visits"]) else ""),
                        "config": args.config, "games_per_gpu": games, "visits": visits, "arch": cfg["arch"],
                        "board": "%dx%d win %d" % (X, Y, W), "precision": args.precision,
-                       "network_path": "fused" if args.precision in ("fast", "accurate") and cfg["arch"] == "b6c96"
+                       "network_path": "fused" if args.precision in ("fast", "accurate", "corrected") and cfg["arch"] == "b6c96"
                        else "layered",
                        "rounds_per_step": rps, "window": window, "game_rounds_estimate": game_rounds,
                        "warmup_rounds": warm_rounds, "commit_interval": args.commit_interval,

@@ -106,11 +106,19 @@ int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_n
  *                           b6c96 @ 5x5; the layered kernels otherwise)
  *   COFFEE_NN_ACCURATE      fp16 hi/lo operand pairs on three MFMAs (the fused kernel's
  *                           split instance where it covers the net, the layered kernels
- *                           otherwise): logits within 1e-3 of the fp32 (Eigen-semantics) forward
- *   COFFEE_NN_FAST_LAYERED  fp16 operands on the layered kernels (any architecture) */
+ *                           otherwise): logits within ~1e-5 of the fp32 (Eigen-semantics) forward
+ *   COFFEE_NN_FAST_LAYERED  fp16 operands on the layered kernels (any architecture)
+ *   COFFEE_NN_CORRECTED     fp16 products plus the two fp16-rounding cross terms on
+ *                           block-scaled e4m3 MFMAs (twice the fp16 MFMA work, ~16x more
+ *                           accurate than fast: within 1e-3 of fp32 on trained nets); the
+ *                           fused kernel where it covers the net, else as ACCURATE
+ *   COFFEE_NN_ACCURATE_NB2  ACCURATE on the 2-board bordered fused instance (A/B reference
+ *                           of the borderless 5-board one; same results bit for bit) */
 #define COFFEE_NN_FAST 0
 #define COFFEE_NN_ACCURATE 1
 #define COFFEE_NN_FAST_LAYERED 2
+#define COFFEE_NN_CORRECTED 3
+#define COFFEE_NN_ACCURATE_NB2 4
 int coffee_nn_create2(const char* model_path, int x, int y, int win_len, int precision, coffee_nn** out);
 /* 1 when the handle runs the fused single-launch kernel, 0 for the layered kernels. */
 int coffee_nn_is_fused(coffee_nn* h, int* fused);
@@ -219,7 +227,7 @@ typedef struct coffee_selfplay_config {
                             ahead of new ones.  0 = one full wave of network workgroups
                             (compute units x 8 boards: 2048 on MI355X, / engines_per_device)
                             for the fused kernel, unbounded for the layered kernels */
-  int32_t nn_precision;  /* COFFEE_NN_FAST / _ACCURATE / _FAST_LAYERED (0 = fast) */
+  int32_t nn_precision;  /* COFFEE_NN_FAST / _ACCURATE / _FAST_LAYERED / _CORRECTED (0 = fast) */
   int32_t start_stagger; /* > 0: each slot idles a seeded number of rounds in [0, start_stagger)
                             before its first game (benchmarks: spreads game ends over the
                             run); 0 = all games start in round 0 */

@@ -23,7 +23,7 @@ CSRC = os.path.join(HERE, "csrc")
 NUM_SPATIAL = 15
 COFFEE_OK = 0
 # network precision / path (include/katacoffee.h COFFEE_NN_*)
-PRECISIONS = {"fast": 0, "accurate": 1, "fast-layered": 2}
+PRECISIONS = {"fast": 0, "accurate": 1, "fast-layered": 2, "corrected": 3, "accurate-nb2": 4}
 
 _lib = None
 

@@ -188,8 +188,7 @@ int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_n
 int coffee_nn_create2(const char* model_path, int x, int y, int win_len, int precision, coffee_nn** out) {
   return guarded([&] {
     need(model_path && out, "NULL argument");
-    need(precision == COFFEE_NN_FAST || precision == COFFEE_NN_ACCURATE || precision == COFFEE_NN_FAST_LAYERED,
-         "unknown precision");
+    need(precision >= COFFEE_NN_FAST && precision <= COFFEE_NN_ACCURATE_NB2, "unknown precision");
     checkGeom(x, y, win_len);
     ModelHost m = loadModel(model_path);
     (void)deviceTables(x, y, win_len);

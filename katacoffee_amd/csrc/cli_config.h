@@ -112,8 +112,10 @@ inline void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
       s.nnPrecision = COFFEE_NN_ACCURATE;
     else if(it->second == "fastLayered")
       s.nnPrecision = COFFEE_NN_FAST_LAYERED;
+    else if(it->second == "corrected")
+      s.nnPrecision = COFFEE_NN_CORRECTED;
     else
-      throw std::invalid_argument("nnPrecision must be fast, accurate or fastLayered");
+      throw std::invalid_argument("nnPrecision must be fast, accurate, corrected or fastLayered");
   }
   coffee_search_params& p = s.sp;
   geti("maxVisits", p.max_visits);

@@ -104,6 +104,10 @@ enum NNPath : int {
   NN_ACCURATE = 1,      // fp16 hi/lo operand pairs (fused kernel when it covers the net, else layered):
                         // logits within 1e-3 of fp32 for any net
   NN_FAST_LAYERED = 2,  // fp16 operands on the layered path (comparison / any architecture)
+  NN_CORRECTED = 3,     // fp16 products plus the two cross terms on block-scaled e4m3 MFMAs (2 fp16-MFMA
+                        // equivalents per product, ~2^-14 per product): fused kernel when it covers the
+                        // net, else the layered accurate path
+  NN_ACCURATE_NB2 = 4,  // the 2-board bordered split instance (A/B reference of the borderless one)
 };
 
 class NNEngine {
@@ -123,8 +127,12 @@ class NNEngine {
   double flopsPerEval() const { return flops_; }
   bool fused() const { return !layered_; }
   // rows per launch worth batching: the fused kernel costs one workgroup's latency
-  // per wave of workgroups, so its batch is capped at one wave (cus x 8 boards)
-  int batchCap(int cus) const { return layered_ ? (1 << 30) : cus * NN_BOARDS_PER_WG; }
+  // per wave of workgroups, so its batch is capped at one wave (cus x 8 boards; two
+  // engines sharing a device each launch up to cus x 4, one wave of 5-board
+  // workgroups); the 2-board A/B instance at cus x 2
+  int batchCap(int cus) const {
+    return layered_ ? (1 << 30) : cus * (mode_ == NN_ACCURATE_NB2 ? 2 : NN_BOARDS_PER_WG);
+  }
   static bool fusedSupported(const ModelCfg& c, int X, int Y);
 
  private:
@@ -137,8 +145,9 @@ class NNEngine {
   NNLayout* layoutDev_ = nullptr;
   uint16_t* tabDev_ = nullptr;   // device row tables (nn.hip rowTables), 8 boards per workgroup
   uint16_t* tabDevSm_ = nullptr; // the same for the small-batch instance (NN_SMALL_NB boards)
-  uint16_t* tabDevS_ = nullptr;  // the same for the split-precision instance (2 boards per workgroup)
-  bool split_ = false;           // NN_ACCURATE on the fused kernel: fp16 hi/lo operand pairs
+  uint16_t* tabDevS_ = nullptr;  // the same for the 2-board split instance (NN_ACCURATE_NB2)
+  uint16_t* tabDevB_ = nullptr;  // the same for the borderless 5-board instances (accurate, corrected)
+  int mode_ = NN_FAST;           // NNPath of the fused kernel
   int small_ = 0;                // KATACOFFEE_NN_SMALL=8: small batches on the 8-board instance (A/B runs)
   float* trunk_ = nullptr;       // f32 residual trunk scratch, [workgroup][fragment] (nn.hip)
   size_t trunkBytes_ = 0;        // its size

@@ -41,7 +41,21 @@ namespace kc {
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int SPLIT_ = 0>
+// Operand precision of an instance (MODE): 0 fp16 operands ("fast"); 1 fp16 hi/lo pairs,
+// three MFMAs per product ("accurate"); 2 fp16 hi * hi plus the two cross terms on one
+// block-scaled fp8 MFMA at twice the fp16 rate ("corrected", below).
+enum { NN_MODE_F16 = 0, NN_MODE_SPLIT3 = 1, NN_MODE_F8C = 2 };
+// Corrected mode: w x = hi(w) hi(x) + lo(w) x + w lo(x) + lo(w) lo(x), with lo(v) = v - fp16(v)
+// (|lo(v)| <= 2^-11 |v|).  The first product runs on v_mfma_f32_16x16x32_f16; the two
+// cross terms (the last is below f32 rounding) on v_mfma_scale_f32_16x16x128_f8f6f4 with
+// e4m3 operands: A = [e4m3(lo(w) 2^11) | e4m3(w)], B = [e4m3(x) | e4m3(lo(x) 2^11)] over
+// two K-steps, scale 2^-11 on A.  Each cross term carries e4m3's 2^-4 relative error on a
+// value 2^-11 below the product, so a product is good to ~2^-14 (fp16 operands: 2^-10):
+// tools/precision_study.py measures 2.1e-4 on the trained-net test (fp16: 7.1e-3).
+constexpr int F8C_SHIFT = 11;
+constexpr float F8C_SCALE = 2048.0f;  // 2^F8C_SHIFT
+
+template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int MODE_ = 0, bool BL_ = false>
 struct NNGeo {
   static constexpr int X = X_, Y = Y_, C = C_, A = X_ * Y_;
   // boards per workgroup: 8, or NN_SMALL_NB (5) for batches of at most 5 per CU; one
@@ -51,19 +65,27 @@ struct NNGeo {
   // exposes every LDS and barrier latency: both slower)
   static constexpr int NB = NB_;
   static constexpr int NW = 8, NT = NW * 64;  // waves / threads per workgroup
-  // SPLIT ("accurate" precision, as the layered kernels): every conv operand is an fp16
-  // pair hi + lo (lo = fp16(x - hi)) and each product hi*hi + lo*hi + hi*lo on three
-  // MFMAs; activations carry a second (lo) LDS plane, weight taps a lo block after the
-  // hi one.  2 boards per workgroup so the planes and the ring fit the 160 KiB.
-  static constexpr bool SPLIT = SPLIT_ != 0;
+  static constexpr int MODE = MODE_;
+  // SPLIT (modes 1 and 2): every conv operand carries a second LDS plane and every weight
+  // tap a second block after the hi one -- fp16 lo values (mode 1), or e4m3 pairs
+  // (mode 2: activations [x | lo(x) 2^11], weights [lo(w) 2^11 | w], per 8 channels).
+  static constexpr bool SPLIT = MODE_ != NN_MODE_F16;
   static constexpr int PLANES = SPLIT ? 2 : 1;
-  // weight ring slots.  3 (8-board and SPLIT instances, whose LDS holds no more): tap
+  // BL ("borderless", the 5-board split instances): activations are stored one row per
+  // position, no zero border; a 3x3 tap whose neighbour is off the board reads a shared
+  // zero row instead (per-lane address select per tap).  That halves the activation
+  // planes (129 rows instead of 5 x 49), so two planes of 5 boards and a 2-slot ring of
+  // 36 KiB taps fit the 160 KiB.
+  static constexpr bool BL = BL_;
+  // weight ring slots.  3 (8-board and 2-board SPLIT instances, whose LDS holds no more): tap
   // k+2 is requested at the start of tap k, one barrier per tap.  4 (small-batch
   // instance): taps move in pairs (g, g+1), g even in the stream's global tap count;
   // pair j+1 is requested at the start of pair j and published by one barrier per pair.
+  // 2 (BL): chunks (one 36 KiB slot: a 96-channel tap, or 3 stem taps) alternate; chunk
+  // j+2 is requested right after the barrier that publishes chunk j+1 and frees chunk j.
   // (6 slots, one barrier per 3 taps, would fill all 160 KiB and keep the other game
   // group's search kernels off the CU while the network runs.)
-  static constexpr int RING = (NB_ == NN_SMALL_NB && SPLIT_ == 0) ? 4 : 3;
+  static constexpr int RING = BL ? 2 : ((NB_ == NN_SMALL_NB && !SPLIT) ? 4 : 3);
   static constexpr bool PAIRS = RING == 4;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
@@ -74,9 +96,11 @@ struct NNGeo {
   static constexpr int MROWS = RGROUPS * MAXT * 16;  // computed output rows
   // Activations in LDS are stored per board with a one-cell zero border
   // ((Y+2) x (X+2) cells), so every 3x3 neighbour of an on-board cell is a fixed
-  // row offset away and the implicit-GEMM A reads need no bounds checks.
+  // row offset away and the implicit-GEMM A reads need no bounds checks (BL: row r is
+  // output row r, and row ZROW = MROWS is all zeros).
   static constexpr int PX = X + 2, PY = Y + 2, PA = PX * PY;
-  static constexpr int PROWS = NB * PA;
+  static constexpr int ZROW = MROWS;
+  static constexpr int PROWS = BL ? MROWS + 1 : NB * PA;
   // fp16 per activation row: 56-dword rows make the A-fragment ds_read_b128 (lane
   // groups {0-3,12-15,20-27}, ... ; 16 rows x 4 k-quarters) bank-conflict free.
   static constexpr int ASTR = C + 16;
@@ -84,7 +108,7 @@ struct NNGeo {
   static constexpr int NCT = C / 32;     // 16-col tiles per wave
   static constexpr int NCT_ALL = C / 16;
   static constexpr int P = 4 * A;
-  static constexpr int PLANE_BYTES = (PROWS * ROWB + 15) / 16 * 16;  // one fp16 plane (hi or lo)
+  static constexpr int PLANE_BYTES = (PROWS * ROWB + 15) / 16 * 16;  // one plane (hi, or lo / e4m3 pairs)
   static constexpr int ACT_BYTES = PLANES * PLANE_BYTES;
   // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
@@ -94,6 +118,7 @@ struct NNGeo {
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap and plane
   static constexpr int WSLOT = PLANES * WBUF;           // one ring slot
+  static constexpr int SLOT_PIECES = WSLOT / 64;        // its 1-KiB pieces
   // row tables (u16): rowPa[MROWS], rowBP[MROWS], bpRow[ROWS] -- built on the host
   static constexpr int NTAB = 2 * MROWS + ROWS;
   static constexpr int OFF_TAB = OFF_BIAS + NB * 64 * 4;
@@ -109,8 +134,9 @@ struct NNGeo {
   static_assert(OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
   static_assert(96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
   static_assert(RING * WSLOT * 16 >= RING_VH + NB * 64 * 4, "head linear weights and vh must fit in the ring");
-  static_assert((PLANES - 1) * PLANE_BYTES + 2 * PA * ROWB + 2 * 64 < 65536,
+  static_assert((PLANES - 1) * PLANE_BYTES + (BL ? 0 : 2 * PA * ROWB) + 2 * 64 < 65536,
                 "A-read offsets must fit the ds_read immediate");
+  static_assert(!BL || (MODE_ != NN_MODE_F16 && C == 96), "borderless instances: split modes of b6c96");
   static_assert(LDS <= 163840, "LDS budget");
 };
 
@@ -304,6 +330,187 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
   }
 }
 
+// ---- borderless (BL) instances ----------------------------------------------
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// Per tile: the byte address of this lane's A-fragment row (row r = output row r, plus
+// the lane's k-quarter) and a 9-bit mask of the 3x3 taps whose neighbour is on the
+// board (padding rows: none).  Tap ky*3 + kx reads row r + (ky-1) X + (kx-1).
+template <class G>
+KC_D void aRowsBL(int (&rb)[G::MAXT], uint32_t (&vm)[G::MAXT], int tstart, int lane) {
+#pragma unroll
+  for(int t = 0; t < G::MAXT; t++) {
+    const int r = (tstart + t) * 16 + (lane & 15);
+    const int p = r % G::A, y = p / G::X, x = p - y * G::X;
+    uint32_t m = 0;
+#pragma unroll
+    for(int tap = 0; tap < 9; tap++) {
+      const int ny = y + tap / 3 - 1, nx = x + tap % 3 - 1;
+      if(r < G::ROWS && ny >= 0 && ny < G::Y && nx >= 0 && nx < G::X)
+        m |= 1u << tap;
+    }
+    rb[t] = r * G::ROWB + 16 * (lane >> 4);
+    vm[t] = m;
+  }
+}
+
+// A weight chunk (`pieces` 1-KiB pieces, contiguous in the stream) into a ring slot.
+template <int NW>
+KC_D void stageChunk(const h16x8* __restrict__ src, uint32_t slotAddr, int pieces, int wave, int lane) {
+  for(int c = wave; c < pieces; c += NW)
+    glds16s(src + c * 64, (uint32_t)lane * 16u, slotAddr + c * 1024);
+}
+
+// Implicit-GEMM convolution of a BL instance, computed transposed like convTiles.
+// Weights stream through the 2-slot ring in chunks of TPC taps (one slot: a 96-channel
+// tap, or three stem taps); chunk j of this conv lives in slot (PAR + j) & 1, PAR the
+// parity of the conv's first chunk in the whole stream.  On entry chunk 0 is resident and
+// published (the caller retired its DMA before the barrier that published the conv's
+// input) and chunk 1's slot is free: chunk 1 is requested at once (or, for a one-chunk
+// conv, the next conv's chunk 0).  One barrier per chunk, before the chunk's last K-step:
+// every wave retires its pieces of chunk j+1, the barrier publishes them and frees chunk
+// j's slot (all its fragment reads are complete: lgkmcnt(0)), and chunk j+2 is requested
+// into it (this conv's, or the next conv's chunk 0).  A-fragment addresses are formed per
+// tap: the neighbour row, or the zero row when the neighbour is off the board.
+//   MODE 1: acc += hi(w) hi(x) + lo(w) hi(x) + hi(w) lo(x)  (three f16 MFMAs per step)
+//   MODE 2: acc += hi(w) hi(x) per step (f16 MFMA), and per pair of steps one scaled e4m3
+//           MFMA over [lo(w) 2^11 | w] x [x | lo(x) 2^11] of both steps, scale 2^-11
+template <class G, int NTAPS, int NCB, int PAR>
+KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
+                     f32x4 (&acc)[G::MAXT][G::NCT], const int (&rb)[G::MAXT], const uint32_t (&vm)[G::MAXT],
+                     int cg, int lane, int tid, const h16x8* __restrict__ wNext, int nextPieces) {
+  constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap and plane
+  constexpr int CH = CHP * G::PLANES;    // per tap
+  constexpr int TPC = G::SLOT_PIECES / CH >= 1 ? G::SLOT_PIECES / CH : 1;
+  static_assert(TPC * CH <= G::SLOT_PIECES, "a tap must fit one ring slot");
+  constexpr int NCH = (NTAPS + TPC - 1) / TPC;
+  constexpr int STEPS = NTAPS * NCB;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t ring = ldsAddr(wl);
+  auto slotAddr = [&](int j) { return ring + (uint32_t)(((PAR + j) & 1) * G::WSLOT * 16); };
+  auto chunkPieces = [&](int j) { return (NTAPS - j * TPC < TPC ? NTAPS - j * TPC : TPC) * CH; };
+  // the request of stream chunk j of this conv (j >= NCH: the next conv's chunk 0)
+  auto request = [&](int j) {
+    if(j < NCH)
+      stageChunk<G::NW>(w + (size_t)j * TPC * CH * 64, slotAddr(j), chunkPieces(j), wave, lane);
+    else if(j == NCH && nextPieces > 0)
+      stageChunk<G::NW>(wNext, slotAddr(j), nextPieces, wave, lane);
+  };
+  request(1);
+  const char* actB = reinterpret_cast<const char*>(act);
+  const int zb = G::ZROW * G::ROWB + 16 * (lane >> 4);
+  const h16x8* wlane = wl + (cg * G::NCT) * 64 + lane;
+  int at[G::MAXT];  // this tap's A-fragment row addresses
+  auto tapAddr = [&](int tap) {
+    const int tb = NTAPS == 9 ? tap : 4;  // 1x1: the centre tap
+    const int off = ((tb / 3 - 1) * G::X + (tb % 3 - 1)) * G::ROWB;
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++)
+      at[t] = ((vm[t] >> tb) & 1u) ? rb[t] + off : zb;
+  };
+  h16x8 af[2][G::MAXT], bf[2][G::NCT];
+  // second planes: fp16 lo fragments, double buffered (mode 1); e4m3 pairs (mode 2), the
+  // two steps of an MFMA pair in the low / high half of one 8-register operand, so the
+  // scaled MFMA reads its operands in place (the halves are the double buffer)
+  h16x8 afl[G::MODE == NN_MODE_SPLIT3 ? 2 : 1][G::MAXT], bfl[G::MODE == NN_MODE_SPLIT3 ? 2 : 1][G::NCT];
+  i32x8 aq[G::MAXT], bq[G::NCT];
+  auto loadStep = [&](int st, int buf) {
+    const int tap = st / NCB, cb = st - tap * NCB;
+    const int chunk = tap / TPC, tc = tap - chunk * TPC;
+    const h16x8* wb = wlane + ((PAR + chunk) & 1) * G::WSLOT + tc * CH * 64 + cb * G::NCT_ALL * 64;
+#pragma unroll
+    for(int ct = 0; ct < G::NCT; ct++) {
+      bf[buf][ct] = wb[ct * 64];
+      if constexpr(G::MODE == NN_MODE_SPLIT3) {
+        bfl[buf][ct] = wb[CHP * 64 + ct * 64];
+      } else {
+        const i32x4 v = __builtin_bit_cast(i32x4, wb[CHP * 64 + ct * 64]);
+        if(buf)
+          bq[ct].hi = v;
+        else
+          bq[ct].lo = v;
+      }
+    }
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++) {
+      af[buf][t] = *reinterpret_cast<const h16x8*>(actB + at[t] + cb * 64);
+      const h16x8 v = *reinterpret_cast<const h16x8*>(actB + G::PLANE_BYTES + at[t] + cb * 64);
+      if constexpr(G::MODE == NN_MODE_SPLIT3) {
+        afl[buf][t] = v;
+      } else {
+        if(buf)
+          aq[t].hi = __builtin_bit_cast(i32x4, v);
+        else
+          aq[t].lo = __builtin_bit_cast(i32x4, v);
+      }
+    }
+  };
+  auto f8pair = [&]() {
+    // one scaled e4m3 MFMA over the pair of steps held in aq / bq
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++)
+        acc[t][ct] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bq[ct], aq[t], acc[t][ct], 0, 0, 0,
+                                                                       127 - F8C_SHIFT, 0, 127);
+  };
+  tapAddr(0);
+  loadStep(0, 0);
+#pragma unroll
+  for(int st = 0; st < STEPS; st++) {
+    const int tap = st / NCB, cb = st - tap * NCB;
+    const int chunk = tap / TPC;
+    const bool chunkEnd = cb == NCB - 1 && (tap == NTAPS - 1 || (tap + 1) % TPC == 0);
+    if(chunkEnd && chunk + 1 < NCH) {
+      // retire this wave's pieces of chunk+1, publish them, free chunk's slot, request chunk+2
+      waitVm<0>();
+      barrierKeepDma();
+      request(chunk + 2);
+    }
+    if constexpr(G::MODE == NN_MODE_F8C) {
+      if(st & 1)
+        f8pair();  // steps st - 1 (low halves) and st (high halves)
+    }
+    if(st + 1 < STEPS) {
+      if(cb == NCB - 1)
+        tapAddr(tap + 1);
+      loadStep(st + 1, (st + 1) & 1);
+    }
+    // keep the next step's LDS reads ahead of this step's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    const int b = st & 1;
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++)
+        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b][ct], af[b][t], acc[t][ct], 0, 0, 0);
+    if constexpr(G::MODE == NN_MODE_SPLIT3) {
+      // + lo(w) * hi(x), then + hi(w) * lo(x) (the other split kernels' order)
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+        for(int ct = 0; ct < G::NCT; ct++)
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfl[b][ct], af[b][t], acc[t][ct], 0, 0, 0);
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++)
+#pragma unroll
+        for(int ct = 0; ct < G::NCT; ct++)
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b][ct], afl[b][t], acc[t][ct], 0, 0, 0);
+    }
+    if constexpr(G::MODE == NN_MODE_F8C) {
+      if(st == STEPS - 1 && !(st & 1)) {
+        // an odd step count: the last step pairs with zeros (stale weights x 0)
+#pragma unroll
+        for(int t = 0; t < G::MAXT; t++)
+          aq[t].hi = i32x4{0, 0, 0, 0};
+        f8pair();
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 // Copies a [96][rows] f32 matrix (a [rows][96] linear layer the host stored
@@ -391,12 +598,36 @@ KC_D uint2 packH4lo(float a, float b, float c, float d) {
   auto lo = [](float x) { return x - (float)(_Float16)x; };
   return packH4(lo(a), lo(b), lo(c), lo(d));
 }
-// Four activated channels of one row into act: the hi plane, and the lo plane (SPLIT).
+// e4m3 (OCP e4m3fn, round to nearest even) of two values, saturated at +-448, in the
+// low (HI false) or high half of `old`: byte 0 / 2 = a, byte 1 / 3 = b
+template <bool HI>
+KC_D int e4m3x2(float a, float b, int old) {
+  a = fminf(fmaxf(a, -448.0f), 448.0f);
+  b = fminf(fmaxf(b, -448.0f), 448.0f);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
+}
+// Four activated channels of one row into act: the hi plane, and the second plane --
+// fp16 lo (mode 1), or e4m3 x and e4m3 lo(x) 2^11 (mode 2: the channel octet's 16 bytes
+// are [x of its 8 channels | lo(x) 2^11 of its 8 channels]).
 template <class G>
 KC_D void storeAct4(uint16_t* act, int row, int ch, float y0, float y1, float y2, float y3) {
   *reinterpret_cast<uint2*>(act + row * G::ASTR + ch) = packH4(y0, y1, y2, y3);
-  if constexpr(G::SPLIT)
+  if constexpr(G::MODE == NN_MODE_SPLIT3)
     *reinterpret_cast<uint2*>(act + G::PLANE_BYTES / 2 + row * G::ASTR + ch) = packH4lo(y0, y1, y2, y3);
+  if constexpr(G::MODE == NN_MODE_F8C) {
+    auto lo = [](float x) { return (x - (float)(_Float16)x) * F8C_SCALE; };
+    char* q = reinterpret_cast<char*>(act) + G::PLANE_BYTES + row * G::ROWB + (ch >> 3) * 16 + (ch & 7);
+    *reinterpret_cast<int*>(q) = e4m3x2<true>(y2, y3, e4m3x2<false>(y0, y1, 0));
+    *reinterpret_cast<int*>(q + 8) = e4m3x2<true>(lo(y2), lo(y3), e4m3x2<false>(lo(y0), lo(y1), 0));
+  }
+}
+// BL: zero the shared zero row in every plane (after act was used as f32 scratch).
+template <class G>
+KC_D void zeroRowBL(uint16_t* act, int tid) {
+  constexpr int N = G::ROWB / 16;
+  for(int i = tid; i < G::PLANES * N; i += G::NT)
+    reinterpret_cast<uint4*>(reinterpret_cast<char*>(act) + (i / N) * G::PLANE_BYTES + G::ZROW * G::ROWB)[i % N] =
+        uint4{0u, 0u, 0u, 0u};
 }
 
 // act[pad(row)][ch..ch+3] = f16(relu(v * s[ch] + b[ch])) for on-board rows, all channels.
@@ -602,13 +833,13 @@ KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ W
   return src >= 0 ? WF[src] : 0.0f;
 }
 
-template <int X, int Y, int C, int NB, int SPLIT>
+template <int X, int Y, int C, int NB, int MODE, bool BL>
 __global__ void __launch_bounds__(512, 2)
     kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
                const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
                const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
                float* __restrict__ out, float* __restrict__ trunk) {
-  using G = NNGeo<X, Y, C, NB, SPLIT>;
+  using G = NNGeo<X, Y, C, NB, MODE, BL>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
   const int count = countDev ? min(*countDev, n) : n;
@@ -637,9 +868,14 @@ __global__ void __launch_bounds__(512, 2)
   {
     constexpr int CH0 = G::NCT_ALL * G::PLANES;  // 1-KiB pieces per stem tap (one 32-channel block)
     const uint32_t ring = ldsAddr(wl);
+    if constexpr(G::BL) {
+      // the stem's chunk 0 (taps 0-2) into slot 0
+      stageChunk<G::NW>(WB + L->wInit, ring, 3 * CH0, wave, lane);
+    } else {
 #pragma unroll
-    for(int tap = 0; tap < 2; tap++)
-      stageTapDma<G::NW>(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WSLOT * 16, CH0, wave, lane);
+      for(int tap = 0; tap < 2; tap++)
+        stageTapDma<G::NW>(WB + L->wInit + (size_t)tap * CH0 * 64, ring + tap * G::WSLOT * 16, CH0, wave, lane);
+    }
   }
   // ---- row tables; unpack the packed V1 planes into the zero-bordered act ----
   constexpr int NPK = (G::NPRM + G::NT - 1) / G::NT;  // parameter-slab elements per thread
@@ -669,7 +905,10 @@ __global__ void __launch_bounds__(512, 2)
         const int i = k * 64 + lane;
         if(i < NBITS && ((words[k] >> lane) & 1ULL)) {
           const int c = i / G::A, p = i - c * G::A;
-          act[padCell<G>(b, p) * G::ASTR + c] = (uint16_t)0x3c00;
+          const int row = G::BL ? b * G::A + p : padCell<G>(b, p);
+          act[row * G::ASTR + c] = (uint16_t)0x3c00;  // 1.0
+          if constexpr(G::MODE == NN_MODE_F8C)  // e4m3 1.0 (its lo is 0)
+            reinterpret_cast<uint8_t*>(act)[G::PLANE_BYTES + row * G::ROWB + (c >> 3) * 16 + (c & 7)] = 0x38;
         }
       }
     }
@@ -679,13 +918,24 @@ __global__ void __launch_bounds__(512, 2)
 
   NN_PHASE(1);
   int ab[G::MAXT];
-  aBases<G>(ab, rowPa, tstart, lane);
+  int rb[G::MAXT];
+  uint32_t vm[G::MAXT];
+  if constexpr(G::BL)
+    aRowsBL<G>(rb, vm, tstart, lane);
+  else
+    aBases<G>(ab, rowPa, tstart, lane);
+  // pieces of the first weight chunk of a conv of C -> C (or the head's): one tap
+  constexpr int CHUNK96 = G::SLOT_PIECES;
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
-  convTiles<G, 9, 1, 0, 0, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
-                        L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
-                        L->nblocks > 0 ? 9 : 1, 0);
+  if constexpr(G::BL)
+    convTilesB<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, rb, vm, cg, lane, tid,
+                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96);
+  else
+    convTiles<G, 9, 1, 0, 0, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
+                                    L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
+                                    L->nblocks > 0 ? 9 : 1, 0);
   {
     // + linear_global(input_global) broadcast (model_pytorch.py:1587-1589); gin == 1
 #pragma unroll
@@ -722,8 +972,14 @@ __global__ void __launch_bounds__(512, 2)
     for(int j = 0; j < NPK; j++)
       pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
-    convTiles<G, 9, G::C / 32, 1, 0, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid, WB + L->wConv2[blk],
-                                  (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, 9, 9 + 18 * blk);
+    if constexpr(G::BL)
+      // chunk parity: stem 3 chunks, each block's convs 9 + 9 (a 64-channel tap is one chunk too)
+      convTilesB<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, rb, vm, cg, lane, tid, WB + L->wConv2[blk],
+                                     (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES);
+    else
+      convTiles<G, 9, G::C / 32, 1, 0, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid,
+                                              WB + L->wConv2[blk],
+                                              (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, 9, 9 + 18 * blk);
 #pragma unroll
     for(int j = 0; j < NPK; j++)
       if(tid + j * G::NT < G::NPRM)
@@ -746,8 +1002,11 @@ __global__ void __launch_bounds__(512, 2)
       waitVm<0>();
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, G::C / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                    3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
+      if constexpr(G::BL)
+        convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW, CHUNK96);
+      else
+        convTiles<G, 9, G::C / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                                3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
     } else {
@@ -801,7 +1060,10 @@ __global__ void __launch_bounds__(512, 2)
       __syncthreads();
       f32x4 tr[G::MAXT][G::NCT];  // the parked trunk, in flight during the epilogue
       loadTrunk<G>(tr, park, trunk, wave, lane);
-      zeroBorders<G>(act, tid);  // the f32 scratch overwrote border cells (disjoint from r-epi cells)
+      if constexpr(G::BL)
+        zeroRowBL<G>(act, tid);  // the f32 scratch overwrote the zero row
+      else
+        zeroBorders<G>(act, tid);  // the f32 scratch overwrote border cells (disjoint from r-epi cells)
       NN_PHASE(52);
       {
         // r branch + gpool bias -> BN2-ReLU -> f16 act (channels < Cr)
@@ -835,8 +1097,12 @@ __global__ void __launch_bounds__(512, 2)
       waitVm<0>();
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
-      convTiles<G, 9, (G::C - 32) / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
-                                           3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
+      if constexpr(G::BL)
+        convTilesB<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW,
+                                              CHUNK96);
+      else
+        convTiles<G, 9, (G::C - 32) / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
+                                                       3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
       if(!lastBlk)
         storeTrunk<G>(trunk, park, acc, wave, lane);
     }
@@ -850,7 +1116,11 @@ __global__ void __launch_bounds__(512, 2)
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
-  convTiles<G, 1, G::C / 32, 1, 0, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0, 9 + 18 * L->nblocks);
+  if constexpr(G::BL)
+    convTilesB<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, rb, vm, cg, lane, tid, nullptr, 0);
+  else
+    convTiles<G, 1, G::C / 32, 1, 0, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0,
+                                            9 + 18 * L->nblocks);
   __syncthreads();  // act dead from here: f32 [MROWS][SCR] value branch at actF, g branch at scr
   NN_PHASE(41);
   {
@@ -1014,22 +1284,57 @@ static float h2f(uint16_t h) {
   return f;
 }
 
-// split: after each tap's hi fragments the same fragments of lo = fp16(w - hi)
-// (convTiles' SPLIT ring slot layout).
+// float -> OCP e4m3fn (bias 7, max 448), round to nearest even, saturating at +-448
+// (the device's e4m3x2 on activations).
+static uint8_t f2e4m3(float f) {
+  const uint8_t sign = std::signbit(f) ? 0x80 : 0x00;
+  const float a = std::fabs(f);
+  if(!(a < 448.0f))
+    return sign | 0x7e;
+  if(a < 0.015625f)  // below 2^-6: subnormal, quantum 2^-9 (a carry into 0x08 is 2^-6 itself)
+    return sign | (uint8_t)std::nearbyint(a * 512.0f);
+  int e;
+  const float m = std::frexp(a, &e);  // a = m 2^e, m in [0.5, 1)
+  int q = (int)std::nearbyint((m * 2.0f - 1.0f) * 8.0f);
+  int E = e - 1;
+  if(q == 8) {
+    q = 0;
+    E++;
+  }
+  if(E + 7 > 15 || (E + 7 == 15 && q == 7))
+    return sign | 0x7e;
+  return sign | (uint8_t)(((E + 7) << 3) | q);
+}
+
+// mode 1: after each tap's hi fragments the same fragments of lo = fp16(w - hi);
+// mode 2: after them the e4m3 pairs [lo(w) 2^11 of the fragment's 8 k | w of the same 8 k]
+// (convTiles' / convTilesB's SPLIT ring slot layout).
 static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout,
-                     const std::function<float(int, int, int)>& W, bool split = false) {
+                     const std::function<float(int, int, int)>& W, int mode = NN_MODE_F16) {
   const int ncb = cinPad / 32, nct = cout / 16;
   for(int tap = 0; tap < ntaps; tap++)
-    for(int part = 0; part < (split ? 2 : 1); part++)
+    for(int part = 0; part < (mode != NN_MODE_F16 ? 2 : 1); part++)
       for(int cb = 0; cb < ncb; cb++)
         for(int ct = 0; ct < nct; ct++)
-          for(int l = 0; l < 64; l++)
-            for(int j = 0; j < 8; j++) {
-              const int co = ct * 16 + (l & 15), ci = cb * 32 + 8 * (l >> 4) + j;
-              const float w = W(co, ci, tap);
-              const uint16_t hi = f2h(w);
-              dst.push_back(part == 0 ? hi : f2h(w - h2f(hi)));
+          for(int l = 0; l < 64; l++) {
+            float w[8];
+            for(int j = 0; j < 8; j++)
+              w[j] = W(ct * 16 + (l & 15), cb * 32 + 8 * (l >> 4) + j, tap);
+            if(part == 0 || mode == NN_MODE_SPLIT3) {
+              for(int j = 0; j < 8; j++) {
+                const uint16_t hi = f2h(w[j]);
+                dst.push_back(part == 0 ? hi : f2h(w[j] - h2f(hi)));
+              }
+            } else {
+              uint8_t b[16];
+              for(int j = 0; j < 8; j++) {
+                b[j] = f2e4m3((w[j] - h2f(f2h(w[j]))) * F8C_SCALE);
+                b[8 + j] = f2e4m3(w[j]);
+              }
+              for(int j = 0; j < 8; j++)
+                dst.push_back((uint16_t)(b[2 * j] | (b[2 * j + 1] << 8)));
             }
+          }
 }
 
 // Output-row order of a workgroup's NB boards: row r takes a cell whose padded
@@ -1042,6 +1347,15 @@ static std::vector<uint16_t> rowTables() {
   uint16_t* rowPa = tab.data();
   uint16_t* rowBP = rowPa + G::MROWS;
   uint16_t* bpRow = rowBP + G::MROWS;
+  if(G::BL) {  // borderless: output row r is activation row r, position r
+    for(int r = 0; r < G::MROWS; r++) {
+      rowPa[r] = (uint16_t)(r < G::ROWS ? r : G::ZROW);
+      rowBP[r] = (uint16_t)(r < G::ROWS ? r : 0xFFFF);
+    }
+    for(int r = 0; r < G::ROWS; r++)
+      bpRow[r] = (uint16_t)r;
+    return tab;
+  }
   std::vector<std::vector<int>> bucket(8);
   for(int b = 0; b < G::NB; b++)
     for(int p = 0; p < G::A; p++) {
@@ -1076,13 +1390,17 @@ bool NNEngine::fusedSupported(const ModelCfg& c, int X, int Y) {
 
 NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.cfg), X_(X), Y_(Y), W_(W) {
   flops_ = modelFlopsPerEval(cfg_, X * Y);
-  if(path != NN_FAST && path != NN_ACCURATE && path != NN_FAST_LAYERED)
+  if(path < NN_FAST || path > NN_ACCURATE_NB2)
     throw std::invalid_argument("NNEngine: unknown precision/path");
   if(path == NN_FAST_LAYERED || !fusedSupported(m.cfg, X, Y)) {
-    layered_.reset(new NNLayered(m, X, Y, W, path == NN_ACCURATE));
+    // the layered kernels have fp16 and hi/lo split operands; corrected maps to split
+    layered_.reset(new NNLayered(m, X, Y, W, path != NN_FAST && path != NN_FAST_LAYERED));
     return;
   }
-  split_ = path == NN_ACCURATE;  // the fused kernel's SPLIT instance (2 boards per workgroup)
+  mode_ = path;
+  // the fused kernel's operand mode: fp16, fp16 hi/lo pairs (accurate: the borderless
+  // 5-board instance, or the 2-board one for A/B), fp16 + e4m3 cross terms (corrected)
+  const int wmode = path == NN_CORRECTED ? NN_MODE_F8C : (path == NN_FAST ? NN_MODE_F16 : NN_MODE_SPLIT3);
   const int C = cfg_.C, Cr = C - cfg_.Cg;
   std::vector<uint16_t> wb;
   std::vector<float> wf;
@@ -1110,7 +1428,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   L.wInit = bfOff();
   packConv(wb, 9, 32, C, [&](int co, int ci, int tap) {
     return ci < cfg_.cin ? m.convInit[((size_t)co * cfg_.cin + ci) * 9 + tap] : 0.0f;
-  }, split_);
+  }, wmode);
   L.globInit = f32(m.globInit);
   for(int i = 0; i < L.nblocks; i++) {
     const ModelBlock& b = m.blocks[i];
@@ -1119,15 +1437,15 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
     L.bn1b[i] = f32(b.bn1b);
     L.wConv1[i] = bfOff();
     if(b.kind == 0) {
-      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv1[((size_t)co * C + ci) * 9 + tap]; }, split_);
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv1[((size_t)co * C + ci) * 9 + tap]; }, wmode);
       L.bn2s[i] = f32(b.bn2s);
       L.bn2b[i] = f32(b.bn2b);
       L.wConv2[i] = bfOff();
-      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * C + ci) * 9 + tap]; }, split_);
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * C + ci) * 9 + tap]; }, wmode);
     } else {
       packConv(wb, 9, C, C, [&](int co, int ci, int tap) {
         return co < Cr ? b.conv1[((size_t)co * C + ci) * 9 + tap] : b.conv1g[((size_t)(co - Cr) * C + ci) * 9 + tap];
-      }, split_);
+      }, wmode);
       L.bngs[i] = f32(b.bngs);
       L.bngb[i] = f32(b.bngb);
       L.linG[i] = f32T(b.linG, Cr);
@@ -1135,7 +1453,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
       L.bn2b[i] = f32(b.bn2b);
       L.wConv2[i] = bfOff();
       packConv(wb, 9, Cr, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * Cr + ci) * 9 + tap]; },
-               split_);
+               wmode);
     }
   }
   L.tips = f32(m.tips);
@@ -1147,7 +1465,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
     if(co < 64)
       return m.pConvG[(size_t)(co - 32) * C + ci];
     return m.vConv1[(size_t)(co - 64) * C + ci];
-  }, split_);
+  }, wmode);
   L.pBiasG = f32(m.pBiasG);
   L.pLinG = f32T(m.pLinG, 32);
   L.pBias2 = f32(m.pBias2);
@@ -1167,8 +1485,13 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipMemcpy(layoutDev_, &L, sizeof(NNLayout), hipMemcpyHostToDevice));
   using G8 = NNGeo<5, 5, 96, 8, 0>;
   using G4 = NNGeo<5, 5, 96, NN_SMALL_NB, 0>;
-  using GS = NNGeo<5, 5, 96, 2, 1>;
-  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>(), tabS = rowTables<GS>();
+  using GS = NNGeo<5, 5, 96, 2, NN_MODE_SPLIT3>;
+  using GB = NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>;
+  using GC = NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>;
+  const std::vector<uint16_t> tab8 = rowTables<G8>(), tab4 = rowTables<G4>(), tabS = rowTables<GS>(),
+                              tabB = rowTables<GB>();
+  KC_HIP(hipMalloc(&tabDevB_, tabB.size() * 2));
+  KC_HIP(hipMemcpy(tabDevB_, tabB.data(), tabB.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&tabDev_, tab8.size() * 2));
   KC_HIP(hipMemcpy(tabDev_, tab8.data(), tab8.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&tabDevSm_, tab4.size() * 2));
@@ -1177,12 +1500,16 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipMemcpy(tabDevS_, tabS.data(), tabS.size() * 2, hipMemcpyHostToDevice));
 
   // function attributes are per device: every engine sets it on its own device
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 8, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G8::LDS));
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              G4::LDS));
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             GS::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, 2, NN_MODE_SPLIT3, false>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, GS::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, GB::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, GC::LDS));
 #ifdef KC_AB_HOOKS
   // A/B builds only (tools/Makefile alt, -DKC_AB_HOOKS): KATACOFFEE_NN_SMALL=8 runs small
   // batches on the 8-board instance too; the product library never reads the variable
@@ -1202,6 +1529,7 @@ NNEngine::~NNEngine() {
   (void)hipFree(tabDev_);
   (void)hipFree(tabDevSm_);
   (void)hipFree(tabDevS_);
+  (void)hipFree(tabDevB_);
 
 }
 
@@ -1222,8 +1550,15 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   // a batch bound that fits NN_SMALL_NB boards per CU (e.g. each of two game groups'
   // batches) runs that many boards per workgroup, half the MFMA work on each
   // workgroup's path.
-  if(split_)  // "accurate": one instance for every batch size (its results never depend on n)
-    launch<NNGeo<5, 5, 96, 2, 1>>(n, inWords, tabDevS_, in, out, st, countDev, rowIdx, e0, e1);
+  // accurate / corrected: one instance for every batch size (results never depend on n)
+  if(mode_ == NN_ACCURATE)
+    launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>>(n, inWords, tabDevB_, in, out, st, countDev, rowIdx,
+                                                               e0, e1);
+  else if(mode_ == NN_CORRECTED)
+    launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>>(n, inWords, tabDevB_, in, out, st, countDev, rowIdx, e0,
+                                                            e1);
+  else if(mode_ == NN_ACCURATE_NB2)
+    launch<NNGeo<5, 5, 96, 2, NN_MODE_SPLIT3, false>>(n, inWords, tabDevS_, in, out, st, countDev, rowIdx, e0, e1);
   else if(n <= NN_SMALL_NB * cus_ && small_ != 8)
     launch<NNGeo<5, 5, 96, NN_SMALL_NB, 0>>(n, inWords, tabDevSm_, in, out, st, countDev, rowIdx, e0, e1);
   else
@@ -1244,7 +1579,7 @@ void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* i
     KC_HIP(hipMalloc(&trunk_, bytes));
     trunkBytes_ = bytes;
   }
-  auto kern = kNNForward<G::X, G::Y, G::C, G::NB, G::SPLIT ? 1 : 0>;
+  auto kern = kNNForward<G::X, G::Y, G::C, G::NB, G::MODE, G::BL>;
   if(e0)
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, e0, e1, 0, layoutDev_, (const h16x8*)wHalf_,
                           wF32_, tab, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);

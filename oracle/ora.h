@@ -98,6 +98,8 @@ struct ModelCfg {
 struct PackedConv {
   int ky = 0, kx = 0, cin = 0, cout = 0;
   std::vector<float> w, p32, p16;
+  // corrected-precision emulation: [3K][cout] = fp16(w) ; e4m3(lo(w) 2^11) / 2^11 ; e4m3(w)
+  std::vector<float> pC;
   void pack();
 };
 struct Model {
@@ -136,7 +138,7 @@ void nnForward(const Model& m, int X, int Y, int n, const float* bin, const floa
 struct NNBatch {
   int n, X, Y, A;
   const float* mask;
-  bool fp16;
+  int mode;  // convolution operands: 0 fp32, 1 fp16 (fast), 2 fp16 + e4m3 cross terms (corrected)
   int threads;
 };
 void convApply(const NNBatch& b, const PackedConv& cv, const float* in, float* out, bool accumulate);

@@ -145,20 +145,20 @@ static PackedConv mkConv(int ky, int kx, int cin, int cout, const float* w) {
 
 int ora_conv_apply(int ky, int kx, int cin, int cout, const float* w, int n, int X, int Y, const float* in, float* out,
                    int mode) {
-  NNBatch b{n, X, Y, X * Y, nullptr, mode == 1, 1};
+  NNBatch b{n, X, Y, X * Y, nullptr, mode, 1};
   convApply(b, mkConv(ky, kx, cin, cout, w), in, out, false);
   return 0;
 }
 
 int ora_bn_apply(int C, const float* s, const float* bias, int relu, int n, int X, int Y, const float* in,
                  const float* mask, float* out) {
-  NNBatch b{n, X, Y, X * Y, mask, false, 1};
+  NNBatch b{n, X, Y, X * Y, mask, 0, 1};
   bnAct(b, C, s, bias, in, C, out, relu != 0);
   return 0;
 }
 
 int ora_gpool_apply(int C, int valueHead, int n, int X, int Y, const float* in, const float* mask, float* out) {
-  NNBatch b{n, X, Y, X * Y, mask, false, 1};
+  NNBatch b{n, X, Y, X * Y, mask, 0, 1};
   gpoolRows(b, C, in, C, out, valueHead != 0);
   return 0;
 }
@@ -170,7 +170,7 @@ int ora_block_apply_parts(int kind, int n, int X, int Y, const float* mask, floa
                           const float* preB, const int* k1, const float* w1, const int* kg, const float* wg,
                           const float* gS, const float* gB, const float* linG, const float* midS, const float* midB,
                           const int* k2, const float* w2, int mode) {
-  NNBatch b{n, X, Y, X * Y, mask, mode == 1, 1};
+  NNBatch b{n, X, Y, X * Y, mask, mode, 1};
   Model::Block blk;
   blk.kind = kind;
   blk.conv1 = mkConv(k1[0], k1[1], k1[2], k1[3], w1);
@@ -199,7 +199,7 @@ int ora_block_apply_blob(int kind, int W, int mid, int Cg, const float* blob, lo
   Model::Block blk;
   if(!blockFromBlob(blob, (size_t)count, kind, W, Cg, mid, blk))
     return 1;
-  NNBatch b{n, X, Y, X * Y, nullptr, mode == 1, 1};
+  NNBatch b{n, X, Y, X * Y, nullptr, mode, 1};
   blockApply(b, blk, x);
   return 0;
 }

@@ -16,6 +16,9 @@
 // tests/test_oracle_nn.py.
 // mode 1 rounds every convolution weight and convolution input to fp16 (RNE),
 // exactly where the HIP kernels do; residual trunks stay f32 as in the kernels.
+// mode 2 restates the "corrected" precision (csrc/nn.hip NN_MODE_F8C): each product is
+// fp16(w) fp16(x) + e4m3(lo(w) 2^11) e4m3(x) / 2^11 + e4m3(w) e4m3(lo(x) 2^11) / 2^11, with
+// lo(v) = v - fp16(v) and e4m3 = OCP e4m3fn, round to nearest even, saturating at 448.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -49,6 +52,26 @@ static inline float f16r(float f) {
   memcpy(&r, &ru, 4);
   return r;
 }
+
+// float -> OCP e4m3fn -> float, round to nearest even, saturating at +-448 (the
+// device's v_cvt_pk_fp8_f32 after a clamp; tools/mfma_f8_probe.hip pins the encoding).
+static inline float e4m3r(float f) {
+  const float a = fabsf(f);
+  float r;
+  if(!(a < 448.0f)) {
+    r = 448.0f;
+  } else if(a < 0.015625f) {  // subnormal: quantum 2^-9
+    r = nearbyintf(a * 512.0f) * (1.0f / 512.0f);
+  } else {
+    int e;
+    const float m = frexpf(a, &e);  // a = m 2^e, m in [0.5, 1): 3 mantissa bits below the leading one
+    r = ldexpf(nearbyintf(m * 16.0f), e - 4);
+    if(r > 448.0f)
+      r = 448.0f;
+  }
+  return std::signbit(f) ? -r : r;
+}
+static const float F8C_SCALE = 2048.0f;
 
 // ---------------------------------------------------------------------------
 // SGEMM: C[M][ldc] (+)= A[M][lda] * B, B packed in 16-column panels
@@ -129,7 +152,7 @@ static void sgemm(int M, int N, int K, const float* A, int lda, const float* Bp,
 // B[k = (ky, kx, ci)][co] from w[co][ci][ky][kx]
 void PackedConv::pack() {
   const int K = ky * kx * cin;
-  std::vector<float> B((size_t)K * cout), B16((size_t)K * cout);
+  std::vector<float> B((size_t)K * cout), B16((size_t)K * cout), BC((size_t)3 * K * cout);
   for(int co = 0; co < cout; co++)
     for(int ci = 0; ci < cin; ci++)
       for(int y = 0; y < ky; y++)
@@ -138,9 +161,13 @@ void PackedConv::pack() {
           const size_t k = ((size_t)y * kx + x) * cin + ci;
           B[k * cout + co] = v;
           B16[k * cout + co] = f16r(v);
+          BC[k * cout + co] = f16r(v);
+          BC[(K + k) * cout + co] = e4m3r((v - f16r(v)) * F8C_SCALE) / F8C_SCALE;
+          BC[(2 * K + k) * cout + co] = e4m3r(v);
         }
   packB(B.data(), K, cout, p32);
   packB(B16.data(), K, cout, p16);
+  packB(BC.data(), 3 * K, cout, pC);
 }
 
 // ConvLayer::apply: "same" convolution, zero outside the board (the masked input is
@@ -149,33 +176,47 @@ void convApply(const NNBatch& b, const PackedConv& cv, const float* in, float* o
   const int A = b.A, rows = b.n * A, K = cv.ky * cv.kx * cv.cin;
   const int ry = cv.ky / 2, rx = cv.kx / 2;
   static const int emu = getenv("ORA_EMU") ? atoi(getenv("ORA_EMU")) : 3;
-  const float* Bp = (b.fp16 && (emu & 1)) ? cv.p16.data() : cv.p32.data();
+  const bool fp16 = b.mode == 1, corr = b.mode == 2;
+  const float* Bp = corr ? cv.pC.data() : ((fp16 && (emu & 1)) ? cv.p16.data() : cv.p32.data());
+  const int KC3 = corr ? 3 * K : K;  // corrected: im2col columns [fp16(x) | e4m3(x) | e4m3(lo(x) 2^11) / 2^11]
   constexpr int CH = 48;  // rows per im2col chunk
   const int chunks = (rows + CH - 1) / CH;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(b.threads > 0 ? b.threads : 1)
   for(int ch = 0; ch < chunks; ch++) {
     const int r0 = ch * CH, r1 = r0 + CH < rows ? r0 + CH : rows;
-    std::vector<float> col((size_t)(r1 - r0) * K);
+    std::vector<float> col((size_t)(r1 - r0) * KC3);
     for(int r = r0; r < r1; r++) {
       const int brd = r / A, p = r - brd * A, y = p / b.X, x = p - y * b.X;
-      float* cr = col.data() + (size_t)(r - r0) * K;
+      float* cr = col.data() + (size_t)(r - r0) * KC3;
       for(int dy = 0; dy < cv.ky; dy++)
         for(int dx = 0; dx < cv.kx; dx++) {
           const int yy = y + dy - ry, xx = x + dx - rx;
           float* dst = cr + ((size_t)dy * cv.kx + dx) * cv.cin;
           if(yy < 0 || yy >= b.Y || xx < 0 || xx >= b.X) {
             memset(dst, 0, sizeof(float) * cv.cin);
+            if(corr) {
+              memset(dst + K, 0, sizeof(float) * cv.cin);
+              memset(dst + 2 * K, 0, sizeof(float) * cv.cin);
+            }
           } else {
             const float* src = in + ((size_t)brd * A + yy * b.X + xx) * cv.cin;
-            if(b.fp16 && (emu & 2))
+            if(corr) {
+              for(int c = 0; c < cv.cin; c++) {
+                const float h = f16r(src[c]);
+                dst[c] = h;
+                dst[K + c] = e4m3r(src[c]);
+                dst[2 * K + c] = e4m3r((src[c] - h) * F8C_SCALE) / F8C_SCALE;
+              }
+            } else if(fp16 && (emu & 2)) {
               for(int c = 0; c < cv.cin; c++)
                 dst[c] = f16r(src[c]);
-            else
+            } else {
               memcpy(dst, src, sizeof(float) * cv.cin);
+            }
           }
         }
     }
-    sgemm(r1 - r0, cv.cout, K, col.data(), K, Bp, out + (size_t)r0 * cv.cout, cv.cout, accumulate);
+    sgemm(r1 - r0, cv.cout, KC3, col.data(), KC3, Bp, out + (size_t)r0 * cv.cout, cv.cout, accumulate);
   }
 }
 
@@ -429,7 +470,7 @@ void nnForward(const Model& m, int X, int Y, int n, const float* bin, const floa
                float* value, float* misc, int mode, int threads) {
   const ModelCfg& c = m.cfg;
   const int A = X * Y, C = c.C;
-  NNBatch b{n, X, Y, A, nullptr, mode == 1, threads};
+  NNBatch b{n, X, Y, A, nullptr, mode, threads};
   const size_t rows = (size_t)n * A;
   std::vector<float> in(rows * c.cin), x(rows * C), a(rows * C);
   for(int i = 0; i < n; i++)

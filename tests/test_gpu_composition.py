@@ -76,16 +76,18 @@ def _rows_of_game_positions(X, Y, W, n, seed):
 
 
 @pytest.mark.parametrize("arch,X,Y,W,precision", [("b6c96", 5, 5, 4, "fast"), ("b6c96", 5, 5, 4, "accurate"),
+                                                  ("b6c96", 5, 5, 4, "corrected"),
                                                   ("b10c128", 5, 5, 4, "fast"),
                                                   ("b18c384nbt", 9, 9, 5, "fast")],
-                         ids=["b6c96-fused", "b6c96-accurate", "b10c128-layered", "b18c384nbt-layered"])
+                         ids=["b6c96-fused", "b6c96-accurate", "b6c96-corrected", "b10c128-layered",
+                              "b18c384nbt-layered"])
 def test_network_row_independence(nets, arch, X, Y, W, precision):
     """A row's logits do not depend on its batch position, the batch size or (fused)
     the 5- / 8-board workgroup variant: a permuted batch gives the permuted outputs."""
     import torch
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     # fused: n > 5 x CUs selects the 8-board instance, the prefix the small (5-board) one
-    n = 5 * cus + 37 if precision == "fast" and arch == "b6c96" else 203
+    n = 5 * cus + 37 if arch == "b6c96" else 203  # fused: two waves of 5-board workgroups
     packed = _rows_of_game_positions(X, Y, W, n, seed=n)
     net = kc.Network(nets[arch], X, Y, W, precision=precision)
     full = net.forward(packed)
@@ -105,8 +107,10 @@ CASES = {
     "c2-fused-nb8": ("b6c96", (5, 5, 4), "fast", 1536, 1, 24, 14, 1300, 420, {}),
     # two game groups on their own streams, each capped (5-board kernel), selfplay1.cfg play
     "c2-fused-two-groups": ("b6c96", (5, 5, 4), "fast", 384, 2, 24, 14, 300, 700, PRODUCTION),
-    # split-precision network (the 1e-3 path) in self-play
+    # split-precision network in self-play
     "c2-accurate": ("b6c96", (5, 5, 4), "accurate", 128, 1, 24, 12, 0, 900, {}),
+    # corrected network (the benchmarked 1e-3 path): two groups, binding cap, selfplay1.cfg play
+    "c2-corrected-two-groups": ("b6c96", (5, 5, 4), "corrected", 384, 2, 24, 14, 300, 700, PRODUCTION),
     # C3 network on the layered kernels
     "c3-layered": ("b10c128", (5, 5, 4), "fast", 256, 1, 24, 12, 200, 900, {}),
     # C5 network (nested bottlenecks) at 9x9 / 5 on the layered kernels

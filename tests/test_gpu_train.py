@@ -4,6 +4,9 @@ kernels to the logits of the torch model.
 
   accurate precision (fp16 hi/lo operand pairs): within 1e-3 absolute of the torch
       fp32 model -- the north-star bound, for a trained net;
+  corrected precision (fp16 products + e4m3 cross terms, the benchmarked path): within
+      1e-3 absolute of the torch fp32 model, and within 2e-4 x max(1, max|logit|) of the
+      oracle's corrected emulation;
   fast precision (fp16 operands, f32 accumulation and trunk): within 2e-3 of the
       largest logit of the oracle's fp16-emulation mode (same roundings, different
       accumulation order, so single operands may round the other way).  Against fp32
@@ -54,6 +57,12 @@ def test_trained_net_runs_on_device_kernel():
     assert acc.fused  # the split-precision instance of the fused kernel
     out_acc = acc.forward(packed)
     acc.close()
+    cor = kc.Network(path, 5, 5, 4, precision="corrected")
+    assert cor.fused
+    out_cor = cor.forward(packed)
+    cor.close()
+    polc, valc, miscc = oracle.Model(path).forward(5, 5, planes, batch["glob"].numpy(), mode=2, threads=8)
+    refc = np.concatenate([polc.reshape(len(ref), -1), valc, miscc], axis=1)
     fast = kc.Network(path, 5, 5, 4)
     assert fast.fused
     out = fast.forward(packed)
@@ -63,9 +72,13 @@ def test_trained_net_runs_on_device_kernel():
     err_acc = float(np.abs(out_acc - ref).max())
     err16 = float(np.abs(out - ref16).max())
     err = float(np.abs(out - ref).max())
-    print("accurate vs torch fp32", err_acc, "| fast vs fp16 oracle", err16, "fast vs torch fp32", err,
-          "| max |ref|", np.abs(ref).max())
+    err_cor = float(np.abs(out_cor - ref).max())
+    err_cor_emu = float(np.abs(out_cor - refc).max())
+    print("accurate vs torch fp32", err_acc, "| corrected vs torch fp32", err_cor, "vs corrected emulation",
+          err_cor_emu, "| fast vs fp16 oracle", err16, "fast vs torch fp32", err, "| max |ref|", np.abs(ref).max())
     assert err_acc <= 1e-3
+    assert err_cor <= 1e-3
+    assert err_cor_emu <= 2e-4 * max(1.0, float(np.abs(ref).max()))
     assert err16 <= 2e-3 * max(1.0, float(np.abs(ref).max()))
     # the fast (fp16-operand) path against fp32 on a trained net: fp16 rounding of the
     # weights and activations moves the logits by ~1e-3 of the largest logit (DESIGN.md
