@@ -15,18 +15,24 @@
 
 namespace kc {
 
-static uint32_t crc32Update(uint32_t crc, const uint8_t* p, size_t n) {
-  static uint32_t table[256];
-  static bool init = false;
-  if(!init) {
+struct Crc32Table {
+  uint32_t t[256];
+  Crc32Table() {
     for(uint32_t i = 0; i < 256; i++) {
       uint32_t c = i;
       for(int k = 0; k < 8; k++)
         c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-      table[i] = c;
+      t[i] = c;
     }
-    init = true;
   }
+};
+
+static uint32_t crc32Update(uint32_t crc, const uint8_t* p, size_t n) {
+  // a function-local static is initialised once, thread-safely: engine threads of the
+  // CLI write files concurrently (the lazily filled table this replaces was a data race,
+  // found by tests/test_sanitizers.py::test_cli_sigterm_under_tsan)
+  static const Crc32Table tab;
+  const uint32_t* table = tab.t;
   crc = ~crc;
   for(size_t i = 0; i < n; i++)
     crc = table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);

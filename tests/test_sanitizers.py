@@ -1,12 +1,19 @@
-"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer (sanitizers
-on the CPU build; the survey found the reference's own encoder overflow this way,
-cpp/game/board.cpp:400).  tests/san/Makefile builds
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer and ThreadSanitizer
+(sanitizers on the CPU build; the survey found the reference's own encoder
+overflow this way, cpp/game/board.cpp:400).  tests/san/Makefile builds
 
   * host_check: the product's host code -- CFNN model I/O (model.cpp), the .npz row
     writer (npzwrite.cpp), geometry / Zobrist tables (tables.cpp, refrand.cpp) and the
     CLI config layer (cli_config.h) -- host side only (hipcc -Xarch_host -fsanitize=...);
   * liboracle_san.so: the oracle (test infrastructure) with gcc's sanitizers, driven
-    from python with the ASan runtime preloaded.
+    from python with the ASan runtime preloaded;
+  * katago_tsan / bench_writer_tsan: the host programs' threads under ThreadSanitizer
+    (the reference's threads: command/selfplay.cpp:271-394 game/server threads and the
+    model poll; selfplaymanager.cpp:330) -- the CLI with several engine threads per
+    device, the shared models-directory watch (a hot reload mid-run), the game counter,
+    the log and SIGTERM; bench.py's engine loop with its .npz writer thread -- over a
+    host-only stand-in of the self-play C ABI (san/fake_engine.cpp) and the product's
+    .npz writer.
 
 Any sanitizer report aborts the run (-fno-sanitize-recover=all), so every check here is
 "exit status 0 and the expected output".  No GPU is touched."""
@@ -120,7 +127,7 @@ m = oracle.Model("MODEL")
 for X, Y, W in [(5, 5, 4), (7, 7, 5)]:
     binp, glob = oracle.encode_batch(X, Y, W, np.zeros((3, X * Y), np.uint8), np.full((3, 5), -1, np.int8),
                                      np.full((3, 5), 4, np.int8), np.ones(3, np.uint8), np.arange(3, dtype=np.int32))
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         m.forward(X, Y, binp, glob.reshape(3, 1), mode=mode, threads=2)
 for (X, Y, W), model in [((5, 5, 4), None), ((9, 9, 5), None), ((5, 5, 4), m)]:
     sp = oracle.Selfplay(X, Y, W, games=4, max_visits=16, node_cap=64, seed=3, nn_cache_log2=6, nn_batch_cap=3,
@@ -147,3 +154,74 @@ def test_oracle_under_sanitizers(built, tmp_path):
     out = _run([sys.executable, "-c", script], cwd=REPO,
                env={"LD_PRELOAD": asan, "ORACLE_LIB": ORA, "PYTHONPATH": REPO})
     assert "oracle ok" in out and out.count("selfplay") == 3, out
+
+
+def _tsan(args, **kw):
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    env.update(kw.pop("env", {}))
+    r = subprocess.run(args, capture_output=True, text=True, env=env, timeout=600, **kw)
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    return r
+
+
+def test_bench_writer_threads_under_tsan(built, tmp_path):
+    r = _tsan([os.path.join(SAN, "_build", "bench_writer_tsan"), str(tmp_path), "2", "30"])
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "written in 30 files" in r.stdout, r.stdout
+    assert len([f for f in os.listdir(tmp_path) if f.endswith(".npz")]) == 30
+
+
+def test_cli_threads_under_tsan(built, tmp_path):
+    """2 devices x 2 engines, a newer model appearing mid-run (every engine switches and
+    writes under the new name), then -max-games-total stops all engines."""
+    import threading
+    import time
+    models = tmp_path / "models"
+    models.mkdir()
+    (models / "netA.cfnn").write_bytes(b"fake")
+    out = tmp_path / "out"
+
+    def drop_new_model():
+        time.sleep(1.5)
+        (models / "netB.cfnn").write_bytes(b"fake2")
+        os.utime(models / "netB.cfnn", (time.time() + 5, time.time() + 5))
+
+    t = threading.Thread(target=drop_new_model)
+    t.start()
+    cmd = [os.path.join(SAN, "_build", "katago_tsan"), "selfplay", "-config",
+           os.path.join(REPO, "configs", "selfplay_coffee5.cfg"), "-models-dir", str(models), "-output-dir", str(out),
+           "-max-games-total", "60000", "-override-config",
+           "numGameThreads=64,numGpus=2,numNNServerThreadsPerModel=4,maxRowsPerTrainFile=500,modelPollSeconds=0.05"]
+    r = _tsan(cmd)
+    t.join()
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    log = r.stdout
+    for g in ("0.0", "0.1", "1.0", "1.1"):
+        assert "gpu %s done" % g in log, log[-3000:]
+        assert "gpu %s: switched to model" % g in log, log[-3000:]
+    for name in ("netA", "netB"):
+        assert os.listdir(out / name / "tdata"), name
+        assert os.listdir(out / name / "sgfs"), name
+
+
+def test_cli_sigterm_under_tsan(built, tmp_path):
+    """SIGTERM (selfplay.cpp:22-29): every engine thread flushes its rows and exits 0."""
+    import signal
+    import time
+    models = tmp_path / "models"
+    models.mkdir()
+    (models / "netA.cfnn").write_bytes(b"fake")
+    out = tmp_path / "out"
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    p = subprocess.Popen([os.path.join(SAN, "_build", "katago_tsan"), "selfplay", "-config",
+                          os.path.join(REPO, "configs", "selfplay_coffee5.cfg"), "-models-dir", str(models),
+                          "-output-dir", str(out), "-override-config",
+                          "numGameThreads=64,numGpus=2,numNNServerThreadsPerModel=2,maxRowsPerTrainFile=100000"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    time.sleep(2.0)
+    p.send_signal(signal.SIGTERM)
+    so, se = p.communicate(timeout=120)
+    assert "ThreadSanitizer" not in se, se[-6000:]
+    assert p.returncode == 0, so[-2000:] + se[-2000:]
+    assert "gpu 0.0 done" in so and "gpu 1.0 done" in so
+    assert os.listdir(out / "netA" / "tdata")  # the pending rows were flushed

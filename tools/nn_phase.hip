@@ -1,6 +1,6 @@
 // Phase timing of the fused network kernel (shader-clock stamps from the first
 // workgroups).  Build: make -C tools nn_phase ; run on the GPU box:
-// tools/_build/nn_phase [boards]
+// tools/_build/nn_phase [boards] [path: 0 fast, 1 accurate, 3 corrected, 4 accurate-nb2]
 #define KC_NN_PROFILE
 #include "../katacoffee_amd/csrc/nn.hip"
 
@@ -12,7 +12,8 @@ using namespace kc;
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 4096;  // <= 5 x CUs: the small-batch (5-board) instance
   ModelHost m = randomModel(modelCfgByName("b6c96"), 1);
-  NNEngine eng(m, 5, 5, 4);
+  const int path = argc > 2 ? atoi(argv[2]) : NN_FAST;
+  NNEngine eng(m, 5, 5, 4, path);
   const int words = (15 * 25 + 63) / 64;
   std::vector<uint64_t> in((size_t)n * words);
   std::mt19937_64 rng(1);
