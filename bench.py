@@ -346,6 +346,32 @@ class Groups:
         for e in self.g:
             e.drain_games()
 
+    # device-resident row hand-off: each engine packs its rows into a device block on
+    # its own stream (coffee_selfplay_stage_rows) at the end of a step; the block of step
+    # s is gathered / copied while step s + 1 runs (two slots)
+    def setup_staging(self, torch, kc, X, Y):
+        rb = kc.row_bytes(X, Y)
+        self.stage_buf = [[torch.empty((e.row_capacity(), rb), dtype=torch.uint8, device="cuda") for e in self.g]
+                          for _ in range(2)]
+        self.stage_cnt = torch.zeros((2, len(self.g)), dtype=torch.int64).pin_memory()
+        self.streams = [torch.cuda.ExternalStream(e.stream_ptr()) for e in self.g]
+        self.events = [[torch.cuda.Event() for _ in self.g] for _ in range(2)]
+        self.torch = torch
+
+    def stage(self, i):
+        for k, e in enumerate(self.g):
+            e.stage_rows(self.stage_buf[i][k], self.stage_cnt[i, k])
+            self.events[i][k].record(self.streams[k])
+
+    def collect(self, i):
+        """This rank's rows staged into slot i, as one device block [n][row_bytes]
+        (waits for the staging only, not for the steps enqueued after it)."""
+        parts = []
+        for k in range(len(self.g)):
+            self.events[i][k].synchronize()
+            parts.append(self.stage_buf[i][k][:int(self.stage_cnt[i, k])])
+        return self.torch.cat(parts) if len(parts) > 1 else parts[0]
+
     def enable_timing(self, every):
         for e in self.g:
             e.enable_timing(every)
@@ -469,24 +495,37 @@ def main():
     rows_gathered = 0
     per_rank_rows = 0
     reloads = 0
+    sp.setup_staging(torch, kc, X, Y)
+
+    def process(i):
+        # step i's rows: device block -> RCCL gather to rank 0 -> host -> writer thread,
+        # while the next step's kernels run on the engine streams
+        nonlocal rows_gathered, per_rank_rows
+        packed = sp.collect(i)
+        per_rank_rows += packed.shape[0]
+        if dist is not None:
+            packed = kcrows.gather_packed_to_rank0(packed, dist)
+        if rank == 0:
+            rows = kcrows.unpack(packed.cpu().numpy(), X, Y)
+            rows_gathered += len(rows["meta"])
+            if writer:
+                writer.put(rows)
+        torch.cuda.current_stream().synchronize()  # slot i's blocks are free for step + 2
+
     barrier()
     t0 = time.perf_counter()
+    prev = None
     for step in range(args.steps):
         if args.reload_every and step and step % args.reload_every == 0:
             reloads += 1
             reload(reloads)
         sp.step(rps)
-        rows = sp.drain_rows()
-        sp.drain_games()
-        per_rank_rows += len(rows["meta"])
-        if dist is not None:
-            # RCCL gather of this step's finished rows to rank 0 (the writer rank)
-            rows = kcrows.gather_to_rank0(rows, X, Y, dist, torch.device("cuda", local))
-        if rank == 0:
-            rows_gathered += len(rows["meta"])
-            if writer:
-                writer.put(rows)
+        sp.stage(step % 2)
+        if prev is not None:
+            process(prev)
+        prev = step % 2
         progress("timed", step, args.steps, t0)
+    process(prev)
     sp.sync()
     if writer:
         writer.close()  # every drained row is on disk before the clock stops

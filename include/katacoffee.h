@@ -284,6 +284,23 @@ int coffee_selfplay_drain_rows(coffee_selfplay* h, int max_rows, uint8_t* bin, f
  *   moves  [g][A][2] u8 (cell = y*x_len + x, direction 0..3 = N, W, NW, NE; 0xFF past the end)
  * Either output pointer may be NULL.  *n_out = records copied. */
 int coffee_selfplay_drain_games(coffee_selfplay* h, int max_games, int32_t* header, uint8_t* moves, int* n_out);
+/* Device-resident row hand-off for multi-GPU writers (the RCCL gather of SURVEY 8e;
+ * trainingwrite.cpp:774-937 writes the rows afterwards).  Enqueued on the engine's own
+ * stream, returns at once: every pending row is packed into dst (DEVICE memory,
+ * [max_rows][coffee_row_bytes] u8, one record per row = bin, glob, pol, gtgt, value,
+ * meta of coffee_selfplay_drain_rows back to back; max_rows >= the engine's row
+ * capacity), the number of rows is copied to *count (HOST memory, pinned for an
+ * asynchronous copy; valid once the engine stream has passed this call: wait on an
+ * event recorded on coffee_selfplay_stream) and the engine's row buffer is emptied.
+ * flags COFFEE_STAGE_DISCARD_GAMES: also drop the finished-game records (a caller that
+ * writes no SGF).  The next steps may be enqueued before the rows are consumed. */
+#define COFFEE_STAGE_DISCARD_GAMES 1
+int coffee_selfplay_stage_rows(coffee_selfplay* h, void* dst, int max_rows, uint64_t* count, int flags);
+int coffee_selfplay_row_capacity(coffee_selfplay* h, int* rows);
+int coffee_row_bytes(int x, int y, int* bytes);
+/* The engine's HIP stream (hipStream_t), for callers that order their own work
+ * (events, copies, collectives) against the engine's. */
+int coffee_selfplay_stream(coffee_selfplay* h, void** stream);
 /* Replaces the network for every subsequent round of every game (the reference's
  * model hot reload with switchNetsMidGame, selfplay.cpp:135-260, play.cpp:1210-1226).
  * On error (unreadable / mismatched model) the current network stays in use. */

@@ -107,6 +107,7 @@ EXPORTS = [
     "coffee_nn_forward", "coffee_nn_forward2", "coffee_nn_destroy", "coffee_nn_create2", "coffee_nn_is_fused", "coffee_fake_net", "coffee_search_params_default",
     "coffee_selfplay_create", "coffee_selfplay_step", "coffee_selfplay_sync", "coffee_selfplay_stats_get",
     "coffee_selfplay_drain_rows", "coffee_selfplay_drain_games", "coffee_selfplay_set_model",
+    "coffee_selfplay_stage_rows", "coffee_selfplay_row_capacity", "coffee_row_bytes", "coffee_selfplay_stream",
     "coffee_selfplay_set_model_bytes",
     "coffee_selfplay_destroy", "coffee_selfplay_game_info",
     "coffee_selfplay_game_tree", "coffee_selfplay_root_policy", "coffee_debug_cdf_table", "coffee_debug_zobrist",
@@ -157,6 +158,10 @@ def lib():
         L.coffee_selfplay_stats_get.argtypes = [c_p, c_p]
         L.coffee_selfplay_drain_rows.argtypes = [c_p, c_i] + [c_p] * 7
         L.coffee_selfplay_drain_games.argtypes = [c_p, c_i, c_p, c_p, c_p]
+        L.coffee_selfplay_stage_rows.argtypes = [c_p, c_p, c_i, c_p, c_i]
+        L.coffee_selfplay_row_capacity.argtypes = [c_p, c_p]
+        L.coffee_row_bytes.argtypes = [c_i, c_i, c_p]
+        L.coffee_selfplay_stream.argtypes = [c_p, c_p]
         L.coffee_selfplay_set_model.argtypes = [c_p, ctypes.c_char_p]
         L.coffee_selfplay_set_model_bytes.argtypes = [c_p, c_p, c_u64]
         L.coffee_selfplay_destroy.argtypes = [c_p]
@@ -355,6 +360,13 @@ def cdf_table(X=5, Y=5, W=4):
     return out
 
 
+def row_bytes(X, Y):
+    """Bytes of one packed row (coffee_row_bytes; katacoffee_amd.rows.row_bytes)."""
+    b = ctypes.c_int()
+    check(lib().coffee_row_bytes(X, Y, ctypes.byref(b)))
+    return b.value
+
+
 def write_npz(path, rows, X, Y):
     """Training rows -> .npz in the reference's format (native writer)."""
     n = len(rows["globalInputNC"])
@@ -433,6 +445,26 @@ class Selfplay:
         check(lib().coffee_selfplay_drain_rows(self.h, n, *[_ptr(rows[k]) for k in order], ctypes.byref(got)))
         assert got.value == n
         return rows
+
+    def row_capacity(self):
+        n = ctypes.c_int()
+        check(lib().coffee_selfplay_row_capacity(self.h, ctypes.byref(n)))
+        return n.value
+
+    def stream_ptr(self):
+        """The engine's hipStream_t (for torch.cuda.ExternalStream)."""
+        p = ctypes.c_void_p()
+        check(lib().coffee_selfplay_stream(self.h, ctypes.byref(p)))
+        return p.value
+
+    def stage_rows(self, dst, count, discard_games=True):
+        """Device-resident row hand-off (coffee_selfplay_stage_rows), enqueued on the
+        engine's stream: dst a device uint8 tensor [>= row_capacity][row_bytes], count a
+        pinned host int64 tensor element (filled asynchronously)."""
+        assert dst.is_cuda and dst.dtype.itemsize == 1 and dst.is_contiguous()
+        assert count.is_pinned() and count.dtype.itemsize == 8
+        check(lib().coffee_selfplay_stage_rows(self.h, ctypes.c_void_p(dst.data_ptr()), dst.shape[0],
+                                               ctypes.c_void_p(count.data_ptr()), 1 if discard_games else 0))
 
     def drain_games(self, max_games=1 << 20):
         """Finished-game records: header [g][4] i32 (slot, game number, moves, winner)

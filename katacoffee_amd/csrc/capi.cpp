@@ -86,7 +86,7 @@ static void checkGeom(int x, int y, int w) {
 extern "C" {
 
 const char* coffee_last_error(void) { return gLastError.c_str(); }
-int coffee_abi_version(void) { return 105; }
+int coffee_abi_version(void) { return 106; }
 
 int coffee_device_count(int* count) {
   return guarded([&] {
@@ -353,6 +353,36 @@ int coffee_selfplay_drain_rows(coffee_selfplay* h, int max_rows, uint8_t* bin, f
   return guarded([&] {
     need(h && h->eng && n_out, "NULL argument");
     *n_out = h->eng->drain(max_rows, bin, glob, pol, gtgt, value, meta);
+  });
+}
+
+int coffee_row_bytes(int x, int y, int* bytes) {
+  return guarded([&] {
+    need(bytes != nullptr, "NULL argument");
+    need(x >= 2 && y >= 2 && x <= MAX_LEN && y <= MAX_LEN, "bad shape");
+    *bytes = rowBytes(x * y);
+  });
+}
+
+int coffee_selfplay_row_capacity(coffee_selfplay* h, int* rows) {
+  return guarded([&] {
+    need(h && h->eng && rows, "NULL argument");
+    *rows = h->eng->dev().rowCap;
+  });
+}
+
+int coffee_selfplay_stream(coffee_selfplay* h, void** stream) {
+  return guarded([&] {
+    need(h && h->eng && stream, "NULL argument");
+    *stream = (void*)h->eng->stream();
+  });
+}
+
+int coffee_selfplay_stage_rows(coffee_selfplay* h, void* dst, int max_rows, uint64_t* count, int flags) {
+  return guarded([&] {
+    need(h && h->eng && dst && count, "NULL argument");
+    need((flags & ~COFFEE_STAGE_DISCARD_GAMES) == 0, "unknown flags");
+    h->eng->stageRows((uint8_t*)dst, max_rows, (unsigned long long*)count, (flags & COFFEE_STAGE_DISCARD_GAMES) != 0);
   });
 }
 

@@ -316,6 +316,7 @@ struct SearchDev {
   DPtr<int32_t> rMeta;        // [rowCap][4]
   DPtr<unsigned long long> rCount;
   DPtr<unsigned long long> rDropped;
+  DPtr<unsigned long long> rStaged;  // rows handed out by coffee_selfplay_stage_rows so far
   // finished-game records (drained by the host for SGF files)
   int gCap;
   DPtr<GameRec> gRec;               // [gCap]
@@ -332,6 +333,12 @@ void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEv
                   hipEvent_t e1 = nullptr, bool resetCommit = false);
 // accumulate: add the batch size to *d.nnTimedEvals (rounds whose network launch is timed)
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate);
+// Packs the device row buffer's rows into dst ([rowCap][rowBytes], rows.py FIELDS order),
+// copies their count to countOut (host, asynchronously) and empties the buffer (and the
+// finished-game records when discardGames); stream-ordered, no host synchronisation.
+void launchStageRows(const SearchDev& d, const SearchDev* dd, uint8_t* dst, unsigned long long* countOut,
+                     bool discardGames, hipStream_t st);
+int rowBytes(int A);  // bytes of one packed row at board area A
 void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
                   hipEvent_t e1 = nullptr);
 void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);  // + kRows

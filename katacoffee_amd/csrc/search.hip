@@ -3352,7 +3352,10 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
 // The thread's need flags and cache bids are loaded once, before the scan (all in
 // flight together when it has at most CP_VEC games), so the kernel waits for one
 // round of loads instead of one per game.
-constexpr int CP_VEC = 16;
+// (up to 32 games per thread: 256 threads cover a group of 8192 games -- a 4-wave
+// workgroup finds room beside the other group's network kernels, where a 1024-thread
+// one waited for a whole CU to drain: 34 us per launch at C3)
+constexpr int CP_VEC = 32;
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
   __shared__ uint32_t wsum[16], wpre[17];
@@ -3562,6 +3565,55 @@ __global__ void kGameTree(const SearchDev* __restrict__ dp, int g, int maxNodes,
 // ---------------------------------------------------------------------------
 static int laneItems(int P) { return P <= 128 ? 2 : (P <= 256 ? 4 : 7); }
 
+// ---------------------------------------------------------------------------
+// Row staging for device-resident gathers (coffee_selfplay_stage_rows): one wave per
+// row packs the row's six arrays into one contiguous record (rows.py FIELDS: bin u8
+// [15][pb], glob f32, pol i16 [2][P], gt f32 [64], val i8 [5][A], meta i32 [4]), so a
+// rank's rows leave as one device block for the RCCL gather.
+int rowBytes(int A) {
+  const int pb = (A + 7) / 8;
+  return NUM_SPATIAL * pb + 4 + 2 * 4 * A * 2 + 64 * 4 + 5 * A + 16;
+}
+
+__global__ void __launch_bounds__(256) kStageRows(const SearchDev* __restrict__ dp, uint8_t* __restrict__ dst,
+                                                  int rb) {
+  const SearchDev& d = *dp;
+  const int A = d.A, P = d.P, pb = (A + 7) / 8;
+  const unsigned long long n = *d.rCount;
+  const int lane = threadIdx.x & 63;
+  const int sz[6] = {NUM_SPATIAL * pb, 4, 4 * P, 256, 5 * A, 16};
+  for(unsigned long long r = blockIdx.x * 4ull + (threadIdx.x >> 6); r < n; r += gridDim.x * 4ull) {
+    const uint8_t* src[6] = {d.rBin + r * sz[0], reinterpret_cast<const uint8_t*>(d.rGlob + r),
+                             reinterpret_cast<const uint8_t*>(d.rPol + r * 2 * P),
+                             reinterpret_cast<const uint8_t*>(d.rGt + r * 64), reinterpret_cast<const uint8_t*>((const int8_t*)d.rVal) + r * sz[4],
+                             reinterpret_cast<const uint8_t*>(d.rMeta + r * 4)};
+    uint8_t* o = dst + r * (unsigned long long)rb;
+#pragma unroll
+    for(int f = 0; f < 6; f++) {
+      for(int i = lane; i < sz[f]; i += 64)
+        o[i] = src[f][i];
+      o += sz[f];
+    }
+  }
+}
+
+__global__ void kStageDone(const SearchDev* __restrict__ dp, int discardGames) {
+  const SearchDev& d = *dp;
+  *d.rStaged += *d.rCount;
+  *d.rCount = 0;
+  if(discardGames)
+    *d.gCount = 0;
+}
+
+void launchStageRows(const SearchDev& d, const SearchDev* dd, uint8_t* dst, unsigned long long* countOut,
+                     bool discardGames, hipStream_t st) {
+  hipLaunchKernelGGL(kStageRows, dim3(1024), dim3(256), 0, st, dd, dst, rowBytes(d.A));
+  KC_HIP(hipGetLastError());
+  KC_HIP(hipMemcpyAsync(countOut, d.rCount, 8, hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(kStageDone, dim3(1), dim3(1), 0, st, dd, discardGames ? 1 : 0);
+  KC_HIP(hipGetLastError());
+}
+
 void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   hipLaunchKernelGGL(kInit, dim3(d.G), dim3(64), 0, st, dd, d.T);
   KC_HIP(hipGetLastError());
@@ -3571,7 +3623,7 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
 // that small fits beside a network workgroup of the other game group on its CU (1024
 // threads need 4 waves per SIMD) and does not wait for a free one.
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate) {
-  const int nt = d.G <= 256 * CP_VEC ? 256 : 1024;
+  const int nt = d.G <= 256 * CP_VEC ? 256 : 1024;  // 1024 only past 8192 games per engine
   hipLaunchKernelGGL(kCompact, dim3(1), dim3(nt), 0, st, dd, accumulate ? 1 : 0);
   KC_HIP(hipGetLastError());
 }

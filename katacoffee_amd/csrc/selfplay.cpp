@@ -201,6 +201,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.rMeta = devAlloc<int32_t>(owned_, (size_t)rowCap * 4, false);
   d.rCount = devAlloc<unsigned long long>(owned_, 1);
   d.rDropped = devAlloc<unsigned long long>(owned_, 1);
+  d.rStaged = devAlloc<unsigned long long>(owned_, 1);
   d.nnNeed = devAlloc<int32_t>(owned_, G);
   d.nnDefer = devAlloc<int32_t>(owned_, G);
   d.nnBid = devAlloc<uint32_t>(owned_, G);
@@ -369,8 +370,10 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
   unsigned long long cnt = 0, dropped = 0;
   KC_HIP(hipMemcpy(&cnt, hd_.rCount, 8, hipMemcpyDeviceToHost));
   KC_HIP(hipMemcpy(&dropped, hd_.rDropped, 8, hipMemcpyDeviceToHost));
+  unsigned long long staged = 0;
+  KC_HIP(hipMemcpy(&staged, hd_.rStaged, 8, hipMemcpyDeviceToHost));
   out.rows_pending = cnt;
-  out.rows_written = rowsDrained_ + cnt;
+  out.rows_written = rowsDrained_ + staged + cnt;
   out.rows_dropped = dropped;
   unsigned long long gdrop = 0;
   KC_HIP(hipMemcpy(&gdrop, hd_.gDropped, 8, hipMemcpyDeviceToHost));
@@ -423,6 +426,30 @@ int SelfplayEngine::drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, 
   KC_HIP(hipMemcpy(hd_.rCount, &left, 8, hipMemcpyHostToDevice));
   rowsDrained_ += n;
   return n;
+}
+
+void SelfplayEngine::stageRows(uint8_t* dst, int maxRows, unsigned long long* countOut, bool discardGames) {
+  if(maxRows < hd_.rowCap)
+    throw std::invalid_argument("stage_rows: the destination must hold the row capacity (" +
+                                std::to_string(hd_.rowCap) + " rows)");
+  launchStageRows(hd_, dd_, dst, countOut, discardGames, stream_);
+  // kernel timings whose events completed are folded in without waiting (a run that
+  // never drains synchronously would otherwise keep every event pending)
+  size_t keep = 0;
+  for(size_t i = 0; i < pending_.size(); i++) {
+    const PendingTiming& p = pending_[i];
+    if(hipEventQuery(p.b) == hipSuccess) {
+      float ms = 0.0f;
+      KC_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+      kernelMs_[p.which] += ms;
+      kernelLaunches_[p.which]++;
+      evPool_.push_back(p.a);
+      evPool_.push_back(p.b);
+    } else {
+      pending_[keep++] = p;
+    }
+  }
+  pending_.resize(keep);
 }
 
 int SelfplayEngine::drainGames(int maxGames, int32_t* header, uint8_t* moves) {

@@ -21,6 +21,11 @@ class SelfplayEngine {
   void stats(coffee_selfplay_stats& out);
   int drain(int maxRows, uint8_t* bin, float* glob, int16_t* pol, float* gt, int8_t* val, int32_t* meta);
   int drainGames(int maxGames, int32_t* header, uint8_t* moves);
+  // Stream-ordered row hand-off (no host synchronisation): packs every pending row into
+  // dst (device, >= rowCap rows), their count into *countOut (host, valid once the
+  // engine stream passes this point) and empties the buffer.
+  void stageRows(uint8_t* dst, int maxRows, unsigned long long* countOut, bool discardGames);
+  hipStream_t stream() const { return stream_; }
   // Replaces the network for all subsequent rounds (all games: switchNetsMidGame).
   void setModel(const char* path);
   // The same from a CFNN image in host memory (weights broadcast from another rank).

@@ -45,26 +45,34 @@ def unpack(buf, X, Y):
     return out
 
 
-def gather_to_rank0(rows, X, Y, dist, device):
-    """Gathers every rank's row block to rank 0 (the writer rank), the engine's only
-    collective.  Counts are all-gathered, blocks padded to the largest.
-    Returns the concatenated rows on rank 0 and None elsewhere."""
+def gather_packed_to_rank0(packed, dist):
+    """Gathers every rank's packed row block (uint8 tensor [n][row_bytes] on the process
+    group's device: the engines' staged rows, coffee_selfplay_stage_rows) to rank 0, the
+    writer rank -- the engine's only collective.  The counts are all-gathered
+    (one small host read on the collective's stream), blocks padded to the largest and
+    gathered (RCCL over xGMI for "nccl"; the rows never visit this rank's host).  Returns
+    the concatenated block on rank 0 (same device) and None elsewhere."""
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
-    buf = pack(rows, X, Y)
-    n = buf.shape[0]
-    cnt = torch.tensor([n], dtype=torch.int64, device=device)
+    n, rb = packed.shape
+    cnt = torch.tensor([n], dtype=torch.int64, device=packed.device)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(cnts, cnt)
     counts = [int(c.item()) for c in cnts]
-    mx = max(counts)
-    rb = row_bytes(X, Y)
-    pad = torch.zeros((max(mx, 1), rb), dtype=torch.uint8, device=device)
+    pad = torch.zeros((max(max(counts), 1), rb), dtype=torch.uint8, device=packed.device)
     if n:
-        pad[:n] = torch.from_numpy(buf).to(device)
+        pad[:n] = packed
     outs = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
     dist.gather(pad, outs, dst=0)
     if rank != 0:
         return None
-    blocks = [o[:c].cpu().numpy() for o, c in zip(outs, counts)]
-    return unpack(np.concatenate(blocks, axis=0), X, Y)
+    return torch.cat([o[:c] for o, c in zip(outs, counts)])
+
+
+def gather_to_rank0(rows, X, Y, dist, device):
+    """gather_packed_to_rank0 for host row dicts: packed, gathered on `device`, unpacked
+    on rank 0 (None elsewhere)."""
+    import torch
+    buf = torch.from_numpy(pack(rows, X, Y)).to(device)
+    out = gather_packed_to_rank0(buf, dist)
+    return None if out is None else unpack(out.cpu().numpy(), X, Y)

@@ -65,6 +65,44 @@ def test_row_gather_world2():
         np.testing.assert_array_equal(gathered[k][sel], ref[k])
 
 
+def _packed_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    rb = R.row_bytes(5, 5)
+    n = [3, 0, 7][rank]  # ragged blocks, one rank with no rows
+    blk = torch.full((n, rb), rank + 1, dtype=torch.uint8)
+    if n:
+        blk[:, 0] = torch.arange(n, dtype=torch.uint8)
+    got = R.gather_packed_to_rank0(blk, dist)
+    q.put((rank, None if got is None else got.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_packed_gather_world3_ragged():
+    """The device-block gather (bench.py's path, here on CPU tensors): ragged counts and
+    an empty rank arrive on rank 0 in rank order, nothing elsewhere."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_packed_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None and res[2] is None
+    got = res[0]
+    assert got.shape == (10, R.row_bytes(5, 5))
+    np.testing.assert_array_equal(got[:3, 1], 1)
+    np.testing.assert_array_equal(got[3:, 1], 3)
+    np.testing.assert_array_equal(got[:3, 0], np.arange(3))
+    np.testing.assert_array_equal(got[3:, 0], np.arange(7))
+
+
 def test_pack_roundtrip():
     rng = np.random.default_rng(0)
     n = 5

@@ -26,6 +26,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
     }                                                                           \
   } while(0)
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h2x __attribute__((ext_vector_type(2)));
+// v_cvt_scalef32_pk_fp8_f16 (scale 1): the corrected network converts fp16 weights
+__global__ void kCvtH(const float* in, int n, unsigned* out) {
+  const int i = threadIdx.x;
+  if(2 * i + 1 < n) {
+    s16x2 o = {0, 0};
+    o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(o, h2x{(_Float16)in[2 * i], (_Float16)in[2 * i + 1]}, 1.0f, false);
+    out[i] = (unsigned)__builtin_bit_cast(int, o) & 0xffffu;
+  }
+}
+
 __global__ void kCvt(const float* in, int n, unsigned* out) {
   const int i = threadIdx.x;
   if(2 * i + 1 < n)
@@ -79,6 +91,17 @@ int main() {
     const unsigned char g = (got[i / 2] >> (8 * (i & 1))) & 0xff;
     const bool skip = i == 7;  // 1000: report only (saturation behaviour)
     printf("cvt %-10g -> 0x%02x (%g)%s\n", vals[i], g, e4m3(g),
+           skip ? "  [past 448: reported]" : (g == want[i] ? "" : "  FAIL"));
+    if(!skip && g != want[i])
+      fails++;
+  }
+  // 1b. the fp16 -> e4m3 conversion (values exact in fp16)
+  hipLaunchKernelGGL(kCvtH, dim3(1), dim3(64), 0, 0, din, n, dout);
+  CK(hipMemcpy(got, dout, 4 * (n / 2), hipMemcpyDeviceToHost));
+  for(int i = 0; i < n; i++) {
+    const unsigned char g = (got[i / 2] >> (8 * (i & 1))) & 0xff;
+    const bool skip = i == 7 || i == 11;
+    printf("cvt f16 %-10g -> 0x%02x (%g)%s\n", vals[i], g, e4m3(g),
            skip ? "  [past 448: reported]" : (g == want[i] ? "" : "  FAIL"));
     if(!skip && g != want[i])
       fails++;
