@@ -86,7 +86,7 @@ struct NNGeo {
   // j+2 is requested right after the barrier that publishes chunk j+1 and frees chunk j.
   // (6 slots, one barrier per 3 taps, would fill all 160 KiB and keep the other game
   // group's search kernels off the CU while the network runs.)
-  static constexpr int RING = BL ? (MODE_ == NN_MODE_F8C ? 3 : 2) : ((NB_ == NN_SMALL_NB && !SPLIT) ? 4 : 3);
+  static constexpr int RING = BL ? 2 : ((NB_ == NN_SMALL_NB && !SPLIT) ? 4 : 3);
   static constexpr bool PAIRS = RING == 4;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
@@ -118,15 +118,8 @@ struct NNGeo {
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap and plane
-  // a tap's second weight block: fp16 lo fragments (mode 1); e4m3 lo(w) 2^11 only, 8 B per
-  // lane and fragment (mode 2: e4m3(w) is converted from the fp16 hi fragment in registers)
-  static constexpr int WPL2 = !SPLIT ? 0 : (MODE_ == NN_MODE_F8C ? WBUF / 2 : WBUF);
-  static constexpr int WSLOT = WBUF + WPL2;             // one ring slot
+  static constexpr int WSLOT = PLANES * WBUF;           // one ring slot
   static constexpr int SLOT_PIECES = WSLOT / 64;        // its 1-KiB pieces
-  // 1-KiB pieces of one tap of a conv with ncb 32-channel input blocks
-  static constexpr int tapPieces(int ncb) {
-    return ncb * NCT_ALL * (!SPLIT ? 2 : (MODE_ == NN_MODE_F8C ? 3 : 4)) / 2;
-  }
   // row tables (u16): rowPa[MROWS], rowBP[MROWS], bpRow[ROWS] -- built on the host
   static constexpr int NTAB = 2 * MROWS + ROWS;
   static constexpr int OFF_TAB = OFF_BIAS + NB * 64 * 4;
@@ -341,8 +334,6 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
 // ---- borderless (BL) instances ----------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef _Float16 h2x __attribute__((ext_vector_type(2)));
 
 // Per tile: the byte address of this lane's A-fragment row (row r = output row r, plus
 // the lane's k-quarter) and a 9-bit mask of the 3x3 taps whose neighbour is on the
@@ -373,46 +364,41 @@ KC_D void stageChunk(const h16x8* __restrict__ src, uint32_t slotAddr, int piece
 }
 
 // Implicit-GEMM convolution of a BL instance, computed transposed like convTiles.
-// Weights stream through the RING-slot ring in chunks of TPC taps (one slot: a 96-channel
-// tap, or three stem taps); chunk j of this conv lives in slot (PAR + j) % RING, PAR the
-// conv's first chunk index in the whole stream (mod RING).  On entry chunks 0 .. RING-2
-// were requested, chunk 0 is resident and published (the caller retired its DMA before
-// the barrier that published the conv's input), and the slot of chunk RING-1 is free: it
-// is requested at once.  One barrier per chunk, before the chunk's last K-step: every
-// wave retires its pieces of chunk j+1 (waitVm<0>: later chunks may land early, which
-// only costs a wait), the barrier publishes them and frees chunk j's slot (all its
-// fragment reads are complete: lgkmcnt(0)), and chunk j+RING is requested into it (this
-// conv's, or the next conv's chunk j+RING-NCH: nextPieces each, nextNCH of them).
-// A-fragment addresses are formed per tap: the neighbour row, or the zero row when the
-// neighbour is off the board.
+// Weights stream through the 2-slot ring in chunks of TPC taps (one slot: a 96-channel
+// tap, or three stem taps); chunk j of this conv lives in slot (PAR + j) & 1, PAR the
+// parity of the conv's first chunk in the whole stream.  On entry chunk 0 is resident and
+// published (the caller retired its DMA before the barrier that published the conv's
+// input) and chunk 1's slot is free: chunk 1 is requested at once (or, for a one-chunk
+// conv, the next conv's chunk 0).  One barrier per chunk, before the chunk's last K-step:
+// every wave retires its pieces of chunk j+1, the barrier publishes them and frees chunk
+// j's slot (all its fragment reads are complete: lgkmcnt(0)), and chunk j+2 is requested
+// into it (this conv's, or the next conv's chunk 0).  A-fragment addresses are formed per
+// tap: the neighbour row, or the zero row when the neighbour is off the board.
 //   MODE 1: acc += hi(w) hi(x) + lo(w) hi(x) + hi(w) lo(x)  (three f16 MFMAs per step)
 //   MODE 2: acc += hi(w) hi(x) per step (f16 MFMA), and per pair of steps one scaled e4m3
-//           MFMA over [lo(w) 2^11 | w] x [x | lo(x) 2^11] of both steps, scale 2^-11;
-//           e4m3(w) is converted from the hi fragment (e4m3(fp16(w)), pk conversions).
+//           MFMA over [lo(w) 2^11 | w] x [x | lo(x) 2^11] of both steps, scale 2^-11
 template <class G, int NTAPS, int NCB, int PAR>
 KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                      f32x4 (&acc)[G::MAXT][G::NCT], const int (&rb)[G::MAXT], const uint32_t (&vm)[G::MAXT],
-                     int cg, int lane, int tid, const h16x8* __restrict__ wNext, int nextPieces, int nextNCH) {
-  constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap of the hi block
-  constexpr int CH = G::tapPieces(NCB);  // per tap
+                     int cg, int lane, int tid, const h16x8* __restrict__ wNext, int nextPieces) {
+  constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap and plane
+  constexpr int CH = CHP * G::PLANES;    // per tap
   constexpr int TPC = G::SLOT_PIECES / CH >= 1 ? G::SLOT_PIECES / CH : 1;
   static_assert(TPC * CH <= G::SLOT_PIECES, "a tap must fit one ring slot");
   constexpr int NCH = (NTAPS + TPC - 1) / TPC;
   constexpr int STEPS = NTAPS * NCB;
-  constexpr int R = G::RING;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t ring = ldsAddr(wl);
-  auto slotOf = [&](int j) { return (PAR + j) % R; };
+  auto slotAddr = [&](int j) { return ring + (uint32_t)(((PAR + j) & 1) * G::WSLOT * 16); };
   auto chunkPieces = [&](int j) { return (NTAPS - j * TPC < TPC ? NTAPS - j * TPC : TPC) * CH; };
-  // the request of stream chunk j of this conv (j >= NCH: the next conv's chunk j - NCH)
+  // the request of stream chunk j of this conv (j >= NCH: the next conv's chunk 0)
   auto request = [&](int j) {
-    const uint32_t dst = ring + (uint32_t)(slotOf(j) * G::WSLOT * 16);
     if(j < NCH)
-      stageChunk<G::NW>(w + (size_t)j * TPC * CH * 64, dst, chunkPieces(j), wave, lane);
-    else if(j - NCH < nextNCH)
-      stageChunk<G::NW>(wNext + (size_t)(j - NCH) * nextPieces * 64, dst, nextPieces, wave, lane);
+      stageChunk<G::NW>(w + (size_t)j * TPC * CH * 64, slotAddr(j), chunkPieces(j), wave, lane);
+    else if(j == NCH && nextPieces > 0)
+      stageChunk<G::NW>(wNext, slotAddr(j), nextPieces, wave, lane);
   };
-  request(R - 1);
+  request(1);
   const char* actB = reinterpret_cast<const char*>(act);
   const int zb = G::ZROW * G::ROWB + 16 * (lane >> 4);
   const h16x8* wlane = wl + (cg * G::NCT) * 64 + lane;
@@ -425,29 +411,26 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
       at[t] = ((vm[t] >> tb) & 1u) ? rb[t] + off : zb;
   };
   h16x8 af[2][G::MAXT], bf[2][G::NCT];
-  // second planes: fp16 lo fragments, double buffered (mode 1); e4m3 (mode 2), the two
-  // steps of an MFMA pair in the low / high half of one 8-register operand, so the
-  // scaled MFMA reads its operands in place (the halves are the double buffer):
-  // aq [x | lo(x) 2^11] per step; bq [lo(w) 2^11 (loaded) | e4m3(hi(w)) (converted)] per step
+  // second planes: fp16 lo fragments, double buffered (mode 1); e4m3 pairs (mode 2), the
+  // two steps of an MFMA pair in the low / high half of one 8-register operand, so the
+  // scaled MFMA reads its operands in place (the halves are the double buffer)
   h16x8 afl[G::MODE == NN_MODE_SPLIT3 ? 2 : 1][G::MAXT], bfl[G::MODE == NN_MODE_SPLIT3 ? 2 : 1][G::NCT];
   i32x8 aq[G::MAXT], bq[G::NCT];
   auto loadStep = [&](int st, int buf) {
     const int tap = st / NCB, cb = st - tap * NCB;
     const int chunk = tap / TPC, tc = tap - chunk * TPC;
-    const h16x8* wb = wlane + slotOf(chunk) * G::WSLOT + tc * CH * 64 + cb * G::NCT_ALL * 64;
+    const h16x8* wb = wlane + ((PAR + chunk) & 1) * G::WSLOT + tc * CH * 64 + cb * G::NCT_ALL * 64;
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++) {
       bf[buf][ct] = wb[ct * 64];
       if constexpr(G::MODE == NN_MODE_SPLIT3) {
         bfl[buf][ct] = wb[CHP * 64 + ct * 64];
       } else {
-        // 8 B of this lane's fragment in the tap's e4m3 block (512 B per fragment)
-        const int frag = cb * G::NCT_ALL + cg * G::NCT + ct;
-        const int2 v = *reinterpret_cast<const int2*>(reinterpret_cast<const char*>(wl) +
-                                                      (size_t)(slotOf(chunk) * G::WSLOT + tc * CH * 64) * 16 +
-                                                      CHP * 1024 + frag * 512 + lane * 8);
-        bq[ct][4 * buf] = v.x;
-        bq[ct][4 * buf + 1] = v.y;
+        const i32x4 v = __builtin_bit_cast(i32x4, wb[CHP * 64 + ct * 64]);
+        if(buf)
+          bq[ct].hi = v;
+        else
+          bq[ct].lo = v;
       }
     }
 #pragma unroll
@@ -463,17 +446,6 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
           aq[t].lo = __builtin_bit_cast(i32x4, v);
       }
     }
-  };
-  // e4m3 of the 8 fp16 weights of a hi fragment into bq[ct] elements 4 buf + 2, + 3
-  auto w8 = [&](int ct, int buf) {
-    const h16x8 h = bf[buf][ct];
-    s16x2 a = {0, 0}, b = {0, 0};
-    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(a, h2x{h[0], h[1]}, 1.0f, false);
-    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(a, h2x{h[2], h[3]}, 1.0f, true);
-    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(b, h2x{h[4], h[5]}, 1.0f, false);
-    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(b, h2x{h[6], h[7]}, 1.0f, true);
-    bq[ct][4 * buf + 2] = __builtin_bit_cast(int, a);
-    bq[ct][4 * buf + 3] = __builtin_bit_cast(int, b);
   };
   auto f8pair = [&]() {
     // one scaled e4m3 MFMA over the pair of steps held in aq / bq
@@ -492,16 +464,12 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
     const int chunk = tap / TPC;
     const bool chunkEnd = cb == NCB - 1 && (tap == NTAPS - 1 || (tap + 1) % TPC == 0);
     if(chunkEnd && chunk + 1 < NCH) {
-      // retire this wave's pieces of chunk+1, publish them, free chunk's slot, request chunk+R
+      // retire this wave's pieces of chunk+1, publish them, free chunk's slot, request chunk+2
       waitVm<0>();
       barrierKeepDma();
-      request(chunk + R);
+      request(chunk + 2);
     }
     if constexpr(G::MODE == NN_MODE_F8C) {
-      // this step's e4m3 weights (its hi fragments are waited for by its MFMAs anyway)
-#pragma unroll
-      for(int ct = 0; ct < G::NCT; ct++)
-        w8(ct, st & 1);
       if(st & 1)
         f8pair();  // steps st - 1 (low halves) and st (high halves)
     }
@@ -902,11 +870,8 @@ __global__ void __launch_bounds__(512, 2)
     constexpr int CH0 = G::NCT_ALL * G::PLANES;  // 1-KiB pieces per stem tap (one 32-channel block)
     const uint32_t ring = ldsAddr(wl);
     if constexpr(G::BL) {
-      // the stem's chunks 0 .. RING-2 (3 taps each) into slots 0 .. RING-2
-      constexpr int SC = 3 * G::tapPieces(1);
-#pragma unroll
-      for(int j = 0; j + 1 < G::RING; j++)
-        stageChunk<G::NW>(WB + L->wInit + (size_t)j * SC * 64, ring + j * G::WSLOT * 16, SC, wave, lane);
+      // the stem's chunk 0 (taps 0-2) into slot 0
+      stageChunk<G::NW>(WB + L->wInit, ring, 3 * CH0, wave, lane);
     } else {
 #pragma unroll
       for(int tap = 0; tap < 2; tap++)
@@ -960,14 +925,14 @@ __global__ void __launch_bounds__(512, 2)
     aRowsBL<G>(rb, vm, tstart, lane);
   else
     aBases<G>(ab, rowPa, tstart, lane);
-  // pieces of a weight chunk of a conv of C -> C (or the head's): one tap
-  constexpr int CHUNK96 = G::tapPieces(G::C / 32);
+  // pieces of the first weight chunk of a conv of C -> C (or the head's): one tap
+  constexpr int CHUNK96 = G::SLOT_PIECES;
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
   if constexpr(G::BL)
     convTilesB<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, rb, vm, cg, lane, tid,
-                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96, L->nblocks > 0 ? 9 : 1);
+                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96);
   else
     convTiles<G, 9, 1, 0, 0, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                                     L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
@@ -1009,11 +974,9 @@ __global__ void __launch_bounds__(512, 2)
       pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
     if constexpr(G::BL)
-      // chunk index mod RING: stem 3 chunks, each block's convs 9 + 9 (a 64-channel tap is one
-      // chunk too), so conv1 starts at 3 (1 mod 2, 0 mod 3) and conv2 at 12 (0)
-      convTilesB<G, 9, G::C / 32, G::RING == 2 ? 1 : 0>(act, WB + L->wConv1[blk], wl, acc, rb, vm, cg, lane, tid,
-                                                       WB + L->wConv2[blk],
-                                                       G::tapPieces(L->kinds[blk] == 0 ? 3 : 2), 9);
+      // chunk parity: stem 3 chunks, each block's convs 9 + 9 (a 64-channel tap is one chunk too)
+      convTilesB<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, rb, vm, cg, lane, tid, WB + L->wConv2[blk],
+                                     (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES);
     else
       convTiles<G, 9, G::C / 32, 1, 0, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid,
                                               WB + L->wConv2[blk],
@@ -1041,8 +1004,7 @@ __global__ void __launch_bounds__(512, 2)
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
-        convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW, CHUNK96,
-                                       nextTaps);
+        convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW, CHUNK96);
       else
         convTiles<G, 9, G::C / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                 3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1138,7 +1100,7 @@ __global__ void __launch_bounds__(512, 2)
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
         convTilesB<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW,
-                                              CHUNK96, nextTaps);
+                                              CHUNK96);
       else
         convTiles<G, 9, (G::C - 32) / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                        3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1156,8 +1118,7 @@ __global__ void __launch_bounds__(512, 2)
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
   if constexpr(G::BL)
-    convTilesB<G, 1, G::C / 32, G::RING == 2 ? 1 : 0>(act, WB + L->wHead, wl, acc, rb, vm, cg, lane, tid, nullptr, 0,
-                                                      0);
+    convTilesB<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, rb, vm, cg, lane, tid, nullptr, 0);
   else
     convTiles<G, 1, G::C / 32, 1, 0, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0,
                                             9 + 18 * L->nblocks);
@@ -1347,8 +1308,7 @@ static uint8_t f2e4m3(float f) {
 }
 
 // mode 1: after each tap's hi fragments the same fragments of lo = fp16(w - hi);
-// mode 2: after them the fragments' e4m3(lo(w) 2^11), 8 bytes per lane (512 B per
-// fragment; e4m3(w) is converted from the hi fragment on the device)
+// mode 2: after them the e4m3 pairs [lo(w) 2^11 of the fragment's 8 k | w of the same 8 k]
 // (convTiles' / convTilesB's SPLIT ring slot layout).
 static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout,
                      const std::function<float(int, int, int)>& W, int mode = NN_MODE_F16) {
@@ -1367,10 +1327,12 @@ static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout
                 dst.push_back(part == 0 ? hi : f2h(w[j] - h2f(hi)));
               }
             } else {
-              uint8_t b[8];
-              for(int j = 0; j < 8; j++)
+              uint8_t b[16];
+              for(int j = 0; j < 8; j++) {
                 b[j] = f2e4m3((w[j] - h2f(f2h(w[j]))) * F8C_SCALE);
-              for(int j = 0; j < 4; j++)
+                b[8 + j] = f2e4m3(w[j]);
+              }
+              for(int j = 0; j < 8; j++)
                 dst.push_back((uint16_t)(b[2 * j] | (b[2 * j + 1] << 8)));
             }
           }
@@ -1438,8 +1400,8 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   }
   mode_ = path;
   if(path == NN_CORRECTED) {
-    // e4m3 holds |w| <= 448 (the device converts fp16 weights without saturation): a net
-    // with a larger convolution weight runs on the split ("accurate") instance instead
+    // e4m3 holds |w| <= 448 (the packed e4m3(w) saturates there): a net with a larger
+    // convolution weight runs on the split ("accurate") instance instead
     float mx = 0.0f;
     auto scan = [&](const std::vector<float>& v) {
       for(float x : v)

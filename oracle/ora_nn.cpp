@@ -17,7 +17,7 @@
 // mode 1 rounds every convolution weight and convolution input to fp16 (RNE),
 // exactly where the HIP kernels do; residual trunks stay f32 as in the kernels.
 // mode 2 restates the "corrected" precision (csrc/nn.hip NN_MODE_F8C): each product is
-// fp16(w) fp16(x) + e4m3(lo(w) 2^11) e4m3(x) / 2^11 + e4m3(fp16(w)) e4m3(lo(x) 2^11) / 2^11, with
+// fp16(w) fp16(x) + e4m3(lo(w) 2^11) e4m3(x) / 2^11 + e4m3(w) e4m3(lo(x) 2^11) / 2^11, with
 // lo(v) = v - fp16(v) and e4m3 = OCP e4m3fn, round to nearest even, saturating at 448.
 #include <cmath>
 #include <cstdio>
@@ -163,7 +163,7 @@ void PackedConv::pack() {
           B16[k * cout + co] = f16r(v);
           BC[k * cout + co] = f16r(v);
           BC[(K + k) * cout + co] = e4m3r((v - f16r(v)) * F8C_SCALE) / F8C_SCALE;
-          BC[(2 * K + k) * cout + co] = e4m3r(f16r(v));  // the device converts the fp16 weight
+          BC[(2 * K + k) * cout + co] = e4m3r(v);
         }
   packB(B.data(), K, cout, p32);
   packB(B16.data(), K, cout, p16);
