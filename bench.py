@@ -97,6 +97,11 @@ def parse():
     ap.add_argument("--play", choices=["benchmark", "production"], default="benchmark",
                     help="benchmark: SURVEY 8d (one row per move at full visits, the metric's mode); "
                          "production: selfplay1.cfg play settings")
+    ap.add_argument("--opening-prop", type=float, default=0.0,
+                    help="short-game variant (benchmark play): each game opens with floor(-ln(u) A P) moves "
+                         "sampled from the raw policy without search or rows (initGamesWithPolicy, "
+                         "playutils.cpp:147-176), the rest is searched at full visits, one row per searched move: "
+                         "rows/s of a long-game config (C5) measured on disk within a short window")
     ap.add_argument("--stagger", type=int, default=-1,
                     help="per-slot start delay range in rounds (-1 = min(one game, 90%% of the warm-up))")
     ap.add_argument("--groups", type=int, default=0,
@@ -410,7 +415,11 @@ def main():
     rps = args.rounds_per_step or cfg["rounds"]
     window = args.window or ("short" if args.config == "C5" else "steady")
     # rounds per game: (visits + root evaluations) per move x ~A/2 moves
-    game_rounds = (visits + 4) * X * Y // 2
+    # (with --opening-prop P the first min(O, L) of a game's L ~ A/2 moves are unsearched
+    # openings, O exponential with mean A P: E = A P (1 - exp(-L / (A P))))
+    L = X * Y / 2.0
+    mo = args.opening_prop * X * Y
+    game_rounds = int((visits + 4) * max(4.0, L - (mo * (1.0 - __import__("math").exp(-L / mo)) if mo > 0 else 0.0)))
     if window == "steady" and not args.rounds_per_step:
         rps = max(rps, -(-3 * game_rounds // (2 * max(1, args.warmup))))
     import numpy as np  # noqa: F401
@@ -440,6 +449,10 @@ def main():
     else:
         stagger = game_rounds if window == "steady" else min(game_rounds, int(0.9 * warm_rounds))
     play = PRODUCTION if args.play == "production" else {}
+    if args.opening_prop > 0:
+        if args.play != "benchmark":
+            raise SystemExit("--opening-prop is a benchmark-play variant")
+        play = dict(init_games_with_policy=1, policy_init_area_prop=args.opening_prop)
     # benchmark mode clears the tree before every move: a search holds at
     # most visits + 1 nodes; production's cheap searches reuse the tree
     node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
@@ -627,7 +640,9 @@ def main():
                        "rounds_per_step": rps, "window": window, "game_rounds_estimate": game_rounds,
                        "warmup_rounds": warm_rounds, "commit_interval": args.commit_interval,
                        "nn_cache_log2": args.nn_cache_log2, "nn_batch_cap": args.nn_batch_cap or "engine default",
-                       "play_settings": args.play, "start_stagger_rounds": stagger, "groups": args.groups, "node_cap": node_cap or "default",
+                       "play_settings": args.play + (" + policy openings (area prop %g)" % args.opening_prop
+                                                     if args.opening_prop > 0 else ""),
+                       "start_stagger_rounds": stagger, "groups": args.groups, "node_cap": node_cap or "default",
                        "parallelism": "game-sharded x%d (RCCL row gather)" % world if world > 1 else "1 GPU"},
             "rccl_world_size": world,
             "rows_per_rank": rank_rows,
