@@ -377,6 +377,26 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
 }
 
+// Cycle accounting of kConvLB (profiling build, `make prof`; tools/convl_phase.py): wave 0
+// of every workgroup adds its cycles per phase into g_convlProf (one atomic per slot and
+// workgroup): 0 workgroups, 1 total, 2 prologue (entry to the first K-step), 3 weight
+// waits (vmcnt + barrier per tap group), 4 stage stores (incl. the wait for the slice's
+// loads), 5 epilogue.
+#ifdef KC_SEARCH_PROFILE
+__device__ unsigned long long g_convlProf[8];
+#define CLP_NOW() clock64()
+#define CLP_ADD(i, v)                                                  \
+  do {                                                                 \
+    if(tid == 0)                                                       \
+      atomicAdd(&g_convlProf[(i)], (unsigned long long)(v));           \
+  } while(0)
+#else
+#define CLP_NOW() 0ll
+#define CLP_ADD(i, v) \
+  do {                \
+  } while(0)
+#endif
+
 // 3x3 fast convolutions with the weights in LDS: the workgroup's B fragments of three
 // taps (3 x NCT pieces of 1 KiB) stream by LDS-DMA into one of two ring slots, so
 // each fragment crosses the L1 once per workgroup instead of once per wave that uses
@@ -401,6 +421,8 @@ __global__ void __launch_bounds__(L_NT, 2) kConvLB(LConvArgs a) {
     return;
   const int nb = min(G::BPW, count - base);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const long long tEntry = CLP_NOW();
+  long long tWait = 0, tStore = 0;
   const int wm = wave / WN, wn = wave % WN;
   const int ctBase = blockIdx.y * NCT + wn * TN;
   char* stage = smem;                          // [2][STAGE]
@@ -466,6 +488,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConvLB(LConvArgs a) {
       af[buf][t] = *reinterpret_cast<const lh16x8*>(st + ab[t] + aoff);
   };
   loadFr(0, 0, 0);
+  const long long tLoop = CLP_NOW();
   // one slice; par = cb & 1 (compile-time: slices run in pairs)
   auto slice = [&](int cb, int par) {
     const bool more = cb + 1 < NCB;
@@ -477,11 +500,16 @@ __global__ void __launch_bounds__(L_NT, 2) kConvLB(LConvArgs a) {
       if(tap % 3 == 0 && q + 1 < Q)
         request(q + 1);
       const int buf = (par + tap) & 1;  // K-step s = 9 cb + tap alternates buffers
-      if(tap == 8 && more)
+      if(tap == 8 && more) {
+        const long long t0 = CLP_NOW();
         stageStore<G, false>(a, sr, stage + (par ^ 1) * G::stage(false), nullptr, cb + 1, base, nb, sS, sB, sG, tid);
+        tStore += CLP_NOW() - t0;
+      }
       if(tap % 3 == 2 && q + 1 < Q) {
+        const long long t0 = CLP_NOW();
         waitVm<0>();
         barrierKeepDma();
+        tWait += CLP_NOW() - t0;
       }
       if(tap < 8)
         loadFr(par, tap + 1, buf ^ 1);
@@ -502,7 +530,19 @@ __global__ void __launch_bounds__(L_NT, 2) kConvLB(LConvArgs a) {
   }
   if(cb < NCB)
     slice(cb, 0);
+  const long long tEpi = CLP_NOW();
   convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
+  CLP_ADD(0, 1);
+  CLP_ADD(1, CLP_NOW() - tEntry);
+  CLP_ADD(2, tLoop - tEntry);
+  CLP_ADD(3, tWait);
+  CLP_ADD(4, tStore);
+  CLP_ADD(5, CLP_NOW() - tEpi);
+  (void)tEntry;
+  (void)tLoop;
+  (void)tEpi;
+  (void)tWait;
+  (void)tStore;
 }
 
 // 1x1 convolutions, split precision (fast: kConv1LP below): no halo, so a stage holds 128
@@ -1324,5 +1364,17 @@ void NNLayered::forward(int n, const uint64_t* in, float* out, hipStream_t st, c
   hipLaunchKernelGGL(kHeadsL, dim3(n), dim3(256), 0, st, bufT_, tW_, X_ * Y_, h, out, rowIdx, n, countDev);
   KC_HIP(hipGetLastError());
 }
+
+#ifdef KC_SEARCH_PROFILE
+// kConvLB cycle accounting (profiling build): the 8 slots of g_convlProf, then reset.
+extern "C" void coffee_debug_convl_profile(unsigned long long* out, int reset) {
+  KC_HIP(hipDeviceSynchronize());
+  KC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_convlProf), 8 * sizeof(unsigned long long)));
+  if(reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    KC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_convlProf), z, sizeof(z)));
+  }
+}
+#endif
 
 }  // namespace kc

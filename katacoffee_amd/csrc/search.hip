@@ -3349,57 +3349,55 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
 // are deferred (nnDefer): their games keep their leaf and skip the next select.  The
 // oracle applies the same rule (ora_search.cpp selfplayRound).
 // accumulate != 0: the count is also added to *d.nnTimedEvals (sampled kernel timing).
-// The thread's need flags and cache bids are loaded once, before the scan (all in
-// flight together when it has at most CP_VEC games), so the kernel waits for one
-// round of loads instead of one per game.
-// (up to 32 games per thread: 256 threads cover a group of 8192 games -- a 4-wave
-// workgroup finds room beside the other group's network kernels, where a 1024-thread
-// one waited for a whole CU to drain: 34 us per launch at C3)
-constexpr int CP_VEC = 32;
+// Layout: the games are cut into 64-game chunks; wave w owns the contiguous chunks
+// [w * cpw, (w + 1) * cpw) and lane l game l of each, so every load and every nnDefer
+// store is one coalesced 256-byte access per chunk.  The need flags and cache bids of
+// all of a lane's chunks are loaded before the first use (up to CP_CH chunks per wave),
+// so the kernel waits for one round of loads.  Positions: a lane's packed count (high
+// half: needing games at or past the round-robin pointer, low half: the others, G <
+// 65536) is summed over the wave and scanned over the waves; inside a wave the chunks
+// are walked in order with a ballot per chunk.
+// (256 threads cover a group of 8192 games: a 4-wave workgroup finds room beside the
+// other group's network kernels, where a 1024-thread one waited for a whole CU to
+// drain: 34 us per launch at C3)
+constexpr int CP_CH = 32;
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
   const SearchDev& d = *dp;
   __shared__ uint32_t wsum[16], wpre[17];
   const int nt = blockDim.x, nw = nt >> 6;  // 256 or 1024 threads (launchCompact)
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, per = (d.G + nt - 1) / nt;
-  const int lo = t * per, hi = min(d.G, lo + per);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nch = (d.G + 63) >> 6;
+  const int cpw = (nch + nw - 1) / nw;  // chunks per wave (<= 64: G < 65536, >= 16 waves past 8192 games)
+  const int g0 = w * cpw * 64 + lane;   // this lane's game in the wave's first chunk
   const int p = *d.nnRR;
-  const bool vec = per <= CP_VEC;
-  uint64_t need = 0;  // bit k: game lo + k needs the network (per <= 64)
-  uint32_t bids[CP_VEC];
+  const bool vec = cpw <= CP_CH;
+  uint64_t need = 0;  // bit k: game g0 + 64 k needs the network
+  uint32_t bids[CP_CH];
   if(vec) {
-    // loads under the block-uniform bound `per` (clamped indices), all issued before
-    // the first use
-    int nd[CP_VEC];
 #pragma unroll
-    for(int k = 0; k < CP_VEC; k++) {
-      nd[k] = 0;
+    for(int k = 0; k < CP_CH; k++) {
       bids[k] = ~0u;
-      if(k < per) {
-        const int i = lo + k < d.G ? lo + k : 0;
-        nd[k] = d.nnNeed[i];
-        bids[k] = d.nnBid[i];
+      if(k < cpw) {
+        const int i = g0 + 64 * k;
+        const int ic = i < d.G ? i : 0;
+        bids[k] = d.nnBid[ic];
+        need |= (uint64_t)(i < d.G && d.nnNeed[ic] ? 1u : 0u) << k;
       }
     }
-#pragma unroll
-    for(int k = 0; k < CP_VEC; k++)
-      need |= (uint64_t)(k < per && lo + k < d.G && nd[k] ? 1u : 0u) << k;
   } else {
-    for(int i = lo; i < hi; i++)
-      need |= (uint64_t)(d.nnNeed[i] ? 1u : 0u) << (i - lo);
+    for(int k = 0; k < cpw; k++) {
+      const int i = g0 + 64 * k;
+      need |= (uint64_t)(i < d.G && d.nnNeed[i] ? 1u : 0u) << k;
+    }
   }
-  // needing games at or past the round-robin pointer count in the high half, the
-  // others (taken after them) in the low half: one scan of packed counts (G < 65536)
-  const uint64_t atOrPast = p <= lo ? ~0ull : (p - lo >= 64 ? 0ull : ~0ull << (p - lo));
-  const uint32_t c = ((uint32_t)__popcll(need & atOrPast) << 16) + (uint32_t)__popcll(need & ~atOrPast);
-  uint32_t incl = c;
+  // bit k of atOrPast: game g0 + 64 k >= p
+  const uint64_t atOrPast = p <= g0 ? ~0ull : (p - g0 > 64 * 63 ? 0ull : ~0ull << ((p - g0 + 63) / 64));
+  uint32_t c = ((uint32_t)__popcll(need & atOrPast) << 16) + (uint32_t)__popcll(need & ~atOrPast);
 #pragma unroll
-  for(int off = 1; off < 64; off <<= 1) {
-    const uint32_t v = (uint32_t)__shfl_up((int)incl, off, 64);
-    if(lane >= off)
-      incl += v;
-  }
-  if(lane == 63)
-    wsum[w] = incl;
+  for(int off = 32; off >= 1; off >>= 1)
+    c += (uint32_t)__shfl_xor((int)c, off, 64);
+  if(lane == 0)
+    wsum[w] = c;
   __syncthreads();
   if(t < 64) {
     uint32_t x = t < nw ? wsum[t] : 0u, xi = x;
@@ -3415,38 +3413,41 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
       wpre[16] = xi;
   }
   __syncthreads();
-  const uint32_t excl = wpre[w] + incl - c, all = wpre[16];
+  const uint32_t all = wpre[16], excl = wpre[w];
   const int totalHi = (int)(all >> 16), total = totalHi + (int)(all & 0xFFFFu), cap = d.nnCap;
-  int oh = (int)(excl >> 16), ol = totalHi + (int)(excl & 0xFFFFu);
-  auto place = [&](int i, uint32_t bid) {
-    const int pos = i >= p ? oh++ : ol++;
-    const bool in = pos < cap;
-    if(in) {
-      d.nnIdx[pos] = i;
-      // the evaluation's bid for its NN-cache slot (kBackup: the highest game stores it)
-      if(bid != ~0u)
-        atomicMax(&d.cTag[bid], (uint32_t)i + 1u);
+  int oh = (int)(excl >> 16), ol = totalHi + (int)(excl & 0xFFFFu);  // wave-uniform running positions
+  const uint64_t below = (1ull << lane) - 1ull;
+  auto chunk = [&](int k, uint32_t bid) {
+    const int i = g0 + 64 * k;
+    const bool nd = (need >> k) & 1u;
+    const uint64_t b = ballot(nd), ge = ballot(nd && i >= p);
+    if(nd) {
+      const int pos = i >= p ? oh + __popcll(ge & below) : ol + __popcll(b & ~ge & below);
+      const bool in = pos < cap;
+      if(in) {
+        d.nnIdx[pos] = i;
+        // the evaluation's bid for its NN-cache slot (kBackup: the highest game stores it)
+        if(bid != ~0u)
+          atomicMax(&d.cTag[bid], (uint32_t)i + 1u);
+      }
+      d.nnDefer[i] = in ? 0 : 1;
+      if(total > cap && pos == cap - 1)
+        *d.nnRR = i + 1 < d.G ? i + 1 : 0;
+    } else if(i < d.G) {
+      d.nnDefer[i] = 0;
     }
-    d.nnDefer[i] = in ? 0 : 1;
-    if(total > cap && pos == cap - 1)
-      *d.nnRR = i + 1 < d.G ? i + 1 : 0;
+    oh += __popcll(ge);
+    ol += __popcll(b & ~ge);
   };
   if(vec) {
 #pragma unroll
-    for(int k = 0; k < CP_VEC; k++) {
-      if(k < per && lo + k < d.G) {
-        if((need >> k) & 1u)
-          place(lo + k, bids[k]);
-        else
-          d.nnDefer[lo + k] = 0;
-      }
-    }
+    for(int k = 0; k < CP_CH; k++)
+      if(k < cpw)
+        chunk(k, bids[k]);
   } else {
-    for(int i = lo; i < hi; i++) {
-      if((need >> (i - lo)) & 1u)
-        place(i, d.nnBid[i]);
-      else
-        d.nnDefer[i] = 0;
+    for(int k = 0; k < cpw; k++) {
+      const int i = g0 + 64 * k;
+      chunk(k, i < d.G ? d.nnBid[i] : ~0u);
     }
   }
   if(t == nt - 1) {
@@ -3619,11 +3620,11 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
   KC_HIP(hipGetLastError());
 }
 
-// 256 threads (one wave per SIMD) while each keeps at most CP_VEC games: a workgroup
+// 256 threads (one wave per SIMD) while each wave keeps at most CP_CH chunks of 64 games: a workgroup
 // that small fits beside a network workgroup of the other game group on its CU (1024
 // threads need 4 waves per SIMD) and does not wait for a free one.
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate) {
-  const int nt = d.G <= 256 * CP_VEC ? 256 : 1024;  // 1024 only past 8192 games per engine
+  const int nt = d.G <= 4 * 64 * CP_CH ? 256 : 1024;  // 1024 only past 8192 games per engine
   hipLaunchKernelGGL(kCompact, dim3(1), dim3(nt), 0, st, dd, accumulate ? 1 : 0);
   KC_HIP(hipGetLastError());
 }

@@ -37,9 +37,14 @@ def test_stage_rows_matches_drain():
     ev.synchronize()
     n = int(cnt[0])
     assert n == n_ref
-    got = R.unpack(buf[:n].cpu().numpy(), 5, 5)
-    for k, _ in R.FIELDS:
-        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    # rows take their buffer slots by atomic counter, so the two engines' row orders may
+    # differ: compare the sets of packed records (each row byte for byte)
+    got = buf[:n].cpu().numpy()
+    want = R.pack(ref, 5, 5).reshape(n, rb)
+    assert got.shape == want.shape
+    order = lambda a: a[np.lexsort(a.T[::-1])]
+    np.testing.assert_array_equal(order(got), order(want))
+    R.unpack(got, 5, 5)  # the staged block parses as rows.py records
     b.sync()
     st = b.stats()
     # the buffer restarted from empty: rows written count both the staged and the new ones
