@@ -4,8 +4,10 @@
 #   test[=PATTERN]   pytest -m gpu (optionally -k PATTERN)
 #   file=PATH        pytest of one test file (gpu-marked tests in it)
 #   bench[=ARGS]     python bench.py ARGS (comma-separated: bench=--config,C3,--steps,10)
+#   benchlong[=ARGS] the same with a 1050 s limit (long-game windows: C5 rows on disk)
 #   smoke            __graft_entry__.smoke()
 #   prof             tools/profile_r03.sh (rocprofv3 trace + PMC passes)
+#   prof4=SECTIONS   tools/profile_r04.sh (comma-separated sections: prof4=c2,corrected,c4,c4pmc)
 #   run=CMD          any other command (comma-separated words), e.g. run=tools/_build/nn_phase,960
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -26,12 +28,16 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest "$arg" -m gpu -x -v --timeout 300 --timeout-method thread > $log 2>&1 ;;
     bench)
       timeout -k 10 600 python -u bench.py ${arg//,/ } > $log 2>&1 ;;
+    benchlong)
+      timeout -k 10 1050 python -u bench.py ${arg//,/ } > $log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
     run)
       timeout -k 10 300 ${arg//,/ } > $log 2>&1 ;;
     prof)
       timeout -k 10 1100 bash tools/profile_r03.sh > $log 2>&1 ;;
+    prof4)
+      timeout -k 10 1100 bash tools/profile_r04.sh ${arg//,/ } > $log 2>&1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -8,5 +8,5 @@ ctr=$2
 shift 2
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 280 rocprofv3 --pmc $ctr -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline "$@" > gpurun_out/prof_$name.log 2>&1 || { echo "profiled run failed rc=$?"; tail -5 gpurun_out/prof_$name.log; exit 1; }
+timeout -k 10 280 rocprofv3 --pmc $ctr -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line "$@" > gpurun_out/prof_$name.log 2>&1 || { echo "profiled run failed rc=$?"; tail -5 gpurun_out/prof_$name.log; exit 1; }
 python tools/reduce_profile.py pmc gpurun_out/prof_$name $name

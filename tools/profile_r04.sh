@@ -1,0 +1,42 @@
+# round-4 profiles (GPU box): rocprofv3 kernel traces of the bench lines and FETCH/WRITE
+# PMC passes (one counter per pass, no trace domains beside --pmc), reduced in place by
+# tools/reduce_profile.py.  Sections: bash tools/profile_r04.sh c2 corrected accurate c3 c4 c4pmc c2pmc
+# Each GPU step has its own time limit; the first failing step ends the script.
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+run() { "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
+trace() {  # name, bench args...
+  local name=$1
+  shift
+  run timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line "$@" > gpurun_out/prof_$name.log 2>&1
+  run python tools/reduce_profile.py trace gpurun_out/prof_$name $name
+  grep '^{' gpurun_out/prof_$name.log > gpurun_out/prof_$name.line.json || true
+}
+pmc() {  # name, counter, bench args...
+  local name=$1 ctr=$2
+  shift 2
+  run timeout -k 10 420 rocprofv3 --pmc $ctr -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line "$@" > gpurun_out/prof_$name.log 2>&1
+  run python tools/reduce_profile.py pmc gpurun_out/prof_$name $name
+}
+SHORT="--window short --warmup 8 --steps 6 --rounds-per-step 200"
+for s in "$@"; do
+  case $s in
+    c2) trace r04_c2 --steps 20 --warmup 5 ;;
+    corrected) trace r04_c2corr --steps 20 --warmup 5 --precision corrected ;;
+    accurate) trace r04_c2acc --steps 20 --warmup 5 --precision accurate ;;
+    c3) trace r04_c3 --config C3 --steps 10 --warmup 5 ;;
+    c4) trace r04_c4 --config C4 $SHORT ;;
+    c4pmc)
+      pmc r04_c4_fetch FETCH_SIZE --config C4 $SHORT
+      pmc r04_c4_write WRITE_SIZE --config C4 $SHORT ;;
+    c2pmc)
+      pmc r04_c2_fetch FETCH_SIZE $SHORT
+      pmc r04_c2_write WRITE_SIZE $SHORT ;;
+    corrpmc)
+      pmc r04_c2corr_fetch FETCH_SIZE $SHORT --precision corrected
+      pmc r04_c2corr_write WRITE_SIZE $SHORT --precision corrected ;;
+    *) echo "unknown section $s"; exit 2 ;;
+  esac
+done
+find gpurun_out/prof_r04_* -type f | head -60
