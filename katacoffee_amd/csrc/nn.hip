@@ -54,6 +54,27 @@ enum { NN_MODE_F16 = 0, NN_MODE_SPLIT3 = 1, NN_MODE_F8C = 2 };
 // value 2^-11 below the product, so a product is good to ~2^-14 (fp16 operands: 2^-10):
 // tools/precision_study.py measures 2.1e-4 on the trained-net test (fp16: 7.1e-3).
 constexpr int F8C_SHIFT = 11;
+// The corrected instance is register-capped so that a 128-VGPR search wave of the other
+// game group fits on each SIMD beside its two network waves (2 x 192 + 128 = 512):
+// it is compiled separately (nn_corr.hip) as kNNForwardCap with amdgpu_num_vgpr
+// KC_F8C_VGPR, which gfx950 counts in register pairs (96 = 192 VGPRs; 0: uncapped, the
+// plain kNNForward instance).  KC_F8C_PARK 1: the f32 trunk is parked in the
+// workgroup-private global scratch during a block's first conv (24 registers);
+// KC_F8C_LATE 1: a K-step's fragments are read after the previous step's MFMAs issue
+// (one fragment buffer).  (A/B builds: tools/Makefile alt, ALT_FLAGS=-DKC_F8C_VGPR=0 ...)
+// Measured (C2 corrected bench, one box, 20 steps): uncapped 19.0 k rows/s (network 144 us,
+// other group's select 105 us: no room beside the network's 233-256-VGPR waves); capped +
+// late 19.5 k (network 163 us, select 71 us, backup 50 -> 59 us: the search waves now share
+// the network's CUs); capped + late + parked trunk 19.3 k; late + parked, uncapped 18.1 k.
+#ifndef KC_F8C_VGPR
+#define KC_F8C_VGPR 96
+#endif
+#ifndef KC_F8C_PARK
+#define KC_F8C_PARK 0
+#endif
+#ifndef KC_F8C_LATE
+#define KC_F8C_LATE 1
+#endif
 constexpr float F8C_SCALE = 2048.0f;  // 2^F8C_SHIFT
 
 template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int MODE_ = 0, bool BL_ = false>
@@ -473,7 +494,8 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
       if(st & 1)
         f8pair();  // steps st - 1 (low halves) and st (high halves)
     }
-    if(st + 1 < STEPS) {
+    constexpr bool LATE = G::MODE == NN_MODE_F8C && KC_F8C_LATE;
+    if(!LATE && st + 1 < STEPS) {
       if(cb == NCB - 1)
         tapAddr(tap + 1);
       loadStep(st + 1, (st + 1) & 1);
@@ -498,6 +520,13 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++)
           acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[b][ct], afl[b][t], acc[t][ct], 0, 0, 0);
+    }
+    if(LATE && st + 1 < STEPS) {
+      // the next step's fragments, read once this step's MFMAs are issued
+      __builtin_amdgcn_sched_barrier(0);
+      if(cb == NCB - 1)
+        tapAddr(tap + 1);
+      loadStep(st + 1, (st + 1) & 1);
     }
     if constexpr(G::MODE == NN_MODE_F8C) {
       if(st == STEPS - 1 && !(st & 1)) {
@@ -537,7 +566,7 @@ KC_D f32x4* trunkBase(float* trunk, int wave, int lane) {
 // parked trunk fits in 24 more registers (< 256, no spill): kept in `reg`, no scratch.
 template <class G>
 constexpr bool regTrunk() {
-  return G::MAXT * G::NCT <= 6;
+  return G::MAXT * G::NCT <= 6 && !(G::MODE == NN_MODE_F8C && KC_F8C_PARK);
 }
 template <class G>
 KC_D void storeTrunk(float* trunk, f32x4 (&reg)[G::MAXT][G::NCT], const f32x4 (&a)[G::MAXT][G::NCT], int wave,
@@ -834,9 +863,13 @@ KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ W
   return src >= 0 ? WF[src] : 0.0f;
 }
 
+#ifndef KC_NN_KERNEL
+#define KC_NN_KERNEL kNNForward
+#define KC_NN_KERNEL_ATTR
+#endif
 template <int X, int Y, int C, int NB, int MODE, bool BL>
-__global__ void __launch_bounds__(512, 2)
-    kNNForward(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
+__global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
+    KC_NN_KERNEL(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
                const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
                const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
                float* __restrict__ out, float* __restrict__ trunk) {
@@ -1242,6 +1275,26 @@ __global__ void __launch_bounds__(512, 2)
   }
 }
 
+#ifndef KC_NN_KERNEL_ONLY
+#if KC_F8C_VGPR
+// the register-capped corrected instance (nn_corr.hip)
+template <int X, int Y, int C, int NB, int MODE, bool BL>
+__global__ void kNNForwardCap(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB,
+                              const float* __restrict__ WF, const uint16_t* __restrict__ tabs, int n,
+                              const int* __restrict__ countDev, const int* __restrict__ rowIdx, int inWords,
+                              float winLen, const uint64_t* __restrict__ in, float* __restrict__ out,
+                              float* __restrict__ trunk);
+#endif
+template <class G>
+constexpr auto nnKernel() {
+#if KC_F8C_VGPR
+  if constexpr(G::MODE == NN_MODE_F8C)
+    return kNNForwardCap<G::X, G::Y, G::C, G::NB, G::MODE, G::BL>;
+  else
+#endif
+    return kNNForward<G::X, G::Y, G::C, G::NB, G::MODE, G::BL>;
+}
+
 // ---------------------------------------------------------------------------
 // Host: pack weights into B-fragment order and launch.
 
@@ -1529,8 +1582,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
                              hipFuncAttributeMaxDynamicSharedMemorySize, GS::LDS));
   KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, GB::LDS));
-  KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, GC::LDS));
+  KC_HIP(hipFuncSetAttribute((const void*)nnKernel<GC>(), hipFuncAttributeMaxDynamicSharedMemorySize, GC::LDS));
 #ifdef KC_AB_HOOKS
   // A/B builds only (tools/Makefile alt, -DKC_AB_HOOKS): KATACOFFEE_NN_SMALL=8 runs small
   // batches on the 8-board instance too; the product library never reads the variable
@@ -1600,7 +1652,7 @@ void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* i
     KC_HIP(hipMalloc(&trunk_, bytes));
     trunkBytes_ = bytes;
   }
-  auto kern = kNNForward<G::X, G::Y, G::C, G::NB, G::MODE, G::BL>;
+  auto kern = nnKernel<G>();
   if(e0)
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, e0, e1, 0, layoutDev_, (const h16x8*)wHalf_,
                           wF32_, tab, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
@@ -1639,5 +1691,6 @@ void launchFakeNet(const DTables* T, int n, const uint64_t* in, float* out, hipS
   hipLaunchKernelGGL(kFakeNet, dim3(n), dim3(64), 0, st, T, n, countDev, rowIdx, in, out);
   KC_HIP(hipGetLastError());
 }
+#endif  // KC_NN_KERNEL_ONLY
 
 }  // namespace kc

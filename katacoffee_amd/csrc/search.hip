@@ -967,18 +967,20 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
     if(slot == n.numChildren) {
       const unsigned long long tExp = SPROF_NOW();
       (void)tExp;
-      // the node's following expansion candidate (non-root): one scan of its policy
-      float nxtPrior = -1.0f;
-      int nxtPos = 0xFFFF;
-      if(!isRoot) {
+      // the node's policy (non-root: the scan for its following expansion candidate) or
+      // the root move's raw prior, requested first: the loads fly while the move is
+      // played and the SVB / transposition probes run, and are consumed afterwards
+      float pvn[NI];
+      float rootPrior = 0.0f;
+      {
         const float* pp = v.pol(ni);
-        float pvn[NI];
 #pragma unroll
         for(int j = 0; j < NI; j++) {
           const int p = v.lane + 64 * j;
-          pvn[j] = p < v.d.P ? pp[p] : -1.0f;
+          pvn[j] = !isRoot && p < v.d.P ? pp[p] : -1.0f;
         }
-        nextExpansion<NI>(v, pvn, n.nextPrior, n.nextPos, nxtPrior, nxtPos);
+        if(isRoot)
+          rootPrior = pp[newPos];
       }
       // child slot `slot` past the inline ones lives in the node's edge-pool block,
       // allocated (16 -> 64 slots) or grown (-> P) here; pool exhaustion ends the
@@ -1004,7 +1006,7 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
         }
         ebase = nb;
       }
-      const float prior = isRoot ? v.pol(ni)[newPos] : n.nextPrior;
+      const float prior = isRoot ? rootPrior : n.nextPrior;
       const int cell = newPos % T.A, dir = newPos / T.A;
       // SVB key of the expansion (needs the board before the move); computed
       // up front so no second board copy stays live across playMoveWave.
@@ -1020,6 +1022,10 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
       int ttSlot = -1;
       int child = sp.useGraph ? ttFind(v, k0, k1, ttSlot) : -1;
       const bool fresh = child < 0;
+      float nxtPrior = -1.0f;
+      int nxtPos = 0xFFFF;
+      if(!isRoot)
+        nextExpansion<NI>(v, pvn, n.nextPrior, n.nextPos, nxtPrior, nxtPos);
       if(fresh) {
         child = allocNode(v, s, b.pla, k0, k1, b.finished != 0, freeIdx);
         if(child < 0) {
