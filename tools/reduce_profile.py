@@ -41,6 +41,21 @@ def main():
         for k, v in gaps.items():
             v.sort()
             out["gap " + k] = {"calls": len(v), "avg_ns": sum(v) / len(v), "p50_ns": v[len(v) // 2]}
+        # the longest dispatches (> 1 ms) with what else ran while they were in flight
+        t0 = seq[0][0] if seq else 0
+        starts = [a for a, _, _ in seq]
+        longest = sorted(seq, key=lambda x: x[0] - x[1])[:8]
+        outl = []
+        for a, b, k in longest:
+            if b - a < 1000000:
+                break
+            import bisect
+            lo = bisect.bisect_left(starts, a - 50000000)
+            hi = bisect.bisect_right(starts, b)
+            over = collections.Counter(k2 for a2, b2, k2 in seq[lo:hi] if b2 > a and a2 < b and (a2, b2) != (a, b))
+            outl.append({"kernel": k, "start_ms": (a - t0) / 1e6, "dur_ms": (b - a) / 1e6,
+                         "overlapping": dict(over.most_common(8))})
+        out["outliers_over_1ms"] = outl
         json.dump(out, open(os.path.join(d, prefix + "_durations.json"), "w"), indent=1)
         os.remove(path)
     else:
