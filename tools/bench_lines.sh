@@ -1,5 +1,6 @@
 # Bench lines of every BASELINE config on one GPU box (gpu.sh run= step or directly):
-# C2 fast (the driver's default command, CPU baseline included), C2 accurate, C3, C4, C5.
+# C2 fast (the driver's default command: CPU baseline and the corrected-precision
+# "compliant" window included), C2 accurate, C3, C4, C5.
 # Each run is time-limited; the JSON lines are collected into gpurun_out/lines.json.
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -14,9 +15,9 @@ run() {
 }
 run c2 --steps 20 --warmup 5
 run c2acc --steps 20 --warmup 5 --precision accurate --no-cpu-baseline
-run c3 --config C3 --no-cpu-baseline
-run c4 --config C4 --no-cpu-baseline
-run c5 --config C5 --no-cpu-baseline
+run c3 --config C3 --steps 20 --warmup 5 --no-cpu-baseline
+run c4 --config C4 --steps 6 --warmup 5 --no-cpu-baseline
+run c5 --config C5 --steps 4 --warmup 2 --no-cpu-baseline
 python - <<'EOF'
 import json
 out = {}

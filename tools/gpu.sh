@@ -5,6 +5,7 @@
 #   file=PATH        pytest of one test file (gpu-marked tests in it)
 #   bench[=ARGS]     python bench.py ARGS (comma-separated: bench=--config,C3,--steps,10)
 #   benchlong[=ARGS] the same with a 1050 s limit (long-game windows: C5 rows on disk)
+#   lines            tools/bench_lines.sh (every config's bench line, gpurun_out/lines.json)
 #   smoke            __graft_entry__.smoke()
 #   prof             tools/profile_r03.sh (rocprofv3 trace + PMC passes)
 #   prof4=SECTIONS   tools/profile_r04.sh (comma-separated sections: prof4=c2,corrected,c4,c4pmc)
@@ -30,6 +31,8 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py ${arg//,/ } > $log 2>&1 ;;
     benchlong)
       timeout -k 10 1050 python -u bench.py ${arg//,/ } > $log 2>&1 ;;
+    lines)
+      timeout -k 10 1100 bash tools/bench_lines.sh > $log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
     run)

@@ -19,6 +19,13 @@ pmc() {  # name, counter, bench args...
   run timeout -k 10 420 rocprofv3 --pmc $ctr -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line "$@" > gpurun_out/prof_$name.log 2>&1
   run python tools/reduce_profile.py pmc gpurun_out/prof_$name $name
 }
+nnpmc() {  # name, counter, nn_bench args... (the network alone; the C4 bench under --pmc
+  # crashed inside the profiler's dispatch path, a host SIGSEGV in the launch call)
+  local name=$1 ctr=$2
+  shift 2
+  run timeout -k 10 300 rocprofv3 --pmc $ctr -d gpurun_out/prof_$name -o $name --output-format csv -- python tools/nn_bench.py "$@" > gpurun_out/prof_$name.log 2>&1
+  run python tools/reduce_profile.py pmc gpurun_out/prof_$name $name
+}
 SHORT="--window short --warmup 8 --steps 6 --rounds-per-step 200"
 for s in "$@"; do
   case $s in
@@ -33,6 +40,12 @@ for s in "$@"; do
     c2pmc)
       pmc r04_c2_fetch FETCH_SIZE $SHORT
       pmc r04_c2_write WRITE_SIZE $SHORT ;;
+    c4nn)
+      nnpmc r04_c4nn_fetch FETCH_SIZE --arch b10c128 --board 7 --n 4096 --iters 5
+      nnpmc r04_c4nn_write WRITE_SIZE --arch b10c128 --board 7 --n 4096 --iters 5 ;;
+    c3nn)
+      nnpmc r04_c3nn_fetch FETCH_SIZE --arch b10c128 --board 5 --n 4450 --iters 5
+      nnpmc r04_c3nn_write WRITE_SIZE --arch b10c128 --board 5 --n 4450 --iters 5 ;;
     corrpmc)
       pmc r04_c2corr_fetch FETCH_SIZE $SHORT --precision corrected
       pmc r04_c2corr_write WRITE_SIZE $SHORT --precision corrected ;;
