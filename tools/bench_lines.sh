@@ -17,7 +17,7 @@ run c2 --steps 20 --warmup 5
 run c2acc --steps 20 --warmup 5 --precision accurate --no-cpu-baseline
 run c3 --config C3 --steps 20 --warmup 5 --no-cpu-baseline
 run c4 --config C4 --steps 6 --warmup 5 --no-cpu-baseline
-run c5 --config C5 --steps 4 --warmup 2 --no-cpu-baseline
+run c5 --config C5 --steps 4 --warmup 2 --rounds-per-step 600 --no-cpu-baseline
 python - <<'EOF'
 import json
 out = {}
