@@ -66,6 +66,8 @@ constexpr int F8C_SHIFT = 11;
 // other group's select 105 us: no room beside the network's 233-256-VGPR waves); capped +
 // late 19.5 k (network 163 us, select 71 us, backup 50 -> 59 us: the search waves now share
 // the network's CUs); capped + late + parked trunk 19.3 k; late + parked, uncapped 18.1 k.
+// Second box: capped + late 19.4 k, capped + parked 19.3 k, capped alone 19.7 k (network
+// 154 us; 49 registers spilled, reloaded outside the K loops): the default.
 #ifndef KC_F8C_VGPR
 #define KC_F8C_VGPR 96
 #endif
@@ -73,7 +75,7 @@ constexpr int F8C_SHIFT = 11;
 #define KC_F8C_PARK 0
 #endif
 #ifndef KC_F8C_LATE
-#define KC_F8C_LATE 1
+#define KC_F8C_LATE 0
 #endif
 constexpr float F8C_SCALE = 2048.0f;  // 2^F8C_SHIFT
 
