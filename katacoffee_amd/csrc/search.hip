@@ -209,22 +209,27 @@ KC_D float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeigh
 }
 
 // ---------------------------------------------------------------------------
-// Transposition table (oracle ttFind / ttInsert): linear probing, 64 slots per step.
+// Transposition table (oracle ttFind / ttInsert): linear probing, PROBE_W slots per step.
 // The node of key (k0, k1) or -1; on a miss emptySlot is where ttInsert would put it
 // (the first free slot of the probe sequence; the table is not changed in between).
-// A window's slot and key loads are issued together.
+// A window's slot and key loads are issued together.  The tables are at most half full,
+// so a probe almost always ends in its first few slots: a 16-slot window (lanes 0-15;
+// 256 B of keys) instead of the whole wave's 64 (1 KB) keeps the same single round trip
+// and cuts the bytes a probe pulls from HBM by 4 (PMC: kSelect read 15 MB per launch).
+constexpr int PROBE_W = 16;
 KC_D int ttFind(const GV& v, uint64_t k0, uint64_t k1, int& emptySlot) {
   const int mask = v.d.ttCap - 1;
   const int start = (int)(k0 & (uint64_t)mask);
   const uint64_t* key = v.ttKey();
   const int32_t* node = v.ttNode();
   emptySlot = -1;
-  for(int base = 0; base < v.d.ttCap; base += 64) {
+  const bool act = v.lane < PROBE_W;
+  for(int base = 0; base < v.d.ttCap; base += PROBE_W) {
     int s = (start + base + v.lane) & mask;
-    const int nd = node[s];
-    const uint64_t ka = key[2 * s], kb = key[2 * s + 1];
-    bool match = nd >= 0 && ka == k0 && kb == k1;
-    uint64_t m = ballot(nd < 0 || match);
+    const int nd = act ? node[s] : 0;
+    const uint64_t ka = act ? key[2 * s] : 0ull, kb = act ? key[2 * s + 1] : 0ull;
+    bool match = act && nd >= 0 && ka == k0 && kb == k1;
+    uint64_t m = ballot(act && (nd < 0 || match));
     if(m) {
       int f = firstLane(m);
       emptySlot = bcastI(s, f);
@@ -246,16 +251,17 @@ KC_D void ttInsertAt(const GV& v, int slot, uint64_t k0, uint64_t k1, int nodeId
 // first probe window, loaded ahead by svbProbe (its latency overlaps other work).
 KC_D uint64_t svbProbe(const GV& v, int sel, uint64_t k) {
   const int mask = v.d.svbCap - 1;
-  return v.d.svbKey[v.svbBase(sel) + (((int)(k & (uint64_t)mask) + v.lane) & mask)];
+  return v.lane < PROBE_W ? v.d.svbKey[v.svbBase(sel) + (((int)(k & (uint64_t)mask) + v.lane) & mask)] : 0ull;
 }
 KC_D int svbFindOrInsert(const GV& v, int sel, uint64_t k, uint64_t first) {
   const int mask = v.d.svbCap - 1;
   const size_t b = v.svbBase(sel);
   const int start = (int)(k & (uint64_t)mask);
-  for(int base = 0; base < v.d.svbCap; base += 64) {
+  const bool act = v.lane < PROBE_W;
+  for(int base = 0; base < v.d.svbCap; base += PROBE_W) {
     int s = (start + base + v.lane) & mask;
-    uint64_t kk = base == 0 ? first : v.d.svbKey[b + s];
-    uint64_t m = ballot(kk == 0 || kk == k);
+    uint64_t kk = base == 0 ? first : (act ? v.d.svbKey[b + s] : 0ull);
+    uint64_t m = ballot(act && (kk == 0 || kk == k));
     if(m) {
       int f = firstLane(m);
       int slot = bcastI(s, f);
