@@ -34,6 +34,7 @@ for s in "$@"; do
     accurate) trace r04_c2acc --steps 20 --warmup 5 --precision accurate ;;
     c3) trace r04_c3 --config C3 --steps 10 --warmup 5 ;;
     c4) trace r04_c4 --config C4 $SHORT ;;
+    c5) trace r04_c5 --config C5 --window short --warmup 2 --steps 3 --rounds-per-step 600 ;;
     c4pmc)
       pmc r04_c4_fetch FETCH_SIZE --config C4 $SHORT
       pmc r04_c4_write WRITE_SIZE --config C4 $SHORT ;;
@@ -46,6 +47,9 @@ for s in "$@"; do
     c3nn)
       nnpmc r04_c3nn_fetch FETCH_SIZE --arch b10c128 --board 5 --n 4450 --iters 5
       nnpmc r04_c3nn_write WRITE_SIZE --arch b10c128 --board 5 --n 4450 --iters 5 ;;
+    accpmc)
+      pmc r04_c2acc_fetch FETCH_SIZE $SHORT --precision accurate
+      pmc r04_c2acc_write WRITE_SIZE $SHORT --precision accurate ;;
     corrpmc)
       pmc r04_c2corr_fetch FETCH_SIZE $SHORT --precision corrected
       pmc r04_c2corr_write WRITE_SIZE $SHORT --precision corrected ;;
