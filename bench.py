@@ -33,6 +33,7 @@ committed moves/s and says so in value_kind.
 GPU, RCCL world size N); under torchrun the environment's WORLD_SIZE is used.
 """
 import argparse
+import faulthandler
 import json
 import os
 import queue
@@ -113,10 +114,12 @@ def parse():
                          "bytes over RCCL; every engine switches (the reference's model hot reload)")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
-    ap.add_argument("--cpu-seconds", type=float, default=40.0, help="timed CPU-baseline window (saturated run)")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
+    ap.add_argument("--cpu-curve-seconds", type=float, default=8.0,
+                    help="timed window of each point of the CPU thread-scaling curve (0: skip the curve)")
     ap.add_argument("--cpu-c1-seconds", type=float, default=20.0,
                     help="timed CPU-baseline window (C1 and single-thread runs)")
-    ap.add_argument("--cpu-warmup-seconds", type=float, default=5.0)
+    ap.add_argument("--cpu-warmup-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-whole-host", action="store_true",
                     help="also time the CPU baseline on every CPU of the affinity mask (default: extrapolated, "
                          "since the GPU box asks to stay within its CPU share)")
@@ -195,77 +198,134 @@ def cpu_info():
 
 
 def cpu_run(oracle, model, X, Y, W, games, visits, threads, warm_s, timed_s, cache_log2):
-    sp = oracle.Selfplay(X, Y, W, games=games, max_visits=visits, node_cap=max(2048, 3 * visits), seed=1, nn_mode=1,
-                         model=model, nn_threads=threads, nn_cache_log2=cache_log2)
-    if threads > 1 and games > 1:
-        sp.set_parallel(threads)
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < warm_s:
-        sp.rounds(8)
-    i0 = [sp.info(g) for g in range(games)]
-    t0 = time.perf_counter()
-    rounds = 0
-    while time.perf_counter() - t0 < timed_s:
-        sp.rounds(8)
-        rounds += 8
-    dt = time.perf_counter() - t0
-    i1 = [sp.info(g) for g in range(games)]
-    d = lambda k: sum(b[k] - a[k] for a, b in zip(i0, i1))
-    return dict(rows_per_sec=d("movesMade") / dt, playouts_per_sec=d("playouts") / dt, nn_evals_per_sec=d("nnEvals") / dt,
-                rounds=rounds, seconds=dt, moves=d("movesMade"), playouts=d("playouts"))
+    """The oracle's self-play on `threads` host threads: `threads` independent game groups
+    of games / threads games, one per thread, each with its own search, network batch
+    (single-threaded forward) and NN cache (1/threads of the entries) -- the reference's
+    shape on a CPU, numGameThreads game threads feeding NN server threads that each run
+    whole batches (selfplay.cpp:271-357, nneval.cpp:341-364), rather than one round-
+    synchronous batch split across threads (0.37 efficiency at 16 threads in round 4).
+    ctypes drops the GIL inside each group's rounds call, so the groups run concurrently.
+    Rows (= committed moves in benchmark play) and playouts per second over the window."""
+    gpt = max(1, games // threads)
+    sps = [oracle.Selfplay(X, Y, W, games=gpt, max_visits=visits, node_cap=max(2048, 3 * visits), seed=1,
+                           slot_base=i * gpt, nn_mode=1, model=model, nn_threads=1,
+                           nn_cache_log2=max(0, cache_log2 - (threads - 1).bit_length()) if cache_log2 else 0)
+           for i in range(threads)]
+    phase = [0]  # 1: window open, 2: window closed
+    marks = [[None, None] for _ in range(threads)]  # per group: (time, rounds, counters) at open / close
+    errs = []
+
+    def counters(sp):
+        return [sum(sp.info(g)[key] for g in range(gpt)) for key in ("movesMade", "playouts", "nnEvals")]
+
+    def worker(k):
+        # each group's counters are read by its own thread between its rounds calls
+        try:
+            done = 0
+            while phase[0] < 2 or marks[k][1] is None:
+                sps[k].rounds(8)
+                done += 8
+                for p in (1, 2):
+                    if phase[0] >= p and marks[k][p - 1] is None:
+                        marks[k][p - 1] = (time.perf_counter(), done, counters(sps[k]))
+        except Exception as e:  # surfaced after the window
+            errs.append(e)
+            for p in (0, 1):
+                marks[k][p] = marks[k][p] or (time.perf_counter(), 0, [0, 0, 0])
+
+    ths = [threading.Thread(target=worker, args=(k,), daemon=True) for k in range(threads)]
+    for t in ths:
+        t.start()
+    time.sleep(warm_s)
+    phase[0] = 1
+    time.sleep(timed_s)
+    phase[0] = 2
+    for t in ths:
+        t.join()
+    if errs:
+        raise errs[0]
+    rate = [0.0, 0.0, 0.0]
+    tot = [0, 0, 0]
+    for (t0, r0, c0), (t1, r1, c1) in marks:
+        for j in range(3):
+            rate[j] += (c1[j] - c0[j]) / (t1 - t0)
+            tot[j] += c1[j] - c0[j]
+    dt = sum(m[1][0] - m[0][0] for m in marks) / threads
+    return dict(rows_per_sec=rate[0], playouts_per_sec=rate[1], nn_evals_per_sec=rate[2],
+                rounds=sum(m[1][1] - m[0][1] for m in marks) // threads, seconds=dt, moves=tot[0], playouts=tot[1],
+                games_per_thread=gpt)
 
 
 def cpu_baseline(args, cfg, model_path):
     """The oracle (C++ restatement: same rules / search / rows, fp32 forward with
     eigenbackend.cpp semantics, convolutions as im2col + a register-blocked AVX2
-    SGEMM) on this host: C1 (1 game, 200 visits) and the GPU's workload saturated
-    (4 x cores games, threads over games and inside the forward, NN cache on)."""
+    SGEMM) on this host: C1 (1 game, 200 visits) and the GPU's workload on the host's CPU
+    share (cpu_run: one independent game group of 8 games per thread), plus the same on one
+    thread for the scaling efficiency and a 1/2/4/8/... thread curve."""
     from oracle import oracle
     cores, model_name, machine = cpu_info()
     model = oracle.Model(model_path)
     visits = args.visits or cfg["visits"]
-    run = lambda games, v, threads, secs: cpu_run(oracle, model, cfg["X"], cfg["Y"], cfg["W"], games, v, threads,
-                                                  args.cpu_warmup_seconds, secs, args.nn_cache_log2)
+    gpt = 8
+    run = lambda games, v, threads, secs, warm=args.cpu_warmup_seconds: cpu_run(
+        oracle, model, cfg["X"], cfg["Y"], cfg["W"], games, v, threads, warm, secs, args.nn_cache_log2)
     c1 = None
     if cfg["arch"] == "b6c96" and (cfg["X"], cfg["Y"]) == (5, 5):
-        c1 = run(1, 200, 1, args.cpu_c1_seconds)
-    sat = run(4 * cores, visits, cores, args.cpu_seconds)
-    one = run(4, visits, 1, args.cpu_c1_seconds) if cores > 1 else sat
-    eff = sat["rows_per_sec"] / (cores * one["rows_per_sec"]) if one["rows_per_sec"] > 0 else None
-    desc = lambda r, g, t: ("%d games x %d visits on %d threads, %.0f s warm-up then %d rounds in %.1f s "
-                            "(%d moves, %d playouts)" % (g, visits, t, args.cpu_warmup_seconds, r["rounds"],
-                                                         r["seconds"], r["moves"], r["playouts"]))
+        c1 = run(1, 200, 1, args.cpu_c1_seconds, 5.0)
+    sat = run(gpt * cores, visits, cores, args.cpu_seconds)
+    one = run(gpt, visits, 1, args.cpu_c1_seconds, 5.0) if cores > 1 else sat
+    eff = sat["playouts_per_sec"] / (cores * one["playouts_per_sec"]) if one["playouts_per_sec"] > 0 else None
+    curve = {}
+    t = 2
+    while t < cores and args.cpu_curve_seconds > 0:
+        curve[t] = run(gpt * t, visits, t, args.cpu_curve_seconds, 2.0)["playouts_per_sec"]  # short: rates only
+        t *= 2
+    curve[1], curve[cores] = one["playouts_per_sec"], sat["playouts_per_sec"]
+    desc = lambda r, g, t, w=5.0: ("%d games x %d visits on %d threads (%d independent groups of %d), %.0f s warm-up "
+                                   "then %.1f s (%d rounds per group, %d moves, %d playouts)"
+                                   % (g, visits, t, t, r["games_per_thread"], w, r["seconds"], r["rounds"], r["moves"],
+                                      r["playouts"]))
     out = {
         "value": sat["rows_per_sec"], "unit": "rows/s", "cores": cores, "kind": "port",
         "playouts_per_sec": sat["playouts_per_sec"], "nn_evals_per_sec": sat["nn_evals_per_sec"],
         "cpu_model": model_name, "host_cpus": machine,
         "sample": "oracle C++ self-play (fp32 im2col+SGEMM forward), %s workload, %s"
-                  % (cfg["label"].split(":")[0], desc(sat, 4 * cores, cores)),
-        "single_thread": {"rows_per_sec": one["rows_per_sec"], "sample": desc(one, 4, 1),
-                          "scaling_efficiency_at_%d" % cores: eff},
+                  % (cfg["label"].split(":")[0], desc(sat, gpt * cores, cores, args.cpu_warmup_seconds)),
+        "single_thread": {"rows_per_sec": one["rows_per_sec"], "playouts_per_sec": one["playouts_per_sec"],
+                          "sample": desc(one, gpt, 1), "scaling_efficiency_at_%d" % cores: eff},
+        "thread_curve_playouts_per_sec": {str(k): curve[k] for k in sorted(curve)},
     }
-    # Whole host (SURVEY 8d: all physical cores, numGameThreads = 2 x cores).  The GPU box
-    # asks that worker pools stay within its CPU share (16 threads per GPU), so by default
-    # the whole-host figure is extrapolated from the share's measured rate, linearly over
-    # every logical CPU of the machine: SMT siblings counted as full cores and no loss of
-    # scaling, i.e. an upper bound on the CPU (a lower bound on the GPU/CPU ratio).
-    # --cpu-whole-host measures it instead (threads = the affinity mask, 2 x threads games).
+    # Whole host (SURVEY 8d: all physical cores).  The GPU box asks that worker pools stay
+    # within its CPU share (16 threads per GPU), so the whole host is not run by default: the
+    # share's measured per-thread rate (groups are independent: the thread curve above is the
+    # check that it scales linearly) is extrapolated to the machine's physical cores, and,
+    # as an upper bound, to every logical CPU (SMT siblings counted as full cores).  The
+    # speed-up is quoted against the upper bound.  --cpu-whole-host measures it instead.
     nproc = machine["nproc"] or cores
-    if args.cpu_whole_host:
+    phys = machine["physical_cores"] or nproc
+    if cores >= nproc:  # the share is the whole machine: the saturated run measured it
+        out["whole_host"] = {"value": sat["rows_per_sec"], "unit": "rows/s", "threads": cores, "kind": "measured",
+                             "physical_cores": phys, "sample": out["sample"]}
+    elif args.cpu_whole_host:
         t = machine["affinity"]
-        wh = run(2 * t, visits, t, args.cpu_seconds)
+        wh = run(gpt * t, visits, t, args.cpu_seconds)
         out["whole_host"] = {"value": wh["rows_per_sec"], "unit": "rows/s", "threads": t, "kind": "measured",
-                             "physical_cores": machine["physical_cores"], "sample": desc(wh, 2 * t, t)}
+                             "physical_cores": machine["physical_cores"],
+                             "sample": desc(wh, gpt * t, t, args.cpu_warmup_seconds)}
     else:
         out["whole_host"] = {"value": sat["rows_per_sec"] * nproc / cores, "unit": "rows/s", "threads": nproc,
-                             "physical_cores": machine["physical_cores"], "kind": "extrapolated",
-                             "method": "measured %d-thread rate x %d logical CPUs / %d (linear, SMT counted as cores; "
-                                       "measured 1->%d thread efficiency %s)"
-                                       % (cores, nproc, cores, cores, "%.2f" % eff if eff else "n/a")}
+                             "physical_cores": phys, "kind": "extrapolated",
+                             "physical_cores_value": sat["rows_per_sec"] * phys / cores,
+                             "method": "measured %d-thread rate (1->%d thread efficiency %s) x %d logical CPUs / %d: "
+                                       "linear, SMT siblings counted as full cores (an upper bound on the CPU); "
+                                       "physical_cores_value: x %d physical cores / %d"
+                                       % (cores, cores, "%.2f" % eff if eff else "n/a", nproc, cores, phys, cores),
+                             "why_not_measured": "the GPU box's CPU share is %d threads per GPU (OMP_NUM_THREADS); "
+                                                 "worker pools stay within it" % cores}
     if c1:
         out["C1"] = {"rows_per_sec": c1["rows_per_sec"], "playouts_per_sec": c1["playouts_per_sec"], "threads": 1,
-                     "sample": "1 game x 200 visits, b6c96 fp32, %.0f s warm-up then %.1f s (%d moves, %d playouts)"
-                               % (args.cpu_warmup_seconds, c1["seconds"], c1["moves"], c1["playouts"])}
+                     "sample": "1 game x 200 visits, b6c96 fp32, 5 s warm-up then %.1f s (%d moves, %d playouts)"
+                               % (c1["seconds"], c1["moves"], c1["playouts"])}
     return out
 
 
@@ -407,6 +467,7 @@ def load_traffic(path):
 
 
 def main():
+    faulthandler.enable()  # a native fault prints the Python stack too
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
@@ -481,6 +542,11 @@ def main():
             sp.step(rps)
             sp.sync()  # bounded launch queue (a profiler's per-dispatch state stays small)
             progress("warm-up", i, args.warmup, tw)
+            if i == 0 and os.environ.get("KATACOFFEE_DUMP_MAPS"):
+                # diagnosis of host faults under profilers: the process map (libraries and
+                # device-memory mappings) once every engine buffer exists, to resolve a
+                # native stack trace's addresses afterwards
+                shutil.copyfile("/proc/self/maps", os.environ["KATACOFFEE_DUMP_MAPS"])
         sp.drain_rows()
         sp.drain_games()
         if not args.no_timing:

@@ -23,7 +23,8 @@ CSRC = os.path.join(HERE, "csrc")
 NUM_SPATIAL = 15
 COFFEE_OK = 0
 # network precision / path (include/katacoffee.h COFFEE_NN_*)
-PRECISIONS = {"fast": 0, "accurate": 1, "fast-layered": 2, "corrected": 3, "accurate-nb2": 4}
+PRECISIONS = {"default": 0, "accurate": 1, "fast-layered": 2, "corrected": 3, "accurate-nb2": 4, "fast": 5}
+PRECISION_NAMES = {v: k for k, v in PRECISIONS.items()}
 
 _lib = None
 
@@ -96,7 +97,7 @@ class SelfplayStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ["rounds", "playouts", "nn_evals", "moves", "games_finished", "rows_written", "rows_pending",
                  "rows_dropped", "games_dropped", "errors", "tree_levels", "tree_children", "errors_node_pool",
-                 "errors_edge_pool", "edge_pool_peak", "edge_pool_cap"]]
+                 "errors_edge_pool", "edge_pool_peak", "edge_pool_cap", "nn_precision"]]
 
 
 # Every symbol include/katacoffee.h declares (checked by tests/test_abi.py).
@@ -104,7 +105,7 @@ EXPORTS = [
     "coffee_last_error", "coffee_abi_version", "coffee_device_count", "coffee_set_device", "coffee_device_compute_units", "coffee_malloc",
     "coffee_free", "coffee_memcpy", "coffee_synchronize", "coffee_rules_batch", "coffee_play_batch",
     "coffee_encode_batch", "coffee_model_write_random", "coffee_model_flops", "coffee_nn_create",
-    "coffee_nn_forward", "coffee_nn_forward2", "coffee_nn_destroy", "coffee_nn_create2", "coffee_nn_is_fused", "coffee_fake_net", "coffee_search_params_default",
+    "coffee_nn_forward", "coffee_nn_forward2", "coffee_nn_destroy", "coffee_nn_create2", "coffee_nn_is_fused", "coffee_nn_precision", "coffee_fake_net", "coffee_search_params_default",
     "coffee_selfplay_create", "coffee_selfplay_step", "coffee_selfplay_sync", "coffee_selfplay_stats_get",
     "coffee_selfplay_drain_rows", "coffee_selfplay_drain_games", "coffee_selfplay_set_model",
     "coffee_selfplay_stage_rows", "coffee_selfplay_row_capacity", "coffee_row_bytes", "coffee_selfplay_stream",
@@ -143,6 +144,8 @@ def lib():
         L.coffee_nn_create.argtypes = [ctypes.c_char_p, c_i, c_i, c_i, c_p]
         L.coffee_nn_create2.argtypes = [ctypes.c_char_p, c_i, c_i, c_i, c_i, c_p]
         L.coffee_nn_is_fused.argtypes = [c_p, c_p]
+        if hasattr(L, "coffee_nn_precision"):  # (absent in round-4 builds run as A/B references)
+            L.coffee_nn_precision.argtypes = [c_p, c_p, c_p]
         L.coffee_nn_forward.argtypes = [c_p, c_i, c_p, c_p, c_p]
         L.coffee_nn_forward2.argtypes = [c_p, c_i, c_p, c_p, c_p, c_p]
         L.coffee_nn_destroy.argtypes = [c_p]
@@ -285,11 +288,13 @@ def model_flops(path, area):
 class Network:
     """NeuralNet compute handle (nninterface.h createComputeHandle / getOutput).
 
-    precision: "fast" (fp16 operands; the fused kernel where it covers the net),
-    "accurate" (fp16 hi/lo operand pairs: within 1e-3 of fp32 for any net) or
-    "fast-layered" (fp16 operands on the per-convolution kernels)."""
+    precision (include/katacoffee.h COFFEE_NN_*): "default" (the 1e-3-of-fp32 path:
+    "corrected" where the fused kernel covers the net, "accurate" otherwise), "corrected"
+    (fp16 products + block-scaled e4m3 cross terms), "accurate" (fp16 hi/lo operand pairs:
+    within 1e-3 of fp32 for any net), "fast" (fp16 operands; the fused kernel where it
+    covers the net) or "fast-layered" (fp16 operands on the per-convolution kernels)."""
 
-    def __init__(self, model_path, X, Y, W, precision="fast"):
+    def __init__(self, model_path, X, Y, W, precision="default"):
         self.X, self.Y, self.W = X, Y, W
         self.h = ctypes.c_void_p()
         check(lib().coffee_nn_create2(model_path.encode(), X, Y, W, PRECISIONS[precision], ctypes.byref(self.h)))
@@ -299,6 +304,14 @@ class Network:
         f = ctypes.c_int()
         check(lib().coffee_nn_is_fused(self.h, ctypes.byref(f)))
         return bool(f.value)
+
+    @property
+    def precision(self):
+        """(name of the precision the handle runs, calibration difference of the default
+        precision's corrected-vs-accurate check or 0.0) -- coffee_nn_precision."""
+        p, e = ctypes.c_int(), ctypes.c_float()
+        check(lib().coffee_nn_precision(self.h, ctypes.byref(p), ctypes.byref(e)))
+        return PRECISION_NAMES[p.value], float(e.value)
 
     def forward_device(self, n, packed_dev, out_dev, stream=None):
         check(lib().coffee_nn_forward(self.h, n, _dp(packed_dev), _dp(out_dev), stream))
@@ -389,7 +402,7 @@ class Selfplay:
     """One device's self-play engine (games [slot_base, slot_base + num_games))."""
 
     def __init__(self, X=5, Y=5, W=4, num_games=4096, max_visits=600, seed=1, slot_base=0, model_path=None,
-                 node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, nn_batch_cap=0, nn_precision="fast",
+                 node_cap=0, row_capacity=0, commit_interval=0, nn_cache_log2=0, nn_batch_cap=0, nn_precision="default",
                  start_stagger=0, engines_per_device=0, **search_over):
         _torch_cuda()
         self.X, self.Y, self.W = X, Y, W
@@ -462,6 +475,12 @@ class Selfplay:
         engine's stream: dst a device uint8 tensor [>= row_capacity][row_bytes], count a
         pinned host int64 tensor element (filled asynchronously)."""
         assert dst.is_cuda and dst.dtype.itemsize == 1 and dst.is_contiguous()
+        # the kernel writes up to dst.shape[0] whole rows: a buffer of another shape or on
+        # another device would be written out of bounds (ADVICE r4)
+        assert dst.dim() == 2 and dst.shape[1] == row_bytes(self.X, self.Y), \
+            "dst must be [rows][row_bytes(X, Y)] uint8, got %s" % (tuple(dst.shape),)
+        import torch
+        assert dst.device.index == torch.cuda.current_device(), "dst must be on the engine's (current) device"
         assert count.is_pinned() and count.dtype.itemsize == 8
         check(lib().coffee_selfplay_stage_rows(self.h, ctypes.c_void_p(dst.data_ptr()), dst.shape[0],
                                                ctypes.c_void_p(count.data_ptr()), 1 if discard_games else 0))

@@ -86,7 +86,7 @@ static void checkGeom(int x, int y, int w) {
 extern "C" {
 
 const char* coffee_last_error(void) { return gLastError.c_str(); }
-int coffee_abi_version(void) { return 106; }
+int coffee_abi_version(void) { return 107; }
 
 int coffee_device_count(int* count) {
   return guarded([&] {
@@ -182,13 +182,13 @@ struct coffee_nn {
 };
 
 int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_nn** out) {
-  return coffee_nn_create2(model_path, x, y, win_len, COFFEE_NN_FAST, out);
+  return coffee_nn_create2(model_path, x, y, win_len, COFFEE_NN_DEFAULT, out);
 }
 
 int coffee_nn_create2(const char* model_path, int x, int y, int win_len, int precision, coffee_nn** out) {
   return guarded([&] {
     need(model_path && out, "NULL argument");
-    need(precision >= COFFEE_NN_FAST && precision <= COFFEE_NN_ACCURATE_NB2, "unknown precision");
+    need(precision >= COFFEE_NN_DEFAULT && precision <= COFFEE_NN_FAST, "unknown precision");
     checkGeom(x, y, win_len);
     ModelHost m = loadModel(model_path);
     (void)deviceTables(x, y, win_len);
@@ -226,6 +226,15 @@ int coffee_nn_is_fused(coffee_nn* h, int* fused) {
   return guarded([&] {
     need(h && h->eng && fused, "NULL argument");
     *fused = h->eng->fused() ? 1 : 0;
+  });
+}
+
+int coffee_nn_precision(coffee_nn* h, int* precision, float* calib_err) {
+  return guarded([&] {
+    need(h && h->eng && precision, "NULL argument");
+    *precision = h->eng->precision();
+    if(calib_err)
+      *calib_err = h->eng->calibrationError();
   });
 }
 

@@ -43,7 +43,9 @@ struct Settings {
   int servers = 1;  // numNNServerThreadsPerModel: self-play engines (own stream, batch, cache) over all GPUs
   float modelPollSeconds = 10.0f;
   int nnCacheLog2 = 21;  // selfplay1.cfg:121 nnCacheSizePowerOfTwo
-  int nnPrecision = COFFEE_NN_FAST;  // nnPrecision = fast | accurate | fastLayered (the reference's useFP16)
+  // nnPrecision = auto | corrected | accurate | fast | fastLayered (the reference's useFP16,
+  // whose default Auto is mapped to the path within 1e-3 of fp32: corrected / accurate)
+  int nnPrecision = COFFEE_NN_DEFAULT;
   int64_t maxGamesTotal = -1;
   uint64_t seed = 0;
   coffee_search_params sp;
@@ -106,7 +108,9 @@ inline void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
   s.nnCacheLog2 = std::max(0, s.nnCacheLog2);
   it = kv.find("nnPrecision");
   if(it != kv.end()) {
-    if(it->second == "fast")
+    if(it->second == "auto")
+      s.nnPrecision = COFFEE_NN_DEFAULT;
+    else if(it->second == "fast")
       s.nnPrecision = COFFEE_NN_FAST;
     else if(it->second == "accurate")
       s.nnPrecision = COFFEE_NN_ACCURATE;
@@ -115,7 +119,7 @@ inline void applyConfig(const std::map<std::string, std::string>& kv, Settings& 
     else if(it->second == "corrected")
       s.nnPrecision = COFFEE_NN_CORRECTED;
     else
-      throw std::invalid_argument("nnPrecision must be fast, accurate, corrected or fastLayered");
+      throw std::invalid_argument("nnPrecision must be auto, corrected, accurate, fast or fastLayered");
   }
   coffee_search_params& p = s.sp;
   geti("maxVisits", p.max_visits);

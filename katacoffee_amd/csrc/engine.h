@@ -1,5 +1,6 @@
 // Host-side declarations shared by the HIP translation units and the C ABI.
 #pragma once
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <vector>
@@ -48,6 +49,8 @@ struct NNLayout {
   int globInit, tips, tipb, pBiasG, pLinG, pBias2, pConv2, vBias1, vLin2, vB2, vLin3, vB3, vLinM, vBM;
   int bn1s[NN_MAX_BLOCKS], bn1b[NN_MAX_BLOCKS], bn2s[NN_MAX_BLOCKS], bn2b[NN_MAX_BLOCKS];
   int bngs[NN_MAX_BLOCKS], bngb[NN_MAX_BLOCKS], linG[NN_MAX_BLOCKS];
+  // corrected instance: each convolution's A scale byte, 127 - 11 + its weights' block exponent
+  int sInit, sHead, sConv1[NN_MAX_BLOCKS], sConv2[NN_MAX_BLOCKS];
 };
 
 // Layered forward (nn_layered.hip): one implicit-GEMM MFMA launch per convolution
@@ -59,6 +62,7 @@ class NNLayered {
   ~NNLayered();
   void forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev, const int* rowIdx);
   static bool supportedGeometry(int X, int Y);
+  bool split() const { return split_; }
 
  private:
   struct Conv {
@@ -100,7 +104,8 @@ class NNLayered {
 
 // Network precision / path (coffee_nn_create2, coffee_selfplay_config.nn_precision)
 enum NNPath : int {
-  NN_FAST = 0,          // fp16 operands, f32 accumulation and trunk: fused kernel when it covers the net
+  NN_DEFAULT = 0,       // the 1e-3 path: NN_CORRECTED (which runs the layered split kernels where the
+                        // fused kernel does not cover the net)
   NN_ACCURATE = 1,      // fp16 hi/lo operand pairs (fused kernel when it covers the net, else layered):
                         // logits within 1e-3 of fp32 for any net
   NN_FAST_LAYERED = 2,  // fp16 operands on the layered path (comparison / any architecture)
@@ -108,12 +113,13 @@ enum NNPath : int {
                         // equivalents per product, ~2^-14 per product): fused kernel when it covers the
                         // net, else the layered accurate path
   NN_ACCURATE_NB2 = 4,  // the 2-board bordered split instance (A/B reference of the borderless one)
+  NN_FAST = 5,          // fp16 operands, f32 accumulation and trunk: fused kernel when it covers the net
 };
 
 class NNEngine {
  public:
   // Builds device weights for geometry X x Y (winLen W feeds the global input).
-  NNEngine(const ModelHost& m, int X, int Y, int W, int path = NN_FAST);
+  NNEngine(const ModelHost& m, int X, int Y, int W, int path = NN_DEFAULT);
   ~NNEngine();
   // in: packed V1 words [n][inWords] (device); out: [n][P+4] f32 (device):
   // policy logits [4][A] in the symmetric frame, value logits (win, loss), misc[2].
@@ -126,16 +132,36 @@ class NNEngine {
   const ModelCfg& cfg() const { return cfg_; }
   double flopsPerEval() const { return flops_; }
   bool fused() const { return !layered_; }
-  // rows per launch worth batching: the fused kernel costs one workgroup's latency
-  // per wave of workgroups, so its batch is capped at one wave (cus x 8 boards; two
-  // engines sharing a device each launch up to cus x 4, one wave of 5-board
-  // workgroups); the 2-board A/B instance at cus x 2
-  int batchCap(int cus) const {
-    return layered_ ? (1 << 30) : cus * (mode_ == NN_ACCURATE_NB2 ? 2 : NN_BOARDS_PER_WG);
+  // rows per launch worth batching for one of `engines` engines sharing the device: the
+  // fused kernel costs one workgroup's latency per wave of workgroups (one per CU), so a
+  // launch is capped at one wave: cus x 8 boards of the fast kernel split between the
+  // engines (two engines each launch up to cus x 4, one wave of its 5-board workgroups);
+  // the accurate / corrected kernels have only the 5-board instance, so at most cus x 5
+  // (cus x 8 was 1.6 waves for a lone engine); the 2-board A/B instance cus x 2
+  int batchCap(int cus, int engines) const {
+    if(layered_)
+      return 1 << 30;
+    if(mode_ == NN_ACCURATE_NB2)
+      return std::max(1, cus * 2 / engines);
+    const int split = std::max(1, cus * NN_BOARDS_PER_WG / engines);
+    return (mode_ == NN_ACCURATE || mode_ == NN_CORRECTED) ? std::min(cus * NN_SMALL_NB, split) : split;
   }
   static bool fusedSupported(const ModelCfg& c, int X, int Y);
+  // the precision the engine runs (NNPath; NN_DEFAULT resolved): NN_CORRECTED or NN_ACCURATE
+  // for the default, NN_ACCURATE / NN_FAST_LAYERED on the layered kernels
+  int precision() const;
+  // the default precision's check: largest |logit| difference between the corrected and
+  // accurate instances on the calibration batch (0 when not run)
+  float calibrationError() const { return calibErr_; }
+  // the default precision takes the corrected instance when that difference is at most this
+  // (a quarter of north_star's 1e-3)
+  static constexpr float NN_AUTO_TOL = 2.5e-4f;
 
  private:
+  void build(const ModelHost& m, int path);
+  void release();
+  float calibrationError(NNEngine& ref, int* hotBoards);
+  float calibErr_ = 0.0f;
   ModelCfg cfg_;
   int X_, Y_, W_;
   double flops_;
@@ -154,7 +180,11 @@ class NNEngine {
   int cus_ = 1;                  // compute units of the engine's device
   template <class G>
   void launch(int n, int inWords, const uint16_t* tab, const uint64_t* in, float* out, hipStream_t st,
-              const int* countDev, const int* rowIdx, hipEvent_t e0, hipEvent_t e1);
+              const int* countDev, const int* rowIdx, hipEvent_t e0, hipEvent_t e1, int* hot = nullptr);
+  int* hot_ = nullptr;      // corrected: per batch position, activations past e4m3 (nn.hip kNNForward)
+  int hotCap_ = 0;
+  bool fallback_ = true;    // corrected: re-evaluate flagged boards on the accurate instance
+  std::unique_ptr<NNEngine> fallbackNet_;  // corrected: that instance (split-packed weights)
   std::unique_ptr<NNLayered> layered_;
 };
 

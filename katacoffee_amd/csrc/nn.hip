@@ -35,6 +35,7 @@
 
 #include "detmath.h"
 #include "engine.h"
+#include "kc_board.h"
 #include "lds_dma.h"
 
 namespace kc {
@@ -49,11 +50,20 @@ enum { NN_MODE_F16 = 0, NN_MODE_SPLIT3 = 1, NN_MODE_F8C = 2 };
 // Corrected mode: w x = hi(w) hi(x) + lo(w) x + w lo(x) + lo(w) lo(x), with lo(v) = v - fp16(v)
 // (|lo(v)| <= 2^-11 |v|).  The first product runs on v_mfma_f32_16x16x32_f16; the two
 // cross terms (the last is below f32 rounding) on v_mfma_scale_f32_16x16x128_f8f6f4 with
-// e4m3 operands: A = [e4m3(lo(w) 2^11) | e4m3(w)], B = [e4m3(x) | e4m3(lo(x) 2^11)] over
-// two K-steps, scale 2^-11 on A.  Each cross term carries e4m3's 2^-4 relative error on a
-// value 2^-11 below the product, so a product is good to ~2^-14 (fp16 operands: 2^-10):
-// tools/precision_study.py measures 2.1e-4 on the trained-net test (fp16: 7.1e-3).
+// e4m3 operands over two K-steps: A = [e4m3(lo(w) 2^(11-sw)) | e4m3(w 2^-sw)] with E8M0
+// scale 2^(sw-11), sw the convolution's block exponent (f8Exp of its largest |w|: the
+// largest weight lands in (224, 448], so no weight saturates and small weights stay in
+// e4m3's normal range), B = [e4m3(x) | e4m3(lo(x) 2^11)] with scale 1.  Each cross term
+// carries e4m3's 2^-4 relative error on a value 2^-11 below the product, so a product is
+// good to ~2^-14 (fp16 operands: 2^-10): tools/precision_study.py.  An activation past
+// e4m3's 448 (its conversion gives NaN) flags its board, and that board is re-evaluated by
+// the accurate (split) instance in a second launch (kNNForward's `hot` argument) -- on
+// realistic nets that launch finds no flag and every workgroup exits at once.
+// (Per-board activation exponents instead of the flag were tried in round 5: their board
+// maxima must be published by a barrier before each epilogue, and the capped instance's
+// spill reloads then wait for the weight DMA in flight: 8 % slower)
 constexpr int F8C_SHIFT = 11;
+constexpr float F8C_MAX = 448.0f;  // largest finite e4m3fn
 // The corrected instance is register-capped so that a 128-VGPR search wave of the other
 // game group fits on each SIMD beside its two network waves (2 x 192 + 128 = 512):
 // it is compiled separately (nn_corr.hip) as kNNForwardCap with amdgpu_num_vgpr
@@ -78,6 +88,17 @@ constexpr int F8C_SHIFT = 11;
 #define KC_F8C_LATE 0
 #endif
 constexpr float F8C_SCALE = 2048.0f;  // 2^F8C_SHIFT
+// Block exponent of the corrected precision's e4m3 weights (oracle/ora_nn.cpp f8Exp, the
+// same integer arithmetic): m 2^-s in (224, 448] for m > 0 (m = f 2^e, f in [0.5, 1):
+// s = e - 9, or e - 8 when f > 0.875, since 448 = 0.875 2^9); 0 for m == 0.
+inline int f8Exp(float m) {
+  if(!(m > 0.0f))
+    return 0;
+  int e;
+  const float f = std::frexp(m, &e);
+  const int s = e - 9 + (f > 0.875f ? 1 : 0);
+  return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
 
 template <int X_, int Y_, int C_, int NB_ = NN_BOARDS_PER_WG, int MODE_ = 0, bool BL_ = false>
 struct NNGeo {
@@ -400,10 +421,11 @@ KC_D void stageChunk(const h16x8* __restrict__ src, uint32_t slotAddr, int piece
 //   MODE 1: acc += hi(w) hi(x) + lo(w) hi(x) + hi(w) lo(x)  (three f16 MFMAs per step)
 //   MODE 2: acc += hi(w) hi(x) per step (f16 MFMA), and per pair of steps one scaled e4m3
 //           MFMA over [lo(w) 2^11 | w] x [x | lo(x) 2^11] of both steps, scale 2^-11
+//   sA (mode 2): the A operand's E8M0 scale, 127 - 11 + the conv's weight exponent sw.
 template <class G, int NTAPS, int NCB, int PAR>
 KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                      f32x4 (&acc)[G::MAXT][G::NCT], const int (&rb)[G::MAXT], const uint32_t (&vm)[G::MAXT],
-                     int cg, int lane, int tid, const h16x8* __restrict__ wNext, int nextPieces) {
+                     int cg, int lane, int tid, const h16x8* __restrict__ wNext, int nextPieces, int sA = 0) {
   constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap and plane
   constexpr int CH = CHP * G::PLANES;    // per tap
   constexpr int TPC = G::SLOT_PIECES / CH >= 1 ? G::SLOT_PIECES / CH : 1;
@@ -476,8 +498,8 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
     for(int t = 0; t < G::MAXT; t++)
 #pragma unroll
       for(int ct = 0; ct < G::NCT; ct++)
-        acc[t][ct] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bq[ct], aq[t], acc[t][ct], 0, 0, 0,
-                                                                       127 - F8C_SHIFT, 0, 127);
+        acc[t][ct] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bq[ct], aq[t], acc[t][ct], 0, 0, 0, sA, 0,
+                                                                       127);
   };
   tapAddr(0);
   loadStep(0, 0);
@@ -630,13 +652,25 @@ KC_D uint2 packH4lo(float a, float b, float c, float d) {
   auto lo = [](float x) { return x - (float)(_Float16)x; };
   return packH4(lo(a), lo(b), lo(c), lo(d));
 }
-// e4m3 (OCP e4m3fn, round to nearest even) of two values, saturated at +-448, in the
-// low (HI false) or high half of `old`: byte 0 / 2 = a, byte 1 / 3 = b
+// e4m3 (OCP e4m3fn, round to nearest even) of two values in the low (HI false) or high half
+// of `old`: byte 0 / 2 = a, byte 1 / 3 = b; past 448 the conversion gives NaN (the epilogue
+// flags the board: the accurate instance re-evaluates it)
 template <bool HI>
 KC_D int e4m3x2(float a, float b, int old) {
-  a = fminf(fmaxf(a, -448.0f), 448.0f);
-  b = fminf(fmaxf(b, -448.0f), 448.0f);
   return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
+}
+// Corrected instance: boards of the lane's tile rows whose activations reached past e4m3's
+// range (m[t] = the lane's largest |value| in tile t) are flagged in hot[base + board].
+template <class G>
+KC_D void flagHot(int* hot, int base, int nb, int tstart, int lane, const float (&m)[G::MAXT]) {
+  if constexpr(G::MODE == NN_MODE_F8C) {
+#pragma unroll
+    for(int t = 0; t < G::MAXT; t++) {
+      const int row = (tstart + t) * 16 + (lane & 15);
+      if(!(m[t] <= F8C_MAX) && row < nb * G::A)  // rare; NaN counts as past the range
+        __hip_atomic_store(hot + base + row / G::A, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 // Four activated channels of one row into act: the hi plane, and the second plane --
 // fp16 lo (mode 1), or e4m3 x and e4m3 lo(x) 2^11 (mode 2: the channel octet's 16 bytes
@@ -665,7 +699,8 @@ KC_D void zeroRowBL(uint16_t* act, int tid) {
 // act[pad(row)][ch..ch+3] = f16(relu(v * s[ch] + b[ch])) for on-board rows, all channels.
 template <class G, class V>
 KC_D void storeBnRelu(uint16_t* act, const uint16_t* rowPa, const V (&v)[G::MAXT][G::NCT], const float* __restrict__ s,
-                      const float* __restrict__ bb, int tstart, int cg, int lane) {
+                      const float* __restrict__ bb, int tstart, int cg, int lane, int* hot = nullptr, int base = 0,
+                      int nb = 0) {
   float4 sc[G::NCT], bi[G::NCT];
 #pragma unroll
   for(int ct = 0; ct < G::NCT; ct++) {
@@ -673,8 +708,10 @@ KC_D void storeBnRelu(uint16_t* act, const uint16_t* rowPa, const V (&v)[G::MAXT
     sc[ct] = *reinterpret_cast<const float4*>(s + ch);
     bi[ct] = *reinterpret_cast<const float4*>(bb + ch);
   }
+  float m[G::MAXT];
 #pragma unroll
   for(int t = 0; t < G::MAXT; t++) {
+    m[t] = 0.0f;
     const int row = (tstart + t) * 16 + (lane & 15);
     if(row >= G::ROWS)
       continue;
@@ -685,8 +722,11 @@ KC_D void storeBnRelu(uint16_t* act, const uint16_t* rowPa, const V (&v)[G::MAXT
       const float y2 = fmaxf((float)v[t][ct][2] * sc[ct].z + bi[ct].z, 0.0f);
       const float y3 = fmaxf((float)v[t][ct][3] * sc[ct].w + bi[ct].w, 0.0f);
       storeAct4<G>(act, (int)rowPa[row], chOf<G>(cg, ct, lane), y0, y1, y2, y3);
+      if constexpr(G::MODE == NN_MODE_F8C)
+        m[t] = fmaxf(m[t], fmaxf(fmaxf(y0, y1), fmaxf(y2, y3)));  // >= 0 (ReLU)
     }
   }
+  flagHot<G>(hot, base, nb, tstart, lane, m);
 }
 
 // Zero the border cells of every board (all channels) after act was used as f32
@@ -874,7 +914,10 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
     KC_NN_KERNEL(const NNLayout* __restrict__ L, const h16x8* __restrict__ WB, const float* __restrict__ WF,
                const uint16_t* __restrict__ tabs, int n, const int* __restrict__ countDev,
                const int* __restrict__ rowIdx, int inWords, float winLen, const uint64_t* __restrict__ in,
-               float* __restrict__ out, float* __restrict__ trunk) {
+               float* __restrict__ out, float* __restrict__ trunk, int* __restrict__ hot) {
+  // hot (batch positions): the corrected instance flags boards with activations past e4m3's
+  // range there; the split instance launched with it re-evaluates the workgroup's boards
+  // only when one of them is flagged (and clears the flags), else exits at once
   using G = NNGeo<X, Y, C, NB, MODE, BL>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   NN_PHASE(0);
@@ -883,6 +926,16 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
   if(base >= count)
     return;
   const int nb = min(G::NB, count - base);
+  // split instance re-evaluating flagged boards: only those boards' outputs are written
+  // (a row's logits stay a function of that row alone)
+  uint32_t hotMask = ~0u;
+  if(G::MODE == NN_MODE_SPLIT3 && hot) {
+    hotMask = 0;
+    for(int b = 0; b < nb; b++)
+      hotMask |= __hip_atomic_load(hot + base + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u << b : 0u;
+    if(!hotMask)
+      return;  // uniform: every thread read the same flags
+  }
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rg = wave >> 1, cg = wave & 1;
   const int tstart = rg * G::MAXT;
@@ -967,7 +1020,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
   zeroAcc<G>(acc);
   if constexpr(G::BL)
     convTilesB<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, rb, vm, cg, lane, tid,
-                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96);
+                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96, L->sInit);
   else
     convTiles<G, 9, 1, 0, 0, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                                     L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
@@ -994,13 +1047,18 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       prm[tid + j * G::NT] = pre[j];
   const int Cr = G::C - L->Cg;
   NN_PHASE(2);
+  const int tidK = tid;
   for(int blk = 0; blk < L->nblocks; blk++) {
+    // the wave index as a scalar (fewer long-lived VGPRs: the corrected instance's cap)
+    const int tid = tidK;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int cg = wave & 1, tstart = (wave >> 1) * G::MAXT;
     // previous conv finished reading act; the parked trunk's stores (and the next
     // conv's weight requests) stay in flight behind the epilogue below
     barrierKeepDma();
     NN_PHASE(3 + 4 * blk);
     const float* P = prm + (blk & 1) * G::NPRM;
-    storeBnRelu<G>(act, rowPa, acc, P, P + 96, tstart, cg, lane);
+    storeBnRelu<G>(act, rowPa, acc, P, P + 96, tstart, cg, lane, hot, base, nb);
     waitVm<0>();
     __syncthreads();
     zeroAcc<G>(acc);
@@ -1011,7 +1069,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
     if constexpr(G::BL)
       // chunk parity: stem 3 chunks, each block's convs 9 + 9 (a 64-channel tap is one chunk too)
       convTilesB<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, rb, vm, cg, lane, tid, WB + L->wConv2[blk],
-                                     (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES);
+                                     (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, L->sConv1[blk]);
     else
       convTiles<G, 9, G::C / 32, 1, 0, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid,
                                               WB + L->wConv2[blk],
@@ -1029,7 +1087,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       // the parked trunk is requested before the epilogue, whose LDS work hides its latency
       f32x4 tr[G::MAXT][G::NCT];
       loadTrunk<G>(tr, park, trunk, wave, lane);
-      storeBnRelu<G>(act, rowPa, acc, P + 192, P + 288, tstart, cg, lane);
+      storeBnRelu<G>(act, rowPa, acc, P + 192, P + 288, tstart, cg, lane, hot, base, nb);
 #pragma unroll
       for(int t = 0; t < G::MAXT; t++)
 #pragma unroll
@@ -1039,7 +1097,8 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
-        convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW, CHUNK96);
+        convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW, CHUNK96,
+                                       L->sConv2[blk]);
       else
         convTiles<G, 9, G::C / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                 3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1105,6 +1164,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
         // r branch + gpool bias -> BN2-ReLU -> f16 act (channels < Cr)
         const float* s2 = P + 192;
         const float* b2 = P + 288;
+        float m[G::MAXT] = {};
 #pragma unroll
         for(int ct = 0; ct < G::NCT; ct++) {
           if(cg * (G::C / 2) + ct * 16 >= Cr)
@@ -1118,12 +1178,16 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
             if(row >= G::ROWS)
               continue;
             const float4 gb = *reinterpret_cast<const float4*>(biasS + ((int)rowBP[row] / G::A) * Cr + ch);
-            storeAct4<G>(act, (int)rowPa[row], ch, fmaxf((acc[t][ct][0] + gb.x) * sc.x + bi.x, 0.0f),
-                         fmaxf((acc[t][ct][1] + gb.y) * sc.y + bi.y, 0.0f),
-                         fmaxf((acc[t][ct][2] + gb.z) * sc.z + bi.z, 0.0f),
-                         fmaxf((acc[t][ct][3] + gb.w) * sc.w + bi.w, 0.0f));
+            const float y0 = fmaxf((acc[t][ct][0] + gb.x) * sc.x + bi.x, 0.0f);
+            const float y1 = fmaxf((acc[t][ct][1] + gb.y) * sc.y + bi.y, 0.0f);
+            const float y2 = fmaxf((acc[t][ct][2] + gb.z) * sc.z + bi.z, 0.0f);
+            const float y3 = fmaxf((acc[t][ct][3] + gb.w) * sc.w + bi.w, 0.0f);
+            storeAct4<G>(act, (int)rowPa[row], ch, y0, y1, y2, y3);
+            if constexpr(G::MODE == NN_MODE_F8C)
+              m[t] = fmaxf(m[t], fmaxf(fmaxf(y0, y1), fmaxf(y2, y3)));
           }
         }
+        flagHot<G>(hot, base, nb, tstart, lane, m);
       }
 #pragma unroll
       for(int t = 0; t < G::MAXT; t++)
@@ -1135,7 +1199,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
         convTilesB<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW,
-                                              CHUNK96);
+                                              CHUNK96, L->sConv2[blk]);
       else
         convTiles<G, 9, (G::C - 32) / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                        3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1147,13 +1211,13 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
   __syncthreads();
   NN_PHASE(40);
   const float* PT = prm + (L->nblocks & 1) * G::NPRM;  // tip slab
-  storeBnRelu<G>(act, rowPa, acc, PT, PT + 96, tstart, cg, lane);
+  storeBnRelu<G>(act, rowPa, acc, PT, PT + 96, tstart, cg, lane, hot, base, nb);
   waitVm<0>();
   __syncthreads();
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
   if constexpr(G::BL)
-    convTilesB<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, rb, vm, cg, lane, tid, nullptr, 0);
+    convTilesB<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, rb, vm, cg, lane, tid, nullptr, 0, L->sHead);
   else
     convTiles<G, 1, G::C / 32, 1, 0, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0,
                                             9 + 18 * L->nblocks);
@@ -1226,7 +1290,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
     s += asF(partner<3>(bitsF(s)));
     s += asF(partner<4>(bitsF(s)));
     s += asF(partner<5>(bitsF(s)));
-    if(k == 0 && b < nb) {
+    if(k == 0 && b < nb && ((hotMask >> b) & 1u)) {
       const int dst = rowIdx ? rowIdx[base + b] : base + b;
       out[(size_t)dst * (G::P + 4) + G::P + o] = s + w3[4 * v2 + o];
     }
@@ -1266,7 +1330,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
         }
         part[d] = s;
       }
-      if((lane >> 4) == 0 && row < G::ROWS && brd < nb) {
+      if((lane >> 4) == 0 && row < G::ROWS && brd < nb && ((hotMask >> brd) & 1u)) {
         const int pp = bp - brd * G::A;
         float* o = out + (size_t)(rowIdx ? rowIdx[base + brd] : base + brd) * (G::P + 4);
 #pragma unroll
@@ -1275,6 +1339,8 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       }
     }
   }
+  if(G::MODE == NN_MODE_SPLIT3 && hot && tid < nb)
+    hot[base + tid] = 0;  // this workgroup re-evaluated its boards (one was flagged)
 }
 
 #ifndef KC_NN_KERNEL_ONLY
@@ -1285,7 +1351,7 @@ __global__ void kNNForwardCap(const NNLayout* __restrict__ L, const h16x8* __res
                               const float* __restrict__ WF, const uint16_t* __restrict__ tabs, int n,
                               const int* __restrict__ countDev, const int* __restrict__ rowIdx, int inWords,
                               float winLen, const uint64_t* __restrict__ in, float* __restrict__ out,
-                              float* __restrict__ trunk);
+                              float* __restrict__ trunk, int* __restrict__ hot);
 #endif
 template <class G>
 constexpr auto nnKernel() {
@@ -1363,11 +1429,24 @@ static uint8_t f2e4m3(float f) {
 }
 
 // mode 1: after each tap's hi fragments the same fragments of lo = fp16(w - hi);
-// mode 2: after them the e4m3 pairs [lo(w) 2^11 of the fragment's 8 k | w of the same 8 k]
+// mode 2: after them the e4m3 pairs [lo(w) 2^(11-sw) of the fragment's 8 k | w 2^-sw of the
+// same 8 k], sw the conv's block exponent (f8Exp of its largest |w|), and *sA = the A
+// operand's E8M0 scale byte, 127 - 11 + sw
 // (convTiles' / convTilesB's SPLIT ring slot layout).
 static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout,
-                     const std::function<float(int, int, int)>& W, int mode = NN_MODE_F16) {
+                     const std::function<float(int, int, int)>& W, int mode = NN_MODE_F16, int* sA = nullptr) {
   const int ncb = cinPad / 32, nct = cout / 16;
+  int sw = 0;
+  if(mode == NN_MODE_F8C) {
+    float mx = 0.0f;
+    for(int co = 0; co < cout; co++)
+      for(int tap = 0; tap < ntaps; tap++)
+        for(int ci = 0; ci < cinPad; ci++)
+          mx = std::max(mx, std::fabs(W(co, ci, tap)));
+    sw = f8Exp(mx);
+    if(sA)
+      *sA = 127 - F8C_SHIFT + sw;
+  }
   for(int tap = 0; tap < ntaps; tap++)
     for(int part = 0; part < (mode != NN_MODE_F16 ? 2 : 1); part++)
       for(int cb = 0; cb < ncb; cb++)
@@ -1384,8 +1463,8 @@ static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout
             } else {
               uint8_t b[16];
               for(int j = 0; j < 8; j++) {
-                b[j] = f2e4m3((w[j] - h2f(f2h(w[j]))) * F8C_SCALE);
-                b[8 + j] = f2e4m3(w[j]);
+                b[j] = f2e4m3(ldexpf((w[j] - h2f(f2h(w[j]))) * F8C_SCALE, -sw));
+                b[8 + j] = f2e4m3(ldexpf(w[j], -sw));
               }
               for(int j = 0; j < 8; j++)
                 dst.push_back((uint16_t)(b[2 * j] | (b[2 * j + 1] << 8)));
@@ -1444,36 +1523,139 @@ bool NNEngine::fusedSupported(const ModelCfg& c, int X, int Y) {
          c.cin == NUM_SPATIAL && c.gin == 1 && (int)c.kinds.size() <= NN_MAX_BLOCKS;
 }
 
+// Calibration positions of the default precision's check: n positions of seeded uniform
+// random legal play from the empty board (position i after i % (A + 1) moves, or fewer if
+// the game ends), symmetry i % 8, encoded on the device (kEncodeBatch).
+static void calibrationBatch(int X, int Y, int W, int n, uint64_t* packedDev, hipStream_t st) {
+  const DTables& T = hostTables(X, Y, W);
+  const int A = X * Y;
+  std::vector<uint8_t> cells((size_t)n * A), pla(n);
+  std::vector<int8_t> hc((size_t)n * HIST), hd((size_t)n * HIST);
+  std::vector<int32_t> sym(n);
+  uint64_t rng = 0x243f6a8885a308d3ULL;
+  auto next = [&]() {
+    rng = rng * 6364136223846793005ULL + 1442695040888963407ULL;
+    return (uint32_t)(rng >> 33);
+  };
+  for(int i = 0; i < n; i++) {
+    DBoard b;
+    boardInit(T, b);
+    for(int k = 0; k < i % (A + 1) && !b.finished; k++) {
+      int legal[4 * MAX_AREA], nl = 0;
+      for(int c = 0; c < A; c++)
+        for(int d = 0; d < 4; d++)
+          if(isLegal(T, b, c, d))
+            legal[nl++] = d * A + c;
+      if(nl == 0)
+        break;
+      const int mv = legal[next() % nl];
+      playMoveSerial(T, b, mv % A, mv / A);
+    }
+    for(int c = 0; c < A; c++)
+      cells[(size_t)i * A + c] = (uint8_t)colorAt(b, c);
+    for(int h = 0; h < HIST; h++) {
+      hc[(size_t)i * HIST + h] = (int8_t)hCell(b, h);
+      hd[(size_t)i * HIST + h] = (int8_t)hDir(b, h);
+    }
+    pla[i] = (uint8_t)b.pla;
+    sym[i] = i % 8;
+  }
+  void* buf = nullptr;
+  const size_t bytes = cells.size() + pla.size() + hc.size() + hd.size() + sym.size() * 4;
+  KC_HIP(hipMalloc(&buf, bytes));
+  char* p = static_cast<char*>(buf);
+  auto up = [&](const void* src, size_t len) {
+    KC_HIP(hipMemcpy(p, src, len, hipMemcpyHostToDevice));
+    char* at = p;
+    p += len;
+    return at;
+  };
+  int32_t* symD = reinterpret_cast<int32_t*>(up(sym.data(), sym.size() * 4));
+  uint8_t* cellsD = reinterpret_cast<uint8_t*>(up(cells.data(), cells.size()));
+  int8_t* hcD = reinterpret_cast<int8_t*>(up(hc.data(), hc.size()));
+  int8_t* hdD = reinterpret_cast<int8_t*>(up(hd.data(), hd.size()));
+  uint8_t* plaD = reinterpret_cast<uint8_t*>(up(pla.data(), pla.size()));
+  launchEncodeBatch(deviceTables(X, Y, W), n, cellsD, hcD, hdD, plaD, symD, packedDev, nullptr, st);
+  KC_HIP(hipStreamSynchronize(st));
+  (void)hipFree(buf);
+}
+
+// Largest |logit| difference between this engine and `ref` on the calibration batch, and
+// (corrected instance) how many of its boards had activations past e4m3's range.
+float NNEngine::calibrationError(NNEngine& ref, int* hotBoards) {
+  constexpr int n = 256;
+  const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64, P = 4 * X_ * Y_;
+  uint64_t* in = nullptr;
+  float* out = nullptr;
+  KC_HIP(hipMalloc(&in, (size_t)n * inWords * 8));
+  KC_HIP(hipMalloc(&out, (size_t)2 * n * (P + 4) * 4));
+  float err = 0.0f;
+  try {
+    calibrationBatch(X_, Y_, W_, n, in, nullptr);
+    if(mode_ == NN_CORRECTED) {
+      // the corrected kernel alone first: the boards it flags (the re-evaluation clears them)
+      fallback_ = false;
+      forward(n, in, out, nullptr);
+      fallback_ = true;
+      std::vector<int> h(n);
+      KC_HIP(hipMemcpy(h.data(), hot_, (size_t)n * 4, hipMemcpyDeviceToHost));
+      *hotBoards = 0;
+      for(int v : h)
+        *hotBoards += v != 0;
+      KC_HIP(hipMemset(hot_, 0, (size_t)n * 4));
+    }
+    forward(n, in, out, nullptr);
+    ref.forward(n, in, out + (size_t)n * (P + 4), nullptr);
+    std::vector<float> h((size_t)2 * n * (P + 4));
+    KC_HIP(hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost));
+    for(size_t i = 0; i < h.size() / 2; i++)
+      err = std::max(err, std::fabs(h[i] - h[i + h.size() / 2]));
+    if(!std::isfinite(err))
+      err = INFINITY;
+  } catch(...) {
+    (void)hipFree(in);
+    (void)hipFree(out);
+    throw;
+  }
+  (void)hipFree(in);
+  (void)hipFree(out);
+  return err;
+}
+
 NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.cfg), X_(X), Y_(Y), W_(W) {
   flops_ = modelFlopsPerEval(cfg_, X * Y);
-  if(path < NN_FAST || path > NN_ACCURATE_NB2)
+  if(path < NN_DEFAULT || path > NN_FAST)
     throw std::invalid_argument("NNEngine: unknown precision/path");
+  if(path != NN_DEFAULT) {
+    build(m, path);
+    return;
+  }
+  // the default (north-star 1e-3) precision: the corrected instance, unless on the
+  // calibration batch its logits differ from the accurate (split) instance's by more than
+  // NN_AUTO_TOL or any board needs the re-evaluation (activations past e4m3's range) --
+  // corrected products are good to ~2^-14 relative, which deep-trained nets with large
+  // logits push towards 1e-3; the split path is good to ~2^-21
+  build(m, NN_CORRECTED);
+  if(layered_)
+    return;  // the layered kernels run "corrected" as the split path already
+  int hotBoards = 0;
+  calibErr_ = calibrationError(*fallbackNet_, &hotBoards);
+  if(!(calibErr_ <= NN_AUTO_TOL) || hotBoards > 0) {
+    release();
+    build(m, NN_ACCURATE);
+  }
+}
+
+void NNEngine::build(const ModelHost& m, int path) {
+  const int X = X_, Y = Y_, W = W_;
   if(path == NN_FAST_LAYERED || !fusedSupported(m.cfg, X, Y)) {
     // the layered kernels have fp16 and hi/lo split operands; corrected maps to split
     layered_.reset(new NNLayered(m, X, Y, W, path != NN_FAST && path != NN_FAST_LAYERED));
     return;
   }
   mode_ = path;
-  if(path == NN_CORRECTED) {
-    // e4m3 holds |w| <= 448 (the packed e4m3(w) saturates there): a net with a larger
-    // convolution weight runs on the split ("accurate") instance instead
-    float mx = 0.0f;
-    auto scan = [&](const std::vector<float>& v) {
-      for(float x : v)
-        mx = std::max(mx, std::fabs(x));
-    };
-    scan(m.convInit);
-    scan(m.pConv1);
-    scan(m.pConvG);
-    scan(m.vConv1);
-    for(const ModelBlock& b : m.blocks) {
-      scan(b.conv1);
-      scan(b.conv1g);
-      scan(b.conv2);
-    }
-    if(!(mx < 448.0f))
-      mode_ = path = NN_ACCURATE;
-  }
+  if(path == NN_CORRECTED)  // the re-evaluation of boards past e4m3's range (forward)
+    fallbackNet_.reset(new NNEngine(m, X, Y, W, NN_ACCURATE));
   // the fused kernel's operand mode: fp16, fp16 hi/lo pairs (accurate: the borderless
   // 5-board instance, or the 2-board one for A/B), fp16 + e4m3 cross terms (corrected)
   const int wmode = path == NN_CORRECTED ? NN_MODE_F8C : (path == NN_FAST ? NN_MODE_F16 : NN_MODE_SPLIT3);
@@ -1504,7 +1686,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   L.wInit = bfOff();
   packConv(wb, 9, 32, C, [&](int co, int ci, int tap) {
     return ci < cfg_.cin ? m.convInit[((size_t)co * cfg_.cin + ci) * 9 + tap] : 0.0f;
-  }, wmode);
+  }, wmode, &L.sInit);
   L.globInit = f32(m.globInit);
   for(int i = 0; i < L.nblocks; i++) {
     const ModelBlock& b = m.blocks[i];
@@ -1513,15 +1695,17 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
     L.bn1b[i] = f32(b.bn1b);
     L.wConv1[i] = bfOff();
     if(b.kind == 0) {
-      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv1[((size_t)co * C + ci) * 9 + tap]; }, wmode);
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv1[((size_t)co * C + ci) * 9 + tap]; }, wmode,
+               &L.sConv1[i]);
       L.bn2s[i] = f32(b.bn2s);
       L.bn2b[i] = f32(b.bn2b);
       L.wConv2[i] = bfOff();
-      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * C + ci) * 9 + tap]; }, wmode);
+      packConv(wb, 9, C, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * C + ci) * 9 + tap]; }, wmode,
+               &L.sConv2[i]);
     } else {
       packConv(wb, 9, C, C, [&](int co, int ci, int tap) {
         return co < Cr ? b.conv1[((size_t)co * C + ci) * 9 + tap] : b.conv1g[((size_t)(co - Cr) * C + ci) * 9 + tap];
-      }, wmode);
+      }, wmode, &L.sConv1[i]);
       L.bngs[i] = f32(b.bngs);
       L.bngb[i] = f32(b.bngb);
       L.linG[i] = f32T(b.linG, Cr);
@@ -1529,7 +1713,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
       L.bn2b[i] = f32(b.bn2b);
       L.wConv2[i] = bfOff();
       packConv(wb, 9, Cr, C, [&](int co, int ci, int tap) { return b.conv2[((size_t)co * Cr + ci) * 9 + tap]; },
-               wmode);
+               wmode, &L.sConv2[i]);
     }
   }
   L.tips = f32(m.tips);
@@ -1541,7 +1725,7 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
     if(co < 64)
       return m.pConvG[(size_t)(co - 32) * C + ci];
     return m.vConv1[(size_t)(co - 64) * C + ci];
-  }, wmode);
+  }, wmode, &L.sHead);
   L.pBiasG = f32(m.pBiasG);
   L.pLinG = f32T(m.pLinG, 32);
   L.pBias2 = f32(m.pBias2);
@@ -1596,16 +1780,28 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   KC_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev));
 }
 
-NNEngine::~NNEngine() {
-  (void)hipFree(trunk_);
-  (void)hipFree(wHalf_);
-  (void)hipFree(wF32_);
-  (void)hipFree(layoutDev_);
-  (void)hipFree(tabDev_);
-  (void)hipFree(tabDevSm_);
-  (void)hipFree(tabDevS_);
-  (void)hipFree(tabDevB_);
+NNEngine::~NNEngine() { release(); }
 
+void NNEngine::release() {
+  for(void* p : {(void*)trunk_, wHalf_, (void*)wF32_, (void*)layoutDev_, (void*)tabDev_, (void*)tabDevSm_,
+                 (void*)tabDevS_, (void*)tabDevB_, (void*)hot_})
+    (void)hipFree(p);
+  trunk_ = nullptr;
+  trunkBytes_ = 0;
+  hot_ = nullptr;
+  hotCap_ = 0;
+  wHalf_ = nullptr;
+  wF32_ = nullptr;
+  layoutDev_ = nullptr;
+  tabDev_ = tabDevSm_ = tabDevS_ = tabDevB_ = nullptr;
+  layered_.reset();
+  fallbackNet_.reset();
+}
+
+int NNEngine::precision() const {
+  if(layered_)
+    return layered_->split() ? NN_ACCURATE : NN_FAST_LAYERED;
+  return mode_;
 }
 
 void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, const int* countDev,
@@ -1629,9 +1825,25 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   if(mode_ == NN_ACCURATE)
     launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>>(n, inWords, tabDevB_, in, out, st, countDev, rowIdx,
                                                                e0, e1);
-  else if(mode_ == NN_CORRECTED)
+  else if(mode_ == NN_CORRECTED) {
+    // the corrected kernel flags boards whose activations pass e4m3's range; the accurate
+    // kernel then re-evaluates the workgroups holding one (the others exit at once)
+    const int grid = (n + NN_SMALL_NB - 1) / NN_SMALL_NB;
+    if(grid * NN_SMALL_NB > hotCap_) {
+      if(hot_)
+        KC_HIP(hipStreamSynchronize(st));
+      (void)hipFree(hot_);
+      hot_ = nullptr;
+      KC_HIP(hipMalloc(&hot_, (size_t)grid * NN_SMALL_NB * 4));
+      KC_HIP(hipMemsetAsync(hot_, 0, (size_t)grid * NN_SMALL_NB * 4, st));
+      hotCap_ = grid * NN_SMALL_NB;
+    }
     launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>>(n, inWords, tabDevB_, in, out, st, countDev, rowIdx, e0,
-                                                            e1);
+                                                            fallback_ ? nullptr : e1, hot_);
+    if(fallback_)  // the accurate engine's split weights, this engine's flags
+      fallbackNet_->launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>>(
+          n, inWords, fallbackNet_->tabDevB_, in, out, st, countDev, rowIdx, nullptr, e1, hot_);
+  }
   else if(mode_ == NN_ACCURATE_NB2)
     launch<NNGeo<5, 5, 96, 2, NN_MODE_SPLIT3, false>>(n, inWords, tabDevS_, in, out, st, countDev, rowIdx, e0, e1);
   else if(n <= NN_SMALL_NB * cus_ && small_ != 8)
@@ -1642,7 +1854,7 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
 
 template <class G>
 void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* in, float* out, hipStream_t st,
-                      const int* countDev, const int* rowIdx, hipEvent_t e0, hipEvent_t e1) {
+                      const int* countDev, const int* rowIdx, hipEvent_t e0, hipEvent_t e1, int* hot) {
   const int grid = (n + G::NB - 1) / G::NB;
   const size_t bytes = regTrunk<G>() ? 0 : (size_t)grid * G::NW * G::MAXT * G::NCT * 64 * 16;
   if(bytes > trunkBytes_) {
@@ -1655,12 +1867,12 @@ void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* i
     trunkBytes_ = bytes;
   }
   auto kern = nnKernel<G>();
-  if(e0)
+  if(e0 || e1)
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, e0, e1, 0, layoutDev_, (const h16x8*)wHalf_,
-                          wF32_, tab, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
+                          wF32_, tab, n, countDev, rowIdx, inWords, (float)W_, in, out, trunk_, hot);
   else
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, layoutDev_, (const h16x8*)wHalf_, wF32_, tab, n,
-                       countDev, rowIdx, inWords, (float)W_, in, out, trunk_);
+                       countDev, rowIdx, inWords, (float)W_, in, out, trunk_, hot);
   KC_HIP(hipGetLastError());
 }
 

@@ -14,6 +14,6 @@ namespace kc {
 template __global__ void kNNForwardCap<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>(
     const NNLayout* __restrict__, const h16x8* __restrict__, const float* __restrict__, const uint16_t* __restrict__,
     int, const int* __restrict__, const int* __restrict__, int, float, const uint64_t* __restrict__, float* __restrict__,
-    float* __restrict__);
+    float* __restrict__, int* __restrict__);
 #endif
 }  // namespace kc

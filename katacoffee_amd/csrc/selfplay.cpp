@@ -379,6 +379,7 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
   KC_HIP(hipMemcpy(&gdrop, hd_.gDropped, 8, hipMemcpyDeviceToHost));
   out.games_dropped = gdrop;
   out.edge_pool_cap = (uint64_t)hd_.edgePoolCap;
+  out.nn_precision = nn_ ? (uint64_t)nn_->precision() : 0;
   if(out.errors)
     throw InternalError("self-play device invariant violated in " + std::to_string(out.errors) +
                         " game slot(s): " + std::to_string(out.errors_node_pool) + " node pool exhausted, " +
@@ -496,7 +497,7 @@ int SelfplayEngine::nnCapFor(int G) const {
     return std::min(G, cus_ * NN_BOARDS_PER_WG);
   if(!nn_->fused())
     return G;
-  return std::min(G, std::max(1, nn_->batchCap(cus_) / enginesPerDevice_));
+  return std::min(G, nn_->batchCap(cus_, enginesPerDevice_));
 }
 
 void SelfplayEngine::setModel(const char* path) {

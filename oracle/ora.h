@@ -98,7 +98,8 @@ struct ModelCfg {
 struct PackedConv {
   int ky = 0, kx = 0, cin = 0, cout = 0;
   std::vector<float> w, p32, p16;
-  // corrected-precision emulation: [3K][cout] = fp16(w) ; e4m3(lo(w) 2^11) / 2^11 ; e4m3(w)
+  // corrected-precision emulation: [3K][cout] = fp16(w) ; E(lo(w) 2^11, sw) / 2^11 ; E(w, sw)
+  // (ora_nn.cpp: e4m3 at the convolution's block exponent sw)
   std::vector<float> pC;
   void pack();
 };
@@ -140,6 +141,7 @@ struct NNBatch {
   const float* mask;
   int mode;  // convolution operands: 0 fp32, 1 fp16 (fast), 2 fp16 + e4m3 cross terms (corrected)
   int threads;
+  int* hot = nullptr;  // mode 2: [n] set for boards with a convolution input past e4m3's 448
 };
 void convApply(const NNBatch& b, const PackedConv& cv, const float* in, float* out, bool accumulate);
 // BatchNormLayer::apply (eigenbackend.cpp:717-734): (x [+ perBoard]) * s + b, act, mask

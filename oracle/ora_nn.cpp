@@ -17,8 +17,12 @@
 // mode 1 rounds every convolution weight and convolution input to fp16 (RNE),
 // exactly where the HIP kernels do; residual trunks stay f32 as in the kernels.
 // mode 2 restates the "corrected" precision (csrc/nn.hip NN_MODE_F8C): each product is
-// fp16(w) fp16(x) + e4m3(lo(w) 2^11) e4m3(x) / 2^11 + e4m3(w) e4m3(lo(x) 2^11) / 2^11, with
-// lo(v) = v - fp16(v) and e4m3 = OCP e4m3fn, round to nearest even, saturating at 448.
+//   fp16(w) fp16(x) + E(lo(w) 2^11, sw) e4m3(x) / 2^11 + E(w, sw) e4m3(lo(x) 2^11) / 2^11,
+// lo(v) = v - fp16(v), e4m3 = OCP e4m3fn, round to nearest even, E(v, s) = e4m3(v 2^-s) 2^s
+// with sw the convolution's block exponent (the E8M0 scale operand of the block-scaled
+// MFMA; f8Exp: its largest |weight| lands in (224, 448]).  A board with a convolution input
+// past e4m3's 448 is "hot": the device re-evaluates it on the accurate (split) instance,
+// here its outputs are the fp32 forward's (mode 0; the split path is within ~1e-5 of it).
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -72,6 +76,19 @@ static inline float e4m3r(float f) {
   return std::signbit(f) ? -r : r;
 }
 static const float F8C_SCALE = 2048.0f;
+// Block exponent s of the corrected precision's e4m3 operands: m 2^-s in (224, 448] for
+// m > 0 (m = f 2^e, f in [0.5, 1): s = e - 9, or e - 8 when f > 0.875, since 448 = 0.875 2^9),
+// 0 for m == 0 (csrc/nn.hip f8Exp, the same integer arithmetic).
+static inline int f8Exp(float m) {
+  if(!(m > 0.0f))
+    return 0;
+  int e;
+  const float f = frexpf(m, &e);
+  int s = e - 9 + (f > 0.875f ? 1 : 0);
+  return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
+// e4m3 of v at block exponent s, back in v's units
+static inline float e4m3s(float v, int s) { return ldexpf(e4m3r(ldexpf(v, -s)), s); }
 
 // ---------------------------------------------------------------------------
 // SGEMM: C[M][ldc] (+)= A[M][lda] * B, B packed in 16-column panels
@@ -153,7 +170,11 @@ static void sgemm(int M, int N, int K, const float* A, int lda, const float* Bp,
 void PackedConv::pack() {
   const int K = ky * kx * cin;
   std::vector<float> B((size_t)K * cout), B16((size_t)K * cout), BC((size_t)3 * K * cout);
-  for(int co = 0; co < cout; co++)
+  float mx = 0.0f;  // the convolution's block exponent (corrected precision)
+  for(float v : w)
+    mx = fmaxf(mx, fabsf(v));
+  const int sw = f8Exp(mx);
+  for(int co = 0; co < cout; co++) {
     for(int ci = 0; ci < cin; ci++)
       for(int y = 0; y < ky; y++)
         for(int x = 0; x < kx; x++) {
@@ -162,9 +183,10 @@ void PackedConv::pack() {
           B[k * cout + co] = v;
           B16[k * cout + co] = f16r(v);
           BC[k * cout + co] = f16r(v);
-          BC[(K + k) * cout + co] = e4m3r((v - f16r(v)) * F8C_SCALE) / F8C_SCALE;
-          BC[(2 * K + k) * cout + co] = e4m3r(v);
+          BC[(K + k) * cout + co] = e4m3s((v - f16r(v)) * F8C_SCALE, sw) / F8C_SCALE;
+          BC[(2 * K + k) * cout + co] = e4m3s(v, sw);
         }
+  }
   packB(B.data(), K, cout, p32);
   packB(B16.data(), K, cout, p16);
   packB(BC.data(), 3 * K, cout, pC);
@@ -181,6 +203,13 @@ void convApply(const NNBatch& b, const PackedConv& cv, const float* in, float* o
   const int KC3 = corr ? 3 * K : K;  // corrected: im2col columns [fp16(x) | e4m3(x) | e4m3(lo(x) 2^11) / 2^11]
   constexpr int CH = 48;  // rows per im2col chunk
   const int chunks = (rows + CH - 1) / CH;
+  if(corr && b.hot)  // corrected: boards whose convolution input passes e4m3's range
+    for(int brd = 0; brd < b.n; brd++)
+      for(size_t i = 0; i < (size_t)A * cv.cin; i++)
+        if(!(fabsf(in[(size_t)brd * A * cv.cin + i]) <= 448.0f)) {
+          b.hot[brd] = 1;
+          break;
+        }
 #pragma omp parallel for schedule(dynamic, 1) num_threads(b.threads > 0 ? b.threads : 1)
   for(int ch = 0; ch < chunks; ch++) {
     const int r0 = ch * CH, r1 = r0 + CH < rows ? r0 + CH : rows;
@@ -470,7 +499,8 @@ void nnForward(const Model& m, int X, int Y, int n, const float* bin, const floa
                float* value, float* misc, int mode, int threads) {
   const ModelCfg& c = m.cfg;
   const int A = X * Y, C = c.C;
-  NNBatch b{n, X, Y, A, nullptr, mode, threads};
+  std::vector<int> hot(mode == 2 ? n : 0, 0);
+  NNBatch b{n, X, Y, A, nullptr, mode, threads, mode == 2 ? hot.data() : nullptr};
   const size_t rows = (size_t)n * A;
   std::vector<float> in(rows * c.cin), x(rows * C), a(rows * C);
   for(int i = 0; i < n; i++)
@@ -531,6 +561,27 @@ void nnForward(const Model& m, int X, int Y, int n, const float* bin, const floa
     t = t > 0.0f ? t : 0.0f;
   matmulRows(n, c.v2, 2, vh.data(), m.vLin3.data(), m.vB3.data(), value);
   matmulRows(n, c.v2, 2, vh.data(), m.vLinM.data(), m.vBM.data(), misc);
+  if(mode == 2) {
+    // hot boards: the accurate re-evaluation, i.e. the fp32 forward's outputs
+    std::vector<float> hb, hg;
+    std::vector<int> idx;
+    for(int i = 0; i < n; i++)
+      if(hot[i]) {
+        idx.push_back(i);
+        hb.insert(hb.end(), bin + (size_t)i * c.cin * A, bin + (size_t)(i + 1) * c.cin * A);
+        hg.insert(hg.end(), glob + (size_t)i * c.gin, glob + (size_t)(i + 1) * c.gin);
+      }
+    if(!idx.empty()) {
+      const int k = (int)idx.size();
+      std::vector<float> p((size_t)k * 4 * A), v((size_t)k * 2), mi((size_t)k * 2);
+      nnForward(m, X, Y, k, hb.data(), hg.data(), p.data(), v.data(), mi.data(), 0, threads);
+      for(int j = 0; j < k; j++) {
+        memcpy(policy + (size_t)idx[j] * 4 * A, &p[(size_t)j * 4 * A], sizeof(float) * 4 * A);
+        memcpy(value + (size_t)idx[j] * 2, &v[(size_t)j * 2], sizeof(float) * 2);
+        memcpy(misc + (size_t)idx[j] * 2, &mi[(size_t)j * 2], sizeof(float) * 2);
+      }
+    }
+  }
 }
 
 }  // namespace ora

@@ -63,4 +63,11 @@ def test_stage_rows_rejects_small_destination():
     cnt = torch.zeros(1, dtype=torch.int64).pin_memory()
     with pytest.raises(kc.CoffeeError):
         e.stage_rows(small, cnt[0])
+    # a flat byte buffer with as many "rows" as the capacity holds far fewer rows
+    flat = torch.empty((e.row_capacity(),), dtype=torch.uint8, device="cuda")
+    with pytest.raises(AssertionError):
+        e.stage_rows(flat, cnt[0])
+    wide = torch.empty((e.row_capacity(), rb - 1), dtype=torch.uint8, device="cuda")
+    with pytest.raises(AssertionError):
+        e.stage_rows(wide, cnt[0])
     e.close()

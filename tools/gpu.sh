@@ -24,9 +24,9 @@ for step in "$@"; do
     test)
       k=()
       [ -n "$arg" ] && k=(-k "$arg")
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1 ;;
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1 ;;
     file)
-      timeout -k 10 900 python -u -m pytest "$arg" -m gpu -x -v --timeout 300 --timeout-method thread > $log 2>&1 ;;
+      timeout -k 10 900 python -u -m pytest "$arg" -m gpu -x -v -rP --timeout 300 --timeout-method thread > $log 2>&1 ;;
     bench)
       timeout -k 10 600 python -u bench.py ${arg//,/ } > $log 2>&1 ;;
     benchlong)

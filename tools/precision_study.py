@@ -13,7 +13,18 @@ last = head 1x1):
   f8c      hi*hi (fp16) + e4m3(lo(w)*S)/S * e4m3(x) + e4m3(w) * e4m3(lo(x)*S)/S
            (one fp16 MFMA + two fp8 MFMAs at twice the rate: 2 fp16-MFMA equivalents)
   f8cw     hi*hi + e4m3(lo(w)*S)/S * e4m3(x) (weights corrected only)
-Usage: python tools/precision_study.py [--scheme-per-layer]
+  f8cs     the shipped corrected kernel (round 5): f8c with the weights' e4m3 at the
+           convolution's block exponent (largest weight in (224, 448], oracle/ora_nn.cpp
+           f8Exp) and boards whose activations pass e4m3's 448 re-evaluated exactly
+           (the device: on the split instance)
+Usage: python tools/precision_study.py [--per-layer] [--steps N] [--big-act F]
+  --steps N     Adam steps of the trained net (10: the test_gpu_train.py net)
+  --big-act F   scale the first block's BN2 by F and its conv2 by 1/F (same function,
+                activations F times larger entering that convolution; the weights get
+                F times smaller, so fp16 subnormals hurt every fp16 scheme)
+  --hot M       scale the first block's BN2 so its conv2 reads activations up to M, and
+                the later blocks' BN1 and the tip BN by the same 1/F (weights untouched;
+                tests/test_gpu_train.py's large-activation net)
 """
 import argparse
 import os
@@ -29,7 +40,7 @@ sys.path.insert(0, REPO)
 from katacoffee_amd import train  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-S = 2.0 ** 12
+S = 2.0 ** 11
 
 
 def r16(t):
@@ -38,6 +49,22 @@ def r16(t):
 
 def r8(t):
     return t.clamp(-448, 448).to(torch.float32).to(torch.float8_e4m3fn).to(torch.float64)
+
+
+def r8n(t):
+    """e4m3 without the clamp (the scaled operands never exceed 448)."""
+    return t.to(torch.float32).to(torch.float8_e4m3fn).to(torch.float64)
+
+
+def f8exp(m):
+    """oracle/ora_nn.cpp f8Exp: s with m 2^-s in (224, 448]; 0 for m == 0."""
+    f, e = torch.frexp(m)
+    s = e - 9 + (f > 0.875).to(e.dtype)
+    return torch.where(m > 0, s, torch.zeros_like(s)).clamp(-100, 100).to(torch.float64)
+
+
+def e4m3s(v, s):
+    return r8n(v * torch.pow(2.0, -s)) * torch.pow(2.0, s)
 
 
 def quant_conv(x, w, scheme, conv):
@@ -55,13 +82,31 @@ def quant_conv(x, w, scheme, conv):
         return conv(xh, wh) + conv(xh, r16(wl)) + conv(r16(xl), wh)
     if scheme == "f8c":
         return conv(xh, wh) + conv(r8(x), r8(wl * S) / S) + conv(r8(xl * S) / S, r8(w))
+    if scheme == "f8cs":
+        sw = f8exp(w.abs().max())
+        HOT[0] = HOT[0] | (x.abs().flatten(1).max(1).values > 448)
+        return conv(xh, wh) + conv(r8(x), e4m3s(wl * S, sw) / S) + conv(r8(xl * S) / S, e4m3s(w, sw))
     if scheme == "f8cw":
         return conv(xh, wh) + conv(r8(x), r8(wl * S) / S)
     raise ValueError(scheme)
 
 
+HOT = [False]  # f8cs: boards with an activation past e4m3's range (re-evaluated exactly)
+
+
 def forward(net, binp, glob, schemes):
-    """train.CoffeeNet.forward in float64 with per-convolution operand rounding."""
+    """train.CoffeeNet.forward in float64 with per-convolution operand rounding (f8cs:
+    hot boards take the exact forward's outputs)."""
+    if "f8cs" in schemes:
+        HOT[0] = torch.zeros(len(binp), dtype=torch.bool)
+        out = forward_(net, binp, glob, schemes)
+        if HOT[0].any():
+            out[HOT[0]] = forward_(net, binp[HOT[0]], glob[HOT[0]], ["split3"] * len(schemes))
+        return out
+    return forward_(net, binp, glob, schemes)
+
+
+def forward_(net, binp, glob, schemes):
     it = iter(schemes)
     c3 = lambda x, w: F.conv2d(x, w, padding=1)
     c1 = lambda x, w: torch.einsum("nchw,oc->nohw", x, w)
@@ -96,8 +141,26 @@ def forward(net, binp, glob, schemes):
     return torch.cat([policy, vh @ P["vLin3"].t() + P["vB3"], vh @ P["vLinM"].t() + P["vBM"]], 1)
 
 
-def trained_net():
-    """The net of tests/test_gpu_train.py (same seeds)."""
+@torch.no_grad()
+def hot_net(net, batch, M):
+    """Scale block 0's BN2 by F so its conv2 reads activations up to M (trunk F times
+    larger from there), and the later blocks' BN1 and the tip BN by 1/F (weights untouched,
+    logits stay moderate).  Returns F.  (tests/test_gpu_train.py _hot_net: the same.)"""
+    b0 = net.blocks[0]
+    x = F.conv2d(batch["binp"], net.convInit, padding=1) + (batch["glob"] @ net.globInit.t())[:, :, None, None]
+    a = F.relu(x * b0.bn1s[:, None, None] + b0.bn1b[:, None, None])
+    a2 = F.relu(F.conv2d(a, b0.conv1, padding=1) * b0.bn2s[:, None, None] + b0.bn2b[:, None, None])
+    f = M / float(a2.max())
+    b0.bn2s.mul_(f)
+    b0.bn2b.mul_(f)
+    for b in net.blocks[1:]:
+        b.bn1s.div_(f)
+    net.tips.div_(f)
+    return f
+
+
+def trained_net(steps=10):
+    """The net of tests/test_gpu_train.py (same seeds; 10 steps there)."""
     sp = oracle.Selfplay(5, 5, 4, games=4, max_visits=24, node_cap=128, seed=33)
     sp.rounds(1500)
     rows = sp.rows()
@@ -105,7 +168,7 @@ def trained_net():
     torch.manual_seed(1)
     net = train.CoffeeNet("b6c96")
     opt = torch.optim.Adam(net.parameters(), lr=1e-3)
-    for _ in range(10):
+    for _ in range(steps):
         train.train_step(net, opt, batch)
     return net, batch
 
@@ -113,15 +176,27 @@ def trained_net():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--per-layer", action="store_true", help="f16 everywhere except one layer exact, and vice versa")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--big-act", type=float, default=0.0)
+    ap.add_argument("--hot", type=float, default=0.0)
     args = ap.parse_args()
-    net, batch = trained_net()
+    net, batch = trained_net(args.steps)
+    if args.big_act:
+        with torch.no_grad():
+            b = net.blocks[0]
+            b.bn2s.mul_(args.big_act)
+            b.bn2b.mul_(args.big_act)
+            b.conv2.div_(args.big_act)
+    if args.hot:
+        F_ = hot_net(net, batch, args.hot)
+        print("hot: block 0 BN2 x %.1f" % F_)
     binp = batch["binp"].to(torch.float64)
     glob = batch["glob"].to(torch.float64)
     nconv = 2 + 2 * len(net.blocks)
     with torch.no_grad():
         ref = forward(net, binp, glob, ["f32"] * nconv)
         print("n=%d max|logit| %.3f" % (len(ref), ref.abs().max().item()))
-        for sch in ("f16", "wsplit", "asplit", "f8cw", "f8c", "split3"):
+        for sch in ("f16", "wsplit", "asplit", "f8cw", "f8c", "f8cs", "split3"):
             out = forward(net, binp, glob, [sch] * nconv)
             e = (out - ref).abs()
             print("%-7s max err %.3e  (policy %.3e, value %.3e, misc %.3e)" % (
