@@ -87,7 +87,8 @@ def parse():
     ap.add_argument("--window", choices=["steady", "short"], default=None,
                     help="steady: warm-up past the first game ends, value = rows written/s; short: value = moves/s "
                          "(default: steady except C5)")
-    ap.add_argument("--precision", choices=["fast", "accurate", "fast-layered", "corrected"], default="fast")
+    ap.add_argument("--precision", choices=["fast", "default", "accurate", "fast-layered", "corrected"], default="fast",
+                    help="network precision of the headline window (default: the C ABI's default, the 1e-3 path)")
     # 16: a game whose search is done waits at most 15 rounds for its move, and every
     # group's round chain carries half the commit / row launches of 8 (C2: +2.4 %)
     ap.add_argument("--commit-interval", type=int, default=16)
@@ -115,7 +116,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
-    ap.add_argument("--cpu-curve-seconds", type=float, default=8.0,
+    ap.add_argument("--cpu-curve-seconds", type=float, default=0.0,
                     help="timed window of each point of the CPU thread-scaling curve (0: skip the curve)")
     ap.add_argument("--cpu-c1-seconds", type=float, default=20.0,
                     help="timed CPU-baseline window (C1 and single-thread runs)")
@@ -125,7 +126,7 @@ def parse():
                          "since the GPU box asks to stay within its CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compliant-line", dest="compliant_line", action="store_false",
-                    help="skip the second window at the 1e-3-compliant (corrected) precision")
+                    help="skip the second window at the 1e-3-compliant (default) precision")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP event timing")
     ap.add_argument("--timing-every", type=int, default=16,
                     help="time every N-th launch of each kernel group (an event pair costs a few us of stream gap)")
@@ -402,7 +403,8 @@ class Groups:
         out = {}
         for e in self.g:
             for k, v in e.stats().items():
-                out[k] = max(out.get(k, 0), v) if k in ("edge_pool_peak", "edge_pool_cap") else out.get(k, 0) + v
+                out[k] = (max(out.get(k, 0), v) if k in ("edge_pool_peak", "edge_pool_cap", "nn_precision")
+                          else out.get(k, 0) + v)
         return out
 
     def drain_rows(self):
@@ -552,6 +554,8 @@ def main():
         if not args.no_timing:
             sp.enable_timing(args.timing_every)
         s0 = sp.stats()
+        # the precision the engines run (the default one resolved by its calibration check)
+        precision = kc.PRECISION_NAMES.get(s0["nn_precision"], precision) if s0["nn_precision"] else precision
         base_ms = [sp.kernel_time(i) for i in range(4)]
         base_timed_evals = sp.timed_nn_evals()
         writer = None
@@ -724,6 +728,9 @@ def main():
                 "model_reloads": reloads,
                 "rows_written_npz_per_sec": (writer.rows / elapsed) if writer else None,
                 "npz_files": writer.files if writer else None,
+                # node-pool / edge-pool headroom of the run (the edge pool is sized
+                # by a heuristic; its peak use is reported beside its capacity)
+                "edge_pool": {"peak_entries": s1["edge_pool_peak"], "cap_entries": s1["edge_pool_cap"]},
                 "kernels": kernels,
                 "roofline": roof or None,
                 "roofline_all": roof_all,
@@ -740,14 +747,16 @@ def main():
         return None
 
     out = measure(args.precision, True)
-    if args.compliant_line and args.precision == "fast" and cfg["arch"] == "b6c96":
+    if args.compliant_line and args.precision == "fast":
         # the north-star tolerance (logits within 1e-3 of fp32 on any net, trained ones
-        # included) holds for the corrected precision, not for fp16 operands on a trained
-        # net: its window is measured here too and reported beside the headline
-        comp = measure("corrected", False)
+        # included) holds for the default precision (corrected or accurate: the engine's
+        # load-time calibration decides), not for fp16 operands on a trained net (DESIGN.md
+        # 3a): its window is measured here too and reported beside the headline
+        comp = measure("default", False)
         if rank == 0:
             out["compliant"] = {
-                "precision": "corrected", "dtype": comp["dtype"], "value": comp["value"], "unit": comp["unit"],
+                "precision": "default -> %s" % comp["config"]["precision"], "dtype": comp["dtype"],
+                "value": comp["value"], "unit": comp["unit"],
                 "value_kind": comp["value_kind"], "ms_per_step": comp["ms_per_step"],
                 "playouts_per_sec": comp["playouts_per_sec"], "rows_written_npz": comp["rows_written_npz"],
                 "tolerance": "logits within 1e-3 absolute of fp32 (tests/test_gpu_train.py, trained b6c96)",

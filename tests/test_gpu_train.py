@@ -175,3 +175,42 @@ def test_trained_net_runs_on_device_kernel():
     # section 5: 7e-3 measured on logits up to 6.4); bound asserted at 3e-3 of it.  The
     # absolute 1e-3 of north_star is met by the accurate path above.
     assert err <= 3e-3 * max(1.0, float(np.abs(ref).max()))
+
+
+@pytest.mark.parametrize("arch,X,Y,W,steps", [("b10c128", 5, 5, 4, 200), ("b10c128", 7, 7, 5, 60),
+                                              ("b18c384nbt", 9, 9, 5, 30)],
+                         ids=["b10c128-5x5", "b10c128-7x7", "b18c384nbt-9x9"])
+def test_layered_trained_net_within_north_star(arch, X, Y, W, steps):
+    """The C3-C5 nets on the layered kernels after training (the configs' compliant path:
+    the default precision, which runs the split kernels for these nets): within 1e-3
+    absolute of the torch fp32 model (eigenbackend.cpp semantics; model_pytorch.py
+    :678-958 for the nested bottleneck blocks).  Trained on the GPU, reference on the CPU."""
+    sp = oracle.Selfplay(X, Y, W, games=4, max_visits=16, node_cap=96, seed=5)
+    sp.rounds(1200 if X == 5 else 2500)
+    rows = sp.rows()
+    assert len(rows["globalTargetsNC"]) > 16
+    batch = train.rows_to_batch(rows, X, Y, device="cuda")
+    torch.manual_seed(2)
+    net = train.CoffeeNet(arch).cuda()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    for _ in range(steps):
+        train.train_step(net, opt, batch)
+    net = net.cpu()
+    cpu = {k: v.cpu() for k, v in batch.items()}
+    with torch.no_grad():
+        pol, val, misc = net(cpu["binp"], cpu["glob"])
+    ref = np.concatenate([pol.numpy(), val.numpy(), misc.numpy()], axis=1)
+    path = os.path.join(tempfile.mkdtemp(), "net.cfnn")
+    train.save_cfnn(net, path)
+    planes = cpu["binp"].numpy().reshape(len(ref), 15, X * Y)
+    h = kc.Network(path, X, Y, W, precision="default")
+    assert not h.fused and h.precision[0] == "accurate"
+    out = h.forward(_pack_u64(planes))
+    h.close()
+    f = kc.Network(path, X, Y, W, precision="fast")
+    out_f = f.forward(_pack_u64(planes))
+    f.close()
+    err, err_f = float(np.abs(out - ref).max()), float(np.abs(out_f - ref).max())
+    print("%s %dx%d after %d steps: max |logit| %.2f, default (split) vs fp32 %.3e, fast-layered %.3e" %
+          (arch, X, Y, steps, np.abs(ref).max(), err, err_f))
+    assert err <= 1e-3
