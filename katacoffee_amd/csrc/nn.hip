@@ -1838,9 +1838,18 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
       KC_HIP(hipMemsetAsync(hot_, 0, (size_t)grid * NN_SMALL_NB * 4, st));
       hotCap_ = grid * NN_SMALL_NB;
     }
+#ifdef KC_AB_NO_FALLBACK
+    launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>>(n, inWords, tabDevB_, in, out, st, countDev, rowIdx, e0, e1,
+                                                            hot_);
+#else
     launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_F8C, true>>(n, inWords, tabDevB_, in, out, st, countDev, rowIdx, e0,
                                                             fallback_ ? nullptr : e1, hot_);
+#endif
+#ifdef KC_AB_NO_FALLBACK  // A/B builds: the cost of the (empty) re-evaluation launch
+    if(false)
+#else
     if(fallback_)  // the accurate engine's split weights, this engine's flags
+#endif
       fallbackNet_->launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>>(
           n, inWords, fallbackNet_->tabDevB_, in, out, st, countDev, rowIdx, nullptr, e1, hot_);
   }
