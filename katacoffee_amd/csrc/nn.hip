@@ -50,10 +50,11 @@ enum { NN_MODE_F16 = 0, NN_MODE_SPLIT3 = 1, NN_MODE_F8C = 2 };
 // Corrected mode: w x = hi(w) hi(x) + lo(w) x + w lo(x) + lo(w) lo(x), with lo(v) = v - fp16(v)
 // (|lo(v)| <= 2^-11 |v|).  The first product runs on v_mfma_f32_16x16x32_f16; the two
 // cross terms (the last is below f32 rounding) on v_mfma_scale_f32_16x16x128_f8f6f4 with
-// e4m3 operands over two K-steps: A = [e4m3(lo(w) 2^(11-sw)) | e4m3(w 2^-sw)] with E8M0
-// scale 2^(sw-11), sw the convolution's block exponent (f8Exp of its largest |w|: the
+// e4m3 operands over two K-steps: A = [e4m3(lo(w) 2^(11-sw)) | e4m3(hi(w) 2^-sw)] with
+// E8M0 scale 2^(sw-11), sw the convolution's block exponent (f8Exp of its largest |w|: the
 // largest weight lands in (224, 448], so no weight saturates and small weights stay in
-// e4m3's normal range), B = [e4m3(x) | e4m3(lo(x) 2^11)] with scale 1.  Each cross term
+// e4m3's normal range), B = [e4m3(hi(x)) | e4m3(lo(x) 2^11)] with scale 1 (the e4m3 of
+// w and x is taken of their fp16 values, hi(v) = fp16(v), as oracle/ora_nn.cpp restates).  Each cross term
 // carries e4m3's 2^-4 relative error on a value 2^-11 below the product, so a product is
 // good to ~2^-14 (fp16 operands: 2^-10): tools/precision_study.py.  An activation past
 // e4m3's 448 (its conversion gives NaN) flags its board, and that board is re-evaluated by
@@ -86,6 +87,24 @@ constexpr float F8C_MAX = 448.0f;  // largest finite e4m3fn
 #endif
 #ifndef KC_F8C_LATE
 #define KC_F8C_LATE 0
+#endif
+// KC_F8C_CVTW 1: the weights' e4m3(hi(w) 2^-sw) is converted from the fp16 fragments in
+// registers (the ring slot holds fp16 hi + e4m3 lo(w): 27 KiB per 96-channel tap), 0: the
+// slot holds host-packed e4m3 [lo(w) | hi(w)] pairs (36 KiB).  KC_F8C_CVTX 1: e4m3(hi(x))
+// is converted from the activation fragments (the second plane holds e4m3 lo(x) only, one
+// byte per channel), 0: the plane holds [hi(x) | lo(x)] pairs.  Either conversion frees
+// the LDS for a 3-slot weight ring (both off: the 2-slot ring, the default).  Measured
+// (round 5, tools/ab_nn.sh, 960 boards): 2-slot 153 us; both converted 191-348 us
+// (register pressure: 72-96 spilled VGPRs under the cap), activations only 186 us,
+// weights only 331 us.  tools/cvt_rate.hip: one v_cvt_scalef32_pk_fp8_f16 costs 13.8
+// cycles per wave at 2 waves per SIMD (v_add_f32: 5.1) and each adds ~11 cycles to the
+// K-step's MFMA stream -- it does not co-issue beside the MFMAs, so the 8-20 conversions
+// per K-step cost more than the deeper ring and the smaller LDS footprint save.
+#ifndef KC_F8C_CVTW
+#define KC_F8C_CVTW 0
+#endif
+#ifndef KC_F8C_CVTX
+#define KC_F8C_CVTX 0
 #endif
 constexpr float F8C_SCALE = 2048.0f;  // 2^F8C_SHIFT
 // Block exponent of the corrected precision's e4m3 weights (oracle/ora_nn.cpp f8Exp, the
@@ -126,11 +145,16 @@ struct NNGeo {
   // k+2 is requested at the start of tap k, one barrier per tap.  4 (small-batch
   // instance): taps move in pairs (g, g+1), g even in the stream's global tap count;
   // pair j+1 is requested at the start of pair j and published by one barrier per pair.
-  // 2 (BL): chunks (one 36 KiB slot: a 96-channel tap, or 3 stem taps) alternate; chunk
-  // j+2 is requested right after the barrier that publishes chunk j+1 and frees chunk j.
-  // (6 slots, one barrier per 3 taps, would fill all 160 KiB and keep the other game
-  // group's search kernels off the CU while the network runs.)
-  static constexpr int RING = BL ? 2 : ((NB_ == NN_SMALL_NB && !SPLIT) ? 4 : 3);
+  // 2 (BL split): chunks (one 36 KiB slot: a 96-channel tap, or 3 stem taps) alternate;
+  // chunk j+2 is requested right after the barrier that publishes chunk j+1 and frees
+  // chunk j.  3 (BL corrected: 27 KiB slots, the e4m3 weights derived from the fp16
+  // fragments in registers): chunk j+3 is requested after that barrier, so a chunk's DMA
+  // has two chunks of MFMAs to land in.  (6 slots, one barrier per 3 taps, would fill all
+  // 160 KiB and keep the other game group's search kernels off the CU while the network
+  // runs.)
+  static constexpr bool F8W = MODE_ == NN_MODE_F8C && KC_F8C_CVTW;  // e4m3(w) converted in registers
+  static constexpr bool F8X = MODE_ == NN_MODE_F8C && KC_F8C_CVTX;  // e4m3(x) converted in registers
+  static constexpr int RING = BL ? ((F8W || F8X) ? 3 : 2) : ((NB_ == NN_SMALL_NB && !SPLIT) ? 4 : 3);
   static constexpr bool PAIRS = RING == 4;
   static constexpr int ROWS = NB * A;
   static constexpr int RT = (ROWS + 15) / 16;
@@ -153,8 +177,13 @@ struct NNGeo {
   static constexpr int NCT = C / 32;     // 16-col tiles per wave
   static constexpr int NCT_ALL = C / 16;
   static constexpr int P = 4 * A;
-  static constexpr int PLANE_BYTES = (PROWS * ROWB + 15) / 16 * 16;  // one plane (hi, or lo / e4m3 pairs)
-  static constexpr int ACT_BYTES = PLANES * PLANE_BYTES;
+  static constexpr int PLANE_BYTES = (PROWS * ROWB + 15) / 16 * 16;  // the hi plane
+  // the second plane: fp16 lo values (mode 1, rows like the hi plane); e4m3(lo(x) 2^11)
+  // (mode 2: one byte per channel, rows of ROWB / 2 bytes, so a lane's address there is
+  // half its hi-plane address; e4m3(x) is converted from the hi fragment in registers)
+  static constexpr int ROWB2 = F8X ? ROWB / 2 : ROWB;
+  static constexpr int PLANE2_BYTES = SPLIT ? (PROWS * ROWB2 + 15) / 16 * 16 : 0;
+  static constexpr int ACT_BYTES = PLANE_BYTES + PLANE2_BYTES;
   // f32 [MROWS][SCR] scratch for the g / value branches: aliases act (dead then)
   static constexpr int SCR = 36;  // f32 scratch row stride: 4-row lane groups hit distinct banks
   // (at least the gpool linear weights' [96][64] f32, staged below it)
@@ -162,8 +191,13 @@ struct NNGeo {
   static constexpr int OFF_POOL = ACT_BYTES;
   static constexpr int OFF_BIAS = OFF_POOL + 2 * NB * 96 * 4;
   static constexpr int WBUF = (C / 32) * NCT_ALL * 64;  // 16-B weight fragments per tap and plane
-  static constexpr int WSLOT = PLANES * WBUF;           // one ring slot
-  static constexpr int SLOT_PIECES = WSLOT / 64;        // its 1-KiB pieces
+  // a tap's second weight block: fp16 lo fragments (mode 1); e4m3(lo(w) 2^(11-sw)) only, 8 B
+  // per lane and fragment (mode 2: e4m3(w 2^-sw) is converted from the hi fragment)
+  static constexpr int WBUF2 = !SPLIT ? 0 : (F8W ? WBUF / 2 : WBUF);
+  static constexpr int WSLOT = WBUF + WBUF2;     // one ring slot (16-B units)
+  static constexpr int SLOT_PIECES = WSLOT / 64;  // its 1-KiB pieces
+  // 1-KiB pieces of one tap of a conv with ncb 32-channel input blocks
+  static constexpr int tapPieces(int ncb) { return ncb * NCT_ALL * (!SPLIT ? 2 : (F8W ? 3 : 4)) / 2; }
   // row tables (u16): rowPa[MROWS], rowBP[MROWS], bpRow[ROWS] -- built on the host
   static constexpr int NTAB = 2 * MROWS + ROWS;
   static constexpr int OFF_TAB = OFF_BIAS + NB * 64 * 4;
@@ -378,6 +412,8 @@ KC_D void convTiles(const uint16_t* __restrict__ act, const h16x8* __restrict__ 
 // ---- borderless (BL) instances ----------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h2x __attribute__((ext_vector_type(2)));
 
 // Per tile: the byte address of this lane's A-fragment row (row r = output row r, plus
 // the lane's k-quarter) and a 9-bit mask of the 3x3 taps whose neighbour is on the
@@ -408,46 +444,63 @@ KC_D void stageChunk(const h16x8* __restrict__ src, uint32_t slotAddr, int piece
 }
 
 // Implicit-GEMM convolution of a BL instance, computed transposed like convTiles.
-// Weights stream through the 2-slot ring in chunks of TPC taps (one slot: a 96-channel
-// tap, or three stem taps); chunk j of this conv lives in slot (PAR + j) & 1, PAR the
-// parity of the conv's first chunk in the whole stream.  On entry chunk 0 is resident and
-// published (the caller retired its DMA before the barrier that published the conv's
-// input) and chunk 1's slot is free: chunk 1 is requested at once (or, for a one-chunk
-// conv, the next conv's chunk 0).  One barrier per chunk, before the chunk's last K-step:
-// every wave retires its pieces of chunk j+1, the barrier publishes them and frees chunk
-// j's slot (all its fragment reads are complete: lgkmcnt(0)), and chunk j+2 is requested
-// into it (this conv's, or the next conv's chunk 0).  A-fragment addresses are formed per
-// tap: the neighbour row, or the zero row when the neighbour is off the board.
+// Weights stream through the RING-slot ring in chunks of TPC taps (one slot: a 96-channel
+// tap, or three stem taps); chunk j of this conv lives in slot (PAR + j) % RING, PAR the
+// index mod RING of the conv's first chunk in the whole stream.  On entry chunks
+// 0 .. RING-2 were requested and are resident and published (the caller retired its DMA
+// before the barrier that published the conv's input), and the slot of chunk RING-1 is
+// free: it is requested at once.  One barrier per chunk, before the chunk's last K-step:
+// every wave retires its pieces of chunk j+1 (the younger requests -- chunk j+2 with three
+// slots -- stay in flight: a counted vmcnt), the barrier publishes them and frees chunk j's
+// slot (all its fragment reads are complete: lgkmcnt(0)), and chunk j+RING is requested
+// into it (this conv's, or the next conv's chunk j+RING-NCH: nextPieces pieces each,
+// nextNCH chunks).  A-fragment addresses are formed per tap: the neighbour row, or the
+// zero row when the neighbour is off the board.
 //   MODE 1: acc += hi(w) hi(x) + lo(w) hi(x) + hi(w) lo(x)  (three f16 MFMAs per step)
 //   MODE 2: acc += hi(w) hi(x) per step (f16 MFMA), and per pair of steps one scaled e4m3
-//           MFMA over [lo(w) 2^11 | w] x [x | lo(x) 2^11] of both steps, scale 2^-11
-//   sA (mode 2): the A operand's E8M0 scale, 127 - 11 + the conv's weight exponent sw.
-template <class G, int NTAPS, int NCB, int PAR>
+//           MFMA over [lo(w) 2^(11-sw) | hi(w) 2^-sw] x [hi(x) | lo(x) 2^11] of both steps,
+//           A scale 2^(sw-11): lo(w) and lo(x) are read from the second weight block /
+//           activation plane (8 bytes per lane and fragment), e4m3 of the hi fragments
+//           is converted in registers (v_cvt_scalef32_pk_fp8_f16, which divides by its
+//           scale: 2^sw for the weights, 1 for the activations).
+//   sA (mode 2): the A operand's E8M0 scale byte, 127 - 11 + the conv's weight exponent sw.
+// DBG (tools/convb_bench.hip ablations only): bit 0 skips the weight requests, bit 1 the
+// chunk waits and barriers, bit 2 the scaled e4m3 MFMAs, bit 3 the second-plane fragment
+// reads, bit 4 every fragment read after the first K-step, bit 5 the chunk waits only.
+template <class G, int NTAPS, int NCB, int PAR, int DBG = 0>
 KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__ w, h16x8* __restrict__ wl,
                      f32x4 (&acc)[G::MAXT][G::NCT], const int (&rb)[G::MAXT], const uint32_t (&vm)[G::MAXT],
-                     int cg, int lane, int tid, const h16x8* __restrict__ wNext, int nextPieces, int sA = 0) {
-  constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap and plane
-  constexpr int CH = CHP * G::PLANES;    // per tap
+                     int cg, int lane, int tid, const h16x8* __restrict__ wNext, int nextPieces, int nextNCH,
+                     int sA = 0) {
+  constexpr int CHP = NCB * G::NCT_ALL;  // 1-KiB pieces per tap of the hi block
+  constexpr int CH = G::tapPieces(NCB);  // per tap
   constexpr int TPC = G::SLOT_PIECES / CH >= 1 ? G::SLOT_PIECES / CH : 1;
   static_assert(TPC * CH <= G::SLOT_PIECES, "a tap must fit one ring slot");
   constexpr int NCH = (NTAPS + TPC - 1) / TPC;
   constexpr int STEPS = NTAPS * NCB;
+  constexpr int R = G::RING;
+  constexpr bool F8C = G::MODE == NN_MODE_F8C;
+  // fewest pieces any wave issues for a chunk of the next conv (a 64-channel tap: 2 blocks)
+  constexpr int NEXT_MIN = G::tapPieces(2) / G::NW;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t ring = ldsAddr(wl);
-  auto slotAddr = [&](int j) { return ring + (uint32_t)(((PAR + j) & 1) * G::WSLOT * 16); };
+  auto slotOf = [&](int j) { return (PAR + j) % R; };
   auto chunkPieces = [&](int j) { return (NTAPS - j * TPC < TPC ? NTAPS - j * TPC : TPC) * CH; };
-  // the request of stream chunk j of this conv (j >= NCH: the next conv's chunk 0)
+  // the request of stream chunk j of this conv (j >= NCH: the next conv's chunk j - NCH)
   auto request = [&](int j) {
+    if(DBG & 1)
+      return;
+    const uint32_t dst = ring + (uint32_t)(slotOf(j) * G::WSLOT * 16);
     if(j < NCH)
-      stageChunk<G::NW>(w + (size_t)j * TPC * CH * 64, slotAddr(j), chunkPieces(j), wave, lane);
-    else if(j == NCH && nextPieces > 0)
-      stageChunk<G::NW>(wNext, slotAddr(j), nextPieces, wave, lane);
+      stageChunk<G::NW>(w + (size_t)j * TPC * CH * 64, dst, chunkPieces(j), wave, lane);
+    else if(j - NCH < nextNCH && nextPieces > 0)
+      stageChunk<G::NW>(wNext + (size_t)(j - NCH) * nextPieces * 64, dst, nextPieces, wave, lane);
   };
-  request(1);
+  request(R - 1);
   const char* actB = reinterpret_cast<const char*>(act);
   const int zb = G::ZROW * G::ROWB + 16 * (lane >> 4);
   const h16x8* wlane = wl + (cg * G::NCT) * 64 + lane;
-  int at[G::MAXT];  // this tap's A-fragment row addresses
+  int at[G::MAXT];  // this tap's A-fragment row addresses (hi plane; mode 2's plane: half)
   auto tapAddr = [&](int tap) {
     const int tb = NTAPS == 9 ? tap : 4;  // 1x1: the centre tap
     const int off = ((tb / 3 - 1) * G::X + (tb % 3 - 1)) * G::ROWB;
@@ -456,39 +509,85 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
       at[t] = ((vm[t] >> tb) & 1u) ? rb[t] + off : zb;
   };
   h16x8 af[2][G::MAXT], bf[2][G::NCT];
-  // second planes: fp16 lo fragments, double buffered (mode 1); e4m3 pairs (mode 2), the
-  // two steps of an MFMA pair in the low / high half of one 8-register operand, so the
-  // scaled MFMA reads its operands in place (the halves are the double buffer)
+  // second planes: fp16 lo fragments, double buffered (mode 1); e4m3 (mode 2), the two
+  // steps of an MFMA pair in the low / high half of one 8-register operand, so the scaled
+  // MFMA reads its operands in place (the halves are the double buffer): per step
+  // bq = [lo(w) (loaded) | hi(w) (converted)], aq = [hi(x) (converted) | lo(x) (loaded)]
   h16x8 afl[G::MODE == NN_MODE_SPLIT3 ? 2 : 1][G::MAXT], bfl[G::MODE == NN_MODE_SPLIT3 ? 2 : 1][G::NCT];
   i32x8 aq[G::MAXT], bq[G::NCT];
+  // 2^sw: the weights' conversion scale (the conversion divides by it)
+  const float wScale = __builtin_bit_cast(float, (uint32_t)(sA - 127 + F8C_SHIFT + 127) << 23);
   auto loadStep = [&](int st, int buf) {
     const int tap = st / NCB, cb = st - tap * NCB;
     const int chunk = tap / TPC, tc = tap - chunk * TPC;
-    const h16x8* wb = wlane + ((PAR + chunk) & 1) * G::WSLOT + tc * CH * 64 + cb * G::NCT_ALL * 64;
+    const int slot = slotOf(chunk);
+    const h16x8* wb = wlane + slot * G::WSLOT + tc * CH * 64 + cb * G::NCT_ALL * 64;
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++) {
       bf[buf][ct] = wb[ct * 64];
-      if constexpr(G::MODE == NN_MODE_SPLIT3) {
+      if constexpr(DBG & 8) {
+      } else if constexpr(G::MODE == NN_MODE_SPLIT3) {
         bfl[buf][ct] = wb[CHP * 64 + ct * 64];
-      } else {
-        const i32x4 v = __builtin_bit_cast(i32x4, wb[CHP * 64 + ct * 64]);
+      } else if constexpr(!G::F8W) {
+        const i32x4 v = __builtin_bit_cast(i32x4, wb[CHP * 64 + ct * 64]);  // [lo(w) | w] pairs
         if(buf)
           bq[ct].hi = v;
         else
           bq[ct].lo = v;
+      } else {
+        // this lane's 8 bytes of the fragment in the tap's e4m3 block (512 B per fragment)
+        const int frag = cb * G::NCT_ALL + cg * G::NCT + ct;
+        const int2 v = *reinterpret_cast<const int2*>(reinterpret_cast<const char*>(wl) +
+                                                      (size_t)(slot * G::WSLOT + tc * CH * 64) * 16 + CHP * 1024 +
+                                                      frag * 512 + lane * 8);
+        bq[ct][4 * buf] = v.x;
+        bq[ct][4 * buf + 1] = v.y;
       }
     }
 #pragma unroll
     for(int t = 0; t < G::MAXT; t++) {
       af[buf][t] = *reinterpret_cast<const h16x8*>(actB + at[t] + cb * 64);
-      const h16x8 v = *reinterpret_cast<const h16x8*>(actB + G::PLANE_BYTES + at[t] + cb * 64);
-      if constexpr(G::MODE == NN_MODE_SPLIT3) {
-        afl[buf][t] = v;
-      } else {
+      if constexpr(DBG & 8) {
+      } else if constexpr(G::MODE == NN_MODE_SPLIT3) {
+        afl[buf][t] = *reinterpret_cast<const h16x8*>(actB + G::PLANE_BYTES + at[t] + cb * 64);
+      } else if constexpr(!G::F8X) {
+        const i32x4 v = __builtin_bit_cast(i32x4, *reinterpret_cast<const h16x8*>(actB + G::PLANE_BYTES + at[t] + cb * 64));
         if(buf)
-          aq[t].hi = __builtin_bit_cast(i32x4, v);
+          aq[t].hi = v;
         else
-          aq[t].lo = __builtin_bit_cast(i32x4, v);
+          aq[t].lo = v;
+      } else {
+        const int2 v = *reinterpret_cast<const int2*>(actB + G::PLANE_BYTES + (at[t] >> 1) + cb * 32);
+        aq[t][4 * buf + 2] = v.x;
+        aq[t][4 * buf + 3] = v.y;
+      }
+    }
+  };
+  // mode 2: e4m3 of a step's hi fragments (8 fp16 values -> 8 bytes in two registers)
+  auto e4m3x8 = [](const h16x8& h, float scale, int oldA, int oldB) {
+    // (both halves of each register are written: the old contents only save a zeroing move)
+    s16x2 a = __builtin_bit_cast(s16x2, oldA), b = __builtin_bit_cast(s16x2, oldB);
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(a, h2x{h[0], h[1]}, scale, false);
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(a, h2x{h[2], h[3]}, scale, true);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(b, h2x{h[4], h[5]}, scale, false);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(b, h2x{h[6], h[7]}, scale, true);
+    return int2{__builtin_bit_cast(int, a), __builtin_bit_cast(int, b)};
+  };
+  auto convertStep = [&](int buf) {
+    if constexpr(G::F8W) {
+#pragma unroll
+      for(int ct = 0; ct < G::NCT; ct++) {
+        const int2 v = e4m3x8(bf[buf][ct], wScale, bq[ct][4 * buf + 2], bq[ct][4 * buf + 3]);
+        bq[ct][4 * buf + 2] = v.x;
+        bq[ct][4 * buf + 3] = v.y;
+      }
+    }
+    if constexpr(G::F8X) {
+#pragma unroll
+      for(int t = 0; t < G::MAXT; t++) {
+        const int2 v = e4m3x8(af[buf][t], 1.0f, aq[t][4 * buf], aq[t][4 * buf + 1]);
+        aq[t][4 * buf] = v.x;
+        aq[t][4 * buf + 1] = v.y;
       }
     }
   };
@@ -508,18 +607,37 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
     const int tap = st / NCB, cb = st - tap * NCB;
     const int chunk = tap / TPC;
     const bool chunkEnd = cb == NCB - 1 && (tap == NTAPS - 1 || (tap + 1) % TPC == 0);
-    if(chunkEnd && chunk + 1 < NCH) {
-      // retire this wave's pieces of chunk+1, publish them, free chunk's slot, request chunk+2
-      waitVm<0>();
+    if(chunkEnd && chunk + 1 < NCH && !(DBG & 2)) {
+      // retire this wave's pieces of chunk+1 (with three slots chunk+2's requests, at
+      // least NW2 per wave, may stay in flight), publish them, free chunk's slot, request
+      // chunk+R
+      if constexpr(DBG & 32) {
+      } else if constexpr(R == 3) {
+        // (chunk is a constant after unrolling: one branch remains; the next conv's chunk
+        // exists unless nextPieces / nextNCH say otherwise -- then nothing younger is in
+        // flight and every request must be retired)
+        static_assert(NTAPS % TPC == 0, "three-slot ring: whole chunks");
+        if(chunk + 2 < NCH)
+          waitVm<TPC * CH / G::NW>();
+        else if(nextPieces > 0 && chunk + 2 - NCH < nextNCH)
+          waitVm<NEXT_MIN>();
+        else
+          waitVm<0>();
+      } else {
+        waitVm<0>();
+      }
       barrierKeepDma();
-      request(chunk + 2);
+      request(chunk + R);
     }
-    if constexpr(G::MODE == NN_MODE_F8C) {
-      if(st & 1)
+    if constexpr(F8C) {
+      convertStep(st & 1);  // this step's fragments were read in the previous iteration
+      if((st & 1) && !(DBG & 4))
         f8pair();  // steps st - 1 (low halves) and st (high halves)
     }
-    constexpr bool LATE = G::MODE == NN_MODE_F8C && KC_F8C_LATE;
-    if(!LATE && st + 1 < STEPS) {
+    if(chunkEnd && chunk + 1 < NCH && (DBG & 2) && !(DBG & 1))
+      request(chunk + R);  // ablation: the requests without their waits / barriers
+    constexpr bool LATE = F8C && KC_F8C_LATE;
+    if(!LATE && st + 1 < STEPS && !(DBG & 16)) {
       if(cb == NCB - 1)
         tapAddr(tap + 1);
       loadStep(st + 1, (st + 1) & 1);
@@ -552,8 +670,8 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
         tapAddr(tap + 1);
       loadStep(st + 1, (st + 1) & 1);
     }
-    if constexpr(G::MODE == NN_MODE_F8C) {
-      if(st == STEPS - 1 && !(st & 1)) {
+    if constexpr(F8C) {
+      if(st == STEPS - 1 && !(st & 1) && !(DBG & 4)) {
         // an odd step count: the last step pairs with zeros (stale weights x 0)
 #pragma unroll
         for(int t = 0; t < G::MAXT; t++)
@@ -673,8 +791,8 @@ KC_D void flagHot(int* hot, int base, int nb, int tstart, int lane, const float 
   }
 }
 // Four activated channels of one row into act: the hi plane, and the second plane --
-// fp16 lo (mode 1), or e4m3 x and e4m3 lo(x) 2^11 (mode 2: the channel octet's 16 bytes
-// are [x of its 8 channels | lo(x) 2^11 of its 8 channels]).
+// fp16 lo (mode 1), or e4m3(lo(x) 2^11), one byte per channel (mode 2; e4m3(x) is
+// converted from the hi plane's fp16 value inside the convolution).
 template <class G>
 KC_D void storeAct4(uint16_t* act, int row, int ch, float y0, float y1, float y2, float y3) {
   *reinterpret_cast<uint2*>(act + row * G::ASTR + ch) = packH4(y0, y1, y2, y3);
@@ -682,18 +800,27 @@ KC_D void storeAct4(uint16_t* act, int row, int ch, float y0, float y1, float y2
     *reinterpret_cast<uint2*>(act + G::PLANE_BYTES / 2 + row * G::ASTR + ch) = packH4lo(y0, y1, y2, y3);
   if constexpr(G::MODE == NN_MODE_F8C) {
     auto lo = [](float x) { return (x - (float)(_Float16)x) * F8C_SCALE; };
-    char* q = reinterpret_cast<char*>(act) + G::PLANE_BYTES + row * G::ROWB + (ch >> 3) * 16 + (ch & 7);
-    *reinterpret_cast<int*>(q) = e4m3x2<true>(y2, y3, e4m3x2<false>(y0, y1, 0));
-    *reinterpret_cast<int*>(q + 8) = e4m3x2<true>(lo(y2), lo(y3), e4m3x2<false>(lo(y0), lo(y1), 0));
+    if constexpr(G::F8X) {
+      *reinterpret_cast<int*>(reinterpret_cast<char*>(act) + G::PLANE_BYTES + row * G::ROWB2 + ch) =
+          e4m3x2<true>(lo(y2), lo(y3), e4m3x2<false>(lo(y0), lo(y1), 0));
+    } else {
+      // the channel octet's 16 bytes: [hi(x) of its 8 channels | lo(x) 2^11 of its 8 channels]
+      auto hi = [](float x) { return (float)(_Float16)x; };
+      char* q = reinterpret_cast<char*>(act) + G::PLANE_BYTES + row * G::ROWB + (ch >> 3) * 16 + (ch & 7);
+      *reinterpret_cast<int*>(q) = e4m3x2<true>(hi(y2), hi(y3), e4m3x2<false>(hi(y0), hi(y1), 0));
+      *reinterpret_cast<int*>(q + 8) = e4m3x2<true>(lo(y2), lo(y3), e4m3x2<false>(lo(y0), lo(y1), 0));
+    }
   }
 }
 // BL: zero the shared zero row in every plane (after act was used as f32 scratch).
 template <class G>
 KC_D void zeroRowBL(uint16_t* act, int tid) {
-  constexpr int N = G::ROWB / 16;
-  for(int i = tid; i < G::PLANES * N; i += G::NT)
-    reinterpret_cast<uint4*>(reinterpret_cast<char*>(act) + (i / N) * G::PLANE_BYTES + G::ZROW * G::ROWB)[i % N] =
-        uint4{0u, 0u, 0u, 0u};
+  constexpr int N = G::ROWB / 16, N2 = G::SPLIT ? G::ROWB2 / 16 : 0;
+  char* a = reinterpret_cast<char*>(act);
+  if(tid < N)
+    reinterpret_cast<uint4*>(a + G::ZROW * G::ROWB)[tid] = uint4{0u, 0u, 0u, 0u};
+  else if(tid < N + N2)
+    reinterpret_cast<uint4*>(a + G::PLANE_BYTES + G::ZROW * G::ROWB2)[tid - N] = uint4{0u, 0u, 0u, 0u};
 }
 
 // act[pad(row)][ch..ch+3] = f16(relu(v * s[ch] + b[ch])) for on-board rows, all channels.
@@ -955,11 +1082,13 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
   // the stem's first weight taps (as many as the ring prefetches) stream into the ring
   // while the input is unpacked
   {
-    constexpr int CH0 = G::NCT_ALL * G::PLANES;  // 1-KiB pieces per stem tap (one 32-channel block)
+    constexpr int CH0 = G::tapPieces(1);  // 1-KiB pieces per stem tap (one 32-channel block)
     const uint32_t ring = ldsAddr(wl);
     if constexpr(G::BL) {
-      // the stem's chunk 0 (taps 0-2) into slot 0
-      stageChunk<G::NW>(WB + L->wInit, ring, 3 * CH0, wave, lane);
+      // the stem's chunks 0 .. RING-2 (3 taps each) into slots 0 .. RING-2
+#pragma unroll
+      for(int j = 0; j + 1 < G::RING; j++)
+        stageChunk<G::NW>(WB + L->wInit + (size_t)j * 3 * CH0 * 64, ring + j * G::WSLOT * 16, 3 * CH0, wave, lane);
     } else {
 #pragma unroll
       for(int tap = 0; tap < 2; tap++)
@@ -995,8 +1124,8 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
         if(i < NBITS && ((words[k] >> lane) & 1ULL)) {
           const int c = i / G::A, p = i - c * G::A;
           const int row = G::BL ? b * G::A + p : padCell<G>(b, p);
-          act[row * G::ASTR + c] = (uint16_t)0x3c00;  // 1.0
-          if constexpr(G::MODE == NN_MODE_F8C)  // e4m3 1.0 (its lo is 0)
+          act[row * G::ASTR + c] = (uint16_t)0x3c00;  // 1.0 (its lo planes stay 0)
+          if constexpr(G::MODE == NN_MODE_F8C && !G::F8X)  // e4m3 1.0 in the pair plane
             reinterpret_cast<uint8_t*>(act)[G::PLANE_BYTES + row * G::ROWB + (c >> 3) * 16 + (c & 7)] = 0x38;
         }
       }
@@ -1020,7 +1149,8 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
   zeroAcc<G>(acc);
   if constexpr(G::BL)
     convTilesB<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, rb, vm, cg, lane, tid,
-                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96, L->sInit);
+                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96, L->nblocks > 0 ? 9 : 1,
+                           L->sInit);
   else
     convTiles<G, 9, 1, 0, 0, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                                     L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
@@ -1067,9 +1197,11 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       pre[j] = loadParam(L, WF, blk + 1, tid + j * G::NT);  // next slab: its latency hides behind conv1
     NN_PHASE(4 + 4 * blk);
     if constexpr(G::BL)
-      // chunk parity: stem 3 chunks, each block's convs 9 + 9 (a 64-channel tap is one chunk too)
-      convTilesB<G, 9, G::C / 32, 1>(act, WB + L->wConv1[blk], wl, acc, rb, vm, cg, lane, tid, WB + L->wConv2[blk],
-                                     (L->kinds[blk] == 0 ? 3 : 2) * G::NCT_ALL * G::PLANES, L->sConv1[blk]);
+      // first chunk mod RING: stem 3 chunks, each block's convs 9 + 9 (a 64-channel tap is one
+      // chunk too), so conv1 starts at 3 + 18 blk (1 mod 2, 0 mod 3) and conv2 at 12 + 18 blk (0)
+      convTilesB<G, 9, G::C / 32, G::RING == 2 ? 1 : 0>(act, WB + L->wConv1[blk], wl, acc, rb, vm, cg, lane, tid,
+                                                       WB + L->wConv2[blk],
+                                                       G::tapPieces(L->kinds[blk] == 0 ? 3 : 2), 9, L->sConv1[blk]);
     else
       convTiles<G, 9, G::C / 32, 1, 0, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid,
                                               WB + L->wConv2[blk],
@@ -1098,7 +1230,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
         convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW, CHUNK96,
-                                       L->sConv2[blk]);
+                                       nextTaps, L->sConv2[blk]);
       else
         convTiles<G, 9, G::C / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                 3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1199,7 +1331,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
         convTilesB<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW,
-                                              CHUNK96, L->sConv2[blk]);
+                                              CHUNK96, nextTaps, L->sConv2[blk]);
       else
         convTiles<G, 9, (G::C - 32) / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                        3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1217,7 +1349,8 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
   // ---- heads: one 1x1 conv C -> [p1 | g1 | v1] ----
   zeroAcc<G>(acc);
   if constexpr(G::BL)
-    convTilesB<G, 1, G::C / 32, 1>(act, WB + L->wHead, wl, acc, rb, vm, cg, lane, tid, nullptr, 0, L->sHead);
+    convTilesB<G, 1, G::C / 32, G::RING == 2 ? 1 : 0>(act, WB + L->wHead, wl, acc, rb, vm, cg, lane, tid, nullptr, 0,
+                                                      0, L->sHead);
   else
     convTiles<G, 1, G::C / 32, 1, 0, false>(act, WB + L->wHead, wl, acc, ab, cg, lane, tid, nullptr, 0, 0,
                                             9 + 18 * L->nblocks);
@@ -1429,10 +1562,10 @@ static uint8_t f2e4m3(float f) {
 }
 
 // mode 1: after each tap's hi fragments the same fragments of lo = fp16(w - hi);
-// mode 2: after them the e4m3 pairs [lo(w) 2^(11-sw) of the fragment's 8 k | w 2^-sw of the
-// same 8 k], sw the conv's block exponent (f8Exp of its largest |w|), and *sA = the A
-// operand's E8M0 scale byte, 127 - 11 + sw
-// (convTiles' / convTilesB's SPLIT ring slot layout).
+// mode 2: after them e4m3(lo(w) 2^(11-sw)) of each fragment's 8 k, 8 bytes per lane (512 B
+// per fragment; e4m3(hi(w) 2^-sw) is converted from the hi fragment on the device), sw the
+// conv's block exponent (f8Exp of its largest |w|), and *sA = the A operand's E8M0 scale
+// byte, 127 - 11 + sw (convTiles' / convTilesB's SPLIT ring slot layout).
 static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout,
                      const std::function<float(int, int, int)>& W, int mode = NN_MODE_F16, int* sA = nullptr) {
   const int ncb = cinPad / 32, nct = cout / 16;
@@ -1460,11 +1593,17 @@ static void packConv(std::vector<uint16_t>& dst, int ntaps, int cinPad, int cout
                 const uint16_t hi = f2h(w[j]);
                 dst.push_back(part == 0 ? hi : f2h(w[j] - h2f(hi)));
               }
+            } else if(KC_F8C_CVTW) {
+              uint8_t b[8];
+              for(int j = 0; j < 8; j++)
+                b[j] = f2e4m3(ldexpf((w[j] - h2f(f2h(w[j]))) * F8C_SCALE, -sw));
+              for(int j = 0; j < 4; j++)
+                dst.push_back((uint16_t)(b[2 * j] | (b[2 * j + 1] << 8)));
             } else {
               uint8_t b[16];
               for(int j = 0; j < 8; j++) {
                 b[j] = f2e4m3(ldexpf((w[j] - h2f(f2h(w[j]))) * F8C_SCALE, -sw));
-                b[8 + j] = f2e4m3(ldexpf(w[j], -sw));
+                b[8 + j] = f2e4m3(ldexpf(h2f(f2h(w[j])), -sw));
               }
               for(int j = 0; j < 8; j++)
                 dst.push_back((uint16_t)(b[2 * j] | (b[2 * j + 1] << 8)));

@@ -17,8 +17,9 @@
 // mode 1 rounds every convolution weight and convolution input to fp16 (RNE),
 // exactly where the HIP kernels do; residual trunks stay f32 as in the kernels.
 // mode 2 restates the "corrected" precision (csrc/nn.hip NN_MODE_F8C): each product is
-//   fp16(w) fp16(x) + E(lo(w) 2^11, sw) e4m3(x) / 2^11 + E(w, sw) e4m3(lo(x) 2^11) / 2^11,
+//   fp16(w) fp16(x) + E(lo(w) 2^11, sw) e4m3(fp16(x)) / 2^11 + E(fp16(w), sw) e4m3(lo(x) 2^11) / 2^11,
 // lo(v) = v - fp16(v), e4m3 = OCP e4m3fn, round to nearest even, E(v, s) = e4m3(v 2^-s) 2^s
+// (the device converts e4m3(w) and e4m3(x) from the fp16 fragments in registers)
 // with sw the convolution's block exponent (the E8M0 scale operand of the block-scaled
 // MFMA; f8Exp: its largest |weight| lands in (224, 448]).  A board with a convolution input
 // past e4m3's 448 is "hot": the device re-evaluates it on the accurate (split) instance,
@@ -184,7 +185,7 @@ void PackedConv::pack() {
           B16[k * cout + co] = f16r(v);
           BC[k * cout + co] = f16r(v);
           BC[(K + k) * cout + co] = e4m3s((v - f16r(v)) * F8C_SCALE, sw) / F8C_SCALE;
-          BC[(2 * K + k) * cout + co] = e4m3s(v, sw);
+          BC[(2 * K + k) * cout + co] = e4m3s(f16r(v), sw);
         }
   }
   packB(B.data(), K, cout, p32);
@@ -233,7 +234,7 @@ void convApply(const NNBatch& b, const PackedConv& cv, const float* in, float* o
               for(int c = 0; c < cv.cin; c++) {
                 const float h = f16r(src[c]);
                 dst[c] = h;
-                dst[K + c] = e4m3r(src[c]);
+                dst[K + c] = e4m3r(h);
                 dst[2 * K + c] = e4m3r((src[c] - h) * F8C_SCALE) / F8C_SCALE;
               }
             } else if(fp16 && (emu & 2)) {

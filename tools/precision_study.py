@@ -15,8 +15,9 @@ last = head 1x1):
   f8cw     hi*hi + e4m3(lo(w)*S)/S * e4m3(x) (weights corrected only)
   f8cs     the shipped corrected kernel (round 5): f8c with the weights' e4m3 at the
            convolution's block exponent (largest weight in (224, 448], oracle/ora_nn.cpp
-           f8Exp) and boards whose activations pass e4m3's 448 re-evaluated exactly
-           (the device: on the split instance)
+           f8Exp), e4m3(w) and e4m3(x) converted from the fp16 values (the device converts
+           the fp16 fragments in registers), and boards whose activations pass e4m3's 448
+           re-evaluated exactly (the device: on the split instance)
 Usage: python tools/precision_study.py [--per-layer] [--steps N] [--big-act F]
   --steps N     Adam steps of the trained net (10: the test_gpu_train.py net)
   --big-act F   scale the first block's BN2 by F and its conv2 by 1/F (same function,
@@ -85,7 +86,7 @@ def quant_conv(x, w, scheme, conv):
     if scheme == "f8cs":
         sw = f8exp(w.abs().max())
         HOT[0] = HOT[0] | (x.abs().flatten(1).max(1).values > 448)
-        return conv(xh, wh) + conv(r8(x), e4m3s(wl * S, sw) / S) + conv(r8(xl * S) / S, e4m3s(w, sw))
+        return conv(xh, wh) + conv(r8(xh), e4m3s(wl * S, sw) / S) + conv(r8(xl * S) / S, e4m3s(wh, sw))
     if scheme == "f8cw":
         return conv(xh, wh) + conv(r8(x), r8(wl * S) / S)
     raise ValueError(scheme)
