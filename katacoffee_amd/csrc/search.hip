@@ -3583,11 +3583,6 @@ static int laneItems(int P) { return P <= 128 ? 2 : (P <= 256 ? 4 : 7); }
 // row packs the row's six arrays into one contiguous record (rows.py FIELDS: bin u8
 // [15][pb], glob f32, pol i16 [2][P], gt f32 [64], val i8 [5][A], meta i32 [4]), so a
 // rank's rows leave as one device block for the RCCL gather.
-int rowBytes(int A) {
-  const int pb = (A + 7) / 8;
-  return NUM_SPATIAL * pb + 4 + 2 * 4 * A * 2 + 64 * 4 + 5 * A + 16;
-}
-
 __global__ void __launch_bounds__(256) kStageRows(const SearchDev* __restrict__ dp, uint8_t* __restrict__ dst,
                                                   int rb) {
   const SearchDev& d = *dp;
@@ -3671,12 +3666,6 @@ void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEv
     default: launchEv(kBackup<7>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
   }
   KC_HIP(hipGetLastError());
-}
-
-size_t commitLdsBytes(int cap) {
-  size_t b = (size_t)MAX_P * 4 * 4 + 16;
-  b += (size_t)(cap / 32) * 4 + (size_t)cap * 2;
-  return (b + 15) / 16 * 16;
 }
 
 void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st) {

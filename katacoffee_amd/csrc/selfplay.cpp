@@ -74,6 +74,19 @@ SP toSP(const coffee_search_params& p) {
   return s;
 }
 
+// Bytes of one staged row (kStageRows; rows.py FIELDS): bin, glob, pol, gtgt, value, meta.
+int rowBytes(int A) {
+  const int pb = (A + 7) / 8;
+  return NUM_SPATIAL * pb + 4 + 2 * 4 * A * 2 + 64 * 4 + 5 * A + 16;
+}
+
+// Dynamic LDS of the commit kernel (kCommit's policy scratch, live-node bits and BFS queue).
+size_t commitLdsBytes(int cap) {
+  size_t b = (size_t)MAX_P * 4 * 4 + 16;
+  b += (size_t)(cap / 32) * 4 + (size_t)cap * 2;
+  return (b + 15) / 16 * 16;
+}
+
 template <class T>
 static T* devAlloc(std::vector<void*>& owned, size_t count, bool zero = true) {
   void* p = nullptr;

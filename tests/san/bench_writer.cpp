@@ -1,11 +1,14 @@
 // bench.py's host threading restated in C++ for ThreadSanitizer (tests/test_sanitizers.py):
 // the main thread steps K engine groups in interleaved chunks (bench.py Groups.step),
-// drains their rows after every step and hands each step's block to a writer thread
-// through a queue; the writer writes <dir>/rows%06d.npz via a .tmp file and rename
+// collects their rows after every step -- drained to host buffers, or (stage mode, the
+// bench's multi-GPU path) staged on the "device" by coffee_selfplay_stage_rows and copied
+// back once the engine stream has passed it -- and hands each step's block to a writer
+// thread through a queue; the writer writes <dir>/rows%06d.npz via a .tmp file and rename
 // (bench.py NpzWriter, trainingwrite.cpp:566-587 / :765-769) while the engines keep
 // stepping; close() sends the sentinel and joins before the clock would stop.  Linked
-// with fake_engine.cpp (the C ABI without a GPU) and the product's npzwrite.cpp.
-//   bench_writer <dir> [groups] [steps]
+// with the product's host code (capi.cpp, selfplay.cpp, npzwrite.cpp, ...) over
+// fake_device.cpp (host memory for the GPU, stand-in kernels).
+//   bench_writer <dir> [groups] [steps] [stage]
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -13,6 +16,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/katacoffee.h"
@@ -84,34 +88,68 @@ int main(int argc, char** argv) {
     return 2;
   const std::string dir = argv[1];
   const int groups = argc > 2 ? atoi(argv[2]) : 2, steps = argc > 3 ? atoi(argv[3]) : 40;
+  const bool stage = argc > 4 && std::string(argv[4]) == "stage";
   const int X = 5, Y = 5, A = X * Y, pb = (A + 7) / 8, P = 4 * A, games = 256, chunk = 16, rps = 200;
-  std::string model = dir + "/model.cfnn";
-  FILE* f = fopen(model.c_str(), "w");
-  if(!f)
-    return 2;
-  fputs("fake", f);
-  fclose(f);
+  const int rowCap = 4096;
+  int rb = 0;
+  if(coffee_row_bytes(X, Y, &rb) != COFFEE_OK)
+    return 3;
   std::vector<coffee_selfplay*> g(groups);
+  std::vector<void*> dst(groups, nullptr);
   for(int k = 0; k < groups; k++) {
     coffee_selfplay_config c = {};
+    coffee_search_params_default(&c.search);
     c.x = X;
     c.y = Y;
     c.win_len = 4;
     c.num_games = games / groups;
     c.slot_base = k * (games / groups);
-    c.model_path = model.c_str();
+    c.use_fake_net = 1;
+    c.row_capacity = rowCap;
+    c.node_cap = 1024;
+    c.commit_interval = 16;
     c.engines_per_device = groups;
-    if(coffee_selfplay_create(&c, &g[k]) != COFFEE_OK)
+    if(coffee_selfplay_create(&c, &g[k]) != COFFEE_OK) {
+      fprintf(stderr, "create: %s\n", coffee_last_error());
+      return 3;
+    }
+    if(stage && coffee_malloc(&dst[k], (uint64_t)rowCap * rb) != COFFEE_OK)
       return 3;
   }
   Writer w(dir, X, Y);
   long drained = 0;
+  std::vector<uint8_t> staged((size_t)rowCap * rb);
   for(int s = 0; s < steps; s++) {
     for(int done = 0; done < rps; done += chunk)
       for(auto* e : g)
         coffee_selfplay_step(e, chunk, nullptr);
     Block* b = new Block;
-    for(auto* e : g) {
+    for(size_t k = 0; k < g.size(); k++) {
+      coffee_selfplay* e = g[k];
+      if(stage) {
+        // the row buffer packed on the engine stream; the count is valid once the stream
+        // has passed the call (coffee_selfplay_sync here; bench.py waits on an event)
+        uint64_t n = 0;
+        if(coffee_selfplay_stage_rows(e, dst[k], rowCap, &n, COFFEE_STAGE_DISCARD_GAMES) != COFFEE_OK ||
+           coffee_selfplay_sync(e) != COFFEE_OK || coffee_memcpy(staged.data(), dst[k], n * rb, 1) != COFFEE_OK)
+          return 4;
+        for(uint64_t r = 0; r < n; r++) {
+          const uint8_t* q = staged.data() + r * rb;
+          auto take = [&](auto& vec, size_t count) {
+            using T = typename std::remove_reference<decltype(vec)>::type::value_type;
+            const T* src = reinterpret_cast<const T*>(q);
+            vec.insert(vec.end(), src, src + count);
+            q += count * sizeof(T);
+          };
+          take(b->bin, (size_t)15 * pb);
+          take(b->glob, 1);
+          take(b->pol, (size_t)2 * P);
+          take(b->gt, 64);
+          take(b->val, (size_t)5 * A);
+        }
+        b->n += (int)n;
+        continue;
+      }
       const int cap = 4096;
       std::vector<uint8_t> bin((size_t)cap * 15 * pb);
       std::vector<float> glob(cap), gt((size_t)cap * 64);
@@ -137,6 +175,9 @@ int main(int argc, char** argv) {
   w.close();
   for(auto* e : g)
     coffee_selfplay_destroy(e);
+  for(void* p : dst)
+    if(p)
+      coffee_free(p);
   printf("bench writer: %ld rows drained, %ld written in %d files%s\n", drained, w.rows(), w.files(),
          w.failed() ? " (write error)" : "");
   return drained == w.rows() && !w.failed() ? 0 : 1;

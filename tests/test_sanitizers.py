@@ -10,10 +10,13 @@ overflow this way, cpp/game/board.cpp:400).  tests/san/Makefile builds
   * katago_tsan / bench_writer_tsan: the host programs' threads under ThreadSanitizer
     (the reference's threads: command/selfplay.cpp:271-394 game/server threads and the
     model poll; selfplaymanager.cpp:330) -- the CLI with several engine threads per
-    device, the shared models-directory watch (a hot reload mid-run), the game counter,
-    the log and SIGTERM; bench.py's engine loop with its .npz writer thread -- over a
-    host-only stand-in of the self-play C ABI (san/fake_engine.cpp) and the product's
-    .npz writer.
+    device, the shared models-directory watch (a hot reload mid-run: real CFNN files
+    through the product's loader), the game counter, the log and SIGTERM; bench.py's
+    engine loop with its .npz writer thread, rows drained or staged -- over the
+    PRODUCT's host code, instrumented: capi.cpp (C ABI, thread-local errors, the
+    process-wide device-table cache), selfplay.cpp (engine, round loop, timing events,
+    drain / stage / game records, model switch), model.cpp, tables.cpp, refrand.cpp and
+    npzwrite.cpp, on san/fake_device.cpp (host memory for the GPU, stand-in kernels).
 
 Any sanitizer report aborts the run (-fno-sanitize-recover=all), so every check here is
 "exit status 0 and the expected output".  No GPU is touched."""
@@ -164,11 +167,22 @@ def _tsan(args, **kw):
     return r
 
 
-def test_bench_writer_threads_under_tsan(built, tmp_path):
-    r = _tsan([os.path.join(SAN, "_build", "bench_writer_tsan"), str(tmp_path), "2", "30"])
+@pytest.mark.parametrize("mode", ["drain", "stage"])
+def test_bench_writer_threads_under_tsan(built, tmp_path, mode):
+    r = _tsan([os.path.join(SAN, "_build", "bench_writer_tsan"), str(tmp_path), "2", "30", mode])
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert "written in 30 files" in r.stdout, r.stdout
-    assert len([f for f in os.listdir(tmp_path) if f.endswith(".npz")]) == 30
+    files = sorted(f for f in os.listdir(tmp_path) if f.endswith(".npz"))
+    assert len(files) == 30
+    with np.load(os.path.join(str(tmp_path), files[-1])) as z:
+        assert z["binaryInputNCHWPacked"].shape[1:] == (15, 4) and z["globalInputNC"].shape[0] > 0
+
+
+def _models(d, names):
+    import katacoffee_amd as kc
+    d.mkdir()
+    for i, n in enumerate(names):
+        kc.write_random_model("b2c32nbt", 7 + i, str(d / (n + ".cfnn")))
 
 
 def test_cli_threads_under_tsan(built, tmp_path):
@@ -177,13 +191,14 @@ def test_cli_threads_under_tsan(built, tmp_path):
     import threading
     import time
     models = tmp_path / "models"
-    models.mkdir()
-    (models / "netA.cfnn").write_bytes(b"fake")
+    _models(models, ["netA"])
+    staged = tmp_path / "staged"
+    _models(staged, ["netB"])
     out = tmp_path / "out"
 
     def drop_new_model():
         time.sleep(1.5)
-        (models / "netB.cfnn").write_bytes(b"fake2")
+        os.replace(staged / "netB.cfnn", models / "netB.cfnn")
         os.utime(models / "netB.cfnn", (time.time() + 5, time.time() + 5))
 
     t = threading.Thread(target=drop_new_model)
@@ -209,8 +224,7 @@ def test_cli_sigterm_under_tsan(built, tmp_path):
     import signal
     import time
     models = tmp_path / "models"
-    models.mkdir()
-    (models / "netA.cfnn").write_bytes(b"fake")
+    _models(models, ["netA"])
     out = tmp_path / "out"
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
     p = subprocess.Popen([os.path.join(SAN, "_build", "katago_tsan"), "selfplay", "-config",
@@ -225,3 +239,32 @@ def test_cli_sigterm_under_tsan(built, tmp_path):
     assert p.returncode == 0, so[-2000:] + se[-2000:]
     assert "gpu 0.0 done" in so and "gpu 1.0 done" in so
     assert os.listdir(out / "netA" / "tdata")  # the pending rows were flushed
+
+
+def test_tsan_harness_sees_the_product_cache(built, tmp_path):
+    """Negative control: the same CLI run over a copy of capi.cpp whose device-table cache
+    lock (kc::tablesFor, the cache every engine thread shares) is removed must be reported
+    by ThreadSanitizer -- the harness instruments the product's host code itself."""
+    cs = os.path.join(REPO, "katacoffee_amd", "csrc")
+    src = open(os.path.join(cs, "capi.cpp")).read()
+    lock = "  std::lock_guard<std::mutex> lk(gTablesMu);\n"
+    assert src.count(lock) == 1
+    racy = tmp_path / "capi_racy.cpp"
+    racy.write_text(src.replace(lock, ""))
+    obj = tmp_path / "capi_racy.o"
+    subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-std=c++17", "-O1", "-g", "-fPIC",
+                    "-ffp-contract=off", "-Xarch_host", "-fsanitize=thread", "-Xarch_host", "-fno-omit-frame-pointer",
+                    "-I", cs, "-c", str(racy), "-o", str(obj)], check=True)
+    tobj = os.path.join(SAN, "_build", "t")
+    others = [os.path.join(tobj, f) for f in sorted(os.listdir(tobj)) if f.endswith(".o") and f != "capi.o"]
+    exe = tmp_path / "katago_racy"
+    subprocess.run(["/opt/rocm/lib/llvm/bin/clang++", "-std=c++17", "-O1", "-g", "-fPIC", "-fsanitize=thread", "-o",
+                    str(exe), os.path.join(cs, "cli_selfplay.cpp"), str(obj)] + others + ["-lpthread"], check=True)
+    models = tmp_path / "models"
+    _models(models, ["netA"])
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([str(exe), "selfplay", "-config", os.path.join(REPO, "configs", "selfplay_coffee5.cfg"),
+                        "-models-dir", str(models), "-output-dir", str(tmp_path / "out"), "-max-games-total", "2000",
+                        "-override-config", "numGameThreads=64,numGpus=2,numNNServerThreadsPerModel=4"],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert "ThreadSanitizer: data race" in r.stderr and "tablesFor" in r.stderr, r.stderr[-3000:]
