@@ -88,7 +88,8 @@ def parse():
                     help="steady: warm-up past the first game ends, value = rows written/s; short: value = moves/s "
                          "(default: steady except C5)")
     ap.add_argument("--precision", choices=["fast", "default", "accurate", "fast-layered", "corrected"], default="fast",
-                    help="network precision of the headline window (default: the C ABI's default, the 1e-3 path)")
+                    help="network precision of the headline window (fast: fp16 operands, the configs' precision "
+                         "class; with fast the run also measures a window at 'default', the C ABI's 1e-3 path)")
     # 16: a game whose search is done waits at most 15 rounds for its move, and every
     # group's round chain carries half the commit / row launches of 8 (C2: +2.4 %)
     ap.add_argument("--commit-interval", type=int, default=16)
@@ -115,6 +116,9 @@ def parse():
                          "bytes over RCCL; every engine switches (the reference's model hot reload)")
     ap.add_argument("--seed", type=int, default=20250217)
     ap.add_argument("--no-npz", action="store_true", help="do not write .npz files in the timed region")
+    ap.add_argument("--row-sink", choices=["local", "gather"], default="local",
+                    help="N > 1: local = every rank writes its own games' rows (sharded games, no collective in "
+                         "the loop); gather = rows gathered to rank 0 over RCCL each step (one writer)")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
     ap.add_argument("--cpu-curve-seconds", type=float, default=0.0,
                     help="timed window of each point of the CPU thread-scaling curve (0: skip the curve)")
@@ -334,8 +338,8 @@ class NpzWriter:
     """Writes row blocks to .npz files on a background thread (trainingwrite.cpp
     writeToZipFile :566-587 then rename :765-769, via the native coffee_write_npz)."""
 
-    def __init__(self, kc, X, Y, outdir):
-        self.kc, self.X, self.Y, self.dir = kc, X, Y, outdir
+    def __init__(self, kc, X, Y, outdir, prefix="rows"):
+        self.kc, self.X, self.Y, self.dir, self.prefix = kc, X, Y, outdir, prefix
         self.q = queue.Queue()
         self.rows = 0
         self.files = 0
@@ -351,7 +355,7 @@ class NpzWriter:
             try:
                 n = len(rows["meta"])
                 if n:
-                    path = os.path.join(self.dir, "rows%06d.npz" % self.files)
+                    path = os.path.join(self.dir, "%s%06d.npz" % (self.prefix, self.files))
                     self.kc.write_npz(path + ".tmp", rows, self.X, self.Y)
                     os.replace(path + ".tmp", path)
                     self.files += 1
@@ -559,9 +563,12 @@ def main():
         base_ms = [sp.kernel_time(i) for i in range(4)]
         base_timed_evals = sp.timed_nn_evals()
         writer = None
-        if rank == 0 and not args.no_npz:
+        local_sink = dist is None or args.row_sink == "local"
+        if (rank == 0 or local_sink) and not args.no_npz:
             os.makedirs(os.path.join(tmpdir, "tdata"), exist_ok=True)
-            writer = NpzWriter(kc, X, Y, os.path.join(tmpdir, "tdata"))
+            # one writer per rank (local sink: each rank's own files), or rank 0's for all
+            writer = NpzWriter(kc, X, Y, os.path.join(tmpdir, "tdata"), prefix="rank%d_rows" % rank)
+        sink = kcrows.RowSink(X, Y, dist, "local" if local_sink else "gather", writer)
 
         def barrier():
             if dist is not None:
@@ -579,24 +586,14 @@ def main():
                 kcweights.broadcast_model(path, dist, torch.device("cuda", local))
             sp.set_model_bytes(data)
 
-        rows_gathered = 0
-        per_rank_rows = 0
         reloads = 0
         sp.setup_staging(torch, kc, X, Y)
 
         def process(i):
-            # step i's rows: device block -> RCCL gather to rank 0 -> host -> writer thread,
-            # while the next step's kernels run on the engine streams
-            nonlocal rows_gathered, per_rank_rows
-            packed = sp.collect(i)
-            per_rank_rows += packed.shape[0]
-            if dist is not None:
-                packed = kcrows.gather_packed_to_rank0(packed, dist)
-            if rank == 0:
-                rows = kcrows.unpack(packed.cpu().numpy(), X, Y)
-                rows_gathered += len(rows["meta"])
-                if writer:
-                    writer.put(rows)
+            # step i's rows: device block -> this rank's host -> its writer thread (local
+            # sink), or -> RCCL gather to rank 0 first (gather sink), while the next step's
+            # kernels run on the engine streams
+            sink.put(sp.collect(i))
             torch.cuda.current_stream().synchronize()  # slot i's blocks are free for step + 2
 
         barrier()
@@ -622,7 +619,8 @@ def main():
         d = {k: s1[k] - s0[k] for k in ("moves", "playouts", "nn_evals", "tree_levels", "tree_children")}
         kt = [sp.kernel_time(i) for i in range(4)]
         timed_evals = sp.timed_nn_evals() - base_timed_evals
-        rank_rows = [per_rank_rows]
+        rows_gathered, npz_rows, npz_files, rank_rows = sink.totals(
+            torch.device("cuda", local), writer.rows if writer else 0, writer.files if writer else 0)
         if dist is not None:
             t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -632,10 +630,6 @@ def main():
             dist.all_reduce(c, op=dist.ReduceOp.SUM)
             for k, v in zip(keys, c.tolist()):
                 d[k] = v
-            pr = torch.tensor([per_rank_rows], dtype=torch.int64, device="cuda")
-            allr = [torch.zeros_like(pr) for _ in range(world)]
-            dist.all_gather(allr, pr)
-            rank_rows = [int(x.item()) for x in allr]
         if rank == 0:
             names = ["select", "network", "backup", "commit"]
             kernels = {}
@@ -687,7 +681,7 @@ def main():
             cpu = None
             if with_cpu and world == 1 and not args.no_cpu_baseline:
                 cpu = cpu_baseline(args, cfg, model_path)
-            # whole-job rows written (gathered to rank 0, on disk before the clock stopped)
+            # whole-job rows written (every rank's, on disk before the clock stopped)
             rows_per_sec = rows_gathered / elapsed if window == "steady" else d["moves"] / elapsed
             out = {
                 "metric": "self-play training rows/sec + MCTS playouts/sec, 5x5 Coffee b6c96 @600 visits",
@@ -717,17 +711,19 @@ def main():
                            "play_settings": args.play + (" + policy openings (area prop %g)" % args.opening_prop
                                                          if args.opening_prop > 0 else ""),
                            "start_stagger_rounds": stagger, "groups": args.groups, "node_cap": node_cap or "default",
-                           "parallelism": "game-sharded x%d (RCCL row gather)" % world if world > 1 else "1 GPU"},
+                           "parallelism": ("game-sharded x%d (%s)" % (world, "rows written per rank, no collective in "
+                                                                         "the loop" if local_sink else "RCCL row gather "
+                                                                         "to rank 0")) if world > 1 else "1 GPU"},
                 "rccl_world_size": world,
                 "rows_per_rank": rank_rows,
                 "playouts_per_sec": d["playouts"] / elapsed,
                 "moves_per_sec": d["moves"] / elapsed,
                 "nn_evals_per_sec": d["nn_evals"] / elapsed,
                 "rows_drained": rows_gathered,
-                "rows_written_npz": writer.rows if writer else None,
+                "rows_written_npz": npz_rows if writer else None,
                 "model_reloads": reloads,
-                "rows_written_npz_per_sec": (writer.rows / elapsed) if writer else None,
-                "npz_files": writer.files if writer else None,
+                "rows_written_npz_per_sec": (npz_rows / elapsed) if writer else None,
+                "npz_files": npz_files if writer else None,
                 # node-pool / edge-pool headroom of the run (the edge pool is sized
                 # by a heuristic; its peak use is reported beside its capacity)
                 "edge_pool": {"peak_entries": s1["edge_pool_peak"], "cap_entries": s1["edge_pool_cap"]},

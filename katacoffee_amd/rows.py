@@ -30,8 +30,10 @@ def row_bytes(X, Y):
 def pack(rows, X, Y):
     """dict of row arrays -> contiguous uint8 [n][row_bytes]."""
     n = len(rows["meta"])
+    if n == 0:
+        return np.zeros((0, row_bytes(X, Y)), np.uint8)
     parts = [np.ascontiguousarray(rows[f], dtype=t).reshape(n, -1).view(np.uint8) for f, t in FIELDS]
-    return np.concatenate(parts, axis=1) if n else np.zeros((0, row_bytes(X, Y)), np.uint8)
+    return np.concatenate(parts, axis=1)
 
 
 def unpack(buf, X, Y):
@@ -76,3 +78,47 @@ def gather_to_rank0(rows, X, Y, dist, device):
     buf = torch.from_numpy(pack(rows, X, Y)).to(device)
     out = gather_packed_to_rank0(buf, dist)
     return None if out is None else unpack(out.cpu().numpy(), X, Y)
+
+
+class RowSink:
+    """Where a rank's staged row block goes after every bench step.
+
+    mode "local" (the default): every rank unpacks its own block and hands it to its own
+    writer (its own .npz files) -- games are sharded, so no collective runs in the data
+    path and no rank waits for another inside the loop; "gather": the blocks are gathered
+    to rank 0 over RCCL first (gather_packed_to_rank0: one writer for the job, a global
+    synchronisation point per step).  `writer` (None: count only) takes row dicts.
+    totals() all-reduces the counts once the timed window is over."""
+
+    def __init__(self, X, Y, dist=None, mode="local", writer=None):
+        if mode not in ("local", "gather"):
+            raise ValueError("row sink mode must be local or gather")
+        self.X, self.Y, self.dist, self.mode, self.writer = X, Y, dist, mode, writer
+        self.handed = 0    # rows this rank staged
+        self.received = 0  # rows this rank unpacked for writing (every rank's in gather mode on rank 0)
+
+    def put(self, packed):
+        """packed: uint8 tensor [n][row_bytes] on this rank's device."""
+        self.handed += int(packed.shape[0])
+        if self.mode == "gather" and self.dist is not None:
+            packed = gather_packed_to_rank0(packed, self.dist)
+            if packed is None:
+                return
+        rows = unpack(packed.cpu().numpy(), self.X, self.Y)
+        self.received += len(rows["meta"])
+        if self.writer is not None:
+            self.writer.put(rows)
+
+    def totals(self, device, written=0, files=0):
+        """(rows received for writing, rows written, files written) summed over the job,
+        and the rows each rank staged (list by rank)."""
+        if self.dist is None:
+            return self.received, written, files, [self.handed]
+        import torch
+        t = torch.tensor([self.received, written, files], dtype=torch.int64, device=device)
+        self.dist.all_reduce(t)
+        h = torch.tensor([self.handed], dtype=torch.int64, device=device)
+        per = [torch.zeros_like(h) for _ in range(self.dist.get_world_size())]
+        self.dist.all_gather(per, h)
+        r, w, f = (int(x) for x in t.tolist())
+        return r, w, f, [int(x.item()) for x in per]

@@ -146,3 +146,64 @@ def test_model_broadcast_world2(tmp_path):
     back = str(tmp_path / "received.cfnn")
     open(back, "wb").write(got[1])
     assert kc.model_flops(back, 25) == kc.model_flops(path, 25)
+
+
+class _ListWriter:
+    def __init__(self):
+        self.blocks = []
+
+    def put(self, rows):
+        self.blocks.append(rows)
+
+
+def _sink_worker(rank, world, port, mode, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    rng = np.random.default_rng(rank)
+    sh = R.shapes(5, 5)
+    w = _ListWriter() if (mode == "local" or rank == 0) else None
+    sink = R.RowSink(5, 5, dist, mode, w)
+    sent = []
+    for step in range(3):  # bench.py's steps: ragged blocks, one empty
+        n = [(2, 5), (0, 4), (3, 1)][step][rank]
+        rows = {f: rng.integers(0, 100, size=(n,) + sh[f]).astype(t) for f, t in R.FIELDS}
+        rows["meta"][:, 0] = rank
+        sent.append(rows)
+        sink.put(torch.from_numpy(R.pack(rows, 5, 5)))
+    tot = sink.totals("cpu", written=sum(len(b["meta"]) for b in w.blocks) if w else 0, files=len(w.blocks) if w else 0)
+    q.put((rank, tot, None if w is None else [b["meta"] for b in w.blocks], [r["meta"] for r in sent]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["local", "gather"])
+def test_row_sink_world2(mode):
+    """bench.py's per-step row hand-off at world size 2: local -- each rank writes exactly
+    its own rows and no collective runs until totals(); gather -- rank 0 writes every
+    rank's rows in rank order.  Both report the same job totals."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sink_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total = 2 + 5 + 0 + 4 + 3 + 1
+    for rank in (0, 1):
+        received, written, files, per_rank = res[rank][0]
+        assert (received, written) == (total, total) and per_rank == [5, 10]
+    if mode == "local":
+        for rank in (0, 1):
+            got, sent = res[rank][1], res[rank][2]
+            assert np.concatenate(got).tolist() == np.concatenate(sent).tolist()
+        assert res[0][0][2] == 6  # every rank's writer got its 3 blocks
+    else:
+        got = np.concatenate(res[0][1])
+        exp = np.concatenate([np.concatenate([res[0][2][s], res[1][2][s]]) for s in range(3)])
+        assert got.tolist() == exp.tolist()
+        assert res[1][1] is None and res[0][0][2] == 3  # rank 0's writer got one block per step
