@@ -103,6 +103,15 @@ constexpr float F8C_MAX = 448.0f;  // largest finite e4m3fn
 #ifndef KC_F8C_CVTW
 #define KC_F8C_CVTW 0
 #endif
+// KC_FAST_BL 1: the fast (fp16) small-batch instance is borderless too, with ring slots of
+// three taps (one barrier per three taps instead of per pair; 192-VGPR cap, 17 spilled;
+// the branch scratch in ring slot 1); 0: the bordered 5-board instance with the paired
+// 4-slot ring (rounds 3-4, the default).  Measured (round 5, same box): network alone
+// 77.7 vs 75.3 us at 960 boards, C2 bench 22.9-23.1 k vs 24.0 k rows/s (in-bench network
+// 94 vs 84 us: its 149 KB of LDS leaves the other group's search blocks less room).
+#ifndef KC_FAST_BL
+#define KC_FAST_BL 0
+#endif
 #ifndef KC_F8C_CVTX
 #define KC_F8C_CVTX 0
 #endif
@@ -194,10 +203,18 @@ struct NNGeo {
   // a tap's second weight block: fp16 lo fragments (mode 1); e4m3(lo(w) 2^(11-sw)) only, 8 B
   // per lane and fragment (mode 2: e4m3(w 2^-sw) is converted from the hi fragment)
   static constexpr int WBUF2 = !SPLIT ? 0 : (F8W ? WBUF / 2 : WBUF);
-  static constexpr int WSLOT = WBUF + WBUF2;     // one ring slot (16-B units)
+  // one ring slot (16-B units): a tap's blocks, or three fp16 taps (fast borderless)
+  static constexpr int WSLOT = (BL && !SPLIT) ? 3 * WBUF : WBUF + WBUF2;
   static constexpr int SLOT_PIECES = WSLOT / 64;  // its 1-KiB pieces
   // 1-KiB pieces of one tap of a conv with ncb 32-channel input blocks
   static constexpr int tapPieces(int ncb) { return ncb * NCT_ALL * (!SPLIT ? 2 : (F8W ? 3 : 4)) / 2; }
+  // BL ring chunks of a conv with ntaps taps of ncb blocks: taps per chunk, chunks, and the
+  // pieces of its first chunk (what the previous conv requests ahead)
+  static constexpr int chunkTaps(int ncb, int ntaps) {
+    return SLOT_PIECES / tapPieces(ncb) < 1 ? 1 : (SLOT_PIECES / tapPieces(ncb) < ntaps ? SLOT_PIECES / tapPieces(ncb) : ntaps);
+  }
+  static constexpr int chunks(int ncb, int ntaps) { return (ntaps + chunkTaps(ncb, ntaps) - 1) / chunkTaps(ncb, ntaps); }
+  static constexpr int firstChunkPieces(int ncb, int ntaps) { return chunkTaps(ncb, ntaps) * tapPieces(ncb); }
   // row tables (u16): rowPa[MROWS], rowBP[MROWS], bpRow[ROWS] -- built on the host
   static constexpr int NTAB = 2 * MROWS + ROWS;
   static constexpr int OFF_TAB = OFF_BIAS + NB * 64 * 4;
@@ -209,13 +226,21 @@ struct NNGeo {
   static constexpr int OFF_PRM = (OFF_TAB + NTAB * 2 + 15) / 16 * 16;
   static constexpr int OFF_W = OFF_PRM + 2 * NPRM * 4;
   static constexpr int LDS = OFF_W + RING * WSLOT * 16;
+  // the f32 scratch of the g / value branches: in act (dead then), or -- fast borderless,
+  // whose one-plane act is too small -- in ring slot 1, which holds only a consumed chunk
+  // during the gpool mids (conv1's last chunk; conv2's first is in slot 0) and the heads
+  // (the head conv's chunk; the heads' linear weights use slot 0)
+  static constexpr bool SCR_IN_RING = BL && !SPLIT;
+  static constexpr int SCR_OFF = SCR_IN_RING ? OFF_W + WSLOT * 16 : OFF_SCR;
   static_assert(C % 32 == 0, "C must be a multiple of 32");
-  static_assert(OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES, "f32 branch scratch must fit in act");
+  static_assert(SCR_IN_RING ? (MROWS * SCR * 4 <= WSLOT * 16 && RING == 2 && RING_VH + NB * 64 * 4 <= WSLOT * 16)
+                            : OFF_SCR + MROWS * SCR * 4 <= ACT_BYTES,
+                "f32 branch scratch must fit in act (or in ring slot 1)");
   static_assert(96 * 64 * 4 <= OFF_SCR, "gpool linear weights must fit below scr");
   static_assert(RING * WSLOT * 16 >= RING_VH + NB * 64 * 4, "head linear weights and vh must fit in the ring");
   static_assert((PLANES - 1) * PLANE_BYTES + (BL ? 0 : 2 * PA * ROWB) + 2 * 64 < 65536,
                 "A-read offsets must fit the ds_read immediate");
-  static_assert(!BL || (MODE_ != NN_MODE_F16 && C == 96), "borderless instances: split modes of b6c96");
+  static_assert(!BL || C == 96, "borderless instances: b6c96");
   static_assert(LDS <= 163840, "LDS budget");
 };
 
@@ -525,7 +550,7 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
 #pragma unroll
     for(int ct = 0; ct < G::NCT; ct++) {
       bf[buf][ct] = wb[ct * 64];
-      if constexpr(DBG & 8) {
+      if constexpr((DBG & 8) || G::MODE == NN_MODE_F16) {
       } else if constexpr(G::MODE == NN_MODE_SPLIT3) {
         bfl[buf][ct] = wb[CHP * 64 + ct * 64];
       } else if constexpr(!G::F8W) {
@@ -547,7 +572,7 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
 #pragma unroll
     for(int t = 0; t < G::MAXT; t++) {
       af[buf][t] = *reinterpret_cast<const h16x8*>(actB + at[t] + cb * 64);
-      if constexpr(DBG & 8) {
+      if constexpr((DBG & 8) || G::MODE == NN_MODE_F16) {
       } else if constexpr(G::MODE == NN_MODE_SPLIT3) {
         afl[buf][t] = *reinterpret_cast<const h16x8*>(actB + G::PLANE_BYTES + at[t] + cb * 64);
       } else if constexpr(!G::F8X) {
@@ -1068,7 +1093,7 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
   const int tstart = rg * G::MAXT;
   uint16_t* act = reinterpret_cast<uint16_t*>(smem);
   float* actF = reinterpret_cast<float*>(smem);
-  float* scr = reinterpret_cast<float*>(smem + G::OFF_SCR);
+  float* scr = reinterpret_cast<float*>(smem + G::SCR_OFF);
   float* poolP = reinterpret_cast<float*>(smem + G::OFF_POOL);
   float* poolV = poolP + G::NB * 96;
   float* biasS = reinterpret_cast<float*>(smem + G::OFF_BIAS);
@@ -1085,10 +1110,11 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
     constexpr int CH0 = G::tapPieces(1);  // 1-KiB pieces per stem tap (one 32-channel block)
     const uint32_t ring = ldsAddr(wl);
     if constexpr(G::BL) {
-      // the stem's chunks 0 .. RING-2 (3 taps each) into slots 0 .. RING-2
+      // the stem's chunks 0 .. RING-2 into slots 0 .. RING-2 (its chunks are whole: 3 or 9 taps)
+      constexpr int SC = G::firstChunkPieces(1, 9);
 #pragma unroll
-      for(int j = 0; j + 1 < G::RING; j++)
-        stageChunk<G::NW>(WB + L->wInit + (size_t)j * 3 * CH0 * 64, ring + j * G::WSLOT * 16, 3 * CH0, wave, lane);
+      for(int j = 0; j + 1 < G::RING && j < G::chunks(1, 9); j++)
+        stageChunk<G::NW>(WB + L->wInit + (size_t)j * SC * 64, ring + j * G::WSLOT * 16, SC, wave, lane);
     } else {
 #pragma unroll
       for(int tap = 0; tap < 2; tap++)
@@ -1142,15 +1168,14 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
     aRowsBL<G>(rb, vm, tstart, lane);
   else
     aBases<G>(ab, rowPa, tstart, lane);
-  // pieces of the first weight chunk of a conv of C -> C (or the head's): one tap
-  constexpr int CHUNK96 = G::SLOT_PIECES;
   f32x4 acc[G::MAXT][G::NCT];  // the f32 residual trunk between blocks
   f32x4 park[G::MAXT][G::NCT];  // the trunk while a block's first conv owns acc (regTrunk)
   zeroAcc<G>(acc);
   if constexpr(G::BL)
     convTilesB<G, 9, 1, 0>(act, WB + L->wInit, wl, acc, rb, vm, cg, lane, tid,
-                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, CHUNK96, L->nblocks > 0 ? 9 : 1,
-                           L->sInit);
+                           L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead,
+                           L->nblocks > 0 ? G::firstChunkPieces(G::C / 32, 9) : G::firstChunkPieces(G::C / 32, 1),
+                           L->nblocks > 0 ? G::chunks(G::C / 32, 9) : 1, L->sInit);
   else
     convTiles<G, 9, 1, 0, 0, false>(act, WB + L->wInit, wl, acc, ab, cg, lane, tid,
                                     L->nblocks > 0 ? WB + L->wConv1[0] : WB + L->wHead, 3 * G::NCT_ALL * G::PLANES,
@@ -1201,7 +1226,10 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       // chunk too), so conv1 starts at 3 + 18 blk (1 mod 2, 0 mod 3) and conv2 at 12 + 18 blk (0)
       convTilesB<G, 9, G::C / 32, G::RING == 2 ? 1 : 0>(act, WB + L->wConv1[blk], wl, acc, rb, vm, cg, lane, tid,
                                                        WB + L->wConv2[blk],
-                                                       G::tapPieces(L->kinds[blk] == 0 ? 3 : 2), 9, L->sConv1[blk]);
+                                                       L->kinds[blk] == 0 ? G::firstChunkPieces(3, 9)
+                                                                          : G::firstChunkPieces(2, 9),
+                                                       L->kinds[blk] == 0 ? G::chunks(3, 9) : G::chunks(2, 9),
+                                                       L->sConv1[blk]);
     else
       convTiles<G, 9, G::C / 32, 1, 0, false>(act, WB + L->wConv1[blk], wl, acc, ab, cg, lane, tid,
                                               WB + L->wConv2[blk],
@@ -1229,8 +1257,9 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       __syncthreads();
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
-        convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW, CHUNK96,
-                                       nextTaps, L->sConv2[blk]);
+        convTilesB<G, 9, G::C / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW,
+                                       G::firstChunkPieces(G::C / 32, nextTaps), G::chunks(G::C / 32, nextTaps),
+                                       L->sConv2[blk]);
       else
         convTiles<G, 9, G::C / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                 3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1331,7 +1360,8 @@ __global__ void __launch_bounds__(512, 2) KC_NN_KERNEL_ATTR
       NN_PHASE(6 + 4 * blk);
       if constexpr(G::BL)
         convTilesB<G, 9, (G::C - 32) / 32, 0>(act, WB + L->wConv2[blk], wl, acc, rb, vm, cg, lane, tid, nextW,
-                                              CHUNK96, nextTaps, L->sConv2[blk]);
+                                              G::firstChunkPieces(G::C / 32, nextTaps),
+                                              G::chunks(G::C / 32, nextTaps), L->sConv2[blk]);
       else
         convTiles<G, 9, (G::C - 32) / 32, 0, 0, false>(act, WB + L->wConv2[blk], wl, acc, ab, cg, lane, tid, nextW,
                                                        3 * G::NCT_ALL * G::PLANES, nextTaps, 18 + 18 * blk);
@@ -1489,7 +1519,7 @@ __global__ void kNNForwardCap(const NNLayout* __restrict__ L, const h16x8* __res
 template <class G>
 constexpr auto nnKernel() {
 #if KC_F8C_VGPR
-  if constexpr(G::MODE == NN_MODE_F8C)
+  if constexpr(G::MODE == NN_MODE_F8C || (G::MODE == NN_MODE_F16 && G::BL))
     return kNNForwardCap<G::X, G::Y, G::C, G::NB, G::MODE, G::BL>;
   else
 #endif
@@ -1908,6 +1938,8 @@ void NNEngine::build(const ModelHost& m, int path) {
   KC_HIP(hipFuncSetAttribute((const void*)kNNForward<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, GB::LDS));
   KC_HIP(hipFuncSetAttribute((const void*)nnKernel<GC>(), hipFuncAttributeMaxDynamicSharedMemorySize, GC::LDS));
+  using GF = NNGeo<5, 5, 96, NN_SMALL_NB, 0, true>;
+  KC_HIP(hipFuncSetAttribute((const void*)nnKernel<GF>(), hipFuncAttributeMaxDynamicSharedMemorySize, GF::LDS));
 #ifdef KC_AB_HOOKS
   // A/B builds only (tools/Makefile alt, -DKC_AB_HOOKS): KATACOFFEE_NN_SMALL=8 runs small
   // batches on the 8-board instance too; the product library never reads the variable
@@ -1994,8 +2026,12 @@ void NNEngine::forward(int n, const uint64_t* in, float* out, hipStream_t st, co
   }
   else if(mode_ == NN_ACCURATE_NB2)
     launch<NNGeo<5, 5, 96, 2, NN_MODE_SPLIT3, false>>(n, inWords, tabDevS_, in, out, st, countDev, rowIdx, e0, e1);
-  else if(n <= NN_SMALL_NB * cus_ && small_ != 8)
-    launch<NNGeo<5, 5, 96, NN_SMALL_NB, 0>>(n, inWords, tabDevSm_, in, out, st, countDev, rowIdx, e0, e1);
+  else if(n <= NN_SMALL_NB * cus_ && small_ != 8) {
+    if(KC_FAST_BL)
+      launch<NNGeo<5, 5, 96, NN_SMALL_NB, 0, true>>(n, inWords, tabDevB_, in, out, st, countDev, rowIdx, e0, e1);
+    else
+      launch<NNGeo<5, 5, 96, NN_SMALL_NB, 0>>(n, inWords, tabDevSm_, in, out, st, countDev, rowIdx, e0, e1);
+  }
   else
     launch<NNGeo<5, 5, 96, 8, 0>>(n, inWords, tabDev_, in, out, st, countDev, rowIdx, e0, e1);
 }
