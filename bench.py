@@ -653,7 +653,9 @@ def main():
                               "kConvL/kGpoolBias/kHeadsL (layered %s forward, one launch group)" % cfg["arch"],
                     "bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / PEAK_F16_TFLOPS,
-                    "traffic": traffic.get("network_bytes_per_launch") if fused and args.config == "C2" else None,
+                    # PMC bytes of this precision's instance (profiles/traffic_latest.json), else null
+                    "traffic": traffic.get("network_bytes_per_launch" + ("" if precision == "fast" else "_" + precision))
+                               if fused and args.config == "C2" else None,
                     "evals_per_launch": per_launch, "flops_per_eval": flops_per_eval,
                     "mfma_per_product": mfma_factor, "avg_launch_us": net["avg_us"],
                     "timed_launches": net["launches_timed"]}
