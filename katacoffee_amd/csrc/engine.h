@@ -51,7 +51,11 @@ struct NNLayout {
   int bngs[NN_MAX_BLOCKS], bngb[NN_MAX_BLOCKS], linG[NN_MAX_BLOCKS];
   // corrected instance: each convolution's A scale byte, 127 - 11 + its weights' block exponent
   int sInit, sHead, sConv1[NN_MAX_BLOCKS], sConv2[NN_MAX_BLOCKS];
+  // f32 offset of the parameter slabs, [nblocks + 1][NN_PRM] (nn.hip loadParam's layout,
+  // gathered on the host so a slab element is one coalesced load)
+  int prmSlabs;
 };
+constexpr int NN_PRM = 448;  // floats per parameter slab (NNGeo::NPRM)
 
 // Layered forward (nn_layered.hip): one implicit-GEMM MFMA launch per convolution
 // over the whole batch; any CFNN architecture (incl. nested bottlenecks) at 5x5,

@@ -222,7 +222,7 @@ struct NNGeo {
   // heads, after the policy-gpool and value linear weights staged there
   static constexpr int RING_VH = (32 + 64) * 96 * 4;
   // per-block f32 parameter slabs (double buffered, filled one block ahead)
-  static constexpr int NPRM = 448;
+  static constexpr int NPRM = NN_PRM;
   static constexpr int OFF_PRM = (OFF_TAB + NTAB * 2 + 15) / 16 * 16;
   static constexpr int OFF_W = OFF_PRM + 2 * NPRM * 4;
   static constexpr int LDS = OFF_W + RING * WSLOT * 16;
@@ -1037,24 +1037,30 @@ KC_D void linear96(const float* wT, int O, const float* in, float* out, int ostr
 // Element `tid` of parameter slab k: block k's BN1/BN2 scale+bias and gpool BN
 // ([0,96) bn1s [96,192) bn1b [192,288) bn2s [288,384) bn2b [384,416) bngs
 // [416,448) bngb), or for k == nblocks the tip BN and head biases ([0,96) tips
-// [96,192) tipb [192,224) pBiasG [224,256) vBias1 [256,288) pBias2).
+// [96,192) tipb [192,224) pBiasG [224,256) vBias1 [256,288) pBias2).  The slabs are
+// gathered on the host (paramSlabSource), so this is one coalesced load: the per-thread
+// source arithmetic it replaces stayed live across the block loop and, in the
+// register-capped corrected instance, was spilled and reloaded behind the weight DMA.
 KC_D float loadParam(const NNLayout* __restrict__ L, const float* __restrict__ WF, int k, int tid) {
-  int src = -1;
+  return tid < NN_PRM ? WF[L->prmSlabs + k * NN_PRM + tid] : 0.0f;
+}
+// Host: the f32 offset (in the weight image) of slab k's element `tid`, -1 for zero.
+static int paramSlabSource(const NNLayout& L, int k, int tid) {
   const int f = tid < 384 ? tid / 96 : (tid < 416 ? 4 : 5), i = tid < 384 ? tid - 96 * f : (tid - 384) & 31;
-  if(k < L->nblocks) {
-    if(f == 0) src = L->bn1s[k] + i;
-    else if(f == 1) src = L->bn1b[k] + i;
-    else if(f == 2) src = L->bn2s[k] + i;
-    else if(f == 3) src = L->bn2b[k] + i;
-    else if(tid < 448 && L->kinds[k] == 1) src = (f == 4 ? L->bngs[k] : L->bngb[k]) + i;
-  } else if(tid < 288) {
-    if(tid < 96) src = L->tips + tid;
-    else if(tid < 192) src = L->tipb + tid - 96;
-    else if(tid < 224) src = L->pBiasG + tid - 192;
-    else if(tid < 256) src = L->vBias1 + tid - 224;
-    else src = L->pBias2 + tid - 256;
+  if(k < L.nblocks) {
+    if(f == 0) return L.bn1s[k] + i;
+    if(f == 1) return L.bn1b[k] + i;
+    if(f == 2) return L.bn2s[k] + i;
+    if(f == 3) return L.bn2b[k] + i;
+    if(tid < NN_PRM && L.kinds[k] == 1) return (f == 4 ? L.bngs[k] : L.bngb[k]) + i;
+    return -1;
   }
-  return src >= 0 ? WF[src] : 0.0f;
+  if(tid >= 288) return -1;
+  if(tid < 96) return L.tips + tid;
+  if(tid < 192) return L.tipb + tid - 96;
+  if(tid < 224) return L.pBiasG + tid - 192;
+  if(tid < 256) return L.vBias1 + tid - 224;
+  return L.pBias2 + tid - 256;
 }
 
 #ifndef KC_NN_KERNEL
@@ -1906,6 +1912,15 @@ void NNEngine::build(const ModelHost& m, int path) {
   L.vB3 = f32(m.vB3);
   L.vLinM = f32(m.vLinM);
   L.vBM = f32(m.vBM);
+  {
+    std::vector<float> slabs((size_t)(L.nblocks + 1) * NN_PRM);
+    for(int k = 0; k <= L.nblocks; k++)
+      for(int t = 0; t < NN_PRM; t++) {
+        const int src = paramSlabSource(L, k, t);
+        slabs[(size_t)k * NN_PRM + t] = src >= 0 ? wf[src] : 0.0f;
+      }
+    L.prmSlabs = f32(slabs);
+  }
   KC_HIP(hipMalloc(&wHalf_, wb.size() * 2));
   KC_HIP(hipMemcpy(wHalf_, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
   KC_HIP(hipMalloc(&wF32_, wf.size() * 4));
