@@ -202,6 +202,13 @@ KC_D int bcastI(int v, int srcLane) { return bcastLane(v, srcLane); }
 
 // Child slots read speculatively with their node record (2 x 128-B lines of Edge).
 constexpr int SPEC_EDGES = INLINE_EDGES;
+// descend(): request the likely next node (most-visited inline child) with the children's
+// records.  A/B switch, off: bit-exact but slower on the C2 bench (kSelect 64.9-65.1 vs
+// 60.3-61.0 us, 23.4 k vs 24.0-24.2 k rows/s, same box: profiles/r05/spec_next_ab.txt) --
+// the argmax sits on the critical path and kSelect<2> spills 7 more registers
+#ifndef KC_SPEC_NEXT
+#define KC_SPEC_NEXT 0
+#endif
 KC_D int firstLane(uint64_t m) { return __builtin_ctzll(m); }
 
 KC_D float childWeight(uint32_t edgeVisits, uint32_t childVisits, float rawWeight) {
@@ -761,7 +768,8 @@ KC_D float exploreScaling(const SP& sp, float totalChildWeight) {
 // broadcast from the lane that holds them (no reload of either after the choice).
 template <int NI>
 KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool isRoot, int& newPos,
-                    uint32_t* hasBits, const Edge& e0, Edge& ce, uint32_t& cVisits, uint32_t& cFlags) {
+                    uint32_t* hasBits, const Edge& e0, Edge& ce, uint32_t& cVisits, uint32_t& cFlags, int* specChild = nullptr,
+                    Edge* specE0 = nullptr, Node* specN = nullptr) {
   const SP& sp = *v.sp;
   const int P = v.d.P;
   const int k = n.numChildren;
@@ -797,6 +805,20 @@ KC_D int selectBest(const GV& v, int ni, const Node& n, const float* pol, bool i
       cw[j] = p < 0.0f ? 0.0f : childWeight(e.visits, cvis[j], c.weightSum);
       if(isRoot)
         atomicOr(&hasBits[e.move >> 5], 1u << (e.move & 31));
+    }
+  }
+  if(specChild) {
+    // the next level, speculatively: the inline child with the most edge visits (the
+    // usual pick once a node has visits) -- its record and inline edges are requested
+    // behind the children's records, so a hit saves the next level's first round trip
+    float sv = v.lane < k && v.lane < SPEC_EDGES ? (float)e0.visits : -1.0f;
+    int si = v.lane;
+    waveArgmax(sv, si);
+    const int sc = sv >= 0.0f ? bcastLane((int)e0.child, si) : -1;
+    *specChild = sc;
+    if(sc >= 0) {
+      *specE0 = v.lane < SPEC_EDGES && v.lane < v.d.P ? v.inlineEdges(sc)[v.lane] : Edge{0u, 0u, 0.0f, 0u};
+      *specN = NS[sc];
     }
   }
   const float probMass = tsum<NI>(probs, k, v.lane);
@@ -962,7 +984,12 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
     const unsigned long long tSel = SPROF_NOW();
     Edge ce{0u, 0u, 0.0f, 0u};
     uint32_t cVisits = 0, cFlags = 0;
-    int slot = selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits, e0, ce, cVisits, cFlags);
+    int specChild = -1;
+    Edge specE0{0u, 0u, 0.0f, 0u};
+    Node specN;
+    int slot = KC_SPEC_NEXT ? selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits, e0, ce, cVisits, cFlags, &specChild,
+                                             &specE0, &specN)
+                            : selectBest<NI>(v, ni, n, pol, isRoot, newPos, hasBits, e0, ce, cVisits, cFlags);
     SPROF_ADD(5, SPROF_NOW() - tSel);
     (void)tSel;
     if(slot < 0) {
@@ -1097,8 +1124,15 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
       b.winner = maxRun(T, b, mv % T.A) >= T.W ? mover : 0;
     }
     ni = child;
-    e0 = loadE0(ni);
-    n = v.nodes()[ni];
+    if(KC_SPEC_NEXT && child == specChild) {
+      // (no node or edge is written before a descent's last level: the speculative
+      // copies are what the loads would return)
+      e0 = specE0;
+      n = specN;
+    } else {
+      e0 = loadE0(ni);
+      n = v.nodes()[ni];
+    }
   }
   s.treeLevels += (uint64_t)s.pathLen;
   s.treeChildren += scanned;
