@@ -560,7 +560,7 @@ def main():
         s0 = sp.stats()
         # the precision the engines run (the default one resolved by its calibration check)
         precision = kc.PRECISION_NAMES.get(s0["nn_precision"], precision) if s0["nn_precision"] else precision
-        base_ms = [sp.kernel_time(i) for i in range(4)]
+        base_ms = [sp.kernel_time(i) for i in range(5)]
         base_timed_evals = sp.timed_nn_evals()
         writer = None
         local_sink = dist is None or args.row_sink == "local"
@@ -617,7 +617,7 @@ def main():
         elapsed = time.perf_counter() - t0
         s1 = sp.stats()
         d = {k: s1[k] - s0[k] for k in ("moves", "playouts", "nn_evals", "tree_levels", "tree_children")}
-        kt = [sp.kernel_time(i) for i in range(4)]
+        kt = [sp.kernel_time(i) for i in range(5)]
         timed_evals = sp.timed_nn_evals() - base_timed_evals
         rows_gathered, npz_rows, npz_files, rank_rows = sink.totals(
             torch.device("cuda", local), writer.rows if writer else 0, writer.files if writer else 0)
@@ -631,7 +631,9 @@ def main():
             for k, v in zip(keys, c.tolist()):
                 d[k] = v
         if rank == 0:
-            names = ["select", "network", "backup", "commit"]
+            # backup_select: a round's backup and the next round's selection in one kernel
+            # (every round not followed by a commit); select / backup: the other rounds
+            names = ["select", "network", "backup", "commit", "backup_select"]
             kernels = {}
             for i, nm in enumerate(names):
                 ms = kt[i][0] - base_ms[i][0]
@@ -662,21 +664,24 @@ def main():
             # tree roofline: per descent, sum over path nodes of 32 B + k * 48 B,
             # counted on the device (tree_levels, tree_children)
             tree_bytes = NODE_B * d["tree_levels"] + CHILD_B * d["tree_children"]
-            for nm in ("select", "backup"):
+            for nm in ("select", "backup", "backup_select"):
                 k = kernels[nm]
                 if k["launches_timed"] and rounds_run:
-                    per_launch_b = tree_bytes / rounds_run
+                    # the fused kernel walks two paths per game: one backup, one descent
+                    per_launch_b = tree_bytes / rounds_run * (2 if nm == "backup_select" else 1)
                     ach = per_launch_b / (k["avg_us"] * 1e-6) / 1e9
-                    roof_all[nm] = {"kernel": "kSelect" if nm == "select" else "kBackup", "bound": "hbm",
+                    roof_all[nm] = {"kernel": {"select": "kSelect", "backup": "kBackup"}.get(nm, "kBackupSelect"),
+                                    "bound": "hbm",
                                     "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
                                     "traffic": traffic.get("%s_bytes_per_launch" % nm) if args.config == "C2" else None,
                                     "algorithmic_bytes_per_launch": per_launch_b,
                                     "path_nodes_per_playout": d["tree_levels"] / max(1, d["playouts"]),
                                     "children_per_path_node": d["tree_children"] / max(1, d["tree_levels"]),
                                     "avg_launch_us": k["avg_us"]}
-            total_ms = {nm: (kernels[nm]["avg_us"] or 0.0) * (1 if nm != "commit" else 1.0 / args.commit_interval)
-                        for nm in names}
-            dominant = max(("network", "select", "backup"), key=lambda nm: total_ms[nm] if nm in roof_all else -1)
+            # every kind is timed on the same every-N-th-launch schedule: summed timed ms ranks them
+            total_ms = {nm: kernels[nm]["ms_timed"] for nm in names}
+            dominant = max(("network", "select", "backup", "backup_select"),
+                           key=lambda nm: total_ms[nm] if nm in roof_all else -1)
             roof = dict(roof_all.get(dominant, {}))
             if roof:
                 roof["timing"] = "HIP events on the engine stream around every %d-th launch" % args.timing_every

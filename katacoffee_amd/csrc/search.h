@@ -61,7 +61,10 @@ enum LeafKind {
   LEAF_CACHED = 6,  // NN output taken from the evaluation cache (SPEC a7)
   LEAF_INIT = 7,    // policy-initialisation move: the root evaluated for a sampled opening move
   LEAF_FORK = 8,    // fork candidate: the position after one candidate move evaluated
-  LEAF_SIDE = 9     // side-position continuation: the position after the search's response
+  LEAF_SIDE = 9,    // side-position continuation: the position after the search's response
+  // fused backup + select (kBackupSelect): the leaf's cache slot is being written by this
+  // round's backups, so the lookup waits for kResolve (which runs after them)
+  LEAF_PENDING = 10
 };
 
 // NN evaluation cache slot of a state key (SPEC a7; oracle ora_search.cpp cacheSlot).
@@ -300,6 +303,7 @@ struct SearchDev {
   DPtr<float> cPol;           // [entries][P] post-processed policy (illegal = -1)
   DPtr<float> cVal;           // [entries][2] white win / loss
   DPtr<uint32_t> cTag;        // [entries] this round's highest bidding game + 1 (0 = none)
+  DPtr<uint32_t> cClear;      // [G] fused rounds: slot + 1 whose tag the game's kResolve clears (0 = none)
   // commit queue
   DPtr<FinRec> fin;           // [G] games finished by the current commit (kRows)
   DPtr<ForkRec> fork;         // [G] fork state (PH_FORK)
@@ -341,6 +345,12 @@ void launchStageRows(const SearchDev& d, const SearchDev* dd, uint8_t* dst, unsi
 int rowBytes(int A);  // bytes of one packed row at board area A
 void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
                   hipEvent_t e1 = nullptr);
+// One kernel for round r's backup and round r+1's selection of every game (no commit in
+// between); the selections whose NN-cache slot this round's backups write are finished by
+// launchResolve, which must run before the next launchCompact.
+void launchBackupSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
+                        hipEvent_t e1 = nullptr);
+void launchResolve(const SearchDev& d, const SearchDev* dd, hipStream_t st);
 void launchCommit(const SearchDev& d, const SearchDev* dd, hipStream_t st);  // + kRows
 void launchGameTree(const SearchDev* dd, int slot, int maxNodes, uint32_t* nodesOut, uint32_t* edgesOut,
                     int32_t* count, hipStream_t st);

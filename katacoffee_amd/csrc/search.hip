@@ -174,16 +174,21 @@ KC_D void storeGame(const GV& v, const GameDev& s) {
     dst[i] = src[i];
 }
 
+// The view's per-game settings from the loaded state.
+KC_D void bindGame(GV& v, const GameDev& s) {
+  // a cheap search without recorded rows runs without root noise and root-specific
+  // settings (runBotWithLimits play.cpp:1024-1037); the flag is uniform
+  v.sp = __builtin_amdgcn_readfirstlane(s.noNoise) ? &v.d.spCheap : &v.d.sp;
+  v.setEdgeSel(s.edgeSel);
+}
+
 KC_D void loadGame(GV& v, GameDev& s) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&v.d.games[v.g]);
   uint32_t* dst = reinterpret_cast<uint32_t*>(&s);
   for(int i = v.lane; i < (int)(sizeof(GameDev) / 4); i += 64)
     dst[i] = src[i];
   waveSync();
-  // a cheap search without recorded rows runs without root noise and root-specific
-  // settings (runBotWithLimits play.cpp:1024-1037); the flag is uniform
-  v.sp = __builtin_amdgcn_readfirstlane(s.noNoise) ? &v.d.spCheap : &v.d.sp;
-  v.setEdgeSel(s.edgeSel);
+  bindGame(v, s);
 }
 
 template <int NI>
@@ -1140,20 +1145,81 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
 
 // ---------------------------------------------------------------------------
 // kSelect: root evaluation or one descent; NN leaves are encoded into the batch.
+
+// NN evaluation cache lookup of an NN leaf (SPEC a7): a state evaluated in an earlier
+// round by any game is taken from the cache instead of the network.  The payload is
+// loaded with the key and a hit copies it into the leaf's policy.  fused (kBackupSelect):
+// the slot's tag is loaded too -- a bid of this round (tag != 0) means this round's
+// backups, running beside this selection, write the slot, so the lookup is left to
+// kResolve (LEAF_PENDING); any other slot is not written during the kernel.
 template <int NI>
-__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp,
-                                                                int resetCommit) {
-  const SearchDev& d = *dp;
-  const int g = blockIdx.x;
-  // the previous commit's list is consumed (kCommit/kRows ran before this kernel);
-  // this round's kBackup appends to an empty one
-  if(resetCommit && g == 0 && threadIdx.x == 0)
-    *d.commitCount = 0;
-  if(g >= d.G)
+KC_D void cacheLookup(const GV& v, GameDev& s, bool fused) {
+  const SearchDev& d = v.d;
+  const uint64_t k0 = v.nodeKey(s.leafNode)[0], k1 = v.nodeKey(s.leafNode)[1];
+  const uint32_t slot = cacheSlot(k0, k1, d.cacheMask);
+  const int P = d.P;
+  const float* cp = d.cPol + (size_t)slot * P;
+  float pv[NI];
+#pragma unroll
+  for(int j = 0; j < NI; j++) {
+    const int pos = v.lane + 64 * j;
+    pv[j] = pos < P ? cp[pos] : 0.0f;
+  }
+  const float cw = d.cVal[2 * (size_t)slot], cl = d.cVal[2 * (size_t)slot + 1];
+  const uint32_t tag = fused ? d.cTag[slot] : 0u;
+  s.cSlot = (int32_t)slot;
+  if(tag != 0u) {
+    s.leafKind = LEAF_PENDING;
     return;
-  __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
-  __shared__ GameDev s;
-  GV v(d, *Tp, g);
+  }
+  if(d.cKey[2 * (size_t)slot] == k0 && d.cKey[2 * (size_t)slot + 1] == k1) {
+    s.leafKind = LEAF_CACHED;
+    s.cHitWin = cw;
+    s.cHitLoss = cl;
+    float* pol = v.pol(s.leafNode);
+#pragma unroll
+    for(int j = 0; j < NI; j++) {
+      const int pos = v.lane + 64 * j;
+      if(pos < P)
+        pol[pos] = pv[j];
+    }
+  }
+}
+
+// The end of a selection: an NN leaf draws its symmetry, the game's batch row is encoded
+// when the leaf needs the network, and the game state is stored.
+KC_D void finishSelect(const GV& v, GameDev& s, DRng& rng) {
+  const SearchDev& d = v.d;
+  const int g = v.g;
+  if(s.leafKind == LEAF_NN)
+    s.leafSym = (int)rng.below(8);
+  s.rngCtr = rng.ctr;
+  const bool needNN =
+      s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT || s.leafKind == LEAF_FORK ||
+      s.leafKind == LEAF_SIDE;
+  if(v.lane == 0) {
+    d.nnNeed[g] = needNN ? 1 : 0;
+    if(needNN)
+      d.nnBid[g] = s.leafKind == LEAF_NN && d.cacheOn ? (uint32_t)s.cSlot : ~0u;
+  }
+  if(needNN) {
+    // the game's own batch row: no shared counter (a same-address atomic from
+    // every block serialises at L2); kCompact lists the rows the network evaluates
+    const int slot = g;
+    s.nnSlot = slot;
+    s.nnEvals++;
+    encodePackedWave(v.T, s.leaf, s.leafSym, d.nnIn + (size_t)slot * d.inWords);
+  }
+  waveSync();
+  storeGame(v, s);
+}
+
+// One game's selection.  s: the game's LDS copy, already holding its stored state when
+// `loaded` (the fused kernel's backup just stored it).  rootPol: LDS [MAX_P].
+template <int NI>
+KC_D void selectBody(const SearchDev& d, const DTables& T, int g, GameDev& s, bool loaded, bool fused,
+                     uint32_t* hasBits, float* rootPol) {
+  GV v(d, T, g);
   SPROF_INIT();
   const unsigned long long t0 = SPROF_NOW();
   if(d.nnDefer[g]) {
@@ -1163,7 +1229,10 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
       d.nnNeed[g] = 1;
     return;
   }
-  loadGame(v, s);
+  if(loaded)
+    bindGame(v, s);
+  else
+    loadGame(v, s);
   if(s.phase == PH_COMMIT || s.startDelay > 0) {
     s.leafKind = LEAF_NONE;
     if(v.lane == 0) {
@@ -1212,64 +1281,13 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
     s.leafSym = (int)((s.syms >> (4 * s.rootK)) & 15u);
     s.leaf = s.root;
   } else {
-    __shared__ float rootPol[MAX_P];
     descend<NI>(v, s, hasBits, rootPol);
-    if(s.leafKind == LEAF_NN && d.cacheOn) {
-      // NN evaluation cache (SPEC a7): a state evaluated in an earlier round by any
-      // game is taken from the cache instead of the network.  The payload is loaded
-      // with the key and a hit copies it into the leaf's policy here: this round's
-      // kBackup writes the winning bidders' evaluations into the table.
-      const uint64_t k0 = v.nodeKey(s.leafNode)[0], k1 = v.nodeKey(s.leafNode)[1];
-      const uint32_t slot = cacheSlot(k0, k1, d.cacheMask);
-      const int P = d.P;
-      const float* cp = d.cPol + (size_t)slot * P;
-      float pv[NI];
-#pragma unroll
-      for(int j = 0; j < NI; j++) {
-        const int pos = v.lane + 64 * j;
-        pv[j] = pos < P ? cp[pos] : 0.0f;
-      }
-      const float cw = d.cVal[2 * (size_t)slot], cl = d.cVal[2 * (size_t)slot + 1];
-      s.cSlot = (int32_t)slot;
-      if(d.cKey[2 * (size_t)slot] == k0 && d.cKey[2 * (size_t)slot + 1] == k1) {
-        s.leafKind = LEAF_CACHED;
-        s.cHitWin = cw;
-        s.cHitLoss = cl;
-        float* pol = v.pol(s.leafNode);
-#pragma unroll
-        for(int j = 0; j < NI; j++) {
-          const int pos = v.lane + 64 * j;
-          if(pos < P)
-            pol[pos] = pv[j];
-        }
-      }
-    }
-    if(s.leafKind == LEAF_NN)
-      s.leafSym = (int)rng.below(8);
+    if(s.leafKind == LEAF_NN && d.cacheOn)
+      cacheLookup<NI>(v, s, fused);
   }
   const unsigned long long t2 = SPROF_NOW();
   (void)t2;
-  s.rngCtr = rng.ctr;
-  const bool needNN =
-      s.leafKind == LEAF_NN || s.leafKind == LEAF_ROOTEVAL || s.leafKind == LEAF_INIT || s.leafKind == LEAF_FORK ||
-      s.leafKind == LEAF_SIDE;
-  if(v.lane == 0) {
-    d.nnNeed[g] = needNN ? 1 : 0;
-    if(needNN)
-      d.nnBid[g] = s.leafKind == LEAF_NN && d.cacheOn ? (uint32_t)s.cSlot : ~0u;
-  }
-  if(needNN) {
-    // the game's own batch row: no shared counter (a same-address atomic from
-    // every block serialises at L2); kCompact lists the rows the network evaluates
-    const int slot = g;
-    s.nnSlot = slot;
-    s.nnEvals++;
-    encodePackedWave(v.T, s.leaf, s.leafSym, d.nnIn + (size_t)slot * d.inWords);
-  }
-  const unsigned long long t3 = SPROF_NOW();
-  (void)t3;
-  waveSync();
-  storeGame(v, s);
+  finishSelect(v, s, rng);
   SPROF_ADD(0, 1);
   SPROF_MAX(24, SPROF_NOW() - t0);
   SPROF_MAX(25, s.pathLen);
@@ -1277,8 +1295,52 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
   SPROF_ADD(2, t1 - t0);
   SPROF_ADD(3, t2 - t1);
   SPROF_ADD(4, s.pathLen);
-  SPROF_ADD(7, t3 - t2);
+  SPROF_ADD(7, SPROF_NOW() - t2);
   SPROF_FLUSH();
+}
+
+template <int NI>
+__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp,
+                                                                int resetCommit) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  // the previous commit's list is consumed (kCommit/kRows ran before this kernel);
+  // this round's kBackup appends to an empty one
+  if(resetCommit && g == 0 && threadIdx.x == 0)
+    *d.commitCount = 0;
+  if(g >= d.G)
+    return;
+  __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
+  __shared__ GameDev s;
+  __shared__ float rootPol[MAX_P];
+  selectBody<NI>(d, *Tp, g, s, false, false, hasBits, rootPol);
+}
+
+// The selections a fused kernel left pending: the cache slot is final now (every backup
+// of the round has run), so the lookup and the rest of the selection complete here, in
+// the order kSelect runs them (the symmetry draw comes after the lookup).  Each round
+// winner also clears the tag it left for this kernel (before the next kCompact bids).
+template <int NI>
+__global__ void __launch_bounds__(64) kResolve(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  if(g >= d.G)
+    return;
+  const int lane = laneId();
+  const uint32_t cc = d.cClear[g];
+  if(cc != 0u && lane == 0) {
+    d.cTag[cc - 1u] = 0u;
+    d.cClear[g] = 0u;
+  }
+  if(d.games[g].leafKind != LEAF_PENDING)
+    return;
+  __shared__ GameDev s;
+  GV v(d, *Tp, g);
+  loadGame(v, s);
+  s.leafKind = LEAF_NN;
+  cacheLookup<NI>(v, s, false);
+  DRng rng = DRng{s.rngSeed, s.rngCtr};
+  finishSelect(v, s, rng);
 }
 
 // oracle postprocess (nneval.cpp:702-815 + copyOutputsWithSymmetry nninputs.cpp:349-357)
@@ -1555,21 +1617,20 @@ KC_D bool initMove(const GV& v, GameDev& s, const float* o, float* scratch /* LD
   return false;
 }
 
+// One game's backup; returns whether s holds the game's stored state afterwards.
+// fused (kBackupSelect): a cache-slot winner leaves the slot's tag set -- the selections
+// running beside it treat the slot as being written -- and kResolve clears it.
 template <int NI>
-__global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
-  const SearchDev& d = *dp;
-  const int g = blockIdx.x;
-  if(g >= d.G || d.nnDefer[g])  // a deferred leaf is backed up in a later round
-    return;
-  __shared__ __attribute__((aligned(16))) float scratch[3 * MAX_P];
-  __shared__ GameDev s;
-  GV v(d, *Tp, g);
+KC_D bool backupBody(const SearchDev& d, const DTables& T, int g, GameDev& s, bool fused, float* scratch) {
+  if(d.nnDefer[g])  // a deferred leaf is backed up in a later round
+    return false;
+  GV v(d, T, g);
   SPROF_INIT();
   const unsigned long long t0 = SPROF_NOW();
   (void)t0;
   loadGame(v, s);
   if(s.leafKind == LEAF_NONE)
-    return;
+    return true;
   unsigned long long tPost = 0, tLeaf = 0, tPath = 0;
   (void)tPost;
   (void)tLeaf;
@@ -1677,7 +1738,10 @@ __global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* 
               d.cVal[2 * (size_t)slot + 1] = l;
               d.cKey[2 * (size_t)slot] = v.nodeKey(s.leafNode)[0];
               d.cKey[2 * (size_t)slot + 1] = v.nodeKey(s.leafNode)[1];
-              d.cTag[slot] = 0;
+              if(fused)
+                d.cClear[g] = slot + 1u;
+              else
+                d.cTag[slot] = 0;
             }
           }
         }
@@ -1728,6 +1792,38 @@ __global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* 
   SPROF_ADD(13, tPath);
   SPROF_ADD(14, tLeaf);
   SPROF_FLUSH();
+  return true;
+}
+
+template <int NI>
+__global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  if(g >= d.G)
+    return;
+  __shared__ __attribute__((aligned(16))) float scratch[3 * MAX_P];
+  __shared__ GameDev s;
+  backupBody<NI>(d, *Tp, g, s, false, scratch);
+}
+
+// Round r's backup and round r+1's selection of one game in one kernel (no commit between
+// them).  Games only read and write their own trees and tables; the one table they share,
+// the NN cache, is handled by the tags (backupBody / cacheLookup / kResolve), so every
+// result is the one the two separate kernels give.  One kernel boundary less per round,
+// and a game's slow backup and slow descent no longer each set a kernel's length.
+template <int NI>
+__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kBackupSelect(const SearchDev* __restrict__ dp,
+                                                                      const DTables* __restrict__ Tp) {
+  const SearchDev& d = *dp;
+  const int g = blockIdx.x;
+  if(g >= d.G)
+    return;
+  __shared__ __attribute__((aligned(16))) float scratch[3 * MAX_P];
+  __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
+  __shared__ GameDev s;
+  const bool loaded = backupBody<NI>(d, *Tp, g, s, true, scratch);
+  // (the selection's root policy reuses the backup's scratch)
+  selectBody<NI>(d, *Tp, g, s, loaded, true, hasBits, scratch);
 }
 
 #ifdef KC_SEARCH_PROFILE
@@ -3698,6 +3794,26 @@ void launchBackup(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEv
     case 2: launchEv(kBackup<2>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
     case 4: launchEv(kBackup<4>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
     default: launchEv(kBackup<7>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+  }
+  KC_HIP(hipGetLastError());
+}
+
+void launchBackupSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const DTables* T = d.T;
+  switch(laneItems(d.P)) {
+    case 2: launchEv(kBackupSelect<2>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+    case 4: launchEv(kBackupSelect<4>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+    default: launchEv(kBackupSelect<7>, dim3(d.G), dim3(64), 0, st, e0, e1, dd, T); break;
+  }
+  KC_HIP(hipGetLastError());
+}
+
+void launchResolve(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
+  const DTables* T = d.T;
+  switch(laneItems(d.P)) {
+    case 2: hipLaunchKernelGGL(kResolve<2>, dim3(d.G), dim3(64), 0, st, dd, T); break;
+    case 4: hipLaunchKernelGGL(kResolve<4>, dim3(d.G), dim3(64), 0, st, dd, T); break;
+    default: hipLaunchKernelGGL(kResolve<7>, dim3(d.G), dim3(64), 0, st, dd, T); break;
   }
   KC_HIP(hipGetLastError());
 }

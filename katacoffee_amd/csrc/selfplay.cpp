@@ -246,6 +246,11 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     d.cVal = devAlloc<float>(owned_, entries * 2, false);
     d.cTag = devAlloc<uint32_t>(owned_, entries);
   }
+  d.cClear = devAlloc<uint32_t>(owned_, G);
+  {
+    const char* f = getenv("COFFEE_FUSED_ROUNDS");
+    fuseRounds_ = !(f && f[0] == '0');
+  }
   d.gCap = 2 * G;
   d.gRec = devAlloc<GameRec>(owned_, (size_t)d.gCap, false);
   d.gCount = devAlloc<unsigned long long>(owned_, 1);
@@ -328,11 +333,17 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
   if(!st)
     st = stream_;
   const SearchDev& d = hd_;
+  bool selected = false;  // this round's selections ran in the previous round's fused kernel
   for(int r = 0; r < rounds; r++) {
-    const bool t0 = sampleNow(0), t1 = sampleNow(1), t2 = sampleNow(2);
+    const bool t1 = sampleNow(1);
     // select, network and backup are timed by their own dispatches (kernel start to
     // end, like rocprofv3); compact and cache write run untimed between them
-    timedKernel(0, t0, [&](hipEvent_t a, hipEvent_t b) { launchSelect(d, dd_, st, a, b, commitReset_); });
+    if(selected) {
+      launchResolve(d, dd_, st);  // the selections whose cache slot was being written
+    } else {
+      const bool t0 = sampleNow(0);
+      timedKernel(0, t0, [&](hipEvent_t a, hipEvent_t b) { launchSelect(d, dd_, st, a, b, commitReset_); });
+    }
     commitReset_ = false;
     launchCompact(d, dd_, st, t1);
     timedKernel(1, t1, [&](hipEvent_t a, hipEvent_t b) {
@@ -347,9 +358,18 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
           KC_HIP(hipEventRecord(b, st));
       }
     });
-    timedKernel(2, t2, [&](hipEvent_t a, hipEvent_t b) { launchBackup(d, dd_, st, a, b); });
+    const bool commitNow = (rounds_ + 1) % (uint64_t)commitInterval_ == 0 || r == rounds - 1;
+    if(fuseRounds_ && !commitNow) {
+      const bool t4 = sampleNow(4);
+      timedKernel(4, t4, [&](hipEvent_t a, hipEvent_t b) { launchBackupSelect(d, dd_, st, a, b); });
+      selected = true;
+    } else {
+      const bool t2 = sampleNow(2);
+      timedKernel(2, t2, [&](hipEvent_t a, hipEvent_t b) { launchBackup(d, dd_, st, a, b); });
+      selected = false;
+    }
     rounds_++;
-    if(rounds_ % (uint64_t)commitInterval_ == 0 || r == rounds - 1) {
+    if(commitNow) {
       const bool t3 = sampleNow(3);
       timed(3, st, [&] { launchCommit(d, dd_, st); }, t3);
       commitReset_ = true;  // the next kSelect zeroes the count (no separate memset)
@@ -599,8 +619,8 @@ uint64_t SelfplayEngine::timedNNEvals() {
 
 void SelfplayEngine::kernelTime(int which, double& ms, uint64_t& launches) {
   resolveTiming();
-  if(which < 0 || which > 3)
-    throw std::invalid_argument("which must be 0..3");
+  if(which < 0 || which > 4)
+    throw std::invalid_argument("which must be 0..4");
   ms = kernelMs_[which];
   launches = kernelLaunches_[which];
 }

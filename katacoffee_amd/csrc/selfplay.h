@@ -73,9 +73,13 @@ class SelfplayEngine {
   bool commitReset_ = false;  // a commit ran: the next kSelect zeroes the commit count
   uint64_t rowsDrained_ = 0;
   int timingEvery_ = 0;
-  uint64_t groupLaunches_[4] = {0, 0, 0, 0};
-  double kernelMs_[4] = {0, 0, 0, 0};
-  uint64_t kernelLaunches_[4] = {0, 0, 0, 0};
+  // kernel timing slots: 0 select, 1 network, 2 backup, 3 commit, 4 backup + next select (fused)
+  uint64_t groupLaunches_[5] = {0, 0, 0, 0, 0};
+  double kernelMs_[5] = {0, 0, 0, 0, 0};
+  uint64_t kernelLaunches_[5] = {0, 0, 0, 0, 0};
+  // a round's backup and the next round's selection run as one kernel unless a commit
+  // comes between them (COFFEE_FUSED_ROUNDS=0 keeps them apart: same results)
+  bool fuseRounds_ = true;
 };
 
 }  // namespace kc

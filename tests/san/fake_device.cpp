@@ -147,6 +147,14 @@ void launchBackup(const SearchDev& d, const SearchDev*, hipStream_t, hipEvent_t 
   stamp(e1);
 }
 
+void launchBackupSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  stamp(e0);
+  launchBackup(d, dd, st, nullptr, nullptr);
+  launchSelect(d, dd, st, nullptr, nullptr, false);
+  stamp(e1);
+}
+void launchResolve(const SearchDev&, const SearchDev*, hipStream_t) {}
+
 // one move per game; a game ends every 12 moves with one row per move and a record
 void launchCommit(const SearchDev& d, const SearchDev*, hipStream_t) {
   const int A = d.A, P = d.P, pb = (A + 7) / 8;
