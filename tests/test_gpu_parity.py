@@ -228,6 +228,62 @@ def test_selfplay_network_smoke(model_path):
     sp.close()
 
 
+def _engine(fused, **kw):
+    # the engine reads COFFEE_FUSED_ROUNDS when it is created
+    old = os.environ.pop("COFFEE_FUSED_ROUNDS", None)
+    if not fused:
+        os.environ["COFFEE_FUSED_ROUNDS"] = "0"
+    try:
+        return kc.Selfplay(5, 5, 4, **kw)
+    finally:
+        os.environ.pop("COFFEE_FUSED_ROUNDS", None)
+        if old is not None:
+            os.environ["COFFEE_FUSED_ROUNDS"] = old
+
+
+# Fused rounds (kBackupSelect + kResolve) against separate kSelect / kBackup launches:
+# with commit intervals > 1 most rounds run fused, and a 32-entry cache has nearly every
+# lookup hit a slot that the same round's backups write (the kResolve path).  Every game's
+# state, search tree and row must be identical.  (The oracle has no commit interval; the
+# separate kernels are pinned against it at interval 1 above.)
+@pytest.mark.parametrize("games,visits,rounds,seed,cache_log2,ci,play,net",
+                         [(64, 32, 700, 61, 5, 4, {}, False), (48, 24, 900, 67, 12, 16, PRODUCTION, False),
+                          (32, 24, 600, 71, 5, 3, dict(FORKS, side_position_prob=0.3), False),
+                          (64, 16, 500, 73, 5, 8, {}, True)],
+                         ids=["cache32-ci4", "production-ci16", "forks-side-ci3", "network-ci8"])
+def test_fused_rounds_match_separate_kernels(games, visits, rounds, seed, cache_log2, ci, play, net, model_path):
+    kw = dict(num_games=games, max_visits=visits, seed=seed, node_cap=128, commit_interval=ci,
+              nn_cache_log2=cache_log2, **play)
+    if net:
+        kw["model_path"] = model_path
+    a, b = _engine(True, **kw), _engine(False, **kw)
+    a.enable_timing(1)
+    b.enable_timing(1)
+    done = 0
+    for chunk in [5, 37, 200, rounds]:  # step ends fall inside commit intervals too
+        a.step(chunk - done)
+        b.step(chunk - done)
+        done = chunk
+        for g in range(games):
+            ga, gb = a.game_info(g), b.game_info(g)
+            assert ga == gb, (done, g, ga, gb)
+            na, ea = a.game_tree(g)
+            nb, eb = b.game_tree(g)
+            np.testing.assert_array_equal(na, nb, err_msg="round %d game %d nodes" % (done, g))
+            np.testing.assert_array_equal(ea, eb, err_msg="round %d game %d edges" % (done, g))
+    sa, sb = a.stats(), b.stats()
+    assert sa["games_finished"] > 0
+    for k in ("playouts", "nn_evals", "moves", "games_finished", "rows_pending"):
+        assert sa[k] == sb[k], k
+    ra, rb = _sorted_rows(a.drain_rows()), _sorted_rows(b.drain_rows())
+    assert len(ra["meta"]) > 0
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
+    assert a.kernel_time(4)[1] > rounds // 2 and b.kernel_time(4)[1] == 0  # fused launches ran in a only
+    a.close()
+    b.close()
+
+
 def test_game_records_match_rows_and_rules(model_path):
     """Finished-game records (SGF source) agree with the rows of the same games and
     replay legally under the reference-pinned rules to the recorded result."""
