@@ -10,7 +10,7 @@ import sys
 
 
 def short(name):
-    for k in ["kNNForwardCap", "kNNForward", "kConv1L", "kConvLB", "kConvL", "kGpoolBias", "kHeadsL", "kSelect", "kBackup", "kCommit", "kRows", "kCacheWrite",
+    for k in ["kNNForwardCap", "kNNForward", "kConv1L", "kConvLB", "kConvL", "kGpoolBias", "kHeadsL", "kBackupSelect", "kResolve", "kSelect", "kBackup", "kCommit", "kRows", "kCacheWrite",
               "kCompact", "kFakeNet", "kInit", "fillBuffer", "copyBuffer"]:
         if k in name:
             return k
