@@ -303,7 +303,9 @@ struct SearchDev {
   DPtr<float> cPol;           // [entries][P] post-processed policy (illegal = -1)
   DPtr<float> cVal;           // [entries][2] white win / loss
   DPtr<uint32_t> cTag;        // [entries] this round's highest bidding game + 1 (0 = none)
-  DPtr<uint32_t> cClear;      // [G] fused rounds: slot + 1 whose tag the game's kResolve clears (0 = none)
+  DPtr<uint32_t> cClear;      // [G] fused rounds: slot + 1 whose tag kResolve clears (0 = none)
+  DPtr<int32_t> pendList;     // [G] fused rounds: games whose cache lookup waits for kResolve (LEAF_PENDING)
+  DPtr<int32_t> pendCount;    // entries in pendList (zeroed by the next kCompact)
   // commit queue
   DPtr<FinRec> fin;           // [G] games finished by the current commit (kRows)
   DPtr<ForkRec> fork;         // [G] fork state (PH_FORK)

@@ -1170,6 +1170,8 @@ KC_D void cacheLookup(const GV& v, GameDev& s, bool fused) {
   s.cSlot = (int32_t)slot;
   if(tag != 0u) {
     s.leafKind = LEAF_PENDING;
+    if(v.lane == 0)
+      d.pendList[atomicAdd(d.pendCount, 1)] = v.g;  // rare: a same-round transposition
     return;
   }
   if(d.cKey[2 * (size_t)slot] == k0 && d.cKey[2 * (size_t)slot + 1] == k1) {
@@ -1319,28 +1321,31 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
 // The selections a fused kernel left pending: the cache slot is final now (every backup
 // of the round has run), so the lookup and the rest of the selection complete here, in
 // the order kSelect runs them (the symmetry draw comes after the lookup).  Each round
-// winner also clears the tag it left for this kernel (before the next kCompact bids).
+// winner's tag is cleared too (before the next kCompact bids).  A small grid: block b
+// clears the tags of games b, b + grid, ... and completes pending entries b, b + grid, ...
+constexpr int RESOLVE_GRID = 64;
 template <int NI>
 __global__ void __launch_bounds__(64) kResolve(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
-  const int g = blockIdx.x;
-  if(g >= d.G)
-    return;
   const int lane = laneId();
-  const uint32_t cc = d.cClear[g];
-  if(cc != 0u && lane == 0) {
-    d.cTag[cc - 1u] = 0u;
-    d.cClear[g] = 0u;
+  for(int i = blockIdx.x * 64 + lane; i < d.G; i += RESOLVE_GRID * 64) {
+    const uint32_t cc = d.cClear[i];
+    if(cc != 0u) {
+      d.cTag[cc - 1u] = 0u;
+      d.cClear[i] = 0u;
+    }
   }
-  if(d.games[g].leafKind != LEAF_PENDING)
-    return;
+  const int np = *d.pendCount;
   __shared__ GameDev s;
-  GV v(d, *Tp, g);
-  loadGame(v, s);
-  s.leafKind = LEAF_NN;
-  cacheLookup<NI>(v, s, false);
-  DRng rng = DRng{s.rngSeed, s.rngCtr};
-  finishSelect(v, s, rng);
+  for(int k = blockIdx.x; k < np; k += RESOLVE_GRID) {
+    const int g = __builtin_amdgcn_readfirstlane(d.pendList[k]);
+    GV v(d, *Tp, g);
+    loadGame(v, s);
+    s.leafKind = LEAF_NN;
+    cacheLookup<NI>(v, s, false);
+    DRng rng = DRng{s.rngSeed, s.rngCtr};
+    finishSelect(v, s, rng);
+  }
 }
 
 // oracle postprocess (nneval.cpp:702-815 + copyOutputsWithSymmetry nninputs.cpp:349-357)
@@ -3595,6 +3600,7 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
   if(t == nt - 1) {
     const int count = min(total, cap);
     *d.nnCount = count;
+    *d.pendCount = 0;  // the pending list kResolve (before this kernel) completed
     if(accumulate)
       *d.nnTimedEvals += (unsigned long long)count;
   }
@@ -3811,9 +3817,9 @@ void launchBackupSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st,
 void launchResolve(const SearchDev& d, const SearchDev* dd, hipStream_t st) {
   const DTables* T = d.T;
   switch(laneItems(d.P)) {
-    case 2: hipLaunchKernelGGL(kResolve<2>, dim3(d.G), dim3(64), 0, st, dd, T); break;
-    case 4: hipLaunchKernelGGL(kResolve<4>, dim3(d.G), dim3(64), 0, st, dd, T); break;
-    default: hipLaunchKernelGGL(kResolve<7>, dim3(d.G), dim3(64), 0, st, dd, T); break;
+    case 2: hipLaunchKernelGGL(kResolve<2>, dim3(RESOLVE_GRID), dim3(64), 0, st, dd, T); break;
+    case 4: hipLaunchKernelGGL(kResolve<4>, dim3(RESOLVE_GRID), dim3(64), 0, st, dd, T); break;
+    default: hipLaunchKernelGGL(kResolve<7>, dim3(RESOLVE_GRID), dim3(64), 0, st, dd, T); break;
   }
   KC_HIP(hipGetLastError());
 }

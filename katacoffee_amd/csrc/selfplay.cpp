@@ -247,6 +247,8 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     d.cTag = devAlloc<uint32_t>(owned_, entries);
   }
   d.cClear = devAlloc<uint32_t>(owned_, G);
+  d.pendList = devAlloc<int32_t>(owned_, G, false);
+  d.pendCount = devAlloc<int32_t>(owned_, 1);
   {
     const char* f = getenv("COFFEE_FUSED_ROUNDS");
     fuseRounds_ = !(f && f[0] == '0');
