@@ -1816,8 +1816,15 @@ __global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* 
 // the NN cache, is handled by the tags (backupBody / cacheLookup / kResolve), so every
 // result is the one the two separate kernels give.  One kernel boundary less per round,
 // and a game's slow backup and slow descent no longer each set a kernel's length.
+// waves per SIMD the fused kernel is compiled for at 5x5 (A/B switch: 4 = 128 VGPRs, as
+// kSelect / kBackup; beside a network workgroup's two waves a SIMD holds one such wave.
+// 6 (80 VGPRs: two fit) spills 332 B per lane and ran 18.0 k against 24.4 k rows/s, 5
+// 21.6 k: profiles/r05/fused_occupancy_ab.txt)
+#ifndef KC_FUSED_OCC
+#define KC_FUSED_OCC 4
+#endif
 template <int NI>
-__global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kBackupSelect(const SearchDev* __restrict__ dp,
+__global__ void __launch_bounds__(64, NI <= 2 ? KC_FUSED_OCC : 2) kBackupSelect(const SearchDev* __restrict__ dp,
                                                                       const DTables* __restrict__ Tp) {
   const SearchDev& d = *dp;
   const int g = blockIdx.x;
