@@ -1216,8 +1216,8 @@ KC_D void finishSelect(const GV& v, GameDev& s, DRng& rng) {
   storeGame(v, s);
 }
 
-// One game's selection.  s: the game's LDS copy, already holding its stored state when
-// `loaded` (the fused kernel's backup just stored it).  rootPol: LDS [MAX_P].
+// One game's selection.  s: the game's LDS copy, already holding its state when `loaded`
+// (the fused kernel's backup just ran; every path below then stores it).  rootPol: LDS [MAX_P].
 template <int NI>
 KC_D void selectBody(const SearchDev& d, const DTables& T, int g, GameDev& s, bool loaded, bool fused,
                      uint32_t* hasBits, float* rootPol) {
@@ -1237,6 +1237,15 @@ KC_D void selectBody(const SearchDev& d, const DTables& T, int g, GameDev& s, bo
     loadGame(v, s);
   if(s.phase == PH_COMMIT || s.startDelay > 0) {
     s.leafKind = LEAF_NONE;
+    if(loaded) {
+      // the fused kernel's backup left the state to be stored here
+      if(s.startDelay > 0)
+        s.startDelay = s.startDelay - 1;
+      storeGame(v, s);
+      if(v.lane == 0)
+        d.nnNeed[g] = 0;
+      return;
+    }
     if(v.lane == 0) {
       d.games[g].leafKind = LEAF_NONE;
       if(s.startDelay > 0)
@@ -1622,7 +1631,8 @@ KC_D bool initMove(const GV& v, GameDev& s, const float* o, float* scratch /* LD
   return false;
 }
 
-// One game's backup; returns whether s holds the game's stored state afterwards.
+// One game's backup; returns whether s holds the game's state afterwards (fused: not yet
+// stored -- selectBody stores it on every path).
 // fused (kBackupSelect): a cache-slot winner leaves the slot's tag set -- the selections
 // running beside it treat the slot as being written -- and kResolve clears it.
 template <int NI>
@@ -1789,7 +1799,8 @@ KC_D bool backupBody(const SearchDev& d, const DTables& T, int g, GameDev& s, bo
   }
   s.leafKind = LEAF_NONE;
   waveSync();
-  storeGame(v, s);
+  if(!fused)  // fused: the selection that follows stores the state once (408 B per game less)
+    storeGame(v, s);
   SPROF_ADD(10, 1);
   SPROF_MAX(26, SPROF_NOW() - t0);
   SPROF_ADD(11, SPROF_NOW() - t0);
