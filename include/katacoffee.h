@@ -354,9 +354,9 @@ int coffee_debug_zobrist(int x, int y, int win_len, uint64_t* board, uint64_t* b
 
 /* Kernel timing (HIP events on the engine stream) for roofline reporting:
  * which: 0 select, 1 network, 2 backup, 3 commit (+ rows), 4 backup + the next
- * round's select in one kernel (every round not followed by a commit, unless the
- * environment sets COFFEE_FUSED_ROUNDS=0).  Summed ms and launch count of the timed
- * launches.  enable = 0 off, N > 0: every N-th launch of each
+ * round's select in one kernel (every round not followed by a commit, with the fast
+ * fused network or the stand-in; the environment's COFFEE_FUSED_ROUNDS=0 / 1 at
+ * creation: never / always).  Summed ms and launch count of the timed launches.  enable = 0 off, N > 0: every N-th launch of each
  * group is bracketed by an event pair (each pair costs a few microseconds of stream
  * gap, so N > 1 keeps a timed run representative of an untimed one). */
 int coffee_selfplay_enable_timing(coffee_selfplay* h, int enable);

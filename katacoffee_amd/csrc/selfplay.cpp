@@ -251,7 +251,7 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   d.pendCount = devAlloc<int32_t>(owned_, 1);
   {
     const char* f = getenv("COFFEE_FUSED_ROUNDS");
-    fuseRounds_ = !(f && f[0] == '0');
+    fuseRounds_ = f && f[0] == '0' ? 0 : (f && f[0] == '1' ? 1 : -1);
   }
   d.gCap = 2 * G;
   d.gRec = devAlloc<GameRec>(owned_, (size_t)d.gCap, false);
@@ -331,10 +331,17 @@ void SelfplayEngine::resolveTiming() {
   pending_.clear();
 }
 
+bool SelfplayEngine::fuseNow() const {
+  if(fuseRounds_ >= 0)
+    return fuseRounds_ == 1;
+  return !nn_ || (nn_->fused() && nn_->precision() == NN_FAST);
+}
+
 void SelfplayEngine::step(int rounds, hipStream_t st) {
   if(!st)
     st = stream_;
   const SearchDev& d = hd_;
+  const bool fuse = fuseNow();
   bool selected = false;  // this round's selections ran in the previous round's fused kernel
   for(int r = 0; r < rounds; r++) {
     const bool t1 = sampleNow(1);
@@ -361,7 +368,7 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
       }
     });
     const bool commitNow = (rounds_ + 1) % (uint64_t)commitInterval_ == 0 || r == rounds - 1;
-    if(fuseRounds_ && !commitNow) {
+    if(fuse && !commitNow) {
       const bool t4 = sampleNow(4);
       timedKernel(4, t4, [&](hipEvent_t a, hipEvent_t b) { launchBackupSelect(d, dd_, st, a, b); });
       selected = true;

@@ -78,8 +78,11 @@ class SelfplayEngine {
   double kernelMs_[5] = {0, 0, 0, 0, 0};
   uint64_t kernelLaunches_[5] = {0, 0, 0, 0, 0};
   // a round's backup and the next round's selection run as one kernel unless a commit
-  // comes between them (COFFEE_FUSED_ROUNDS=0 keeps them apart: same results)
-  bool fuseRounds_ = true;
+  // comes between them -- with the fast fused network or the stand-in (measured: with the
+  // corrected network, which bounds the round, the longer-lived search waves delay its
+  // workgroups: 202 vs 161 us).  COFFEE_FUSED_ROUNDS=0: never, 1: always (same results)
+  int fuseRounds_ = -1;  // -1 auto, 0 never, 1 always
+  bool fuseNow() const;
 };
 
 }  // namespace kc

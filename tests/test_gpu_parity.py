@@ -228,13 +228,12 @@ def test_selfplay_network_smoke(model_path):
     sp.close()
 
 
-def _engine(fused, **kw):
+def _engine(fused, X=5, Y=5, W=4, **kw):
     # the engine reads COFFEE_FUSED_ROUNDS when it is created
     old = os.environ.pop("COFFEE_FUSED_ROUNDS", None)
-    if not fused:
-        os.environ["COFFEE_FUSED_ROUNDS"] = "0"
+    os.environ["COFFEE_FUSED_ROUNDS"] = "1" if fused else "0"
     try:
-        return kc.Selfplay(5, 5, 4, **kw)
+        return kc.Selfplay(X, Y, W, **kw)
     finally:
         os.environ.pop("COFFEE_FUSED_ROUNDS", None)
         if old is not None:
@@ -246,14 +245,20 @@ def _engine(fused, **kw):
 # lookup hit a slot that the same round's backups write (the kResolve path).  Every game's
 # state, search tree and row must be identical.  (The oracle has no commit interval; the
 # separate kernels are pinned against it at interval 1 above.)
-@pytest.mark.parametrize("games,visits,rounds,seed,cache_log2,ci,play,net",
-                         [(64, 32, 700, 61, 5, 4, {}, False), (48, 24, 900, 67, 12, 16, PRODUCTION, False),
-                          (32, 24, 600, 71, 5, 3, dict(FORKS, side_position_prob=0.3), False),
-                          (64, 16, 500, 73, 5, 8, {}, True)],
-                         ids=["cache32-ci4", "production-ci16", "forks-side-ci3", "network-ci8"])
-def test_fused_rounds_match_separate_kernels(games, visits, rounds, seed, cache_log2, ci, play, net, model_path):
-    kw = dict(num_games=games, max_visits=visits, seed=seed, node_cap=128, commit_interval=ci,
-              nn_cache_log2=cache_log2, **play)
+@pytest.mark.parametrize("games,visits,rounds,seed,cache_log2,ci,play,net,geo",
+                         [(64, 32, 700, 61, 5, 4, {}, False, (5, 5, 4)),
+                          (48, 24, 900, 67, 12, 16, PRODUCTION, False, (5, 5, 4)),
+                          (32, 24, 600, 71, 5, 3, dict(FORKS, side_position_prob=0.3), False, (5, 5, 4)),
+                          (64, 16, 500, 73, 5, 8, {}, True, (5, 5, 4)),
+                          (48, 24, 2400, 79, 6, 4, {}, False, (7, 7, 5)),
+                          (32, 24, 3000, 83, 6, 5, PRODUCTION, False, (9, 9, 5))],
+                         ids=["cache32-ci4", "production-ci16", "forks-side-ci3", "network-ci8", "7x7-ci4",
+                              "9x9-production-ci5"])
+def test_fused_rounds_match_separate_kernels(games, visits, rounds, seed, cache_log2, ci, play, net, geo,
+                                             model_path):
+    X, Y, W = geo
+    kw = dict(X=X, Y=Y, W=W, num_games=games, max_visits=visits, seed=seed, node_cap=visits + 96,
+              commit_interval=ci, nn_cache_log2=cache_log2, **play)
     if net:
         kw["model_path"] = model_path
     a, b = _engine(True, **kw), _engine(False, **kw)
@@ -272,7 +277,7 @@ def test_fused_rounds_match_separate_kernels(games, visits, rounds, seed, cache_
             np.testing.assert_array_equal(na, nb, err_msg="round %d game %d nodes" % (done, g))
             np.testing.assert_array_equal(ea, eb, err_msg="round %d game %d edges" % (done, g))
     sa, sb = a.stats(), b.stats()
-    assert sa["games_finished"] > 0
+    assert sa["games_finished"] > 0 and sa["moves"] > 0
     for k in ("playouts", "nn_evals", "moves", "games_finished", "rows_pending"):
         assert sa[k] == sb[k], k
     ra, rb = _sorted_rows(a.drain_rows()), _sorted_rows(b.drain_rows())
