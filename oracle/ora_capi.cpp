@@ -271,10 +271,22 @@ void ora_sp_set_netfn(void* h, void (*fn)(int, const uint64_t*, float*)) {
 // CPU baseline: threads over games in select / backup (numGameThreads, selfplay.cpp:90)
 void ora_sp_set_parallel(void* h, int threads) { ((Selfplay*)h)->cfg.parallelGames = threads; }
 
+// n rounds on the device engine's schedule (selfplay.cpp SelfplayEngine::step): moves
+// are committed in rounds r with (r + 1) % commitInterval == 0 and in the call's last round.
 int ora_sp_rounds(void* h, int n) {
   Selfplay* s = (Selfplay*)h;
+  const uint64_t ci = (uint64_t)s->cfg.commitInterval;
   for(int i = 0; i < n; i++)
-    selfplayRound(*s);
+    selfplayRound(*s, ci <= 1 || (s->rounds + 1) % ci == 0 || i == n - 1);
+  return 0;
+}
+// Round schedule, before the first round: commit interval (coffee_selfplay_config
+// commit_interval) and staggered starts (start_stagger).
+int ora_sp_set_schedule(void* h, int commitInterval, int startStagger) {
+  Selfplay* s = (Selfplay*)h;
+  if(s->rounds != 0 || commitInterval < 1 || startStagger < 0)
+    return -1;
+  selfplaySchedule(*s, commitInterval, startStagger);
   return 0;
 }
 

@@ -1419,7 +1419,23 @@ struct Ctx {
 
   void finishGame();
   void commitMove();
+  void commitPending();
 };
+
+// A game in PH_COMMIT at a commit round (device kCommit search.hip:3358-3507): a
+// policy-initialisation move that ended the game finishes it (nothing searched, no rows,
+// play.cpp:1262-1264); otherwise the search's move is committed.
+void Ctx::commitPending() {
+  if(gm.root.finished) {
+    finishGame();
+    gm.gamesFinished++;
+    gm.gameNum++;
+    gm.sideNext = 0;
+    afterGame();
+    return;
+  }
+  commitMove();
+}
 
 void Ctx::commitMove() {
   int posv[MAX_P];
@@ -1755,7 +1771,7 @@ void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames) {
   }
 }
 
-void selfplayRound(Selfplay& s) {
+void selfplayRound(Selfplay& s, bool commitNow) {
   const Geom& g = s.cfg.g;
   const int G = (int)s.games.size();
   const int A = g.A;
@@ -1776,6 +1792,13 @@ void selfplayRound(Selfplay& s) {
     Ctx cx(s, gm);
     if(gm.nnDeferred) {  // the leaf (already encoded) waits for the network
       need[i] = 1;
+      continue;
+    }
+    if(gm.phase == PH_COMMIT || gm.startDelay > 0) {
+      // waits for the commit round, or for its staggered start (device kSelect)
+      if(gm.startDelay > 0)
+        gm.startDelay--;
+      gm.leafKind = LEAF_NONE;
       continue;
     }
     if(gm.phase == PH_INIT) {
@@ -1896,19 +1919,16 @@ void selfplayRound(Selfplay& s) {
     Game& gm = s.games[i];
     if(gm.nnDeferred)  // backed up in the round its row is evaluated
       continue;
+    if(gm.leafKind == LEAF_NONE)  // idle this round (PH_COMMIT or a staggered start)
+      continue;
     Ctx cx(s, gm);
     const float* o = &out[(size_t)i * (g.P + 4)];
     if(gm.leafKind == LEAF_INIT || gm.leafKind == LEAF_FORK || gm.leafKind == LEAF_SIDE) {
 #pragma omp critical(ora_rows)
       {
         if(gm.leafKind == LEAF_INIT) {
-          if(cx.initMove(o)) {  // the opening ended the game: nothing searched, no rows
-            cx.finishGame();
-            gm.gamesFinished++;
-            gm.gameNum++;
-            gm.sideNext = 0;
-            cx.afterGame();
-          }
+          if(cx.initMove(o))  // the opening ended the game: finished at the commit round
+            gm.phase = PH_COMMIT;
         } else if(gm.leafKind == LEAF_FORK) {
           cx.forkEval(o);
         } else {
@@ -1952,10 +1972,8 @@ void selfplayRound(Selfplay& s) {
           cx.addLeafValue(gm.rootIdx, r.nnWin - r.nnLoss, false, true);
         cx.noiseAndTemp(rp, gm.rootNoised.data());
         gm.phase = PH_SEARCH;
-        if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit) {
-#pragma omp critical(ora_rows)
-          cx.commitMove();
-        }
+        if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit)
+          gm.phase = PH_COMMIT;
       }
       continue;
     }
@@ -1994,10 +2012,8 @@ void selfplayRound(Selfplay& s) {
       cx.recompute(pn, 1, pn == gm.rootIdx);
     }
     gm.playouts++;
-    if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit) {
-#pragma omp critical(ora_rows)
-      cx.commitMove();
-    }
+    if(cx.N(gm.rootIdx).visits >= (uint32_t)gm.visitLimit)
+      gm.phase = PH_COMMIT;
   }
   // ---- cache write: after every read of this round; in game order, so a slot ends
   // up holding its highest-numbered evaluator (the device's atomicMax bid) ----
@@ -2011,7 +2027,32 @@ void selfplayRound(Selfplay& s) {
     s.cacheVal[2 * c.slot] = c.w;
     s.cacheVal[2 * c.slot + 1] = c.l;
   }
+  // ---- commit (device kCommit after kBackup): every game waiting in PH_COMMIT; the
+  // others stay idle until a commit round (cache writes above are staged copies, so
+  // tree reuse / compaction here cannot touch them) ----
+  if(commitNow) {
+#pragma omp parallel for schedule(dynamic, 4) num_threads(par > 1 ? par : 1) if(par > 1)
+    for(int i = 0; i < G; i++) {
+      Game& gm = s.games[i];
+      if(gm.phase != PH_COMMIT)
+        continue;
+      Ctx cx(s, gm);
+#pragma omp critical(ora_rows)
+      cx.commitPending();
+    }
+  }
   s.rounds++;
+}
+
+void selfplaySchedule(Selfplay& s, int commitInterval, int startStagger) {
+  s.cfg.commitInterval = commitInterval > 0 ? commitInterval : 1;
+  s.cfg.startStagger = startStagger > 0 ? startStagger : 0;
+  // device kInit (search.hip:3640-3646): the slot's own seeded delay
+  for(Game& gm : s.games)
+    gm.startDelay = s.cfg.startStagger > 0
+                        ? (int)(mix64(s.cfg.seed ^ 0x5a5a5a5a5a5a5a5aULL ^ (uint64_t)(s.cfg.slotBase + gm.slot)) %
+                                (uint64_t)s.cfg.startStagger)
+                        : 0;
 }
 
 }  // namespace ora

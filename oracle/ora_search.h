@@ -93,7 +93,10 @@ struct Node {
 
 enum LeafKind { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2, LEAF_CATCHUP = 3, LEAF_NOCHILD = 4, LEAF_ROOTEVAL = 5,
                LEAF_CACHED = 6, LEAF_INIT = 7, LEAF_FORK = 8, LEAF_SIDE = 9 };
-enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_INIT = 3, PH_FORK = 4, PH_SIDEEVAL = 5 };
+// PH_COMMIT: the root reached its visit limit (or a policy-init move ended the game) and
+// the game idles until the next commit round (device kBackup -> kCommit every
+// commit_interval rounds, selfplay.cpp SelfplayEngine::step)
+enum Phase { PH_ROOTEVAL = 0, PH_SEARCH = 1, PH_COMMIT = 2, PH_INIT = 3, PH_FORK = 4, PH_SIDEEVAL = 5 };
 constexpr int MAX_SIDE = 8;  // side positions queued per game (device search.h)
 
 struct TurnRec {
@@ -137,6 +140,12 @@ struct SelfplayCfg {
   int cacheLog2 = 0;       // NN evaluation cache of 2^cacheLog2 entries, 0 = off (SPEC a7)
   int nnCap = 1 << 30;     // rows per network batch; the rest wait for the next round (device kCompact)
   int parallelGames = 0;   // > 1: select / backup threads over games (CPU baseline only)
+  // Round schedule of the device engine (coffee_selfplay_config): moves are committed
+  // in rounds r with (r + 1) % commitInterval == 0 and in the last round of every
+  // rounds() call (ora_sp_rounds); startStagger > 0: each slot idles a seeded number of
+  // rounds in [0, startStagger) before its first game (the bench's staggered starts).
+  int commitInterval = 1;
+  int startStagger = 0;
 };
 
 struct Game {
@@ -180,6 +189,7 @@ struct Game {
   // playout scratch
   int leafKind = LEAF_NONE, leafNode = -1, leafSym = 0, cacheSlot = 0;
   int nnDeferred = 0;      // the leaf missed the previous batch and waits for the network
+  int startDelay = 0;      // rounds this slot still idles before its first game (startStagger)
   Board leafBoard;
   std::vector<int> pathNode, pathSlot;
   // game record
@@ -205,8 +215,11 @@ struct Selfplay {
 };
 
 void selfplayInit(Selfplay& s, const SelfplayCfg& cfg, int numGames);
-// One round = select for every game, one batched NN eval, backup for every game.
-void selfplayRound(Selfplay& s);
+// One round = select for every game, one batched NN eval, backup for every game, then
+// (commitNow) the moves of every game in PH_COMMIT.
+void selfplayRound(Selfplay& s, bool commitNow = true);
+// Sets the round schedule (before the first round): commit interval and start stagger.
+void selfplaySchedule(Selfplay& s, int commitInterval, int startStagger);
 // The deterministic stand-in network (analogue of nneval.cpp:442-500 debugSkipNeuralNet).
 void fakeNet(const Geom& g, const float* bin, float* policy, float* value, float* misc);
 void packPlanes(const Geom& g, const float* bin, uint64_t* words);

@@ -64,6 +64,7 @@ def _setup(L):
                                                                                                             ctypes.c_int]
         L.ora_sp_set_parallel.argtypes = [P, ctypes.c_int]
         L.ora_sp_set_netfn.argtypes = [P, P]
+        L.ora_sp_set_schedule.argtypes = [P, ctypes.c_int, ctypes.c_int]
         L.ora_model_free.argtypes = [P]
         _load_tables(L)
     return L
@@ -245,10 +246,16 @@ class Selfplay:
     """Round-synchronous self-play engine (select -> batched NN -> backup per round)."""
 
     def __init__(self, X, Y, W, games, max_visits, node_cap=2048, seed=1, slot_base=0, nn_mode=0, model=None,
-                 nn_threads=1, nn_cache_log2=0, nn_batch_cap=0, f64=False, **play):
+                 nn_threads=1, nn_cache_log2=0, nn_batch_cap=0, f64=False, commit_interval=1, start_stagger=0,
+                 **play):
         """play: PLAY_SETTINGS keywords (the device's coffee_search_params names).
         f64: search statistics in f64 (the reference's precision) instead of the
-        device's f32; node dumps (nodes/game_tree) are f32-layout only."""
+        device's f32; node dumps (nodes/game_tree) are f32-layout only.
+        commit_interval / start_stagger: the device engine's round schedule
+        (coffee_selfplay_config): a game whose root reached its visit limit idles
+        until the next commit round ((round + 1) % commit_interval == 0, or the last
+        round of a rounds() call, as kc.Selfplay.step commits); each slot idles a seeded
+        number of rounds in [0, start_stagger) before its first game."""
         self.L = lib(f64)
         self.f64 = f64
         self.X, self.Y, self.W, self.games = X, Y, W, games
@@ -263,6 +270,9 @@ class Selfplay:
                                      ptr(self._play), nn_batch_cap)
         if not self.h:
             raise RuntimeError("oracle selfplay create failed")
+        if commit_interval != 1 or start_stagger != 0:
+            if self.L.ora_sp_set_schedule(self.h, int(commit_interval), int(start_stagger)) != 0:
+                raise ValueError("bad schedule: commit_interval %r start_stagger %r" % (commit_interval, start_stagger))
 
     def rounds(self, n):
         self.L.ora_sp_rounds(self.h, n)

@@ -14,6 +14,8 @@ cpp/search/searchnnhelpers.cpp:39-129.
 It relies on the network being a pure function of each row's input: the same row gives
 the same logits at any batch position, batch size and workgroup variant -- asserted
 first (test_network_row_independence)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -118,8 +120,37 @@ CASES = {
 }
 
 
+def _engine(fused, X, Y, W, **kw):
+    # the engine reads COFFEE_FUSED_ROUNDS when it is created (None: its own choice)
+    old = os.environ.pop("COFFEE_FUSED_ROUNDS", None)
+    if fused is not None:
+        os.environ["COFFEE_FUSED_ROUNDS"] = "1" if fused else "0"
+    try:
+        return kc.Selfplay(X, Y, W, **kw)
+    finally:
+        os.environ.pop("COFFEE_FUSED_ROUNDS", None)
+        if old is not None:
+            os.environ["COFFEE_FUSED_ROUNDS"] = old
+
+
 @pytest.mark.parametrize("name", list(CASES))
 def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
+    _run_case(nets, name, (1, None, 0))
+
+
+# The product's round schedule with the real networks: commit interval 16 (bench.py, the
+# CLI), staggered starts, each group's NN cache shared by its games -- so a lookup's hit
+# depends on the other games' timing -- with separate and with fused round kernels
+# (the fast headline fuses; the corrected network runs them separately by default).
+# The oracle runs the same schedule (oracle.Selfplay commit_interval / start_stagger).
+@pytest.mark.parametrize("sched", [(16, False, 29), (16, True, 29)], ids=["ci16-stagger", "ci16-stagger-fused"])
+@pytest.mark.parametrize("name", ["c2-fused-nb8", "c2-corrected-two-groups"])
+def test_selfplay_real_network_scheduled_bit_exact_vs_oracle(nets, name, sched):
+    _run_case(nets, name, sched)
+
+
+def _run_case(nets, name, sched):
+    ci, fused, stagger = sched
     arch, (X, Y, W), precision, G, groups, visits, cache, cap, rounds, play = CASES[name]
     path = nets[arch]
     net = kc.Network(path, X, Y, W, precision=precision)
@@ -132,16 +163,18 @@ def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
     cap_node = 4 * visits + 32
     gpus, oras = [], []
     for k in range(groups):
-        gpus.append(kc.Selfplay(X, Y, W, num_games=G, max_visits=visits, seed=777, slot_base=k * G, model_path=path,
-                                node_cap=cap_node, commit_interval=1, nn_cache_log2=cache, nn_batch_cap=cap,
-                                nn_precision=precision, row_capacity=1 << 16, **play))
+        gpus.append(_engine(fused, X, Y, W, num_games=G, max_visits=visits, seed=777, slot_base=k * G,
+                            model_path=path, node_cap=cap_node, commit_interval=ci, start_stagger=stagger,
+                            nn_cache_log2=cache, nn_batch_cap=cap, nn_precision=precision, row_capacity=1 << 16,
+                            **play))
+        gpus[-1].enable_timing(1)
         ora = oracle.Selfplay(X, Y, W, games=G, max_visits=visits, node_cap=cap_node, seed=777, slot_base=k * G,
-                              nn_cache_log2=cache, nn_batch_cap=cap, **play)
+                              nn_cache_log2=cache, nn_batch_cap=cap, commit_interval=ci, start_stagger=stagger, **play)
         ora.set_net(device_net)
         oras.append(ora)
     sample = sorted(set(list(range(min(G, 8))) + list(np.random.default_rng(3).integers(0, G, 24))))
     done = 0
-    for chunk in [1, 30, rounds]:
+    for chunk in [1, 30, 97, rounds]:
         for gpu in gpus:  # the groups' rounds overlap on their streams
             gpu.step(chunk - done)
         for ora in oras:
@@ -164,5 +197,8 @@ def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
             if len(bad):  # which rows (slot, game, turn) and which columns differ
                 print(k, "mismatches (meta, column):", [(gr["meta"][r].tolist(), int(c)) for r, c in bad[:20]])
             np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
+        if fused is not None:  # the schedule ran as named
+            n4 = gpu.kernel_time(4)[1]
+            assert (n4 > rounds // 2) if fused else (n4 == 0), n4
         gpu.close()
     net.close()

@@ -161,9 +161,26 @@ FORKS = dict(early_fork_game_prob=0.5, early_fork_game_expected_move_prop=0.2, f
 REDUCED = dict(reduce_visits=1, reduce_visits_threshold=0.2, reduced_visits_min=8, reduced_visits_weight=0.3)
 
 
+# The round schedules the tests pin (commit interval, forced fused rounds, staggered
+# starts): interval 1 (a move is committed in the round its search ends); the product's
+# interval 16 (bench.py, the CLI) with staggered starts on separate kernels, and the same
+# with fused rounds (kBackupSelect + kResolve: the bench's fast headline).  Games whose
+# root reached its visit limit idle until the commit round; the oracle restates that
+# schedule (ora_sp_rounds), so with a shared NN cache -- where a hit depends on the
+# other games' timing -- the device is compared with the oracle on the same schedule.
+SCHEDULES = [(1, False, 0), (16, False, 37), (16, True, 37)]
+SCHEDULE_IDS = ["ci1", "ci16-stagger", "ci16-stagger-fused"]
+
+
+def _scheduled_engine(sched, X=5, Y=5, W=4, **kw):
+    ci, fused, stagger = sched
+    return _engine(fused, X, Y, W, commit_interval=ci, start_stagger=stagger, **kw)
+
+
 # cache_log2: 0 = no NN cache; 5 = a 32-entry cache, so slots are contended and
 # overwritten every round (the round-synchronous write order decides the contents);
 # 14 = hits across games (SPEC a7).  play: benchmark mode ({}) or selfplay1.cfg-like.
+@pytest.mark.parametrize("sched", SCHEDULES, ids=SCHEDULE_IDS)
 @pytest.mark.parametrize("games,visits,rounds,seed,cache_log2,play",
                          [(6, 40, 1200, 3, 0, {}), (4, 24, 900, 99, 0, {}), (8, 40, 1400, 3, 5, {}),
                           (12, 32, 1000, 7, 14, {}), (8, 40, 1200, 11, 0, PRODUCTION), (8, 32, 1200, 5, 12, REDUCED),
@@ -180,14 +197,17 @@ REDUCED = dict(reduce_visits=1, reduce_visits_threshold=0.2, reduced_visits_min=
                          ids=["bench-a", "bench-b", "cache32", "cache16k", "production", "reduced", "batch-cap",
                               "production-cap", "production-init", "policy-init", "forks", "side-positions",
                               "everything"])
-def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2, play):
+def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2, play, sched):
     cap = 128
-    gpu = kc.Selfplay(5, 5, 4, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,
-                      nn_cache_log2=cache_log2, **play)
+    if sched[0] > 1:
+        rounds *= 2  # idle rounds (commit waits, staggered starts): finish games all the same
+    gpu = _scheduled_engine(sched, num_games=games, max_visits=visits, seed=seed, node_cap=cap,
+                            nn_cache_log2=cache_log2, row_capacity=1 << 15, **play)
+    gpu.enable_timing(1)
     ora = oracle.Selfplay(5, 5, 4, games=games, max_visits=visits, node_cap=cap, seed=seed,
-                          nn_cache_log2=cache_log2, **play)
+                          nn_cache_log2=cache_log2, commit_interval=sched[0], start_stagger=sched[2], **play)
     done = 0
-    for chunk in [1, 4, 20, rounds]:
+    for chunk in [1, 4, 20, 61, rounds]:  # step ends fall inside commit intervals too
         step = chunk - done
         if step <= 0:
             continue
@@ -211,6 +231,10 @@ def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cach
     assert len(gr["meta"]) == len(orr["meta"]) > 0
     for k in orr:
         np.testing.assert_array_equal(gr[k], orr[k], err_msg=k)
+    # the schedule ran as named: fused launches (kernel 4) only in the fused schedule
+    fused_launches = gpu.kernel_time(4)[1]
+    assert (fused_launches > rounds // 2) if sched[1] else (fused_launches == 0), fused_launches
+    gpu.close()
 
 
 def test_selfplay_network_smoke(model_path):
@@ -243,8 +267,8 @@ def _engine(fused, X=5, Y=5, W=4, **kw):
 # Fused rounds (kBackupSelect + kResolve) against separate kSelect / kBackup launches:
 # with commit intervals > 1 most rounds run fused, and a 32-entry cache has nearly every
 # lookup hit a slot that the same round's backups write (the kResolve path).  Every game's
-# state, search tree and row must be identical.  (The oracle has no commit interval; the
-# separate kernels are pinned against it at interval 1 above.)
+# state, search tree and row must be identical.  (Both are also pinned against the oracle
+# on the same schedule: test_selfplay_fake_net_bit_exact_vs_oracle's ci16 cases.)
 @pytest.mark.parametrize("games,visits,rounds,seed,cache_log2,ci,play,net,geo",
                          [(64, 32, 700, 61, 5, 4, {}, False, (5, 5, 4)),
                           (48, 24, 900, 67, 12, 16, PRODUCTION, False, (5, 5, 4)),
@@ -355,12 +379,15 @@ def _compare_game(gpu, ora, g, og, done):
                           (9, 9, 5, 4, 24, 1500, 7, 0, {}), (9, 9, 5, 6, 20, 1500, 11, 12,
                                                              dict(PRODUCTION, side_position_prob=0.2, **FORKS))],
                          ids=["7x7-bench", "7x7-production", "9x9-bench", "9x9-everything"])
-def test_selfplay_geometries_bit_exact_vs_oracle(X, Y, W, games, visits, rounds, seed, cache_log2, play):
+@pytest.mark.parametrize("sched", [SCHEDULES[0], SCHEDULES[2]], ids=[SCHEDULE_IDS[0], SCHEDULE_IDS[2]])
+def test_selfplay_geometries_bit_exact_vs_oracle(X, Y, W, games, visits, rounds, seed, cache_log2, play, sched):
     cap = 128
-    gpu = kc.Selfplay(X, Y, W, num_games=games, max_visits=visits, seed=seed, node_cap=cap, commit_interval=1,
-                      nn_cache_log2=cache_log2, **play)
+    if sched[0] > 1:
+        rounds *= 2
+    gpu = _scheduled_engine(sched, X, Y, W, num_games=games, max_visits=visits, seed=seed, node_cap=cap,
+                            nn_cache_log2=cache_log2, row_capacity=1 << 15, **play)
     ora = oracle.Selfplay(X, Y, W, games=games, max_visits=visits, node_cap=cap, seed=seed,
-                          nn_cache_log2=cache_log2, **play)
+                          nn_cache_log2=cache_log2, commit_interval=sched[0], start_stagger=sched[2], **play)
     done = 0
     for chunk in [1, 7, 200, rounds]:
         gpu.step(chunk - done)
@@ -422,21 +449,28 @@ def test_tree_position_weight_above_one_rejected():
                     record_tree_target_weight=1.5)
 
 
-def test_selfplay_full_scale_sampled_slots_bit_exact():
+@pytest.mark.parametrize("sched", [(1, False, 0), (16, True, 600)], ids=["ci1", "ci16-stagger-fused"])
+def test_selfplay_full_scale_sampled_slots_bit_exact(sched):
     """C2 scale on the device (4096 games, 600 visits, node_cap 2048, deep trees) with
     the stand-in network; 12 sampled slots replayed one by one in the oracle from the
     same per-slot streams (slot_base).  Games are independent once the NN cache is off
-    and the batch cap never binds (cap = games), so each slot must match exactly."""
+    and the batch cap never binds (cap = games), so each slot must match exactly -- also
+    on the bench's schedule (commit interval 16, fused rounds, staggered starts), which
+    the oracle restates per slot."""
     G, visits, rounds, cap = 4096, 600, 2600, 2048
-    gpu = kc.Selfplay(5, 5, 4, num_games=G, max_visits=visits, seed=2025, node_cap=cap, commit_interval=1,
-                      nn_cache_log2=0, nn_batch_cap=G)
-    gpu.step(rounds)
+    ci, fused, stagger = sched
+    gpu = _engine(fused, 5, 5, 4, num_games=G, max_visits=visits, seed=2025, node_cap=cap, commit_interval=ci,
+                  nn_cache_log2=0, nn_batch_cap=G, start_stagger=stagger)
+    for chunk in (rounds // 2, rounds - rounds // 2):  # the bench steps in chunks
+        gpu.step(chunk)
     st = gpu.stats()
     assert st["errors"] == 0 and st["moves"] >= G  # every game committed moves
     slots = [0, 1, 17, 511, 777, 1024, 2047, 2048, 3000, 3333, 4000, 4095]
     for s in slots:
-        ora = oracle.Selfplay(5, 5, 4, games=1, max_visits=visits, node_cap=cap, seed=2025, slot_base=s)
-        ora.rounds(rounds)
+        ora = oracle.Selfplay(5, 5, 4, games=1, max_visits=visits, node_cap=cap, seed=2025, slot_base=s,
+                              commit_interval=ci, start_stagger=stagger)
+        ora.rounds(rounds // 2)
+        ora.rounds(rounds - rounds // 2)
         _compare_game(gpu, ora, s, 0, rounds)
     gpu.close()
 

@@ -258,3 +258,46 @@ def test_external_network_hook_matches_builtin():
     assert len(ra["meta"]) > 0
     for k in ra:
         np.testing.assert_array_equal(ra[k], rb[k])
+
+
+def _games_rows(r):
+    """rows keyed by (slot, game number), each game's rows in turn order"""
+    out = {}
+    meta = r["meta"]
+    for key in {(int(m[0]), int(m[1])) for m in meta}:
+        sel = np.flatnonzero((meta[:, 0] == key[0]) & (meta[:, 1] == key[1]))
+        sel = sel[np.argsort(meta[sel, 2], kind="stable")]
+        out[key] = {k: v[sel] for k, v in r.items()}
+    return out
+
+
+def test_commit_interval_and_stagger_delay_but_do_not_change_independent_games():
+    """The device's round schedule (commit_interval, start_stagger) restated: a game whose
+    root reached its visit limit idles until the commit round, and a staggered slot idles
+    before its first game.  With nothing shared between games (NN cache off, batch cap not
+    binding) this only shifts each game in time: every game both runs finish has the same
+    rows.  (With a shared NN cache it does not hold -- hits depend on the other games'
+    timing; the GPU tests pin that case against the oracle run on the same schedule.)"""
+    kw = dict(games=6, max_visits=24, node_cap=128, seed=31)
+    a = oracle.Selfplay(5, 5, 4, **kw)
+    b = oracle.Selfplay(5, 5, 4, commit_interval=16, start_stagger=200, **kw)
+    for n in (5, 100, 1500):  # commits also fall on the last round of every rounds() call
+        a.rounds(n)
+        b.rounds(n)
+    ga, gb = _games_rows(a.rows()), _games_rows(b.rows())
+    both = set(ga) & set(gb)
+    assert len(both) >= 6 and len(gb) < len(ga)  # b lost rounds to idling
+    for key in both:
+        for k in ga[key]:
+            np.testing.assert_array_equal(ga[key][k], gb[key][k], err_msg="%s %s" % (key, k))
+    # at the end of a rounds() call every game has been committed: none waits in PH_COMMIT
+    assert all(b.info(g)["phase"] != 2 for g in range(6))
+    # the idle rounds: fewer playouts than rounds for b, one per round (after the root
+    # evaluations) for a
+    assert sum(b.info(g)["playouts"] for g in range(6)) < sum(a.info(g)["playouts"] for g in range(6))
+
+
+def test_schedule_rejected_after_first_round():
+    sp = oracle.Selfplay(5, 5, 4, games=2, max_visits=8, node_cap=64, seed=1)
+    sp.rounds(1)
+    assert sp.L.ora_sp_set_schedule(sp.h, 16, 0) != 0
