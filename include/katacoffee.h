@@ -102,18 +102,26 @@ int coffee_model_flops(const char* path, int area, double* flops);
 int coffee_nn_create(const char* model_path, int x, int y, int win_len, coffee_nn** out);
 /* precision (the reference's useFP16 switch, nninterface.h:76-88; its default, Auto,
  * setup.cpp:240-248, maps here to the path that meets the north-star 1e-3 of fp32):
- *   COFFEE_NN_DEFAULT       (0) the 1e-3 path: CORRECTED where the fused kernel covers the
- *                           net (b6c96 @ 5x5), the layered split (ACCURATE) kernels otherwise
+ *   COFFEE_NN_DEFAULT       (0) the 1e-3 path: where the fused kernel covers the net (b6c96
+ *                           @ 5x5), CORRECTED if a load-time calibration batch (corrected vs
+ *                           accurate on 256 seeded positions) differs by at most 2.5e-4 and
+ *                           flags no board, else ACCURATE; the layered split (ACCURATE)
+ *                           kernels for every other net (coffee_nn_precision reports it)
  *   COFFEE_NN_ACCURATE      fp16 hi/lo operand pairs on three MFMAs (the fused kernel's
  *                           split instance where it covers the net, the layered kernels
  *                           otherwise): logits within ~1e-5 of the fp32 (Eigen-semantics) forward
  *   COFFEE_NN_FAST_LAYERED  fp16 operands on the layered kernels (any architecture)
  *   COFFEE_NN_CORRECTED     fp16 products plus the two fp16-rounding cross terms on
- *                           block-scaled e4m3 MFMAs (twice the fp16 MFMA work): e4m3 operands
- *                           carry power-of-two scales per output channel (weights) and per
- *                           board (activations), so nothing saturates at any magnitude;
- *                           within 1e-3 of fp32 on trained nets; the fused kernel where it
- *                           covers the net, else as ACCURATE
+ *                           block-scaled e4m3 MFMAs (twice the fp16 MFMA work): the weights'
+ *                           e4m3 operands carry one power-of-two exponent per convolution
+ *                           (its largest |w| lands in (224, 448], so no weight saturates);
+ *                           activations are unscaled, and a board with a convolution input
+ *                           past e4m3's 448 is flagged and re-evaluated on the ACCURATE
+ *                           instance in a second launch.  A product is good to ~2^-14, so
+ *                           the error grows with the logits: 7e-4 of fp32 on a net trained
+ *                           200 steps (logits ~20), ~1e-3 after 1000 -- not
+ *                           a 1e-3 path for every net, hence DEFAULT's calibration.  The
+ *                           fused kernel where it covers the net, else as ACCURATE
  *   COFFEE_NN_ACCURATE_NB2  ACCURATE on the 2-board bordered fused instance (A/B reference
  *                           of the borderless 5-board one; same results bit for bit)
  *   COFFEE_NN_FAST          fp16 MFMA operands, f32 accumulation and residual trunk (the

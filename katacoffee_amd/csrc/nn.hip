@@ -1801,23 +1801,30 @@ NNEngine::NNEngine(const ModelHost& m, int X, int Y, int W, int path) : cfg_(m.c
   flops_ = modelFlopsPerEval(cfg_, X * Y);
   if(path < NN_DEFAULT || path > NN_FAST)
     throw std::invalid_argument("NNEngine: unknown precision/path");
-  if(path != NN_DEFAULT) {
-    build(m, path);
-    return;
-  }
-  // the default (north-star 1e-3) precision: the corrected instance, unless on the
-  // calibration batch its logits differ from the accurate (split) instance's by more than
-  // NN_AUTO_TOL or any board needs the re-evaluation (activations past e4m3's range) --
-  // corrected products are good to ~2^-14 relative, which deep-trained nets with large
-  // logits push towards 1e-3; the split path is good to ~2^-21
-  build(m, NN_CORRECTED);
-  if(layered_)
-    return;  // the layered kernels run "corrected" as the split path already
-  int hotBoards = 0;
-  calibErr_ = calibrationError(*fallbackNet_, &hotBoards);
-  if(!(calibErr_ <= NN_AUTO_TOL) || hotBoards > 0) {
+  // a constructor that throws runs no destructor: whatever build() or the calibration
+  // allocated before the failure is released here (this path also runs on every hot reload)
+  try {
+    if(path != NN_DEFAULT) {
+      build(m, path);
+      return;
+    }
+    // the default (north-star 1e-3) precision: the corrected instance, unless on the
+    // calibration batch its logits differ from the accurate (split) instance's by more than
+    // NN_AUTO_TOL or any board needs the re-evaluation (activations past e4m3's range) --
+    // corrected products are good to ~2^-14 relative, which deep-trained nets with large
+    // logits push towards 1e-3; the split path is good to ~2^-21
+    build(m, NN_CORRECTED);
+    if(layered_)
+      return;  // the layered kernels run "corrected" as the split path already
+    int hotBoards = 0;
+    calibErr_ = calibrationError(*fallbackNet_, &hotBoards);
+    if(!(calibErr_ <= NN_AUTO_TOL) || hotBoards > 0) {
+      release();
+      build(m, NN_ACCURATE);
+    }
+  } catch(...) {
     release();
-    build(m, NN_ACCURATE);
+    throw;
   }
 }
 

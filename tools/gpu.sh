@@ -10,6 +10,8 @@
 #   prof             tools/profile_r03.sh (rocprofv3 trace + PMC passes)
 #   prof4=SECTIONS   tools/profile_r04.sh (comma-separated sections: prof4=c2,corrected,c4,c4pmc)
 #   prof5=SECTIONS   tools/profile_r05.sh (the same sections named r05_*, plus compliant, c3default, lines34)
+#   prof6=SECTIONS   tools/profile_r06.sh (traces c2, c2default, c3default, c4default; lines main, prodline,
+#                    c3line, c4line, c5line)
 #   run=CMD          any other command (comma-separated words), e.g. run=tools/_build/nn_phase,960
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -44,6 +46,8 @@ for step in "$@"; do
       timeout -k 10 1100 bash tools/profile_r04.sh ${arg//,/ } > $log 2>&1 ;;
     prof5)
       timeout -k 10 1150 bash tools/profile_r05.sh ${arg//,/ } > $log 2>&1 ;;
+    prof6)
+      timeout -k 10 1150 bash tools/profile_r06.sh ${arg//,/ } > $log 2>&1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

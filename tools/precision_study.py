@@ -87,6 +87,23 @@ def quant_conv(x, w, scheme, conv):
         sw = f8exp(w.abs().max())
         HOT[0] = HOT[0] | (x.abs().flatten(1).max(1).values > 448)
         return conv(xh, wh) + conv(r8(xh), e4m3s(wl * S, sw) / S) + conv(r8(xl * S) / S, e4m3s(wh, sw))
+    if scheme in ("f8cs_xex", "f8cs_wex", "f8mx", "f8bx"):
+        sw = f8exp(w.abs().max())
+        HOT[0] = HOT[0] | (x.abs().flatten(1).max(1).values > 448)
+        if scheme == "f8cs_xex":  # only the weights' e4m3 rounding in the cross terms
+            return conv(xh, wh) + conv(xh, e4m3s(wl * S, sw) / S) + conv(xl, e4m3s(wh, sw))
+        if scheme == "f8cs_wex":  # only the activations' e4m3 rounding in the cross terms
+            return conv(xh, wh) + conv(r8(xh), wl) + conv(r8(xl * S) / S, wh)
+        if scheme == "f8bx":  # one exponent per board for hi(x) and one for lo(x)
+            def sc(v):
+                return e4m3s(v, f8exp(v.abs().flatten(1).max(1).values)[:, None, None, None])
+        else:  # per (board, position, 32-channel group) exponents: MX blocks along channels
+            def sc(v):
+                n, c, h, ww = v.shape
+                g = v.reshape(n, c // 32, 32, h, ww) if c % 32 == 0 else v.reshape(n, 1, c, h, ww)
+                m = g.abs().amax(2, keepdim=True)
+                return e4m3s(g, f8exp(m)).reshape(n, c, h, ww)
+        return conv(xh, wh) + conv(sc(xh), e4m3s(wl * S, sw) / S) + conv(sc(xl * S) / S, e4m3s(wh, sw))
     if scheme == "f8cw":
         return conv(xh, wh) + conv(r8(x), r8(wl * S) / S)
     raise ValueError(scheme)
@@ -98,7 +115,7 @@ HOT = [False]  # f8cs: boards with an activation past e4m3's range (re-evaluated
 def forward(net, binp, glob, schemes):
     """train.CoffeeNet.forward in float64 with per-convolution operand rounding (f8cs:
     hot boards take the exact forward's outputs)."""
-    if "f8cs" in schemes:
+    if any(s.startswith("f8cs") or s in ("f8mx", "f8bx") for s in schemes):
         HOT[0] = torch.zeros(len(binp), dtype=torch.bool)
         out = forward_(net, binp, glob, schemes)
         if HOT[0].any():
@@ -180,6 +197,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--big-act", type=float, default=0.0)
     ap.add_argument("--hot", type=float, default=0.0)
+    ap.add_argument("--schemes", default="f16,wsplit,asplit,f8cw,f8c,f8cs,f8cs_xex,f8cs_wex,f8bx,f8mx,split3")
     args = ap.parse_args()
     net, batch = trained_net(args.steps)
     if args.big_act:
@@ -197,7 +215,7 @@ def main():
     with torch.no_grad():
         ref = forward(net, binp, glob, ["f32"] * nconv)
         print("n=%d max|logit| %.3f" % (len(ref), ref.abs().max().item()))
-        for sch in ("f16", "wsplit", "asplit", "f8cw", "f8c", "f8cs", "split3"):
+        for sch in args.schemes.split(","):
             out = forward(net, binp, glob, [sch] * nconv)
             e = (out - ref).abs()
             print("%-7s max err %.3e  (policy %.3e, value %.3e, misc %.3e)" % (

@@ -1,0 +1,37 @@
+# round-6 profiles and bench lines (GPU box): rocprofv3 kernel traces of bench lines,
+# reduced in place by tools/reduce_profile.py, and the JSON lines of every config.
+# Sections: bash tools/profile_r06.sh c2 c2default c3default c4default lines prodline
+# Each GPU step has its own time limit; the first failing step ends the script.
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+run() { "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
+trace() {  # name, bench args...
+  local name=$1
+  shift
+  run timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line --trained-steps 0 "$@" > gpurun_out/prof_$name.log 2>&1
+  run python tools/reduce_profile.py trace gpurun_out/prof_$name $name
+  grep '^{' gpurun_out/prof_$name.log > gpurun_out/prof_$name.line.json || true
+}
+line() {  # name, limit, bench args...
+  local name=$1 lim=$2
+  shift 2
+  run timeout -k 10 $lim python -u bench.py "$@" > gpurun_out/line_r06_$name.log 2>&1
+  grep '^{' gpurun_out/line_r06_$name.log > gpurun_out/line_r06_$name.json || true
+  echo "== line $name"
+}
+for s in "$@"; do
+  case $s in
+    c2) trace r06_c2 --steps 20 --warmup 5 ;;
+    c2default) trace r06_c2default --steps 20 --warmup 5 --precision default ;;
+    c3default) trace r06_c3default --config C3 --steps 10 --warmup 5 ;;
+    c4default) trace r06_c4default --config C4 --window short --warmup 8 --steps 6 --rounds-per-step 200 ;;
+    main) line c2 600 --steps 20 --warmup 5 ;;
+    prodline) line c2prod 600 --steps 20 --warmup 5 --play production --no-cpu-baseline --trained-steps 0 ;;
+    c3line) line c3 700 --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    c4line) line c4 500 --config C4 --steps 6 --warmup 5 --no-cpu-baseline ;;
+    c5line) line c5 500 --config C5 --steps 4 --warmup 2 --rounds-per-step 600 --no-cpu-baseline ;;
+    *) echo "unknown section $s"; exit 2 ;;
+  esac
+done
+find gpurun_out/prof_r06_* -type f 2>/dev/null | head -60
