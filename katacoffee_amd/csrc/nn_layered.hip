@@ -243,6 +243,39 @@ KC_D void convEpilogue(const LConvArgs& a, const lf32x4 (&acc)[TM][TN], int base
   }
 }
 
+// Cycle accounting of kConvLB and kConvL (profiling build, `make prof`; tools/convl_phase.py): wave 0
+// of every workgroup adds its cycles per phase into g_convlProf (one atomic per slot and
+// workgroup): 0 workgroups, 1 total, 2 prologue (entry to the first K-step), 3 weight
+// waits (vmcnt + barrier per tap group; kConvL: the barrier per slice), 4 stage stores (incl. the wait for the slice's
+// loads), 5 epilogue.
+#ifdef KC_SEARCH_PROFILE
+__device__ unsigned long long g_convlProf[8];
+#define CLP_NOW() clock64()
+#define CLP_ADD(i, v)                                                  \
+  do {                                                                 \
+    if(tid == 0)                                                       \
+      atomicAdd(&g_convlProf[(i)], (unsigned long long)(v));           \
+  } while(0)
+#else
+#define CLP_NOW() 0ll
+#define CLP_ADD(i, v) \
+  do {                \
+  } while(0)
+#endif
+
+// Same-box A/B switches (tools/build_variant.sh): KC_CONVL_LATE_PRO 1 requests the first
+// slice and weights after the prologue's barrier, KC_CONVL_LATE_STORE 1 runs the next
+// slice's prologue after the last tap (both: the round-5 kernel); KC_CONVL_STORE_TAP the
+// tap before which it runs otherwise
+#ifndef KC_CONVL_LATE_PRO
+#define KC_CONVL_LATE_PRO 0
+#endif
+#ifndef KC_CONVL_LATE_STORE
+#define KC_CONVL_LATE_STORE 0
+#endif
+#ifndef KC_CONVL_STORE_TAP
+#define KC_CONVL_STORE_TAP 5
+#endif
 template <int X, int Y, int KT, int TN, bool SPLIT, int WN>
 __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   using G = LGeo<X, Y>;
@@ -257,12 +290,43 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     return;
   const int nb = min(G::BPW, count - base);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const long long tEntry = CLP_NOW();
+  long long tWait = 0, tStore = 0;
   const int wm = wave / WN, wn = wave % WN;
   const int ctBase = blockIdx.y * NCT + wn * TN;  // this wave's first global column tile
   char* stage = smem;                                        // [2][PLANES][STAGE]
   float* sS = reinterpret_cast<float*>(smem + 2 * PLANES * G::stage(SPLIT));  // [cin]
   float* sB = sS + a.cin;
   float* sG = sB + a.cin;  // [BPW][gbLd]
+  const int NCB = a.cin / 32;
+  // B fragments: step s = cb*T + tap; a ring of R register slots loaded R-1 steps
+  // ahead (3x3: R = 3, slot = tap % 3 since 9 % 3 == 0; 1x1: R = 2, slot = cb & 1)
+  constexpr int R = T % 3 == 0 ? 3 : 2;
+  const lh16x8* wl = a.w + (size_t)ctBase * 64 + lane;
+  const lh16x8* wlo = SPLIT ? a.wlo + (size_t)ctBase * 64 + lane : nullptr;
+  const size_t stepStride = (size_t)a.coutTiles * 64;
+  lh16x8 bh[R][TN], bl[R][SPLIT ? TN : 1];
+  auto loadB = [&](int s, int slot) {
+#pragma unroll
+    for(int c = 0; c < TN; c++) {
+      bh[slot][c] = wl[(size_t)s * stepStride + c * 64];
+      if constexpr(SPLIT)
+        bl[slot][c] = wlo[(size_t)s * stepStride + c * 64];
+    }
+  };
+  const int S = NCB * T;
+  StageRegs<G> sr;
+#if !KC_CONVL_LATE_PRO
+  // the first slice's activations and the first K steps' weights are requested before the
+  // LDS clear and the parameter copy, so their latency overlaps them (round 5 issued them
+  // after that barrier: 10.2 k of the split conv's 100.9 k cycles per workgroup were its
+  // prologue, tools/convl_phase.py)
+  stageLoad<G>(a, sr, 0, base, nb, tid);
+#pragma unroll
+  for(int i = 0; i < R - 1; i++)
+    if(i < S)
+      loadB(i, i);
+#endif
   // zero both stages (borders and boards past the batch stay zero), parameters to LDS
   for(int i = tid; i < 2 * PLANES * G::stage(SPLIT) / 16; i += L_NT)
     reinterpret_cast<uint4*>(smem)[i] = uint4{0u, 0u, 0u, 0u};
@@ -275,9 +339,9 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     for(int i = tid; i < nb * a.gbLd; i += L_NT)
       sG[i] = a.gb[(size_t)base * a.gbLd + i];
   __syncthreads();
-  const int NCB = a.cin / 32;
-  StageRegs<G> sr;
+#if KC_CONVL_LATE_PRO
   stageLoad<G>(a, sr, 0, base, nb, tid);
+#endif
   stageStore<G, SPLIT>(a, sr, stage, stage + G::stage(SPLIT), 0, base, nb, sS, sB, sG, tid);
 
   // per-lane A row bases (bytes, shifted to the (-r,-r) neighbour), padding rows -> row 0
@@ -299,26 +363,12 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     for(int c = 0; c < TN; c++)
       acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-  // B fragments: step s = cb*T + tap; a ring of R register slots loaded R-1 steps
-  // ahead (3x3: R = 3, slot = tap % 3 since 9 % 3 == 0; 1x1: R = 2, slot = cb & 1)
-  constexpr int R = T % 3 == 0 ? 3 : 2;
-  const lh16x8* wl = a.w + (size_t)ctBase * 64 + lane;
-  const lh16x8* wlo = SPLIT ? a.wlo + (size_t)ctBase * 64 + lane : nullptr;
-  const size_t stepStride = (size_t)a.coutTiles * 64;
-  lh16x8 bh[R][TN], bl[R][SPLIT ? TN : 1];
-  auto loadB = [&](int s, int slot) {
-#pragma unroll
-    for(int c = 0; c < TN; c++) {
-      bh[slot][c] = wl[(size_t)s * stepStride + c * 64];
-      if constexpr(SPLIT)
-        bl[slot][c] = wlo[(size_t)s * stepStride + c * 64];
-    }
-  };
-  const int S = NCB * T;
+#if KC_CONVL_LATE_PRO
 #pragma unroll
   for(int i = 0; i < R - 1; i++)
     if(i < S)
       loadB(i, i);
+#endif
   __syncthreads();
 
   // one K step: tap of slice cb from the stage at stHi/stLo, B slot `slot`
@@ -353,19 +403,36 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
     const char* stLo = stHi + G::stage(SPLIT);
     if(cb + 1 < NCB)
       stageLoad<G>(a, sr, cb + 1, base, nb, tid);
+    // the next slice's prologue (BN-ReLU, hi/lo split, LDS stores into the other stage,
+    // which no wave reads during this slice) runs between this slice's taps STORE_TAP - 1
+    // and STORE_TAP, so its VALU work and LDS writes overlap the MFMAs in flight instead
+    // of running after them (round 5: after the last tap, 9.1 k cycles per workgroup)
+    constexpr int STORE_TAP = KC_CONVL_LATE_STORE ? T : (T % 3 == 0 ? KC_CONVL_STORE_TAP : T);
+    auto storeNext = [&]() {
+      if(cb + 1 < NCB) {
+        char* nHi = stage + ((cb + 1) & 1) * PLANES * G::stage(SPLIT);
+        const long long t0 = CLP_NOW();
+        stageStore<G, SPLIT>(a, sr, nHi, nHi + G::stage(SPLIT), cb + 1, base, nb, sS, sB, sG, tid);
+        tStore += CLP_NOW() - t0;
+      }
+    };
     if constexpr(T % 3 == 0) {
 #pragma unroll
-      for(int tap = 0; tap < T; tap++)
+      for(int tap = 0; tap < T; tap++) {
+        if(tap == STORE_TAP)
+          storeNext();
         step(cb, tap, tap % 3, stHi, stLo);
+      }
     } else {
       step(cb, 0, parity, stHi, stLo);
     }
-    if(cb + 1 < NCB) {
-      char* nHi = stage + ((cb + 1) & 1) * PLANES * G::stage(SPLIT);
-      stageStore<G, SPLIT>(a, sr, nHi, nHi + G::stage(SPLIT), cb + 1, base, nb, sS, sB, sG, tid);
-    }
+    if(STORE_TAP == T)
+      storeNext();
+    const long long t1 = CLP_NOW();
     __syncthreads();
+    tWait += CLP_NOW() - t1;
   };
+  const long long tLoop = CLP_NOW();
   int cb = 0;
   for(; cb + 1 < NCB; cb += 2) {
     slice(cb, 0);
@@ -374,28 +441,21 @@ __global__ void __launch_bounds__(L_NT, 2) kConvL(LConvArgs a) {
   if(cb < NCB)
     slice(cb, 0);
 
+  const long long tEpi = CLP_NOW();
   convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
+  CLP_ADD(0, 1);
+  CLP_ADD(1, CLP_NOW() - tEntry);
+  CLP_ADD(2, tLoop - tEntry);
+  CLP_ADD(3, tWait);
+  CLP_ADD(4, tStore);
+  CLP_ADD(5, CLP_NOW() - tEpi);
+  (void)tEntry;
+  (void)tLoop;
+  (void)tEpi;
+  (void)tWait;
+  (void)tStore;
 }
 
-// Cycle accounting of kConvLB (profiling build, `make prof`; tools/convl_phase.py): wave 0
-// of every workgroup adds its cycles per phase into g_convlProf (one atomic per slot and
-// workgroup): 0 workgroups, 1 total, 2 prologue (entry to the first K-step), 3 weight
-// waits (vmcnt + barrier per tap group), 4 stage stores (incl. the wait for the slice's
-// loads), 5 epilogue.
-#ifdef KC_SEARCH_PROFILE
-__device__ unsigned long long g_convlProf[8];
-#define CLP_NOW() clock64()
-#define CLP_ADD(i, v)                                                  \
-  do {                                                                 \
-    if(tid == 0)                                                       \
-      atomicAdd(&g_convlProf[(i)], (unsigned long long)(v));           \
-  } while(0)
-#else
-#define CLP_NOW() 0ll
-#define CLP_ADD(i, v) \
-  do {                \
-  } while(0)
-#endif
 
 // 3x3 fast convolutions with the weights in LDS: the workgroup's B fragments of three
 // taps (3 x NCT pieces of 1 KiB) stream by LDS-DMA into one of two ring slots, so

@@ -1,4 +1,4 @@
-"""Cycle accounting of the layered 3x3 conv kernel (kConvLB) over network forwards of
+"""Cycle accounting of the layered 3x3 conv kernel (kConvLB, or kConvL with --precision accurate) over network forwards of
 random positions: per workgroup, the cycles of its prologue, weight waits (vmcnt +
 barrier per tap group), slice stage stores (with the wait for the slice's loads) and
 epilogue, against the MFMA issue floor of its K loop.
@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--board", type=int, default=5)
     ap.add_argument("--n", default="4450")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--precision", default="fast", help="fast: kConvLB (fast-layered); accurate: kConvL split")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -33,7 +34,7 @@ def main():
     A = X * Y
     path = os.path.join(tempfile.mkdtemp(), "m.cfnn")
     kc.write_random_model(a.arch, 1, path)
-    net = kc.Network(path, X, Y, W, precision="fast")
+    net = kc.Network(path, X, Y, W, precision=a.precision)
     prof = (ctypes.c_ulonglong * 8)()
     for n in [int(v) for v in a.n.split(",")]:
         rng = np.random.default_rng(0)
@@ -56,8 +57,8 @@ def main():
         names = ["total", "prologue", "weight waits", "stage stores", "epilogue"]
         row = {nm: prof[i + 1] / wgs for i, nm in enumerate(names)}
         row["k loop rest"] = row["total"] - sum(row[k] for k in names[1:])
-        print("%s %dx%d n=%d: %d kConvLB workgroups/forward; cycles per workgroup: %s" %
-              (a.arch, X, Y, n, prof[0] // a.iters, ", ".join("%s %.0f" % (k, v) for k, v in row.items())),
+        print("%s %dx%d n=%d %s: %d %s workgroups/forward; cycles per workgroup: %s" %
+              (a.arch, X, Y, n, a.precision, prof[0] // a.iters, "kConvLB" if a.precision.startswith("fast") else "kConvL", ", ".join("%s %.0f" % (k, v) for k, v in row.items())),
               flush=True)
     net.close()
 
