@@ -215,7 +215,10 @@ def trained_model(kc, torch, cfg, steps, src_model, path, seed):
         pol, val, misc = net(batch["binp"][:2048], batch["glob"][:2048])
         mx = max(float(t.abs().max()) for t in (pol, val, misc))
     train.save_cfnn(net.cpu(), path)
-    return {"adam_steps": steps, "minibatch": min(512, n), "rows": n, "selfplay": "512 games x 64 visits, random-init net",
+    h = kc.Network(path, X, Y, W, precision="default")
+    resolved, calib = h.precision  # the load-time calibration
+    h.close()
+    return {"default_resolves_to": resolved, "calibration_max_abs_diff": calib, "adam_steps": steps, "minibatch": min(512, n), "rows": n, "selfplay": "512 games x 64 visits, random-init net",
             "final_losses": {"policy": losses[0], "value": losses[1]} if losses else None,
             "max_abs_logit_on_rows": mx, "seconds": time.perf_counter() - t0}
 
@@ -799,7 +802,7 @@ def main():
 
     out = measure(args.precision, True)
 
-    def window(comp, tolerance):
+    def side_window(comp, tolerance):
         return {"precision": "default -> %s" % comp["config"]["precision"], "dtype": comp["dtype"],
                 "value": comp["value"], "unit": comp["unit"],
                 "value_kind": comp["value_kind"], "ms_per_step": comp["ms_per_step"],
@@ -815,8 +818,11 @@ def main():
         comp = measure("default", False)
         if rank == 0:
             compliant = comp
-            out["compliant"] = window(comp, "logits within 1e-3 absolute of fp32 (tests/test_gpu_train.py, "
+            out["compliant"] = side_window(comp, "logits within 1e-3 absolute of fp32 (tests/test_gpu_train.py, "
                                             "tests/test_gpu_nn.py)")
+            h = kc.Network(model_path, X, Y, W, precision="default")
+            out["compliant"]["calibration_max_abs_diff"] = h.precision[1]
+            h.close()
     if args.trained_steps > 0:
         # the same precision on a trained net: the calibration then decides on the nets
         # production loads (cpp/program/setup.cpp:240-248 useFP16 auto)
@@ -830,7 +836,7 @@ def main():
                 open(tpath, "wb").write(data)
         comp = measure("default", False, tpath)
         if rank == 0:
-            out["compliant_trained"] = window(comp, "logits within 1e-3 absolute of fp32 "
+            out["compliant_trained"] = side_window(comp, "logits within 1e-3 absolute of fp32 "
                                                     "(tests/test_gpu_train.py, trained b6c96)")
             out["compliant_trained"]["trained_net"] = info
     if rank == 0:
