@@ -463,7 +463,8 @@ class Groups:
         out = {}
         for e in self.g:
             for k, v in e.stats().items():
-                out[k] = (max(out.get(k, 0), v) if k in ("edge_pool_peak", "edge_pool_cap", "nn_precision")
+                out[k] = (max(out.get(k, 0), v) if k in ("edge_pool_peak", "edge_pool_cap", "nn_precision",
+                                                          "nn_audit_max_diff")
                           else out.get(k, 0) + v)
         return out
 
@@ -790,6 +791,9 @@ def main():
                 # node-pool / edge-pool headroom of the run (the edge pool is sized
                 # by a heuristic; its peak use is reported beside its capacity)
                 "edge_pool": {"peak_entries": s1["edge_pool_peak"], "cap_entries": s1["edge_pool_cap"]},
+                # the default precision's audit on self-play's own batches (corrected instance only)
+                "nn_audit": {"audited_launches": s1["nn_audits"], "max_abs_diff_vs_accurate": s1["nn_audit_max_diff"],
+                             "switches_to_accurate": s1["nn_audit_switches"]},
                 "kernels": kernels,
                 "roofline": roof or None,
                 "roofline_all": roof_all,
@@ -807,7 +811,8 @@ def main():
                 "value": comp["value"], "unit": comp["unit"],
                 "value_kind": comp["value_kind"], "ms_per_step": comp["ms_per_step"],
                 "playouts_per_sec": comp["playouts_per_sec"], "rows_written_npz": comp["rows_written_npz"],
-                "tolerance": tolerance, "roofline": comp["roofline"], "kernels": comp["kernels"]}
+                "tolerance": tolerance, "nn_audit": comp["nn_audit"], "roofline": comp["roofline"],
+                "kernels": comp["kernels"]}
 
     compliant = out if args.precision == "default" else None
     if args.compliant_line and args.precision == "fast":

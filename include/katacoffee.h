@@ -281,6 +281,13 @@ typedef struct coffee_selfplay_stats {
   uint64_t edge_pool_peak;  /* largest edge-pool use of any slot so far (entries) */
   uint64_t edge_pool_cap;   /* edge-pool entries per slot and buffer */
   uint64_t nn_precision;    /* the precision the network runs (coffee_nn_precision; 0 = stand-in net) */
+  /* Default precision on self-play's own positions: every 128th network launch of an engine
+   * running the corrected instance re-evaluates its first 256 rows on the accurate one; the
+   * largest |logit| difference is read at every stats / drain call and, past 2.5e-4, the
+   * engine switches to the accurate instance for the rest of the run (the same model). */
+  uint64_t nn_audits;         /* audited launches so far */
+  uint64_t nn_audit_switches; /* switches to the accurate instance (0 or 1 per model) */
+  double nn_audit_max_diff;   /* largest difference seen so far (0 before the first audit) */
 } coffee_selfplay_stats;
 
 int coffee_selfplay_create(const coffee_selfplay_config* cfg, coffee_selfplay** out);

@@ -97,7 +97,8 @@ class SelfplayStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ["rounds", "playouts", "nn_evals", "moves", "games_finished", "rows_written", "rows_pending",
                  "rows_dropped", "games_dropped", "errors", "tree_levels", "tree_children", "errors_node_pool",
-                 "errors_edge_pool", "edge_pool_peak", "edge_pool_cap", "nn_precision"]]
+                 "errors_edge_pool", "edge_pool_peak", "edge_pool_cap", "nn_precision", "nn_audits",
+                 "nn_audit_switches"]] + [("nn_audit_max_diff", ctypes.c_double)]
 
 
 # Every symbol include/katacoffee.h declares (checked by tests/test_abi.py).

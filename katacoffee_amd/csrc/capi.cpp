@@ -86,7 +86,7 @@ static void checkGeom(int x, int y, int w) {
 extern "C" {
 
 const char* coffee_last_error(void) { return gLastError.c_str(); }
-int coffee_abi_version(void) { return 107; }
+int coffee_abi_version(void) { return 108; }
 
 int coffee_device_count(int* count) {
   return guarded([&] {

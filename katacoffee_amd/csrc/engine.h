@@ -160,6 +160,15 @@ class NNEngine {
   // the default precision takes the corrected instance when that difference is at most this
   // (a quarter of north_star's 1e-3)
   static constexpr float NN_AUTO_TOL = 2.5e-4f;
+  // Self-play audit of the corrected instance (the default precision's check on the
+  // positions self-play actually evaluates, not only the calibration batch): re-evaluates
+  // rows [0, min(n, NN_AUDIT_ROWS)) of a batch `forward` just wrote to `out` on the
+  // accurate instance into `scratch` (rows addressed like `out`) and folds the largest
+  // |difference| into *maxBits (float bits, device).  No-op unless the engine runs the
+  // corrected instance.
+  static constexpr int NN_AUDIT_ROWS = 256;
+  void audit(int n, const uint64_t* in, const float* out, float* scratch, unsigned* maxBits, hipStream_t st,
+             const int* countDev, const int* rowIdx);
 
  private:
   void build(const ModelHost& m, int path);

@@ -82,6 +82,11 @@ constexpr float F8C_MAX = 448.0f;  // largest finite e4m3fn
 #ifndef KC_F8C_VGPR
 #define KC_F8C_VGPR 96
 #endif
+// KC_ACC_CAP 1: the accurate (split) borderless instance runs under the same cap (222 VGPRs
+// uncapped: no search wave of the other game group fits beside it); 0: uncapped (A/B)
+#ifndef KC_ACC_CAP
+#define KC_ACC_CAP 1
+#endif
 #ifndef KC_F8C_PARK
 #define KC_F8C_PARK 0
 #endif
@@ -1525,7 +1530,8 @@ __global__ void kNNForwardCap(const NNLayout* __restrict__ L, const h16x8* __res
 template <class G>
 constexpr auto nnKernel() {
 #if KC_F8C_VGPR
-  if constexpr(G::MODE == NN_MODE_F8C || (G::MODE == NN_MODE_F16 && G::BL))
+  if constexpr(G::MODE == NN_MODE_F8C || (G::MODE == NN_MODE_F16 && G::BL) ||
+               (KC_ACC_CAP && G::MODE == NN_MODE_SPLIT3 && G::BL))
     return kNNForwardCap<G::X, G::Y, G::C, G::NB, G::MODE, G::BL>;
   else
 #endif
@@ -2079,6 +2085,41 @@ void NNEngine::launch(int n, int inWords, const uint16_t* tab, const uint64_t* i
   else
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, layoutDev_, (const h16x8*)wHalf_, wF32_, tab, n,
                        countDev, rowIdx, inWords, (float)W_, in, out, trunk_, hot);
+  KC_HIP(hipGetLastError());
+}
+
+// Self-play audit of the default precision: the largest |difference| of
+// two network outputs over the batch rows [0, min(n, *countDev)) (rows addressed through
+// rowIdx like the network's), folded into *maxBits as float bits (non-negative floats
+// order like their bits; NaN and infinity count as infinity).  One wave per row.
+__global__ void __launch_bounds__(64) kAuditDiff(int n, const int* __restrict__ countDev, const int* __restrict__ rowIdx,
+                                                 const float* __restrict__ a, const float* __restrict__ b, int width,
+                                                 unsigned* __restrict__ maxBits) {
+  const int count = countDev ? min(*countDev, n) : n;
+  if((int)blockIdx.x >= count)
+    return;
+  const size_t row = (size_t)(rowIdx ? rowIdx[blockIdx.x] : (int)blockIdx.x) * width;
+  float m = 0.0f;
+  for(int j = threadIdx.x; j < width; j += 64) {
+    const float d = fabsf(a[row + j] - b[row + j]);
+    m = fmaxf(m, d <= 3.0e38f ? d : INFINITY);
+  }
+  for(int o = 32; o > 0; o >>= 1)
+    m = fmaxf(m, __shfl_xor(m, o));
+  if(threadIdx.x == 0)
+    atomicMax(maxBits, __float_as_uint(m));
+}
+
+void NNEngine::audit(int n, const uint64_t* in, const float* out, float* scratch, unsigned* maxBits, hipStream_t st,
+                     const int* countDev, const int* rowIdx) {
+  if(layered_ || mode_ != NN_CORRECTED || !fallbackNet_ || n <= 0)
+    return;
+  const int m = std::min(n, NN_AUDIT_ROWS);
+  const int inWords = (NUM_SPATIAL * X_ * Y_ + 63) / 64;
+  // the accurate instance over the same rows (every board evaluated: no hot flags)
+  fallbackNet_->launch<NNGeo<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>>(m, inWords, fallbackNet_->tabDevB_, in, scratch,
+                                                                           st, countDev, rowIdx, nullptr, nullptr);
+  hipLaunchKernelGGL(kAuditDiff, dim3(m), dim3(64), 0, st, m, countDev, rowIdx, out, scratch, 4 * X_ * Y_ + 4, maxBits);
   KC_HIP(hipGetLastError());
 }
 

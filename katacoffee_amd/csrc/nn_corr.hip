@@ -21,5 +21,12 @@ template __global__ void kNNForwardCap<5, 5, 96, NN_SMALL_NB, NN_MODE_F16, true>
     const NNLayout* __restrict__, const h16x8* __restrict__, const float* __restrict__, const uint16_t* __restrict__,
     int, const int* __restrict__, const int* __restrict__, int, float, const uint64_t* __restrict__, float* __restrict__,
     float* __restrict__, int* __restrict__);
+#if KC_ACC_CAP
+// the accurate (split) borderless instance under the same cap (222 VGPRs uncapped)
+template __global__ void kNNForwardCap<5, 5, 96, NN_SMALL_NB, NN_MODE_SPLIT3, true>(
+    const NNLayout* __restrict__, const h16x8* __restrict__, const float* __restrict__, const uint16_t* __restrict__,
+    int, const int* __restrict__, const int* __restrict__, int, float, const uint64_t* __restrict__, float* __restrict__,
+    float* __restrict__, int* __restrict__);
+#endif
 #endif
 }  // namespace kc

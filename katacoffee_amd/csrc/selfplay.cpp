@@ -149,8 +149,8 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   if(!c.use_fake_net) {
     if(!c.model_path)
       throw std::invalid_argument("model_path required unless use_fake_net");
-    ModelHost m = loadModel(c.model_path);
-    nn_.reset(new NNEngine(m, c.x, c.y, c.win_len, c.nn_precision));
+    model_.reset(new ModelHost(loadModel(c.model_path)));
+    nn_.reset(new NNEngine(*model_, c.x, c.y, c.win_len, c.nn_precision));
   }
   nnPath_ = c.nn_precision;
   xLen_ = c.x;
@@ -253,6 +253,16 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
     const char* f = getenv("COFFEE_FUSED_ROUNDS");
     fuseRounds_ = f && f[0] == '0' ? 0 : (f && f[0] == '1' ? 1 : -1);
   }
+  {
+    const char* e = getenv("COFFEE_NN_AUDIT_EVERY");
+    if(e)
+      auditEvery_ = std::max(0, atoi(e));
+    const char* t = getenv("COFFEE_NN_AUDIT_TOL");
+    if(t)
+      auditTol_ = (float)atof(t);
+  }
+  auditOut_ = devAlloc<float>(owned_, (size_t)G * (P + 4), false);
+  auditMax_ = devAlloc<unsigned>(owned_, 1);
   d.gCap = 2 * G;
   d.gRec = devAlloc<GameRec>(owned_, (size_t)d.gCap, false);
   d.gCount = devAlloc<unsigned long long>(owned_, 1);
@@ -367,6 +377,11 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
           KC_HIP(hipEventRecord(b, st));
       }
     });
+    if(nn_ && nnPath_ == NN_DEFAULT && auditEvery_ > 0 && nn_->precision() == NN_CORRECTED &&
+       nnLaunches_++ % (uint64_t)auditEvery_ == 0) {
+      nn_->audit(std::min(d.G, d.nnCap), d.nnIn, d.nnOut, auditOut_, auditMax_, st, d.nnCount, d.nnIdx);
+      audits_++;
+    }
     const bool commitNow = (rounds_ + 1) % (uint64_t)commitInterval_ == 0 || r == rounds - 1;
     if(fuse && !commitNow) {
       const bool t4 = sampleNow(4);
@@ -389,6 +404,31 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
 void SelfplayEngine::sync() {
   KC_HIP(hipStreamSynchronize(stream_));
   resolveTiming();
+  auditCheck();
+}
+
+void SelfplayEngine::auditCheck() {
+  if(!nn_ || audits_ == 0)
+    return;
+  unsigned bits = 0;
+  KC_HIP(hipMemcpy(&bits, auditMax_, 4, hipMemcpyDeviceToHost));
+  float m;
+  memcpy(&m, &bits, 4);
+  auditSeen_ = std::max(auditSeen_, m);
+  if(!(auditSeen_ <= auditTol_) && nn_->precision() == NN_CORRECTED && nnPath_ == NN_DEFAULT) {
+    // the corrected instance missed the default precision's bound on self-play positions:
+    // the same model on the accurate instance from here on (cached evaluations cleared)
+    nn_.reset(new NNEngine(*model_, xLen_, yLen_, winLen_, NN_ACCURATE));
+    auditSwitches_++;
+    const int cap = nnCapFor(hd_.G);
+    if(cap != hd_.nnCap) {
+      hd_.nnCap = cap;
+      KC_HIP(hipMemcpy(&dd_->nnCap, &cap, sizeof(int), hipMemcpyHostToDevice));
+    }
+    if(hd_.cacheOn)
+      KC_HIP(hipMemsetAsync(hd_.cKey, 0, sizeof(uint64_t) * 2 * ((size_t)hd_.cacheMask + 1), stream_));
+    KC_HIP(hipStreamSynchronize(stream_));
+  }
 }
 
 void SelfplayEngine::stats(coffee_selfplay_stats& out) {
@@ -422,6 +462,9 @@ void SelfplayEngine::stats(coffee_selfplay_stats& out) {
   out.games_dropped = gdrop;
   out.edge_pool_cap = (uint64_t)hd_.edgePoolCap;
   out.nn_precision = nn_ ? (uint64_t)nn_->precision() : 0;
+  out.nn_audits = audits_;
+  out.nn_audit_switches = (uint64_t)auditSwitches_;
+  out.nn_audit_max_diff = auditSeen_;
   if(out.errors)
     throw InternalError("self-play device invariant violated in " + std::to_string(out.errors) +
                         " game slot(s): " + std::to_string(out.errors_node_pool) + " node pool exhausted, " +
@@ -556,8 +599,13 @@ void SelfplayEngine::setModelBytes(const void* data, size_t bytes) {
 
 void SelfplayEngine::switchModel(const ModelHost& m) {
   std::unique_ptr<NNEngine> next(new NNEngine(m, xLen_, yLen_, winLen_, nnPath_));
+  std::unique_ptr<ModelHost> keep(new ModelHost(m));
   sync();
   nn_ = std::move(next);
+  model_ = std::move(keep);
+  // the audit starts over for the new model
+  auditSeen_ = 0.0f;
+  KC_HIP(hipMemset(auditMax_, 0, 4));
   // a reload may change the network path (fused <-> layered) and with it the default cap
   const int cap = nnCapFor(hd_.G);
   if(cap != hd_.nnCap) {

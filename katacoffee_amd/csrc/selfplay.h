@@ -83,6 +83,24 @@ class SelfplayEngine {
   // workgroups: 202 vs 161 us).  COFFEE_FUSED_ROUNDS=0: never, 1: always (same results)
   int fuseRounds_ = -1;  // -1 auto, 0 never, 1 always
   bool fuseNow() const;
+  // Audit of the default precision on self-play's own positions: every
+  // auditEvery_-th network launch of an engine whose default precision resolved to the
+  // corrected instance is re-evaluated (its first NN_AUDIT_ROWS rows) on the accurate
+  // instance; sync() -- every stats / drain / game-record call -- reads the largest
+  // difference so far and, past auditTol_ (NNEngine::NN_AUTO_TOL), rebuilds the network
+  // at the accurate precision (same model; the NN cache is cleared).  The switch happens
+  // only at those host synchronisation points, so runs stay reproducible.
+  // COFFEE_NN_AUDIT_EVERY (0 = off) and COFFEE_NN_AUDIT_TOL override the defaults.
+  void auditCheck();
+  std::unique_ptr<ModelHost> model_;  // the network's model (rebuilt on an audit switch)
+  float* auditOut_ = nullptr;         // device [G][P+4]: the accurate instance's rows
+  unsigned* auditMax_ = nullptr;      // device: largest difference so far (float bits)
+  int auditEvery_ = 128;
+  float auditTol_ = NNEngine::NN_AUTO_TOL;
+  uint64_t nnLaunches_ = 0;
+  uint64_t audits_ = 0;
+  float auditSeen_ = 0.0f;            // largest difference read back so far
+  int auditSwitches_ = 0;
 };
 
 }  // namespace kc

@@ -36,7 +36,7 @@ def test_header_and_exports_agree(L):
 
 
 def test_abi_version_and_defaults(L):
-    assert L.coffee_abi_version() == 107
+    assert L.coffee_abi_version() == 108
     p = kc.default_search_params()
     # cpp/configs/training/selfplay1.cfg values
     assert p.max_visits == 600

@@ -13,6 +13,15 @@ trace() {  # name, bench args...
   run python tools/reduce_profile.py trace gpurun_out/prof_$name $name
   grep '^{' gpurun_out/prof_$name.log > gpurun_out/prof_$name.line.json || true
 }
+pmcr() {  # name, counter, bench args...: counters only for the search kernels' dispatches
+  # 3000-3399 of each (rounds ~1500-1700 of two game groups: past the first full-visit
+  # searches, trees at their steady per-move size); every dispatch is still traced by the
+  # profiler, so a crash in its dispatch path (profiles/r05/c4_pmc_crash.txt) still ends it
+  local name=$1 ctr=$2
+  shift 2
+  run timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-include-regex "kSelect|kBackup|kCompact" --kernel-iteration-range "[3000-3399]" -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line --trained-steps 0 "$@" > gpurun_out/prof_$name.log 2>&1
+  run python tools/reduce_profile.py pmc gpurun_out/prof_$name $name
+}
 line() {  # name, limit, bench args...
   local name=$1 lim=$2
   shift 2
@@ -26,6 +35,9 @@ for s in "$@"; do
     c2default) trace r06_c2default --steps 20 --warmup 5 --precision default ;;
     c3default) trace r06_c3default --config C3 --steps 10 --warmup 5 ;;
     c4default) trace r06_c4default --config C4 --window short --warmup 8 --steps 6 --rounds-per-step 200 ;;
+    c4pmc)
+      pmcr r06_c4steady_fetch FETCH_SIZE --config C4 --window short --warmup 9 --steps 1 --rounds-per-step 200
+      pmcr r06_c4steady_write WRITE_SIZE --config C4 --window short --warmup 9 --steps 1 --rounds-per-step 200 ;;
     main) line c2 600 --steps 20 --warmup 5 ;;
     prodline) line c2prod 600 --steps 20 --warmup 5 --play production --no-cpu-baseline --trained-steps 0 ;;
     c3line) line c3 700 --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
