@@ -118,7 +118,7 @@ def parse():
     ap.add_argument("--groups", type=int, default=0,
                     help="independent game groups per GPU, each on its own stream (overlaps one group's network "
                          "with another's search kernels; the reference's numNNServerThreadsPerModel); "
-                         "0 = 2 except for b18c384nbt (C5), whose forward is throughput-bound")
+                         "0 = 4 at C2, 2 at C3/C4, 1 for b18c384nbt (C5), whose forward is throughput-bound")
     ap.add_argument("--reload-every", type=int, default=0,
                     help="hot reload every K timed steps: rank 0 writes a new random model and broadcasts its "
                          "bytes over RCCL; every engine switches (the reference's model hot reload)")
@@ -529,8 +529,18 @@ def load_traffic(path):
         return {}
 
 
+# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default): with
+# more streams than queues, streams share a queue and their kernels serialise.  The bench
+# runs one stream per game group plus torch's, so 4 groups need more than 4 queues (C2,
+# same box: 4 groups on 4 queues 10.4 k rows/s at the default precision, on 8 queues 17.1 k;
+# profiles/r06/groups_hwqueues_ab.txt).  Set before anything initialises the HIP runtime;
+# ranks started by launch_ranks inherit it.
+HW_QUEUES = "8"
+
+
 def main():
     faulthandler.enable()  # a native fault prints the Python stack too
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", HW_QUEUES)
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
@@ -584,9 +594,11 @@ def main():
     # most visits + 1 nodes; production's cheap searches reuse the tree
     node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
     if args.groups == 0:
-        # latency-bound rounds gain from two overlapped chains (measured: C2 +8 %, C3 +12 %,
-        # C4 +10 % rows/s); b18c384nbt's forward is throughput-bound (C5: -12 % playouts/s)
-        args.groups = 2 if cfg["arch"] != "b18c384nbt" else 1
+        # latency-bound rounds gain from overlapped chains (measured: two groups C2 +8 %, C3
+        # +12 %, C4 +10 % rows/s over one; four groups on 8 hardware queues C2 +5 % fast, +2.5 %
+        # default precision over two, six or eight groups -30 %: profiles/r06/groups_hwqueues_ab*.txt);
+        # b18c384nbt's forward is throughput-bound (C5: -12 % playouts/s with two)
+        args.groups = {"C2": 4}.get(args.config, 2) if cfg["arch"] != "b18c384nbt" else 1
     def measure(precision, with_cpu, model_path=model_path):
         """One timed window at `precision` with the network `model_path`; rank 0 returns the
         JSON dict."""
