@@ -533,14 +533,19 @@ def load_traffic(path):
 # more streams than queues, streams share a queue and their kernels serialise.  The bench
 # runs one stream per game group plus torch's, so 4 groups need more than 4 queues (C2,
 # same box: 4 groups on 4 queues 10.4 k rows/s at the default precision, on 8 queues 17.1 k;
-# profiles/r06/groups_hwqueues_ab.txt).  Set before anything initialises the HIP runtime;
-# ranks started by launch_ranks inherit it.
-HW_QUEUES = "8"
+# profiles/r06/groups_hwqueues_ab.txt).  Raised to at least 8 (the GPU box exports 4) before
+# anything initialises the HIP runtime; ranks started by launch_ranks inherit it.
+HW_QUEUES = 8
 
 
 def main():
     faulthandler.enable()  # a native fault prints the Python stack too
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", HW_QUEUES)
+    try:
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        queues = 0
+    if queues < HW_QUEUES:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
@@ -786,7 +791,8 @@ def main():
                            "nn_cache_log2": args.nn_cache_log2, "nn_batch_cap": args.nn_batch_cap or "engine default",
                            "play_settings": args.play + (" + policy openings (area prop %g)" % args.opening_prop
                                                          if args.opening_prop > 0 else ""),
-                           "start_stagger_rounds": stagger, "groups": args.groups, "node_cap": node_cap or "default",
+                           "start_stagger_rounds": stagger, "groups": args.groups,
+                           "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "node_cap": node_cap or "default",
                            "parallelism": ("game-sharded x%d (%s)" % (world, "rows written per rank, no collective in "
                                                                          "the loop" if local_sink else "RCCL row gather "
                                                                          "to rank 0")) if world > 1 else "1 GPU"},
