@@ -734,7 +734,12 @@ def main():
                                if fused and args.config == "C2" else None,
                     "evals_per_launch": per_launch, "flops_per_eval": flops_per_eval,
                     "mfma_per_product": mfma_factor, "avg_launch_us": net["avg_us"],
-                    "timed_launches": net["launches_timed"]}
+                    "timed_launches": net["launches_timed"],
+                    # the game groups' launches overlap, so a launch's own rate understates the
+                    # chip's: all network evaluations of the window x FLOP / the window
+                    "chip_level": {"achieved": d["nn_evals"] / world / elapsed * flops_per_eval / 1e12,
+                                   "frac": d["nn_evals"] / world / elapsed * flops_per_eval / 1e12 / PEAK_F16_TFLOPS,
+                                   "concurrent_groups": args.groups}}
             # tree roofline: per descent, sum over path nodes of 32 B + k * 48 B,
             # counted on the device (tree_levels, tree_children)
             tree_bytes = NODE_B * d["tree_levels"] + CHILD_B * d["tree_children"]

@@ -4,6 +4,9 @@
 # Each GPU step has its own time limit; the first failing step ends the script.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+# bench.py raises the HIP hardware-queue count itself, but under rocprofv3 the runtime may be
+# initialised before bench.py's main runs: give the profiled process the same 8 queues
+export GPU_MAX_HW_QUEUES=8
 mkdir -p gpurun_out
 run() { "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
 trace() {  # name, bench args...
@@ -32,6 +35,8 @@ line() {  # name, limit, bench args...
 for s in "$@"; do
   case $s in
     c2) trace r06_c2 --steps 20 --warmup 5 ;;
+    c2final) trace r06_c2final --steps 20 --warmup 5 ;;
+    c2finaldefault) trace r06_c2finaldefault --steps 20 --warmup 5 --precision default ;;
     c2default) trace r06_c2default --steps 20 --warmup 5 --precision default ;;
     c3default) trace r06_c3default --config C3 --steps 10 --warmup 5 ;;
     c4default) trace r06_c4default --config C4 --window short --warmup 8 --steps 6 --rounds-per-step 200 ;;
