@@ -87,6 +87,13 @@ constexpr float F8C_MAX = 448.0f;  // largest finite e4m3fn
 #ifndef KC_ACC_CAP
 #define KC_ACC_CAP 1
 #endif
+// KC_ACC_LATE 1: the accurate borderless instance reads a K-step's fragments after the
+// previous step's MFMAs issue (one fragment buffer, like KC_F8C_LATE); 0: double-buffered.
+// Measured (round 6, profiles/r06/acc_late_ab.txt): 182 VGPRs and no spills against 17 spilled,
+// but the network alone 3 % slower and the C2 bench equal within noise: off
+#ifndef KC_ACC_LATE
+#define KC_ACC_LATE 0
+#endif
 #ifndef KC_F8C_PARK
 #define KC_F8C_PARK 0
 #endif
@@ -666,7 +673,7 @@ KC_D void convTilesB(const uint16_t* __restrict__ act, const h16x8* __restrict__
     }
     if(chunkEnd && chunk + 1 < NCH && (DBG & 2) && !(DBG & 1))
       request(chunk + R);  // ablation: the requests without their waits / barriers
-    constexpr bool LATE = F8C && KC_F8C_LATE;
+    constexpr bool LATE = (F8C && KC_F8C_LATE) || (G::MODE == NN_MODE_SPLIT3 && G::BL && KC_ACC_LATE);
     if(!LATE && st + 1 < STEPS && !(DBG & 16)) {
       if(cb == NCB - 1)
         tapAddr(tap + 1);
