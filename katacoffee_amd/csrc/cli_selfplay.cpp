@@ -360,6 +360,10 @@ static void runGpu(int gpu, int server, int perGpu, int slot, int share, const S
     logf("gpu %d.%d: %llu games, %llu moves, %lld rows, %.1f rows/s, %.1f moves/s, %.3g playouts/s, %llu rows dropped",
          gpu, server, (unsigned long long)st.games_finished, (unsigned long long)st.moves, (long long)rowsDrained,
          rowsDrained / secs, st.moves / secs, st.playouts / secs, (unsigned long long)st.rows_dropped);
+    if(st.nn_audits > 0 || st.nn_audit_switches > 0)  // the default precision's audit
+      logf("gpu %d.%d: network precision %llu, %llu audited launches, max |corrected - accurate| %.3g%s", gpu, server,
+           (unsigned long long)st.nn_precision, (unsigned long long)st.nn_audits, st.nn_audit_max_diff,
+           st.nn_audit_switches ? ", switched to accurate" : "");
     if(s.maxGamesTotal >= 0 && gGamesDone >= s.maxGamesTotal)
       gStop = true;
   }
