@@ -113,6 +113,10 @@ CASES = {
     "c2-accurate": ("b6c96", (5, 5, 4), "accurate", 128, 1, 24, 12, 0, 900, {}),
     # corrected network (the benchmarked 1e-3 path): two groups, binding cap, selfplay1.cfg play
     "c2-corrected-two-groups": ("b6c96", (5, 5, 4), "corrected", 384, 2, 24, 14, 300, 700, PRODUCTION),
+    # the bench's C2 layout: four game groups on their own streams (fast fused, and the
+    # default precision -> corrected on this net, audited), binding caps, selfplay1.cfg play
+    "c2-fused-four-groups": ("b6c96", (5, 5, 4), "fast", 256, 4, 24, 14, 200, 600, PRODUCTION),
+    "c2-default-four-groups": ("b6c96", (5, 5, 4), "default", 256, 4, 24, 14, 200, 600, PRODUCTION),
     # C3 network on the layered kernels
     "c3-layered": ("b10c128", (5, 5, 4), "fast", 256, 1, 24, 12, 200, 900, {}),
     # C5 network (nested bottlenecks) at 9x9 / 5 on the layered kernels
@@ -133,7 +137,7 @@ def _engine(fused, X, Y, W, **kw):
             os.environ["COFFEE_FUSED_ROUNDS"] = old
 
 
-@pytest.mark.parametrize("name", list(CASES))
+@pytest.mark.parametrize("name", [n for n in CASES if "four-groups" not in n])
 def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
     _run_case(nets, name, (1, None, 0))
 
@@ -146,6 +150,15 @@ def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
 @pytest.mark.parametrize("sched", [(16, False, 29), (16, True, 29)], ids=["ci16-stagger", "ci16-stagger-fused"])
 @pytest.mark.parametrize("name", ["c2-fused-nb8", "c2-corrected-two-groups"])
 def test_selfplay_real_network_scheduled_bit_exact_vs_oracle(nets, name, sched):
+    _run_case(nets, name, sched)
+
+
+# bench.py's default C2 layout (4 groups, commit interval 16, staggered starts; the fast
+# network fuses the rounds, the default precision runs them separately)
+@pytest.mark.parametrize("name,sched", [("c2-fused-four-groups", (16, True, 29)),
+                                        ("c2-default-four-groups", (16, False, 29))],
+                         ids=["fast-fused", "default-separate"])
+def test_selfplay_bench_layout_bit_exact_vs_oracle(nets, name, sched):
     _run_case(nets, name, sched)
 
 
