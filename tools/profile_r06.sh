@@ -25,6 +25,13 @@ pmcr() {  # name, counter, bench args...: counters only for the search kernels' 
   run timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-include-regex "kSelect|kBackup|kCompact" --kernel-iteration-range "[3000-3399]" -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line --trained-steps 0 "$@" > gpurun_out/prof_$name.log 2>&1
   run python tools/reduce_profile.py pmc gpurun_out/prof_$name $name
 }
+pmc() {  # name, counter, bench args...: every dispatch of the short C2 window
+  local name=$1 ctr=$2
+  shift 2
+  run timeout -k 10 420 rocprofv3 --pmc $ctr -d gpurun_out/prof_$name -o $name --output-format csv -- python bench.py --no-cpu-baseline --no-compliant-line --trained-steps 0 "$@" > gpurun_out/prof_$name.log 2>&1
+  run python tools/reduce_profile.py pmc gpurun_out/prof_$name $name
+}
+SHORT="--window short --warmup 8 --steps 6 --rounds-per-step 200"
 line() {  # name, limit, bench args...
   local name=$1 lim=$2
   shift 2
@@ -43,6 +50,15 @@ for s in "$@"; do
     c4pmc)
       pmcr r06_c4steady_fetch FETCH_SIZE --config C4 --window short --warmup 9 --steps 1 --rounds-per-step 200
       pmcr r06_c4steady_write WRITE_SIZE --config C4 --window short --warmup 9 --steps 1 --rounds-per-step 200 ;;
+    c2pmc)
+      pmc r06_c2_fetch FETCH_SIZE $SHORT
+      pmc r06_c2_write WRITE_SIZE $SHORT ;;
+    corrpmc)
+      pmc r06_c2corr_fetch FETCH_SIZE $SHORT --precision corrected
+      pmc r06_c2corr_write WRITE_SIZE $SHORT --precision corrected ;;
+    accpmc)
+      pmc r06_c2acc_fetch FETCH_SIZE $SHORT --precision accurate
+      pmc r06_c2acc_write WRITE_SIZE $SHORT --precision accurate ;;
     main) line c2 600 --steps 20 --warmup 5 ;;
     prodline) line c2prod 600 --steps 20 --warmup 5 --play production --no-cpu-baseline --trained-steps 0 ;;
     c3line) line c3 700 --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
