@@ -118,7 +118,7 @@ def parse():
     ap.add_argument("--groups", type=int, default=0,
                     help="independent game groups per GPU, each on its own stream (overlaps one group's network "
                          "with another's search kernels; the reference's numNNServerThreadsPerModel); "
-                         "0 = 4 at C2, 2 at C3/C4, 1 for b18c384nbt (C5), whose forward is throughput-bound")
+                         "0 = 4 at C2-C4, 1 for b18c384nbt (C5), whose forward is throughput-bound")
     ap.add_argument("--reload-every", type=int, default=0,
                     help="hot reload every K timed steps: rank 0 writes a new random model and broadcasts its "
                          "bytes over RCCL; every engine switches (the reference's model hot reload)")
@@ -600,10 +600,11 @@ def main():
     node_cap = (visits + 64 + 63) // 64 * 64 if args.play == "benchmark" else 0
     if args.groups == 0:
         # latency-bound rounds gain from overlapped chains (measured: two groups C2 +8 %, C3
-        # +12 %, C4 +10 % rows/s over one; four groups on 8 hardware queues C2 +5 % fast, +2.5 %
-        # default precision over two, six or eight groups -30 %: profiles/r06/groups_hwqueues_ab*.txt);
+        # +12 %, C4 +10 % rows/s over one; four groups on 8 hardware queues over two: C2 +5 %
+        # fast, +2.5 % default precision, C3 +4.8 %, C4 +3.4 %; five or more -30 %:
+        # profiles/r06/groups_hwqueues_ab*.txt, line_c3_4groups.json, line_c4_4groups.json);
         # b18c384nbt's forward is throughput-bound (C5: -12 % playouts/s with two)
-        args.groups = {"C2": 4}.get(args.config, 2) if cfg["arch"] != "b18c384nbt" else 1
+        args.groups = 4 if cfg["arch"] != "b18c384nbt" else 1
     def measure(precision, with_cpu, model_path=model_path):
         """One timed window at `precision` with the network `model_path`; rank 0 returns the
         JSON dict."""
