@@ -938,6 +938,13 @@ KC_D void nextExpansion(const GV& v, const float (&pv)[NI], float curPrior, int 
 
 // oracle descend (playoutDescend search.cpp:936-1165, allocateOrFindNode :704-759,
 // maybeCatchUpEdgeVisits :1169-1207)
+// KC_TT_EARLY 1: an expansion that lands on a transposition requests the child's record
+// right after the table probe; 0: after the edge and node stores.  Measured (round 6, C2
+// fast, 4 groups, profiles/r06/tt_early_ab.txt): 25.81 / 25.84 k rows/s early against
+// 25.97 / 25.94 k late, bit-exact either way: off
+#ifndef KC_TT_EARLY
+#define KC_TT_EARLY 0
+#endif
 template <int NI>
 KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* LDS [P] */) {
   const SP& sp = *v.sp;
@@ -1060,6 +1067,15 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
       int ttSlot = -1;
       int child = sp.useGraph ? ttFind(v, k0, k1, ttSlot) : -1;
       const bool fresh = child < 0;
+      // a transposition's record (visits, terminal flag) is requested here, so its latency
+      // overlaps the next-candidate scan and the stores below; nothing in this descent
+      // writes it (a child always holds more stones than its parent: never ni)
+      uint32_t tVisits = 0u, tFlags = 0u;
+      if(KC_TT_EARLY && !fresh) {
+        const Node& cn = v.nodes()[child];
+        tVisits = cn.visits;
+        tFlags = (uint32_t)cn.flags;
+      }
       float nxtPrior = -1.0f;
       int nxtPos = 0xFFFF;
       if(!isRoot)
@@ -1098,8 +1114,8 @@ KC_D void descend(const GV& v, GameDev& s, uint32_t* hasBits, float* rootPol /* 
       SPROF_ADD(6, SPROF_NOW() - tExp);
       // a fresh node has no visits and the terminal flag of b; a transposition's
       // record is read
-      const uint32_t cv = fresh ? 0u : v.nodes()[child].visits;
-      const uint32_t cf = fresh ? (b.finished ? 2u : 0u) : (uint32_t)v.nodes()[child].flags;
+      const uint32_t cv = fresh ? 0u : (KC_TT_EARLY ? tVisits : v.nodes()[child].visits);
+      const uint32_t cf = fresh ? (b.finished ? 2u : 0u) : (KC_TT_EARLY ? tFlags : (uint32_t)v.nodes()[child].flags);
       if(cv > 0) {
         s.leafKind = LEAF_CATCHUP;
         s.leafNode = child;
