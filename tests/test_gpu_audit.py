@@ -6,6 +6,7 @@ drain call, and past the tolerance (NNEngine::NN_AUTO_TOL = 2.5e-4) the engine s
 to the accurate instance for the rest of the run (selfplay.cpp auditCheck)."""
 import os
 
+import numpy as np
 import pytest
 
 import katacoffee_amd as kc
@@ -59,3 +60,28 @@ def test_audit_switches_to_accurate_past_tolerance(tmp_path):
     sp.close()
     assert st2["nn_audits"] == 5 and st2["nn_audit_switches"] == 1
     assert st2["errors"] == 0 and st2["moves"] > moves and len(rows["meta"]) > 0
+
+
+def test_audit_switch_is_reproducible(tmp_path):
+    """The switch happens at the stats / drain calls, so two runs with the same call
+    sequence switch at the same round and play the same games afterwards."""
+    env = {"COFFEE_NN_AUDIT_EVERY": "8", "COFFEE_NN_AUDIT_TOL": "1e-12"}
+    runs = []
+    for _ in range(2):
+        sp = _engine(tmp_path, env)
+        sp.step(40)
+        st = sp.stats()
+        assert st["nn_audit_switches"] == 1
+        sp.step(300)
+        trees = [sp.game_tree(g) for g in (0, 7, 101, 255)]
+        info = [sp.game_info(g) for g in (0, 7, 101, 255)]
+        rows = sp.drain_rows()
+        sp.close()
+        runs.append((trees, info, rows))
+    (t0, i0, r0), (t1, i1, r1) = runs
+    for a, b in zip(t0, t1):
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+    assert i0 == i1
+    for k in r0:
+        np.testing.assert_array_equal(r0[k], r1[k])
