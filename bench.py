@@ -128,8 +128,9 @@ def parse():
                     help="N > 1: local = every rank writes its own games' rows (sharded games, no collective in "
                          "the loop); gather = rows gathered to rank 0 over RCCL each step (one writer)")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
-    ap.add_argument("--cpu-curve-seconds", type=float, default=0.0,
-                    help="timed window of each point of the CPU thread-scaling curve (0: skip the curve)")
+    ap.add_argument("--cpu-curve-seconds", type=float, default=10.0,
+                    help="timed window of each point of the CPU thread-scaling curve (2, 4, 8 threads between the "
+                         "1- and 16-thread runs: the linearity the whole-host extrapolation rests on; 0: skip)")
     ap.add_argument("--cpu-c1-seconds", type=float, default=20.0,
                     help="timed CPU-baseline window (C1 and single-thread runs)")
     ap.add_argument("--cpu-warmup-seconds", type=float, default=10.0)
@@ -338,7 +339,9 @@ def cpu_baseline(args, cfg, model_path):
     curve = {}
     t = 2
     while t < cores and args.cpu_curve_seconds > 0:
-        curve[t] = run(gpt * t, visits, t, args.cpu_curve_seconds, 2.0)["playouts_per_sec"]  # short: rates only
+        # the single-thread run's 5 s warm-up (a group's first rounds are root evaluations,
+        # slower in playouts/s than its steady state)
+        curve[t] = run(gpt * t, visits, t, args.cpu_curve_seconds, 5.0)["playouts_per_sec"]
         t *= 2
     curve[1], curve[cores] = one["playouts_per_sec"], sat["playouts_per_sec"]
     desc = lambda r, g, t, w=5.0: ("%d games x %d visits on %d threads (%d independent groups of %d), %.0f s warm-up "
@@ -354,6 +357,8 @@ def cpu_baseline(args, cfg, model_path):
         "single_thread": {"rows_per_sec": one["rows_per_sec"], "playouts_per_sec": one["playouts_per_sec"],
                           "sample": desc(one, gpt, 1), "scaling_efficiency_at_%d" % cores: eff},
         "thread_curve_playouts_per_sec": {str(k): curve[k] for k in sorted(curve)},
+        # playouts/s at t threads / (t x the 1-thread rate): the whole-host extrapolation's premise
+        "thread_curve_efficiency": {str(k): curve[k] / (k * curve[1]) if curve.get(1) else None for k in sorted(curve)},
     }
     # Whole host (all physical cores).  The GPU box asks that worker pools stay
     # within its CPU share (16 threads per GPU), so the whole host is not run by default: the
