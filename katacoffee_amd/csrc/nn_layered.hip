@@ -750,21 +750,30 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1L(LConvArgs a) {
   convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
 }
 
-// Fast 1x1 convolutions, pipelined: 64-channel stages, double-buffered in LDS; the
-// next stage's global loads are issued before the current stage's MFMAs and converted
-// (BN-ReLU -> fp16) into the other buffer after them, so the HBM latency of the f32
-// input overlaps the MFMAs (kConv1L waits for each stage before any MFMA: 5 % MFMA
-// busy on b18c384nbt's bottleneck convs).  Rows are 40 dwords (64 channels + 16 pad:
-// 10 mod 16 chunks, conflict-free A-fragment reads for contiguous rows).
+// 1x1 convolutions, pipelined: 64-channel stages, double-buffered in LDS; the next stage's
+// global loads are issued before the current stage's MFMAs and converted (BN-ReLU -> fp16,
+// and for SPLIT the lo = x - fp16(x) plane) into the other buffer after them, so the HBM
+// latency of the f32 input overlaps the MFMAs (kConv1L waits for each stage before any
+// MFMA: 5 % MFMA busy on b18c384nbt's bottleneck convs).  Rows are 40 dwords (64 channels +
+// 16 pad: 10 mod 16 chunks, conflict-free A-fragment reads for contiguous rows).  SPLIT
+// (round 6): a stage holds a hi and a lo plane, each K step issues
+// hi*hi, lo(w)*hi(x), hi(w)*lo(x) -- kConv1L's products in kConv1L's order (an A/B
+// option: see kConv1PipeFor).
 constexpr int L1P_SW = 2;                  // 32-channel slices per stage
 constexpr int L1P_STRIDE = 32 * L1P_SW + 16;  // fp16 per staged row
 
-template <int X, int Y, int TN, int WN>
+template <int X, int Y, bool SPLIT>
+constexpr size_t l1pLds(int cin) {
+  return 2 * (SPLIT ? 2 : 1) * (size_t)LGeo<X, Y>::ROWS * L1P_STRIDE * 2 + 2 * (size_t)cin * 4;
+}
+
+template <int X, int Y, int TN, bool SPLIT, int WN>
 __global__ void __launch_bounds__(L_NT, 2) kConv1LP(LConvArgs a) {
   using G = LGeo<X, Y>;
   constexpr int WM = L_WAVES / WN, TM = (G::RT + WM - 1) / WM;
   constexpr int NCT = TN * WN;
-  constexpr int SB = G::ROWS * L1P_STRIDE * 2;
+  constexpr int SB = G::ROWS * L1P_STRIDE * 2;  // one plane of one stage buffer
+  constexpr int PL = SPLIT ? 2 : 1;
   constexpr int CPR = 4 * L1P_SW;           // 8-channel chunks per staged row
   constexpr int TASKS = G::ROWS * CPR;
   constexpr int TPT = (TASKS + L_NT - 1) / L_NT;
@@ -777,7 +786,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1LP(LConvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave / WN, wn = wave % WN;
   const int ctBase = blockIdx.y * NCT + wn * TN;
-  float* sS = reinterpret_cast<float*>(smem + 2 * SB);
+  float* sS = reinterpret_cast<float*>(smem + 2 * PL * SB);
   float* sB = sS + a.cin;
   for(int i = tid; i < a.cin; i += L_NT) {
     sS[i] = i < a.cinReal ? a.ps[i] : 0.0f;
@@ -819,6 +828,18 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1LP(LConvArgs a) {
       hi.z = packHalf2(v[4], v[5]);
       hi.w = packHalf2(v[6], v[7]);
       *reinterpret_cast<uint4*>(buf + (r * L1P_STRIDE + q * 8) * 2) = hi;
+      if constexpr(SPLIT) {
+        float lo[8];
+#pragma unroll
+        for(int j = 0; j < 8; j++)
+          lo[j] = v[j] - (float)(_Float16)v[j];
+        uint4 l4;
+        l4.x = packHalf2(lo[0], lo[1]);
+        l4.y = packHalf2(lo[2], lo[3]);
+        l4.z = packHalf2(lo[4], lo[5]);
+        l4.w = packHalf2(lo[6], lo[7]);
+        *reinterpret_cast<uint4*>(buf + SB + (r * L1P_STRIDE + q * 8) * 2) = l4;
+      }
     }
   };
   int ab[TM];
@@ -836,12 +857,16 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1LP(LConvArgs a) {
     for(int c = 0; c < TN; c++)
       acc[t][c] = lf32x4{0.0f, 0.0f, 0.0f, 0.0f};
   const lh16x8* wl = a.w + (size_t)ctBase * 64 + lane;
+  const lh16x8* wlo = SPLIT ? a.wlo + (size_t)ctBase * 64 + lane : nullptr;
   const size_t stepStride = (size_t)a.coutTiles * 64;
-  lh16x8 bh[2][TN];
+  lh16x8 bh[2][TN], bl[2][SPLIT ? TN : 1];
   auto loadB = [&](int s, int slot) {
 #pragma unroll
-    for(int c = 0; c < TN; c++)
+    for(int c = 0; c < TN; c++) {
       bh[slot][c] = wl[(size_t)s * stepStride + c * 64];
+      if constexpr(SPLIT)
+        bl[slot][c] = wlo[(size_t)s * stepStride + c * 64];
+    }
   };
   load(0);
   loadB(0, 0);
@@ -849,7 +874,7 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1LP(LConvArgs a) {
   store(0, smem);
   __syncthreads();
   for(int st = 0; st < NST; st++) {
-    const char* cur = smem + (st & 1) * SB;
+    const char* cur = smem + (st & 1) * PL * SB;
     if(st + 1 < NST)
       load(st + 1);
 #pragma unroll
@@ -859,18 +884,26 @@ __global__ void __launch_bounds__(L_NT, 2) kConv1LP(LConvArgs a) {
         break;
       if(s + 1 < NCB)
         loadB(s + 1, (j + 1) & 1);
-      lh16x8 ah[TM];
+      lh16x8 ah[TM], al[SPLIT ? TM : 1];
 #pragma unroll
-      for(int t = 0; t < TM; t++)
+      for(int t = 0; t < TM; t++) {
         ah[t] = *reinterpret_cast<const lh16x8*>(cur + ab[t] + 64 * j);
+        if constexpr(SPLIT)
+          al[t] = *reinterpret_cast<const lh16x8*>(cur + SB + ab[t] + 64 * j);
+      }
 #pragma unroll
       for(int t = 0; t < TM; t++)
 #pragma unroll
-        for(int c = 0; c < TN; c++)
+        for(int c = 0; c < TN; c++) {
           acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j & 1][c], ah[t], acc[t][c], 0, 0, 0);
+          if constexpr(SPLIT) {
+            acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j & 1][c], ah[t], acc[t][c], 0, 0, 0);
+            acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j & 1][c], al[t], acc[t][c], 0, 0, 0);
+          }
+        }
     }
     if(st + 1 < NST)
-      store(st + 1, smem + ((st + 1) & 1) * SB);
+      store(st + 1, smem + ((st + 1) & 1) * PL * SB);
     __syncthreads();
   }
   convEpilogue<G, TM, TN>(a, acc, base, nb, wm, ctBase, lane);
@@ -1030,6 +1063,17 @@ constexpr bool kConvLdsB = false;
 #else
 constexpr bool kConvLdsB = true;
 #endif
+// the fast path's 1x1 convs always run the pipelined kernel; the split path's run kConv1L
+// unless built with -DKC_SPLIT_1X1_PIPE (round 6: the pipelined split instance is correct --
+// test_gpu_nn / test_gpu_train green -- but measured equal: b18c384nbt accurate 54.95 vs
+// 54.99 ms, b10c128 1.99-2.02 ms either way, profiles/r06/split_1x1_pipe_ab.txt)
+#ifdef KC_SPLIT_1X1_PIPE
+template <bool SPLIT>
+constexpr bool kConv1PipeFor = true;
+#else
+template <bool SPLIT>
+constexpr bool kConv1PipeFor = !SPLIT;
+#endif
 
 template <int X, int Y, int KT, int TN, bool SPLIT, int WN>
 void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
@@ -1039,11 +1083,11 @@ void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
   if constexpr(KT == 1) {
     if(a.pro != PRO_BN)
       throw std::invalid_argument("1x1 convolutions take a BN-ReLU prologue");
-    if constexpr(!SPLIT) {
-      lds = 2 * (size_t)G::ROWS * L1P_STRIDE * 2 + 2 * (size_t)a.cin * 4;
-      fnp = (const void*)kConv1LP<X, Y, TN, WN>;
+    if(kConv1PipeFor<SPLIT> && l1pLds<X, Y, SPLIT>(a.cin) <= 160 * 1024) {
+      lds = l1pLds<X, Y, SPLIT>(a.cin);
+      fnp = (const void*)kConv1LP<X, Y, TN, SPLIT, WN>;
     } else {
-      lds = 2 * l1StageBytes<G, SPLIT>() + 2 * (size_t)a.cin * 4;
+      lds = (SPLIT ? 2 : 1) * l1StageBytes<G, SPLIT>() + 2 * (size_t)a.cin * 4;
       fnp = (const void*)kConv1L<X, Y, TN, SPLIT, WN>;
     }
   } else if constexpr(kConvLdsB && !SPLIT && WN == 2) {
@@ -1056,21 +1100,25 @@ void launchConvT(const LConvArgs& a, int grid, hipStream_t st) {
   if(lds > 160 * 1024)
     throw std::invalid_argument("layered conv: LDS budget exceeded");
   static std::mutex mu;
-  static std::set<int> done;  // devices whose attribute is set (per device)
+  // (device, kernel) pairs whose attribute is set (per device; an instance may
+  // choose between two 1x1 kernels by its input width)
+  static std::set<std::pair<int, const void*>> done;
   int dev = 0;
   KC_HIP(hipGetDevice(&dev));
   {
     std::lock_guard<std::mutex> lk(mu);
-    if(!done.count(dev)) {
+    if(!done.count({dev, fnp})) {
       KC_HIP(hipFuncSetAttribute(fnp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      done.insert(dev);
+      done.insert({dev, fnp});
     }
   }
   const int gy = (a.coutTiles + TN * WN - 1) / (TN * WN);
-  if constexpr(KT == 1 && !SPLIT)
-    hipLaunchKernelGGL((kConv1LP<X, Y, TN, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
-  else if constexpr(KT == 1)
-    hipLaunchKernelGGL((kConv1L<X, Y, TN, SPLIT, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+  if constexpr(KT == 1) {
+    if(fnp == (const void*)kConv1LP<X, Y, TN, SPLIT, WN>)
+      hipLaunchKernelGGL((kConv1LP<X, Y, TN, SPLIT, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+    else
+      hipLaunchKernelGGL((kConv1L<X, Y, TN, SPLIT, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
+  }
   else if constexpr(kConvLdsB && !SPLIT && WN == 2)
     hipLaunchKernelGGL((kConvLB<X, Y, TN, WN>), dim3(grid, gy), dim3(L_NT), lds, st, a);
   else
