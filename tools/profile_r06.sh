@@ -46,6 +46,7 @@ for s in "$@"; do
     c2finaldefault) trace r06_c2finaldefault --steps 20 --warmup 5 --precision default ;;
     c2default) trace r06_c2default --steps 20 --warmup 5 --precision default ;;
     c3default) trace r06_c3default --config C3 --steps 10 --warmup 5 ;;
+    c5default) trace r06_c5default --config C5 --window short --warmup 2 --steps 3 --rounds-per-step 100 ;;
     c4default) trace r06_c4default --config C4 --window short --warmup 8 --steps 6 --rounds-per-step 200 ;;
     c4pmc)
       pmcr r06_c4steady_fetch FETCH_SIZE --config C4 --window short --warmup 9 --steps 1 --rounds-per-step 200
@@ -63,6 +64,8 @@ for s in "$@"; do
     prodline) line c2prod 600 --steps 20 --warmup 5 --play production --no-cpu-baseline --trained-steps 0 ;;
     c3line) line c3 700 --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
     c4line) line c4 500 --config C4 --steps 6 --warmup 5 --no-cpu-baseline ;;
+    c4g4line) line c4g4 500 --config C4 --steps 6 --warmup 5 --no-cpu-baseline --groups 4 ;;
+    c3g4line) line c3g4 700 --config C3 --steps 20 --warmup 5 --no-cpu-baseline --groups 4 ;;
     c5line) line c5 500 --config C5 --steps 4 --warmup 2 --rounds-per-step 600 --no-cpu-baseline ;;
     *) echo "unknown section $s"; exit 2 ;;
   esac
