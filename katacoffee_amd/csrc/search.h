@@ -338,7 +338,8 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
 void launchSelect(const SearchDev& d, const SearchDev* dd, hipStream_t st, hipEvent_t e0 = nullptr,
                   hipEvent_t e1 = nullptr, bool resetCommit = false);
 // accumulate: add the batch size to *d.nnTimedEvals (rounds whose network launch is timed)
-void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate);
+// resolve: do launchResolve's work first, in the same dispatch (after launchBackupSelect)
+void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate, bool resolve = false);
 // Packs the device row buffer's rows into dst ([rowCap][rowBytes], rows.py FIELDS order),
 // copies their count to countOut (host, asynchronously) and empties the buffer (and the
 // finished-game records when discardGames); stream-ordered, no host synchronisation.

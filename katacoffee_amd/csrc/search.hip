@@ -1349,28 +1349,37 @@ __global__ void __launch_bounds__(64, NI <= 2 ? 4 : 2) kSelect(const SearchDev* 
 // winner's tag is cleared too (before the next kCompact bids).  A small grid: block b
 // clears the tags of games b, b + grid, ... and completes pending entries b, b + grid, ...
 constexpr int RESOLVE_GRID = 64;
-template <int NI>
-__global__ void __launch_bounds__(64) kResolve(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
-  const SearchDev& d = *dp;
-  const int lane = laneId();
-  for(int i = blockIdx.x * 64 + lane; i < d.G; i += RESOLVE_GRID * 64) {
+// The two halves of a resolve, shared by kResolve and the resolving kCompact: clearing
+// the round winners' tags (entries first, first + stride, ...) and completing the pending
+// selections (entries first, first + stride, ...; one wave each, s its LDS game copy).
+KC_D void clearRoundTags(const SearchDev& d, int first, int stride) {
+  for(int i = first; i < d.G; i += stride) {
     const uint32_t cc = d.cClear[i];
     if(cc != 0u) {
       d.cTag[cc - 1u] = 0u;
       d.cClear[i] = 0u;
     }
   }
+}
+template <int NI>
+KC_D void completePending(const SearchDev& d, const DTables& T, int first, int stride, GameDev& s) {
   const int np = *d.pendCount;
-  __shared__ GameDev s;
-  for(int k = blockIdx.x; k < np; k += RESOLVE_GRID) {
+  for(int k = first; k < np; k += stride) {
     const int g = __builtin_amdgcn_readfirstlane(d.pendList[k]);
-    GV v(d, *Tp, g);
+    GV v(d, T, g);
     loadGame(v, s);
     s.leafKind = LEAF_NN;
     cacheLookup<NI>(v, s, false);
     DRng rng = DRng{s.rngSeed, s.rngCtr};
     finishSelect(v, s, rng);
   }
+}
+template <int NI>
+__global__ void __launch_bounds__(64) kResolve(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp) {
+  const SearchDev& d = *dp;
+  clearRoundTags(d, blockIdx.x * 64 + laneId(), RESOLVE_GRID * 64);
+  __shared__ GameDev s;
+  completePending<NI>(d, *Tp, blockIdx.x, RESOLVE_GRID, s);
 }
 
 // oracle postprocess (nneval.cpp:702-815 + copyOutputsWithSymmetry nninputs.cpp:349-357)
@@ -3542,11 +3551,25 @@ __global__ void __launch_bounds__(64) kCommit(const SearchDev* __restrict__ dp, 
 // other group's network kernels, where a 1024-thread one waited for a whole CU to
 // drain: 34 us per launch at C3)
 constexpr int CP_CH = 32;
-__global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, int accumulate) {
+// resolve != 0 (after a fused kBackupSelect): the block first does kResolve's work -- the
+// round winners' tags cleared by every thread, the pending selections completed by waves
+// 0-3 -- and the compaction below reads the need flags and bids those selections wrote
+// after a workgroup barrier: one dispatch fewer on every fused round.
+constexpr int CP_RESOLVE_WAVES = 4;
+template <int NI>
+__global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp,
+                                                 int accumulate, int resolve) {
   const SearchDev& d = *dp;
   __shared__ uint32_t wsum[16], wpre[17];
   const int nt = blockDim.x, nw = nt >> 6;  // 256 or 1024 threads (launchCompact)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if(resolve) {
+    __shared__ GameDev rs[CP_RESOLVE_WAVES];
+    clearRoundTags(d, t, nt);
+    if(w < CP_RESOLVE_WAVES)
+      completePending<NI>(d, *Tp, w, CP_RESOLVE_WAVES, rs[w]);
+    __syncthreads();
+  }
   const int nch = (d.G + 63) >> 6;
   const int cpw = (nch + nw - 1) / nw;  // chunks per wave (<= 64: G < 65536, >= 16 waves past 8192 games)
   const int g0 = w * cpw * 64 + lane;   // this lane's game in the wave's first chunk
@@ -3634,7 +3657,7 @@ __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ d
   if(t == nt - 1) {
     const int count = min(total, cap);
     *d.nnCount = count;
-    *d.pendCount = 0;  // the pending list kResolve (before this kernel) completed
+    *d.pendCount = 0;  // the pending list kResolve (or the resolve phase above) completed
     if(accumulate)
       *d.nnTimedEvals += (unsigned long long)count;
   }
@@ -3800,9 +3823,15 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
 // 256 threads (one wave per SIMD) while each wave keeps at most CP_CH chunks of 64 games: a workgroup
 // that small fits beside a network workgroup of the other game group on its CU (1024
 // threads need 4 waves per SIMD) and does not wait for a free one.
-void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate) {
+void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate, bool resolve) {
   const int nt = d.G <= 4 * 64 * CP_CH ? 256 : 1024;  // 1024 only past 8192 games per engine
-  hipLaunchKernelGGL(kCompact, dim3(1), dim3(nt), 0, st, dd, accumulate ? 1 : 0);
+  const DTables* T = d.T;
+  const int a = accumulate ? 1 : 0, r = resolve ? 1 : 0;
+  switch(laneItems(d.P)) {
+    case 2: hipLaunchKernelGGL(kCompact<2>, dim3(1), dim3(nt), 0, st, dd, T, a, r); break;
+    case 4: hipLaunchKernelGGL(kCompact<4>, dim3(1), dim3(nt), 0, st, dd, T, a, r); break;
+    default: hipLaunchKernelGGL(kCompact<7>, dim3(1), dim3(nt), 0, st, dd, T, a, r); break;
+  }
   KC_HIP(hipGetLastError());
 }
 

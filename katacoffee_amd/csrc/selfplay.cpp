@@ -252,6 +252,8 @@ SelfplayEngine::SelfplayEngine(const coffee_selfplay_config& c) {
   {
     const char* f = getenv("COFFEE_FUSED_ROUNDS");
     fuseRounds_ = f && f[0] == '0' ? 0 : (f && f[0] == '1' ? 1 : -1);
+    const char* r = getenv("COFFEE_SEPARATE_RESOLVE");
+    resolveInCompact_ = !(r && r[0] == '1');
   }
   {
     const char* e = getenv("COFFEE_NN_AUDIT_EVERY");
@@ -358,13 +360,14 @@ void SelfplayEngine::step(int rounds, hipStream_t st) {
     // select, network and backup are timed by their own dispatches (kernel start to
     // end, like rocprofv3); compact and cache write run untimed between them
     if(selected) {
-      launchResolve(d, dd_, st);  // the selections whose cache slot was being written
+      if(!resolveInCompact_)
+        launchResolve(d, dd_, st);  // the selections whose cache slot was being written
     } else {
       const bool t0 = sampleNow(0);
       timedKernel(0, t0, [&](hipEvent_t a, hipEvent_t b) { launchSelect(d, dd_, st, a, b, commitReset_); });
     }
     commitReset_ = false;
-    launchCompact(d, dd_, st, t1);
+    launchCompact(d, dd_, st, t1, selected && resolveInCompact_);
     timedKernel(1, t1, [&](hipEvent_t a, hipEvent_t b) {
       const int rows = std::min(d.G, d.nnCap);  // grid bound; the batch is *d.nnCount rows
       if(nn_) {

@@ -83,6 +83,10 @@ class SelfplayEngine {
   // workgroups: 202 vs 161 us).  COFFEE_FUSED_ROUNDS=0: never, 1: always (same results)
   int fuseRounds_ = -1;  // -1 auto, 0 never, 1 always
   bool fuseNow() const;
+  // after a fused round the pending selections are completed and the round's cache tags
+  // cleared by the compaction's own dispatch (kCompact resolve phase) instead of a separate
+  // kResolve launch; COFFEE_SEPARATE_RESOLVE=1 keeps the separate launch (same results)
+  bool resolveInCompact_ = true;
   // Audit of the default precision on self-play's own positions: every
   // auditEvery_-th network launch of an engine whose default precision resolved to the
   // corrected instance is re-evaluated (its first NN_AUDIT_ROWS rows) on the accurate

@@ -131,7 +131,7 @@ void launchSelect(const SearchDev& d, const SearchDev*, hipStream_t, hipEvent_t 
   stamp(e1);
 }
 
-void launchCompact(const SearchDev& d, const SearchDev*, hipStream_t, bool accumulate) {
+void launchCompact(const SearchDev& d, const SearchDev*, hipStream_t, bool accumulate, bool) {
   const int n = d.G < d.nnCap ? d.G : d.nnCap;
   *d.nnCount = n;
   for(int i = 0; i < n; i++)
