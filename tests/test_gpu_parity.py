@@ -252,16 +252,18 @@ def test_selfplay_network_smoke(model_path):
     sp.close()
 
 
-def _engine(fused, X=5, Y=5, W=4, **kw):
-    # the engine reads COFFEE_FUSED_ROUNDS when it is created
-    old = os.environ.pop("COFFEE_FUSED_ROUNDS", None)
-    os.environ["COFFEE_FUSED_ROUNDS"] = "1" if fused else "0"
+def _engine(fused, X=5, Y=5, W=4, separate_resolve=False, **kw):
+    # the engine reads COFFEE_FUSED_ROUNDS / COFFEE_SEPARATE_RESOLVE when it is created
+    env = {"COFFEE_FUSED_ROUNDS": "1" if fused else "0", "COFFEE_SEPARATE_RESOLVE": "1" if separate_resolve else "0"}
+    old = {k: os.environ.pop(k, None) for k in env}
+    os.environ.update(env)
     try:
         return kc.Selfplay(X, Y, W, **kw)
     finally:
-        os.environ.pop("COFFEE_FUSED_ROUNDS", None)
-        if old is not None:
-            os.environ["COFFEE_FUSED_ROUNDS"] = old
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
 
 
 # Fused rounds (kBackupSelect + kResolve) against separate kSelect / kBackup launches:
@@ -309,6 +311,41 @@ def test_fused_rounds_match_separate_kernels(games, visits, rounds, seed, cache_
     for k in ra:
         np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
     assert a.kernel_time(4)[1] > rounds // 2 and b.kernel_time(4)[1] == 0  # fused launches ran in a only
+    a.close()
+    b.close()
+
+
+# The pending selections and tag clears of a fused round run inside kCompact's dispatch
+# (the default) or in a separate kResolve launch (COFFEE_SEPARATE_RESOLVE=1): the same
+# games, trees and rows.  The 32-entry cache sends most lookups down the pending path.
+@pytest.mark.parametrize("games,visits,rounds,seed,cache_log2,ci,net",
+                         [(64, 32, 700, 61, 5, 4, False), (96, 16, 500, 73, 5, 16, True)],
+                         ids=["cache32-ci4", "network-ci16"])
+def test_resolve_in_compact_matches_separate_resolve(games, visits, rounds, seed, cache_log2, ci, net, model_path):
+    kw = dict(num_games=games, max_visits=visits, seed=seed, node_cap=visits + 96, commit_interval=ci,
+              nn_cache_log2=cache_log2)
+    if net:
+        kw["model_path"] = model_path
+    a, b = _engine(True, **kw), _engine(True, separate_resolve=True, **kw)
+    done = 0
+    for chunk in [37, rounds]:  # the first step ends inside a commit interval
+        a.step(chunk - done)
+        b.step(chunk - done)
+        done = chunk
+        for g in range(games):
+            assert a.game_info(g) == b.game_info(g), (chunk, g)
+            na, ea = a.game_tree(g)
+            nb, eb = b.game_tree(g)
+            np.testing.assert_array_equal(na, nb, err_msg="round %d game %d nodes" % (chunk, g))
+            np.testing.assert_array_equal(ea, eb, err_msg="round %d game %d edges" % (chunk, g))
+    sa, sb = a.stats(), b.stats()
+    for k in ("playouts", "nn_evals", "moves", "games_finished", "rows_pending"):
+        assert sa[k] == sb[k], k
+    assert sa["games_finished"] > 0
+    ra, rb = _sorted_rows(a.drain_rows()), _sorted_rows(b.drain_rows())
+    assert len(ra["meta"]) > 0
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
     a.close()
     b.close()
 
