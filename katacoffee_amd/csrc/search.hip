@@ -3556,14 +3556,17 @@ constexpr int CP_CH = 32;
 // 0-3 -- and the compaction below reads the need flags and bids those selections wrote
 // after a workgroup barrier: one dispatch fewer on every fused round.
 constexpr int CP_RESOLVE_WAVES = 4;
-template <int NI>
+// (The resolving instance alone holds the LDS game copies: the plain one, which the separate
+// round kernels and the default precision's network run beside, keeps its 132 bytes of LDS
+// and fits on a CU next to any network workgroup.)
+template <int NI, bool RESOLVE>
 __global__ void __launch_bounds__(1024) kCompact(const SearchDev* __restrict__ dp, const DTables* __restrict__ Tp,
-                                                 int accumulate, int resolve) {
+                                                 int accumulate) {
   const SearchDev& d = *dp;
   __shared__ uint32_t wsum[16], wpre[17];
   const int nt = blockDim.x, nw = nt >> 6;  // 256 or 1024 threads (launchCompact)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if(resolve) {
+  if constexpr(RESOLVE) {
     __shared__ GameDev rs[CP_RESOLVE_WAVES];
     clearRoundTags(d, t, nt);
     if(w < CP_RESOLVE_WAVES)
@@ -3826,12 +3829,15 @@ void launchSelfplayInit(const SearchDev& d, const SearchDev* dd, hipStream_t st)
 void launchCompact(const SearchDev& d, const SearchDev* dd, hipStream_t st, bool accumulate, bool resolve) {
   const int nt = d.G <= 4 * 64 * CP_CH ? 256 : 1024;  // 1024 only past 8192 games per engine
   const DTables* T = d.T;
-  const int a = accumulate ? 1 : 0, r = resolve ? 1 : 0;
-  switch(laneItems(d.P)) {
-    case 2: hipLaunchKernelGGL(kCompact<2>, dim3(1), dim3(nt), 0, st, dd, T, a, r); break;
-    case 4: hipLaunchKernelGGL(kCompact<4>, dim3(1), dim3(nt), 0, st, dd, T, a, r); break;
-    default: hipLaunchKernelGGL(kCompact<7>, dim3(1), dim3(nt), 0, st, dd, T, a, r); break;
-  }
+  const int a = accumulate ? 1 : 0;
+  if(!resolve)
+    hipLaunchKernelGGL((kCompact<2, false>), dim3(1), dim3(nt), 0, st, dd, T, a);
+  else
+    switch(laneItems(d.P)) {
+      case 2: hipLaunchKernelGGL((kCompact<2, true>), dim3(1), dim3(nt), 0, st, dd, T, a); break;
+      case 4: hipLaunchKernelGGL((kCompact<4, true>), dim3(1), dim3(nt), 0, st, dd, T, a); break;
+      default: hipLaunchKernelGGL((kCompact<7, true>), dim3(1), dim3(nt), 0, st, dd, T, a); break;
+    }
   KC_HIP(hipGetLastError());
 }
 
