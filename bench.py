@@ -35,6 +35,7 @@ GPU, RCCL world size N); under torchrun the environment's WORLD_SIZE is used.
 import argparse
 import faulthandler
 import json
+import math
 import os
 import queue
 import shutil
@@ -746,6 +747,20 @@ def main():
                     "chip_level": {"achieved": d["nn_evals"] / world / elapsed * flops_per_eval / 1e12,
                                    "frac": d["nn_evals"] / world / elapsed * flops_per_eval / 1e12 / PEAK_F16_TFLOPS,
                                    "concurrent_groups": args.groups}}
+                if fused:
+                    # a fused launch runs one workgroup per CU (5 boards each when the batch bound
+                    # fits 5 per CU, else 8; nn.hip NNEngine::forward): its peak is that share of
+                    # the chip's, which the kernel's own efficiency is measured against
+                    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+                    cap = (args.nn_batch_cap // args.groups if args.nn_batch_cap else
+                           (cus * 8 // args.groups if precision == "fast" else min(cus * 5, cus * 8 // args.groups)))
+                    bound = min(-(-games // args.groups), cap)  # the launch's grid bound (selfplay.cpp step)
+                    nb = 8 if precision == "fast" and bound > 5 * cus else 5
+                    wgs = int(math.ceil(per_launch / nb))
+                    share = min(1.0, wgs / cus)
+                    roof_all["network"]["occupied_cu_share"] = {
+                        "workgroups_per_launch": wgs, "boards_per_workgroup": nb, "cus": cus,
+                        "peak": PEAK_F16_TFLOPS * share, "frac": achieved / (PEAK_F16_TFLOPS * share)}
             # tree roofline: per descent, sum over path nodes of 32 B + k * 48 B,
             # counted on the device (tree_levels, tree_children)
             tree_bytes = NODE_B * d["tree_levels"] + CHILD_B * d["tree_children"]
