@@ -193,10 +193,13 @@ def _scheduled_engine(sched, X=5, Y=5, W=4, **kw):
                           (8, 24, 1800, 43, 0, dict(side_position_prob=0.3)),
                           (8, 24, 1800, 37, 10, dict(PRODUCTION, init_games_with_policy=1, cheap_search_visits=8,
                                                      reduced_visits_min=8, nn_batch_cap=5, side_position_prob=0.2,
-                                                     **FORKS))],
+                                                     **FORKS)),
+                          # the smallest searches: one game at one visit (the root's evaluation
+                          # alone picks the move), two games at two visits with a contended cache
+                          (1, 1, 300, 31, 0, {}), (2, 2, 400, 41, 5, {})],
                          ids=["bench-a", "bench-b", "cache32", "cache16k", "production", "reduced", "batch-cap",
                               "production-cap", "production-init", "policy-init", "forks", "side-positions",
-                              "everything"])
+                              "everything", "one-game-one-visit", "two-visits"])
 def test_selfplay_fake_net_bit_exact_vs_oracle(games, visits, rounds, seed, cache_log2, play, sched):
     cap = 128
     if sched[0] > 1:
