@@ -417,8 +417,11 @@ def _compare_game(gpu, ora, g, og, done):
 @pytest.mark.parametrize("X,Y,W,games,visits,rounds,seed,cache_log2,play",
                          [(7, 7, 5, 6, 32, 1500, 3, 0, {}), (7, 7, 5, 8, 24, 1500, 5, 12, PRODUCTION),
                           (9, 9, 5, 4, 24, 1500, 7, 0, {}), (9, 9, 5, 6, 20, 1500, 11, 12,
-                                                             dict(PRODUCTION, side_position_prob=0.2, **FORKS))],
-                         ids=["7x7-bench", "7x7-production", "9x9-bench", "9x9-everything"])
+                                                             dict(PRODUCTION, side_position_prob=0.2, **FORKS)),
+                          # the largest board the ABI takes (10x10: P = 400, NI = 7) and a
+                          # rectangular one (4 symmetries instead of 8)
+                          (10, 10, 5, 3, 16, 1500, 13, 0, {}), (6, 4, 4, 6, 24, 1200, 17, 12, PRODUCTION)],
+                         ids=["7x7-bench", "7x7-production", "9x9-bench", "9x9-everything", "10x10-max", "6x4-rect"])
 @pytest.mark.parametrize("sched", [SCHEDULES[0], SCHEDULES[2]], ids=[SCHEDULE_IDS[0], SCHEDULE_IDS[2]])
 def test_selfplay_geometries_bit_exact_vs_oracle(X, Y, W, games, visits, rounds, seed, cache_log2, play, sched):
     cap = 128
