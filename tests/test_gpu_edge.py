@@ -86,3 +86,18 @@ def test_malformed_arguments_fail():
     cells, last, ldir, pla = _positions(4)
     legal, has = kc.rules_batch(5, 5, 4, cells, last, ldir, pla)
     assert legal.shape == (4, 100) and has.shape == (4,)
+
+
+def test_selfplay_rejects_bad_configuration():
+    """coffee_selfplay_create checks its arguments before allocating anything: a node pool
+    (rounded up to a multiple of 64) that cannot hold one full search (max_visits + 4
+    nodes), one past the 16-bit node index, a negative batch cap."""
+    for kw in (dict(max_visits=100, node_cap=64), dict(max_visits=32, node_cap=70000),
+               dict(max_visits=32, nn_batch_cap=-1)):
+        with pytest.raises(kc.CoffeeError):
+            kc.Selfplay(5, 5, 4, num_games=4, seed=1, **kw)
+    sp = kc.Selfplay(5, 5, 4, num_games=4, max_visits=60, node_cap=64, seed=1)  # the smallest pool
+    sp.step(400)
+    st = sp.stats()
+    assert st["errors"] == 0 and st["moves"] > 0
+    sp.close()
