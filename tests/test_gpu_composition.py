@@ -119,6 +119,10 @@ CASES = {
     "c2-default-four-groups": ("b6c96", (5, 5, 4), "default", 256, 4, 24, 14, 200, 600, PRODUCTION),
     # C3 network on the layered kernels
     "c3-layered": ("b10c128", (5, 5, 4), "fast", 256, 1, 24, 12, 200, 900, {}),
+    # C3 and C4 as the bench runs them: the default precision (the split "accurate" layered
+    # path), game groups on their own streams; C4's 7x7 / 5 with selfplay1.cfg play
+    "c3-layered-default": ("b10c128", (5, 5, 4), "default", 192, 2, 24, 12, 150, 900, {}),
+    "c4-layered-default": ("b10c128", (7, 7, 5), "default", 96, 2, 16, 12, 0, 1500, PRODUCTION),
     # C5 network (nested bottlenecks) at 9x9 / 5 on the layered kernels
     "c5-layered": ("b18c384nbt", (9, 9, 5), "fast", 24, 1, 12, 12, 0, 1500, {}),
 }
@@ -148,7 +152,7 @@ def test_selfplay_real_network_bit_exact_vs_oracle(nets, name):
 # (the fast headline fuses; the corrected network runs them separately by default).
 # The oracle runs the same schedule (oracle.Selfplay commit_interval / start_stagger).
 @pytest.mark.parametrize("sched", [(16, False, 29), (16, True, 29)], ids=["ci16-stagger", "ci16-stagger-fused"])
-@pytest.mark.parametrize("name", ["c2-fused-nb8", "c2-corrected-two-groups"])
+@pytest.mark.parametrize("name", ["c2-fused-nb8", "c2-corrected-two-groups", "c4-layered-default"])
 def test_selfplay_real_network_scheduled_bit_exact_vs_oracle(nets, name, sched):
     _run_case(nets, name, sched)
 
