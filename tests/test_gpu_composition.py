@@ -125,6 +125,8 @@ CASES = {
     "c4-layered-default": ("b10c128", (7, 7, 5), "default", 96, 2, 16, 12, 0, 1500, PRODUCTION),
     # C5 network (nested bottlenecks) at 9x9 / 5 on the layered kernels
     "c5-layered": ("b18c384nbt", (9, 9, 5), "fast", 24, 1, 12, 12, 0, 1500, {}),
+    # and at the default (split) precision C5's bench line runs
+    "c5-layered-default": ("b18c384nbt", (9, 9, 5), "default", 16, 1, 12, 12, 0, 1200, {}),
 }
 
 
