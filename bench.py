@@ -128,12 +128,12 @@ def parse():
     ap.add_argument("--row-sink", choices=["local", "gather"], default="local",
                     help="N > 1: local = every rank writes its own games' rows (sharded games, no collective in "
                          "the loop); gather = rows gathered to rank 0 over RCCL each step (one writer)")
-    ap.add_argument("--cpu-seconds", type=float, default=60.0, help="timed CPU-baseline window (saturated run)")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="timed CPU-baseline window (saturated run)")
     ap.add_argument("--cpu-curve-seconds", type=float, default=10.0,
-                    help="timed window of each point of the CPU thread-scaling curve (2, 4, 8 threads between the "
-                         "1- and 16-thread runs: the linearity the whole-host extrapolation rests on; 0: skip)")
-    ap.add_argument("--cpu-c1-seconds", type=float, default=20.0,
-                    help="timed CPU-baseline window (C1 and single-thread runs)")
+                    help="timed window of the single-thread run and of each point of the CPU thread-scaling curve "
+                         "(2, 4, 8 threads below the share: the linearity the whole-host extrapolation rests on; "
+                         "0: no curve, the single-thread run then takes --cpu-seconds)")
+    ap.add_argument("--cpu-c1-seconds", type=float, default=10.0, help="timed CPU-baseline window (C1)")
     ap.add_argument("--cpu-warmup-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-whole-host", action="store_true",
                     help="also time the CPU baseline on every CPU of the affinity mask (default: extrapolated, "
@@ -335,17 +335,21 @@ def cpu_baseline(args, cfg, model_path):
     if cfg["arch"] == "b6c96" and (cfg["X"], cfg["Y"]) == (5, 5):
         c1 = run(1, 200, 1, args.cpu_c1_seconds, 5.0)
     sat = run(gpt * cores, visits, cores, args.cpu_seconds)
-    one = run(gpt, visits, 1, args.cpu_c1_seconds, 5.0) if cores > 1 else sat
+    # the single-thread run and the curve's points share one regime (the saturated run's
+    # warm-up, then cpu_curve_seconds) and run back to back, so the per-thread rates they
+    # compare saw the same game phase (a group's rate still rises after its first rounds:
+    # +5 % from 5 s to 30 s of warm-up, +28 % to 60 s in the build container) and the same
+    # load from the host's other tenants
+    curve_s = args.cpu_curve_seconds if args.cpu_curve_seconds > 0 else args.cpu_seconds
+    one = run(gpt, visits, 1, curve_s) if cores > 1 else sat
     eff = sat["playouts_per_sec"] / (cores * one["playouts_per_sec"]) if one["playouts_per_sec"] > 0 else None
     curve = {}
     t = 2
     while t < cores and args.cpu_curve_seconds > 0:
-        # the single-thread run's 5 s warm-up (a group's first rounds are root evaluations,
-        # slower in playouts/s than its steady state)
-        curve[t] = run(gpt * t, visits, t, args.cpu_curve_seconds, 5.0)["playouts_per_sec"]
+        curve[t] = run(gpt * t, visits, t, curve_s)["playouts_per_sec"]
         t *= 2
     curve[1], curve[cores] = one["playouts_per_sec"], sat["playouts_per_sec"]
-    desc = lambda r, g, t, w=5.0: ("%d games x %d visits on %d threads (%d independent groups of %d), %.0f s warm-up "
+    desc = lambda r, g, t, w=args.cpu_warmup_seconds: ("%d games x %d visits on %d threads (%d independent groups of %d), %.0f s warm-up "
                                    "then %.1f s (%d rounds per group, %d moves, %d playouts)"
                                    % (g, visits, t, t, r["games_per_thread"], w, r["seconds"], r["rounds"], r["moves"],
                                       r["playouts"]))
@@ -357,6 +361,8 @@ def cpu_baseline(args, cfg, model_path):
                   % (cfg["label"].split(":")[0], desc(sat, gpt * cores, cores, args.cpu_warmup_seconds)),
         "single_thread": {"rows_per_sec": one["rows_per_sec"], "playouts_per_sec": one["playouts_per_sec"],
                           "sample": desc(one, gpt, 1), "scaling_efficiency_at_%d" % cores: eff},
+        # the points below the share: the single-thread run's regime; the share's own point
+        # is the saturated run (its longer window)
         "thread_curve_playouts_per_sec": {str(k): curve[k] for k in sorted(curve)},
         # playouts/s at t threads / (t x the 1-thread rate): the whole-host extrapolation's premise
         "thread_curve_efficiency": {str(k): curve[k] / (k * curve[1]) if curve.get(1) else None for k in sorted(curve)},
