@@ -1859,6 +1859,11 @@ __global__ void __launch_bounds__(64, NI <= 4 ? 4 : 3) kBackup(const SearchDev* 
 #ifndef KC_FUSED_OCC
 #define KC_FUSED_OCC 4
 #endif
+// A/B switch: KC_SEARCH_PRIO > 0 raises the fused search waves' issue priority (s_setprio)
+// over the other group's network waves sharing their SIMD
+#ifndef KC_SEARCH_PRIO
+#define KC_SEARCH_PRIO 0
+#endif
 template <int NI>
 __global__ void __launch_bounds__(64, NI <= 2 ? KC_FUSED_OCC : 2) kBackupSelect(const SearchDev* __restrict__ dp,
                                                                       const DTables* __restrict__ Tp) {
@@ -1866,6 +1871,8 @@ __global__ void __launch_bounds__(64, NI <= 2 ? KC_FUSED_OCC : 2) kBackupSelect(
   const int g = blockIdx.x;
   if(g >= d.G)
     return;
+  if constexpr(KC_SEARCH_PRIO > 0)
+    __builtin_amdgcn_s_setprio(KC_SEARCH_PRIO);
   __shared__ __attribute__((aligned(16))) float scratch[3 * MAX_P];
   __shared__ uint32_t hasBits[(MAX_P + 31) / 32];
   __shared__ GameDev s;
